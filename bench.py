@@ -1,0 +1,208 @@
+"""Headline benchmark: SVGD inner step, N=65536 particles, d=8, GMM(k=4), fp64.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+BASELINE.json metric: particle-updates/s (N x steps / s) at N=65536, d=8
+(cfg3).  One step = SVGD::Step of the reference (SVGD.hpp:373-400):
+median-heuristic scale of X_t, host-side grad log p(X_t) for this rank's rows
+(C++ closed form, OpenMP), phi_hat, Adam increment, X update -- all of it
+inside the timed region, X resident in HBM.  For N GPUs (one process each,
+torchrun) the particles are sharded by rows and the context all-gathers X and
+G over RCCL every step; N is fixed (strong scaling, as the metric specifies).
+
+The JSON line also carries
+  roofline     -- the phi kernel (dominant) measured with HIP events on the
+                  library's own stream: algorithmic flop per launch
+                  (rows x N x (5d+4)) / average launch time,
+                  against the FP64 peak (78.6 TF/s, MI355X spec; vector = matrix).
+  cpu_baseline -- the CPU oracle (a port of the reference's arithmetic) on the
+                  host cores of this box for a bounded row sample of the same
+                  workload (rank 0, N=1 only).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "particle-updates/sec (N×iters/s) + per-step ms, N=65536 d=8, 1/2/4/8 GPU"
+FP64_PEAK_TFLOPS = 78.6  # MI355X spec (not in MI355X_MICROARCH.md; vector = matrix for fp64)
+
+
+def splitmix(shape, scale, seed):
+    """splitmix64 -> uniform[-1,1) (SURVEY §8(d) synthetic inputs), vectorised."""
+    cnt = int(np.prod(shape))
+    with np.errstate(over="ignore"):
+        s = (np.uint64(seed) + np.arange(1, cnt + 1, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+        z = s.copy()
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    u = (z >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    return (scale * (u * 2.0 - 1.0)).reshape(shape)
+
+
+def workload(n, d, k):
+    X0 = splitmix((n, d), 3.0, 0x5EED)
+    mus = splitmix((k, d), 3.0, 0x5EEE)
+    covs = np.stack([np.eye(d) * (1.0 + 0.25 * c) for c in range(k)])
+    return X0, mus, covs
+
+
+def cpu_baseline(X0, mus, covs, rows):
+    """Oracle (CPU port of the reference arithmetic) on a row sample of one step:
+    median work of `rows` rows, their log-gradients, phi_hat and Adam."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+
+    n, d = X0.shape
+    rows = min(rows, n)
+    t0 = time.perf_counter()
+    o.median_rows_work(X0, 0, rows)
+    G = o.logp_grad_gmm(X0, mus, covs)  # all rows: phi needs every G_j
+    a = 0.5  # value irrelevant to the cost
+    ph = o.phi(X0, G, a, rows=(0, rows))
+    Xs = X0[:rows].copy()
+    o.apply_update(Xs, o.Adam((rows, d), 0.1, 0.9, 0.999).step(ph))
+    dt = time.perf_counter() - t0
+    return {
+        "value": rows / dt,
+        "unit": "particle-updates/s",
+        "cores": int(o.num_threads()),
+        "kind": "port",
+        "sample": f"one step of the N={n} d={d} GMM(k=4) workload restricted to {rows} particle rows "
+                  f"(their median pair share, grad log p of all N, phi_hat of {rows} rows against all N, "
+                  f"Adam); {dt:.2f} s, OpenMP threads={o.num_threads()}",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--d", type=int, default=8)
+    ap.add_argument("--k", type=int, default=4)
+    ap.add_argument("--cpu-rows", type=int, default=8192)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import svgdcpp_amd as S
+    from svgdcpp_amd import _capi as C
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+
+    n, d, k = args.n, args.d, args.k
+    X0, mus, covs = workload(n, d, k)
+
+    uid = None
+    if world > 1:
+        box = [S.Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    ctx = S.Context(d, n, device=local_rank, world=world, rank=rank, unique_id=uid)
+    ctx.set_particles(X0)
+    ctx.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+    model = S.GaussianSum(list(mus), list(covs))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        ctx.step_with_model(model)
+    ctx.sync()
+    ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))  # drop warmup events
+    ctx.check(ctx.lib.svgd_set_timing(ctx.h, 1))
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.step_with_model(model)
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    phi_ms, med_ms, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    ctx.check(ctx.lib.svgd_get_timing(ctx.h, ctypes.byref(phi_ms), ctypes.byref(med_ms), ctypes.byref(cnt)))
+    a, med, path = ctx.last_scale()
+    rows = ctx.row1 - ctx.row0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    if rank == 0:
+        phi_avg_s = phi_ms.value / max(1, cnt.value) / 1e3
+        flops_launch = float(rows) * n * (5 * d + 4)
+        achieved = flops_launch / phi_avg_s / 1e12 if phi_avg_s > 0 else None
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "phi_pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("n") == n and pmc.get("d") == d and pmc.get("world") == world:
+                traffic = pmc.get("bytes_per_launch")
+        out = {
+            "metric": METRIC,
+            "value": n * args.steps / elapsed,
+            "unit": "particle-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 X0 = 3*U[-1,1]^d, GMM means 3*U[-1,1]^d, cov_k = (1+0.25k) I)",
+            "config": {
+                "workload": f"cfg3: N={n} d={d} GMM(k={k}) RBF-median + Adam(0.1,0.9,0.999), fp64, "
+                            f"host grad log p per step",
+                "n": n, "d": d, "k": k, "parallelism": f"rows{world}",
+            },
+            "roofline": {
+                "kernel": "k_phi (fused RBF + grad + phi contraction)",
+                "bound": "mfma",
+                "achieved": achieved,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+                "traffic": traffic,
+                "avg_launch_ms": phi_avg_s * 1e3,
+                "flop_per_launch": flops_launch,
+            },
+            "phases_ms_per_step": {"phi": phi_ms.value / max(1, args.steps),
+                                   "median": med_ms.value / max(1, args.steps)},
+            "median_path": ["direct", "bracket", "fallback"][path],
+            "scale_a": a,
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

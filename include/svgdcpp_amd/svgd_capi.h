@@ -1,0 +1,195 @@
+/*
+ * svgd_capi.h -- C-ABI boundary of the MI355X-native SVGD inner step.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (khaiyichin/SVGDCpp, paths relative to the reference root):
+ *
+ *   SVGD::Step            include/SVGDCpp/SVGD.hpp:373-400   -> svgd_step / svgd_begin_step+svgd_finish_step
+ *   SVGD::ComputePhi      include/SVGDCpp/SVGD.hpp:407-454   -> svgd_phi
+ *   GaussianRBFKernel::Step/ComputeScale/ComputeMedian
+ *                         include/SVGDCpp/Kernel/GaussianRBFKernel.hpp:141-156,164-188,222-254
+ *                                                            -> svgd_median_scale
+ *   Kernel::EvaluateKernel/EvaluateKernelGrad (RBF lambda :75-81)
+ *                         include/SVGDCpp/Kernel/Kernel.hpp:279-297 -> fused inside svgd_phi
+ *   Optimizer::Initialize/Step  Adam.hpp:61-83, AdaGrad.hpp:49-65, RMSProp.hpp:58-74
+ *                                                            -> svgd_set_optimizer / svgd_reset_optimizer
+ *   bounds setup/clamp    include/SVGDCpp/SVGD.hpp:184-216,396-399 -> svgd_set_bounds
+ *   coordinate matrix     std::shared_ptr<Eigen::MatrixXd> (SVGD.hpp:494) -> svgd_set_particles / svgd_get_particles
+ *
+ * Conventions
+ *  - Plain C types only.  Host buffers are caller-owned and only touched
+ *    during the call.  Particle matrices use the reference's layout: a
+ *    d x n column-major Eigen matrix, i.e. particle i occupies
+ *    X[i*d .. i*d+d-1] (doubles).
+ *  - A context owns all device memory and one HIP stream; it is driven by a
+ *    single host thread.
+ *  - Multi-GPU: one process (context) per GPU.  Particles are sharded by
+ *    contiguous rows (svgd_shard); per step the context all-gathers the
+ *    coordinates and log-gradients over RCCL and all-reduces the median
+ *    counts.  Every rank must make the same sequence of calls.
+ *  - Errors: every int-returning function returns SVGD_OK (0) or a negative
+ *    SVGD_ERR_* code; svgd_last_error() gives the message, already prefixed
+ *    "SVGDCpp: " like the reference's exceptions (Exceptions.hpp:16-56).
+ */
+#ifndef SVGDCPP_AMD_SVGD_CAPI_H
+#define SVGDCPP_AMD_SVGD_CAPI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ----- return codes (mapped onto the reference's exception types by the
+ *       C++ shim include/SVGDCpp/SVGD.hpp) ------------------------------ */
+#define SVGD_OK 0
+#define SVGD_ERR_DIM -1     /* DimensionMismatchException (SVGD.hpp:172,195,207) */
+#define SVGD_ERR_UNSET -2   /* UnsetException (GaussianRBFKernel.hpp:57) */
+#define SVGD_ERR_ARG -3     /* std::invalid_argument (SVGD.hpp:225-235, Adam.hpp:47) */
+#define SVGD_ERR_HIP -4     /* HIP runtime failure -> std::runtime_error */
+#define SVGD_ERR_RCCL -5    /* RCCL failure        -> std::runtime_error */
+#define SVGD_ERR_RUNTIME -6 /* other runtime error -> std::runtime_error */
+
+/* compute dtype of the device path (host I/O is always double) */
+#define SVGD_F64 0
+#define SVGD_F32 1
+
+/* optimizer kinds (Optimizer/Adam.hpp, AdaGrad.hpp, RMSProp.hpp) */
+#define SVGD_OPT_ADAM 0
+#define SVGD_OPT_ADAGRAD 1
+#define SVGD_OPT_RMSPROP 2
+
+/* kernel scale methods (GaussianRBFKernel::ScaleMethod, GaussianRBFKernel.hpp:25-30).
+ * SVGD_SCALE_FIXED is an extension: M = a*I with a user-set a (the
+ * reference's "TODO: constant scale"; used by the test_svgd scenario). */
+#define SVGD_SCALE_MEDIAN 0
+#define SVGD_SCALE_FIXED 2
+
+/* median path taken by the last svgd_median_scale / step (diagnostics) */
+#define SVGD_MEDIAN_DIRECT 0   /* all pair keys stored and selected exactly */
+#define SVGD_MEDIAN_BRACKET 1  /* sampled bracket + candidate selection (exact) */
+#define SVGD_MEDIAN_FALLBACK 2 /* bracket missed: streamed radix select (exact) */
+
+typedef struct svgd_ctx svgd_ctx;
+
+/* ---- lifetime ---------------------------------------------------------- */
+
+/* Single-GPU context for `dim`-dimensional particles, n of them, on HIP
+ * device `device`.  Replaces SVGD's constructor allocations (SVGD.hpp:151-250). */
+int svgd_create(svgd_ctx **out, int dim, int64_t n, int dtype, int device);
+
+/* Multi-GPU context: rank `rank` of `world`, all ranks passing the same
+ * 128-byte RCCL unique id (from svgd_get_unique_id on one rank, broadcast by
+ * the caller by any means). */
+int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device,
+                     int world, int rank, const void *unique_id128);
+int svgd_get_unique_id(void *unique_id128);
+int svgd_destroy(svgd_ctx *ctx);
+const char *svgd_last_error(const svgd_ctx *ctx);
+
+/* Rows [*row0, *row1) of the particle matrix owned by this context. */
+int svgd_shard(const svgd_ctx *ctx, int64_t *row0, int64_t *row1);
+
+/* ---- plugins ------------------------------------------------------------ */
+
+/* Adam(lr, beta1, beta2, eps) | AdaGrad(lr, eps) | RMSProp(lr, beta=beta1, eps).
+ * Argument checks and messages follow Adam.hpp:45-48, RMSProp.hpp:42-45. */
+int svgd_set_optimizer(svgd_ctx *ctx, int kind, double lr, double beta1, double beta2,
+                       double eps);
+/* Optimizer::Initialize (zero moments, counter = 0). */
+int svgd_reset_optimizer(svgd_ctx *ctx);
+/* d-vector bounds; both NULL = unbounded (SVGD.hpp:184-190). */
+int svgd_set_bounds(svgd_ctx *ctx, const double *lower_d, const double *upper_d);
+/* SVGD_SCALE_MEDIAN (default) or SVGD_SCALE_FIXED with M = fixed_a * I. */
+int svgd_set_scale(svgd_ctx *ctx, int method, double fixed_a);
+
+/* ---- particles ---------------------------------------------------------- */
+
+/* Full n x d matrix (every rank passes the full matrix). */
+int svgd_set_particles(svgd_ctx *ctx, const double *X);
+/* Full n x d matrix (collective in multi-GPU mode). */
+int svgd_get_particles(svgd_ctx *ctx, double *X);
+/* This rank's rows only ((row1-row0) x d). */
+int svgd_get_shard(svgd_ctx *ctx, double *X_shard);
+
+/* ---- the hot path ------------------------------------------------------- */
+
+/* a = ln(n)/med^2 of the current particles (GaussianRBFKernel.hpp:168-188).
+ * Either output may be NULL.  Collective in multi-GPU mode. */
+int svgd_median_scale(svgd_ctx *ctx, double *a_out, double *med_out);
+
+/* phi_hat for this rank's rows given this rank's rows of G = grad log p and
+ * the scale a (SVGD.hpp:407-454).  phi_shard_out may be NULL (device only). */
+int svgd_phi(svgd_ctx *ctx, const double *G_shard, double a, double *phi_shard_out);
+
+/* One SVGD::Step (SVGD.hpp:373-400): scale from X_t, phi_hat from G_shard
+ * (= grad log p at this rank's rows of X_t), optimizer increment, clamp.
+ * X stays device-resident. */
+int svgd_step(svgd_ctx *ctx, const double *G_shard);
+
+/* Split step for overlapping the host log-gradient with the device median:
+ * begin launches the scale computation and copies this rank's rows of X_t
+ * into X_shard_out (returns once that copy is done; may be NULL); the caller
+ * evaluates G there and passes it to finish. */
+int svgd_begin_step(svgd_ctx *ctx, double *X_shard_out);
+int svgd_finish_step(svgd_ctx *ctx, const double *G_shard);
+
+/* Context-owned page-locked host buffers of (row1-row0) x d doubles.
+ * Passing them to svgd_begin_step / svgd_finish_step avoids a staging copy. */
+int svgd_host_buffers(svgd_ctx *ctx, double **x_shard, double **g_shard);
+
+/* Block until all work queued by the context is complete. */
+int svgd_sync(svgd_ctx *ctx);
+
+/* ---- diagnostics / measurement ----------------------------------------- */
+
+/* Scale a and median of the last step (host copies). */
+int svgd_last_scale(const svgd_ctx *ctx, double *a_out, double *med_out, int *median_path);
+/* Enable HIP-event timing of the phi kernel and the median phase on the
+ * context stream; get returns accumulated milliseconds and launch count. */
+int svgd_set_timing(svgd_ctx *ctx, int enable);
+int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *count);
+/* Median tuning knobs (tests force each path): pair count at or below which
+ * all keys are stored (direct path), sample size, candidate capacity.
+ * Values <= 0 keep the current setting. */
+int svgd_set_median_tuning(svgd_ctx *ctx, int64_t direct_max_pairs, int64_t sample_size,
+                           int64_t candidate_capacity);
+/* Upper-triangle squared-distance keys exactly as the device median sees
+ * them, in (i<j) row-major order; n(n-1)/2 doubles (small n only). */
+int svgd_debug_pair_keys(svgd_ctx *ctx, double *out, int64_t capacity);
+
+/* ---- host-side built-in models (no GPU needed) ---------------------------
+ * The target density's log-gradient stays on the host, as in the reference
+ * (Model::EvaluateLogModelGrad, include/SVGDCpp/Model/Model.hpp:335-338).
+ * A model here is the sum of `ncomp` unnormalised Gaussians
+ * exp(-1/2 (x-mu_c)^T cov_c^-1 (x-mu_c)): ncomp = 1 is MultivariateNormal
+ * (MultivariateNormal.hpp:56-61), ncomp > 1 the reference's operator+
+ * composition (Model.hpp:55-92).  mus: ncomp x dim, covs: ncomp x dim x dim. */
+int svgd_model_create(void **model, int dim, int ncomp, const double *mus, const double *covs);
+int svgd_model_destroy(void *model);
+/* G[i] = grad log p(X[i]) for nrows particles (OpenMP over rows). */
+int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G);
+
+/* ---- host-only planning helpers (no GPU needed) ------------------------ */
+
+/* Row shard of rank r among `world` for n particles: equal chunks of
+ * ceil(n/world) rows (trailing ranks may be short or empty). */
+void svgd_plan_rows(int64_t n, int world, int rank, int64_t *row0, int64_t *row1);
+/* Full-list ranks of the median (GaussianRBFKernel.hpp:222-254 over the n^2
+ * distance list incl. n diagonal zeros) mapped onto the ascending list of
+ * the n(n-1)/2 upper-triangle distances.  Writes up to two upper-list ranks
+ * (-1 = a diagonal zero) and returns how many order statistics are averaged
+ * (2 for even n^2, 1 for odd). */
+int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi);
+/* Number of block-level tiles of the median pair sweep owned by rank r
+ * (row blocks of 64; each unordered pair of particles is visited by exactly
+ * one rank), and the (row block, column block) of tile t of that rank. */
+int64_t svgd_plan_pair_tiles(int64_t n, int world, int rank);
+void svgd_plan_pair_tile(int64_t n, int world, int rank, int64_t t, int64_t *row_block,
+                         int64_t *col_block);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SVGDCPP_AMD_SVGD_CAPI_H */

@@ -1,0 +1,129 @@
+// host_models.cpp -- built-in target models, evaluated on the host.
+//
+// The reference keeps ∇log p on the host (Model::EvaluateLogModelGrad,
+// include/SVGDCpp/Model/Model.hpp:335-338) and so does this build: the
+// device step receives G = ∇log p(X_t) once per step.  CppAD is not
+// available, so the built-in models use their closed forms (the "override
+// EvaluateLogModelGrad" route of the reference's doc/instructions.md:234-301):
+//
+//   MultivariateNormal  p(x) = exp(-½ (x-μ)ᵀ Σ⁻¹ (x-μ))     MultivariateNormal.hpp:56-61
+//                       ∇log p = -Σ⁻¹ (x-μ)
+//   mvn_1 + ... + mvn_k log Σ_c exp(-½ q_c(x)), unweighted and unnormalised,
+//                       the reference's Model::operator+ (Model.hpp:55-92)
+//                       ∇log p = Σ_c w_c (-Σ_c⁻¹ (x-μ_c)),  w = softmax(-½ q)
+//
+// Rows are evaluated in parallel with OpenMP (the reference evaluates them
+// serially even in parallel mode, SVGD.hpp:412-416).
+#include <cmath>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/svgdcpp_amd/svgd_capi.h"
+
+namespace {
+
+struct HostModel {
+    int d = 0, k = 0;
+    std::vector<double> mu;   // k x d
+    std::vector<double> prec; // k x d x d (row-major)
+};
+
+// Gauss-Jordan inverse with partial pivoting; false if singular.
+bool invert(const double *A, int d, double *out)
+{
+    std::vector<double> M((size_t)d * 2 * d);
+    for (int r = 0; r < d; ++r)
+        for (int c = 0; c < 2 * d; ++c)
+            M[(size_t)r * 2 * d + c] = c < d ? A[r * d + c] : (c - d == r ? 1.0 : 0.0);
+    for (int c = 0; c < d; ++c) {
+        int p = c;
+        for (int r = c + 1; r < d; ++r)
+            if (std::fabs(M[(size_t)r * 2 * d + c]) > std::fabs(M[(size_t)p * 2 * d + c])) p = r;
+        if (M[(size_t)p * 2 * d + c] == 0.0) return false;
+        if (p != c)
+            for (int q = 0; q < 2 * d; ++q) std::swap(M[(size_t)c * 2 * d + q], M[(size_t)p * 2 * d + q]);
+        const double piv = M[(size_t)c * 2 * d + c];
+        for (int q = 0; q < 2 * d; ++q) M[(size_t)c * 2 * d + q] /= piv;
+        for (int r = 0; r < d; ++r) {
+            if (r == c) continue;
+            const double f = M[(size_t)r * 2 * d + c];
+            if (f == 0.0) continue;
+            for (int q = 0; q < 2 * d; ++q) M[(size_t)r * 2 * d + q] -= f * M[(size_t)c * 2 * d + q];
+        }
+    }
+    for (int r = 0; r < d; ++r)
+        for (int c = 0; c < d; ++c) out[r * d + c] = M[(size_t)r * 2 * d + d + c];
+    return true;
+}
+
+} // namespace
+
+extern "C" {
+
+int svgd_model_create(void **out, int dim, int ncomp, const double *mus, const double *covs)
+{
+    if (!out || dim <= 0 || ncomp <= 0 || !mus || !covs) return SVGD_ERR_ARG;
+    HostModel *m = new (std::nothrow) HostModel();
+    if (!m) return SVGD_ERR_RUNTIME;
+    m->d = dim;
+    m->k = ncomp;
+    m->mu.assign(mus, mus + (size_t)ncomp * dim);
+    m->prec.resize((size_t)ncomp * dim * dim);
+    for (int c = 0; c < ncomp; ++c)
+        if (!invert(covs + (size_t)c * dim * dim, dim, m->prec.data() + (size_t)c * dim * dim)) {
+            delete m;
+            return SVGD_ERR_ARG;
+        }
+    *out = m;
+    return SVGD_OK;
+}
+
+int svgd_model_destroy(void *model)
+{
+    delete static_cast<HostModel *>(model);
+    return SVGD_OK;
+}
+
+int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G)
+{
+    const HostModel *m = static_cast<const HostModel *>(model);
+    if (!m || (!X && nrows > 0) || (!G && nrows > 0)) return SVGD_ERR_ARG;
+    const int d = m->d, k = m->k;
+#pragma omp parallel
+    {
+        std::vector<double> diff(d), gc((size_t)k * d), q(k);
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < nrows; ++i) {
+            const double *x = X + i * d;
+            double qmin = INFINITY;
+            for (int c = 0; c < k; ++c) {
+                const double *P = m->prec.data() + (size_t)c * d * d;
+                const double *mu = m->mu.data() + (size_t)c * d;
+                for (int r = 0; r < d; ++r) diff[r] = x[r] - mu[r];
+                double qq = 0.0;
+                for (int r = 0; r < d; ++r) {
+                    double s = 0.0;
+                    for (int l = 0; l < d; ++l) s += P[r * d + l] * diff[l];
+                    gc[(size_t)c * d + r] = -s;
+                    qq += diff[r] * s;
+                }
+                q[c] = 0.5 * qq;
+                qmin = q[c] < qmin ? q[c] : qmin;
+            }
+            double wsum = 0.0;
+            for (int c = 0; c < k; ++c) {
+                q[c] = std::exp(-(q[c] - qmin));
+                wsum += q[c];
+            }
+            for (int r = 0; r < d; ++r) {
+                double s = 0.0;
+                for (int c = 0; c < k; ++c) s += q[c] * gc[(size_t)c * d + r];
+                G[i * d + r] = s / wsum;
+            }
+        }
+    }
+    return SVGD_OK;
+}
+
+} // extern "C"

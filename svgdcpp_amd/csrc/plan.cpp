@@ -1,0 +1,84 @@
+// plan.cpp -- host-only work partitioning of the SVGD step (no GPU needed).
+//
+// Rows: particle i's phi_hat (SVGD.hpp:407-454) depends on every particle
+// but is written only to row i, and the optimizer state is per particle
+// (Adam.hpp:61-67), so ranks own contiguous row ranges.
+//
+// Median pairs: the reference takes the median over all n^2 distances
+// (GaussianRBFKernel.hpp:185, 222-254): n diagonal zeros plus every
+// off-diagonal distance twice.  Only the n(n-1)/2 upper-triangle values are
+// visited, as 64x64 block tiles: row block I pairs with itself (upper
+// triangle inside the tile) and with column blocks I+1 .. I+H (mod nb),
+// H = floor((nb-1)/2), plus I + nb/2 when nb is even and I < nb/2.  Every
+// unordered pair of blocks then appears exactly once and every row block
+// has the same number of tiles (+-1), so contiguous tile ranges balance the
+// ranks.
+#include <stdint.h>
+
+#include "../../include/svgdcpp_amd/svgd_capi.h"
+
+extern "C" {
+
+// Equal chunks of ceil(n/world) rows (the last ones may be short or empty),
+// so the per-step all-gather is a single in-place ncclAllGather.
+void svgd_plan_rows(int64_t n, int world, int rank, int64_t *row0, int64_t *row1)
+{
+    if (world < 1) world = 1;
+    const int64_t chunk = (n + world - 1) / world;
+    const int64_t r0 = chunk * rank, r1 = chunk * (rank + 1);
+    *row0 = r0 < n ? r0 : n;
+    *row1 = r1 < n ? r1 : n;
+}
+
+int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi)
+{
+    // full sorted list v of n^2 values; index k < n are the diagonal zeros,
+    // index k >= n maps to upper-list rank (k - n) / 2.
+    const int64_t total = n * n;
+    auto map = [n](int64_t k) -> int64_t { return k < n ? -1 : (k - n) / 2; };
+    if (total % 2 == 0) {
+        *rank_lo = map(total / 2 - 1);
+        *rank_hi = map(total / 2);
+        return 2;
+    }
+    *rank_lo = *rank_hi = map(total / 2);
+    return 1;
+}
+
+static int64_t tiles_total(int64_t nb) { return nb * (nb + 1) / 2; }
+
+int64_t svgd_plan_pair_tiles(int64_t n, int world, int rank)
+{
+    const int64_t nb = (n + 63) / 64;
+    const int64_t T = tiles_total(nb);
+    if (world < 1) world = 1;
+    return T * (rank + 1) / world - T * rank / world;
+}
+
+void svgd_plan_pair_tile(int64_t n, int world, int rank, int64_t t, int64_t *row_block,
+                         int64_t *col_block)
+{
+    const int64_t nb = (n + 63) / 64;
+    if (world < 1) world = 1;
+    t += tiles_total(nb) * rank / world;
+    const int64_t H = (nb - 1) / 2;
+    int64_t I, slot;
+    if ((nb & 1) == 0) {
+        const int64_t c1 = H + 2, c2 = H + 1, half = nb / 2;
+        if (t < half * c1) {
+            I = t / c1;
+            slot = t - I * c1;
+        } else {
+            const int64_t u = t - half * c1;
+            I = half + u / c2;
+            slot = u - (I - half) * c2;
+        }
+    } else {
+        I = t / (H + 1);
+        slot = t - I * (H + 1);
+    }
+    *row_block = I;
+    *col_block = slot == 0 ? I : (I + slot) % nb;
+}
+
+} // extern "C"

@@ -1,0 +1,842 @@
+// svgd_capi.cpp -- C-ABI implementation: context, buffers, step orchestration.
+//
+// One context = one GPU (one process per GPU in multi-GPU runs).  The step
+// follows SVGD::Step (reference include/SVGDCpp/SVGD.hpp:373-400):
+//   kernel->Step()  -> median scale (GaussianRBFKernel.hpp:141-188)
+//   ComputePhi()    -> phi_hat      (SVGD.hpp:407-454)
+//   X += opt.Step() -> optimizer + clamp (SVGD.hpp:393-399)
+// with X device-resident and only G (host model gradients, Model.hpp:335)
+// crossing PCIe each step.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/svgdcpp_amd/svgd_capi.h"
+#include "svgd_kernels.h"
+
+using namespace svgd_amd;
+
+namespace {
+
+constexpr int64_t TB = 64;
+
+struct EvPair {
+    hipEvent_t a, b;
+};
+
+} // namespace
+
+struct svgd_ctx {
+    int dim = 0;
+    int64_t n = 0;
+    int dtype = SVGD_F64;
+    int device = 0;
+    int world = 1, rank = 0;
+    ncclComm_t comm = nullptr;
+    int64_t row0 = 0, row1 = 0, nrows = 0, chunk = 0;
+    int KP = 0, NCB = 0, VW = 0;
+    int64_t nb = 0, np = 0; // row blocks; padded rows of the work arrays
+    hipStream_t stream = nullptr;
+
+    // device buffers
+    double *X = nullptr;   // world*chunk x d (first n rows are the particles)
+    double *G = nullptr;   // world*chunk x d
+    double *xc = nullptr;  // np x KP
+    double *nrm = nullptr; // np
+    double *cvec = nullptr;
+    double *V = nullptr;   // np x VW
+    double *phi = nullptr; // nrows x d
+    double *m = nullptr, *v = nullptr;
+    double *lower = nullptr, *upper = nullptr;
+    double *partial = nullptr;
+    int nparts = 64;
+    double *scal = nullptr; // [0] a, [1] med
+
+    // median
+    int64_t direct_max_pairs = int64_t(1) << 24;
+    int64_t sample_size = int64_t(1) << 22;
+    int64_t cand_capacity = 0; // 0 = automatic
+    uint64_t *sample_keys = nullptr;
+    int64_t sample_alloc = 0;
+    uint64_t *regions = nullptr;
+    int64_t regions_alloc = 0;
+    uint32_t *counts = nullptr;
+    unsigned long long *below = nullptr;
+    int collect_grid = 0;
+    unsigned long long *cnt3 = nullptr;
+    SelState *st = nullptr;
+    uint32_t *ghist = nullptr;
+    int64_t own_tiles = 0, tile0 = 0;
+
+    // per-step median plan (set in begin, consumed in finish)
+    int med_path = SVGD_MEDIAN_DIRECT;
+    int64_t reg_cap = 0;
+    int nsel = 0;
+    int64_t sel_rank[2] = {0, 0};
+    int src_lo = -1, src_hi = -1, navg = 1;
+    bool median_pending = false;
+
+    // pinned host
+    double *h_x = nullptr, *h_g = nullptr;
+    unsigned long long *h_cnt = nullptr;
+    SelState *h_st = nullptr;
+    double *h_scal = nullptr;
+    hipEvent_t ev_x = nullptr, ev_cnt = nullptr, ev_scal = nullptr;
+
+    // optimizer
+    int opt_kind = -1;
+    double lr = 0, b1 = 0, b2 = 0, eps = 1e-8;
+    int64_t t = 0;
+    bool bounded = false;
+    int scale_method = SVGD_SCALE_MEDIAN;
+    double fixed_a = 1.0;
+    bool have_particles = false;
+
+    // timing
+    bool timing = false;
+    std::vector<EvPair> ev_phi, ev_med;
+    std::vector<EvPair> ev_pool;
+    double phi_ms = 0, med_ms = 0;
+    int64_t tcount = 0;
+
+    int last_path = SVGD_MEDIAN_DIRECT;
+    std::string err;
+};
+
+namespace {
+
+int fail(svgd_ctx *c, int code, const std::string &msg)
+{
+    if (c) c->err = "SVGDCpp: " + msg;
+    return code;
+}
+
+#define HIPCHK(c, expr)                                                                         \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail((c), SVGD_ERR_HIP,                                                      \
+                        std::string("[HIP Error] ") + #expr + ": " + hipGetErrorString(e_));    \
+    } while (0)
+
+#define NCCLCHK(c, expr)                                                                        \
+    do {                                                                                        \
+        ncclResult_t r_ = (expr);                                                               \
+        if (r_ != ncclSuccess)                                                                  \
+            return fail((c), SVGD_ERR_RCCL,                                                     \
+                        std::string("[RCCL Error] ") + #expr + ": " + ncclGetErrorString(r_));  \
+    } while (0)
+
+#define CHK(expr)                                                                               \
+    do {                                                                                        \
+        int rc_ = (expr);                                                                       \
+        if (rc_ != SVGD_OK) return rc_;                                                         \
+    } while (0)
+
+bool pick_tiles(int d, int *KP, int *NCB)
+{
+    struct {
+        int maxd, kp, ncb;
+    } tab[] = {{4, 4, 1},   {8, 8, 1},   {12, 12, 1}, {15, 16, 1}, {16, 16, 2},
+               {31, 32, 2}, {32, 32, 3}, {63, 64, 4}, {64, 64, 5}};
+    for (auto &e : tab)
+        if (d <= e.maxd) {
+            *KP = e.kp;
+            *NCB = e.ncb;
+            return true;
+        }
+    return false;
+}
+
+template <class T> int dalloc(svgd_ctx *c, T **p, int64_t count)
+{
+    if (*p) {
+        (void)hipFree(*p);
+        *p = nullptr;
+    }
+    if (count <= 0) count = 1;
+    HIPCHK(c, hipMalloc((void **)p, sizeof(T) * (size_t)count));
+    HIPCHK(c, hipMemsetAsync(*p, 0, sizeof(T) * (size_t)count, c->stream));
+    return SVGD_OK;
+}
+
+EvPair take_pair(svgd_ctx *c)
+{
+    EvPair p;
+    if (!c->ev_pool.empty()) {
+        p = c->ev_pool.back();
+        c->ev_pool.pop_back();
+    } else {
+        (void)hipEventCreate(&p.a);
+        (void)hipEventCreate(&p.b);
+    }
+    return p;
+}
+
+int64_t upper_pairs(int64_t n) { return n * (n - 1) / 2; }
+
+// ---------------------------------------------------------- collectives --
+
+int allgather_rows(svgd_ctx *c, double *buf)
+{
+    if (c->world == 1) return SVGD_OK;
+    const size_t cnt = (size_t)c->chunk * c->dim;
+    NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclDouble, c->comm,
+                             c->stream));
+    return SVGD_OK;
+}
+
+int allreduce_u32(svgd_ctx *c, uint32_t *buf, size_t cnt)
+{
+    if (c->world == 1) return SVGD_OK;
+    NCCLCHK(c, ncclAllReduce(buf, buf, cnt, ncclUint32, ncclSum, c->comm, c->stream));
+    return SVGD_OK;
+}
+
+int allreduce_cnt3(svgd_ctx *c)
+{
+    if (c->world == 1) return SVGD_OK;
+    // below and candidate totals are sums, the overflow flag a max
+    NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 2, ncclUint64, ncclSum, c->comm, c->stream));
+    NCCLCHK(c, ncclAllReduce(c->cnt3 + 2, c->cnt3 + 2, 1, ncclUint64, ncclMax, c->comm,
+                             c->stream));
+    return SVGD_OK;
+}
+
+// --------------------------------------------------------------- median --
+
+int center(svgd_ctx *c)
+{
+    HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
+                                 c->nrm, c->stream));
+    return SVGD_OK;
+}
+
+// Upload a fresh select state (ranks, digit 0) from the host.
+int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key)
+{
+    SelState s{};
+    s.nsel = nsel;
+    s.rank[0] = ranks[0];
+    s.rank[1] = nsel > 1 ? ranks[1] : 0;
+    s.shift = 63 - RADIX_BITS;
+    s.width = RADIX_BITS;
+    s.lo_key = lo_key;
+    s.hi_key = hi_key;
+    *c->h_st = s;
+    HIPCHK(c, hipMemcpyAsync(c->st, c->h_st, sizeof(SelState), hipMemcpyHostToDevice, c->stream));
+    return SVGD_OK;
+}
+
+// Phase 1 of the median: candidate bracket + collect pass + counts.
+// Leaves the reduced counts in c->h_cnt (ready at c->ev_cnt).
+int median_begin(svgd_ctx *c)
+{
+    const int64_t n = c->n;
+    int64_t rlo, rhi;
+    c->navg = svgd_plan_median_ranks(n, &rlo, &rhi);
+    // distinct non-negative upper ranks to select
+    c->nsel = 0;
+    c->src_lo = c->src_hi = -1;
+    if (rlo >= 0) {
+        c->sel_rank[c->nsel] = rlo;
+        c->src_lo = c->nsel++;
+    }
+    if (rhi >= 0) {
+        if (c->nsel == 1 && rhi == rlo) {
+            c->src_hi = 0;
+        } else {
+            c->sel_rank[c->nsel] = rhi;
+            c->src_hi = c->nsel++;
+        }
+    }
+    if (c->navg == 1) c->src_hi = c->src_lo;
+    c->median_pending = true;
+    if (c->nsel == 0) { // med = 0 (n <= 1 or all diagonal)
+        c->med_path = SVGD_MEDIAN_DIRECT;
+        return SVGD_OK;
+    }
+
+    const int64_t M = upper_pairs(n);
+    const int64_t tiles = c->own_tiles;
+    c->collect_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, 1024));
+    const int64_t tiles_per_blk = (tiles + c->collect_grid - 1) / c->collect_grid;
+
+    if (M <= c->direct_max_pairs) {
+        // every key is a candidate: bracket [0, ~0)
+        c->med_path = SVGD_MEDIAN_DIRECT;
+        c->reg_cap = tiles_per_blk * TB * TB;
+        uint64_t z[2] = {0, 0};
+        CHK(upload_state(c, 1, z, 0, ~0ull));
+    } else {
+        c->med_path = SVGD_MEDIAN_BRACKET;
+        const int64_t S = std::min<int64_t>(c->sample_size, M);
+        if (c->sample_alloc < S) {
+            CHK(dalloc(c, &c->sample_keys, S));
+            c->sample_alloc = S;
+        }
+        HIPCHK(c, launch_sample_keys(c->xc, c->nrm, n, c->KP, S, c->sample_keys, c->stream));
+        // sample ranks bracketing the target quantiles (6 sigma)
+        const double qlo = (double)c->sel_rank[0] / (double)M;
+        const double qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;
+        const double sig_lo = std::sqrt((double)S * qlo * (1 - qlo)) + 1.0;
+        const double sig_hi = std::sqrt((double)S * qhi * (1 - qhi)) + 1.0;
+        double slo = std::floor(qlo * S - 6.0 * sig_lo) - 1;
+        double shi = std::ceil(qhi * S + 6.0 * sig_hi) + 1;
+        if (slo < 0) slo = 0;
+        if (shi > S - 1) shi = (double)(S - 1);
+        uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
+        CHK(upload_state(c, 2, sr, 0, ~0ull));
+        const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(1024, S / 4096));
+        for (int p = 0; p < 2; ++p) {
+            HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, S, parts, c->st, c->ghist,
+                                          c->stream));
+            HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+        }
+        // bracket [lo_key, hi_key) stays on the device (read by the collect pass)
+        HIPCHK(c, launch_bracket(c->st, c->stream));
+        int64_t pairs_own = tiles * TB * TB;
+        int64_t total = c->cand_capacity;
+        if (total <= 0) {
+            const double frac = (qhi - qlo) + 16.0 / std::sqrt((double)S) + 0.004;
+            total = (int64_t)(2.0 * frac * (double)pairs_own) + 8192 * (int64_t)c->collect_grid;
+        }
+        c->reg_cap = std::max<int64_t>(1, total / c->collect_grid);
+    }
+    const int64_t need = c->reg_cap * c->collect_grid;
+    if (c->regions_alloc < need) {
+        CHK(dalloc(c, &c->regions, need));
+        c->regions_alloc = need;
+    }
+    HIPCHK(c, launch_pair_tiles(c->KP, 0, c->collect_grid, c->xc, c->nrm, n, c->nb, c->tile0,
+                                c->tile0 + tiles, c->regions, c->reg_cap, c->counts, c->below,
+                                c->st, nullptr, nullptr, c->stream));
+    HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->collect_grid, c->reg_cap, c->cnt3,
+                                   c->stream));
+    CHK(allreduce_cnt3(c));
+    HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, 3 * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_cnt, c->stream));
+    return SVGD_OK;
+}
+
+// Phase 2: exact selection among candidates (or streamed fallback), then a.
+int median_finish(svgd_ctx *c)
+{
+    if (!c->median_pending) return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] median not begun.");
+    c->median_pending = false;
+    const double logn = std::log((double)c->n);
+    if (c->nsel == 0) {
+        // every averaged order statistic is a diagonal zero
+        uint64_t z[2] = {0, 0};
+        CHK(upload_state(c, 1, z, 0, 0));
+        HIPCHK(c, launch_finalize(c->st, c->navg, 1, 1, logn, c->scal, c->scal + 1, c->stream));
+        c->last_path = SVGD_MEDIAN_DIRECT;
+        return SVGD_OK;
+    }
+    HIPCHK(c, hipEventSynchronize(c->ev_cnt));
+    const unsigned long long below = c->h_cnt[0], cand = c->h_cnt[1], ovf = c->h_cnt[2];
+    const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
+    bool ok = !ovf && r0 >= below && r1 < below + cand;
+    int path = c->med_path;
+    uint64_t ranks[2];
+    if (ok) {
+        ranks[0] = c->sel_rank[0] - below;
+        ranks[1] = c->sel_rank[c->nsel - 1] - below;
+    } else {
+        path = SVGD_MEDIAN_FALLBACK;
+        ranks[0] = c->sel_rank[0];
+        ranks[1] = c->sel_rank[c->nsel - 1];
+    }
+    CHK(upload_state(c, c->nsel, ranks, 0, ~0ull));
+    for (int p = 0; p < 6; ++p) {
+        if (path == SVGD_MEDIAN_FALLBACK) {
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 2048));
+            HIPCHK(c, launch_pair_tiles(c->KP, 1, grid, c->xc, c->nrm, c->n, c->nb, c->tile0,
+                                        c->tile0 + c->own_tiles, nullptr, 0, nullptr, nullptr,
+                                        c->st, c->ghist, nullptr, c->stream));
+        } else {
+            HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->collect_grid, c->reg_cap, 1,
+                                          c->st, c->ghist, c->stream));
+        }
+        CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
+        HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+    }
+    HIPCHK(c, launch_finalize(c->st, c->navg, c->src_lo < 0 ? 1 : 0, c->src_hi < 0 ? 1 : 0, logn,
+                              c->scal, c->scal + 1, c->stream));
+    (void)c->src_lo;
+    c->last_path = path;
+    return SVGD_OK;
+}
+
+int check_ready(svgd_ctx *c)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (!c->have_particles)
+        return fail(c, SVGD_ERR_UNSET, "[Unset Error] Particle coordinates are unset.");
+    return SVGD_OK;
+}
+
+int upload_g(svgd_ctx *c, const double *G_shard)
+{
+    const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
+    if (!G_shard) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null log-gradient buffer.");
+    if (c->nrows > 0) {
+        if (G_shard != c->h_g) std::memcpy(c->h_g, G_shard, bytes);
+        HIPCHK(c, hipMemcpyAsync(c->G + (size_t)c->row0 * c->dim, c->h_g, bytes,
+                                 hipMemcpyHostToDevice, c->stream));
+    }
+    CHK(allgather_rows(c, c->G));
+    return SVGD_OK;
+}
+
+int run_phi(svgd_ctx *c)
+{
+    HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW, c->V,
+                            c->cvec, c->stream));
+    EvPair ev{};
+    if (c->timing) {
+        ev = take_pair(c);
+        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+    }
+    HIPCHK(c, launch_phi(c->KP, c->NCB, c->xc, c->cvec, c->V, c->scal, c->row0, c->nrows,
+                         (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n, c->phi, c->stream));
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(ev.b, c->stream));
+        c->ev_phi.push_back(ev);
+    }
+    return SVGD_OK;
+}
+
+int run_opt(svgd_ctx *c)
+{
+    if (c->opt_kind < 0)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
+    c->t += 1;
+    double c1 = 1.0, c2 = 1.0;
+    if (c->opt_kind == SVGD_OPT_ADAM) {
+        c1 = 1.0 - std::pow(c->b1, (double)c->t);
+        c2 = 1.0 - std::pow(c->b2, (double)c->t);
+    }
+    const size_t off = (size_t)c->row0 * c->dim;
+    HIPCHK(c, launch_opt_update(c->opt_kind, c->phi, c->m, c->v, c->X + off, c->nrows * c->dim,
+                                c->dim, c->lr, c->b1, c->b2, c->eps, c1, c2,
+                                c->bounded ? c->lower : nullptr, c->bounded ? c->upper : nullptr,
+                                c->stream));
+    CHK(allgather_rows(c, c->X));
+    return SVGD_OK;
+}
+
+int scale_begin(svgd_ctx *c)
+{
+    CHK(center(c));
+    if (c->scale_method == SVGD_SCALE_FIXED) return SVGD_OK;
+    EvPair ev{};
+    if (c->timing) {
+        ev = take_pair(c);
+        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+        c->ev_med.push_back(ev);
+    }
+    return median_begin(c);
+}
+
+int scale_finish(svgd_ctx *c)
+{
+    if (c->scale_method == SVGD_SCALE_FIXED) {
+        c->h_scal[0] = c->fixed_a;
+        c->h_scal[1] = NAN;
+        HIPCHK(c, hipMemcpyAsync(c->scal, c->h_scal, sizeof(double), hipMemcpyHostToDevice,
+                                 c->stream));
+        return SVGD_OK;
+    }
+    CHK(median_finish(c));
+    if (c->timing && !c->ev_med.empty()) HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_scal, c->scal, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_scal, c->stream));
+    return SVGD_OK;
+}
+
+int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
+{
+    if (dim <= 0 || n <= 0)
+        return fail(c, SVGD_ERR_DIM, "[Dimension Error] Particle count and dimension must be positive.");
+    if (dtype != SVGD_F64)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Only the F64 device path is built.");
+    if (!pick_tiles(dim, &c->KP, &c->NCB))
+        return fail(c, SVGD_ERR_DIM, "[Dimension Error] Device path supports dimension <= 64.");
+    c->dim = dim;
+    c->n = n;
+    c->dtype = dtype;
+    c->device = device;
+    c->VW = 16 * c->NCB;
+    c->nb = (n + TB - 1) / TB;
+    c->np = c->nb * TB + TB;
+    c->chunk = (n + c->world - 1) / c->world;
+    svgd_plan_rows(n, c->world, c->rank, &c->row0, &c->row1);
+    c->nrows = c->row1 - c->row0;
+    c->own_tiles = svgd_plan_pair_tiles(n, c->world, c->rank);
+    {
+        const int64_t nbv = c->nb, T = nbv * (nbv + 1) / 2;
+        c->tile0 = T * c->rank / c->world;
+    }
+    HIPCHK(c, hipSetDevice(device));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    const int64_t rows_all = c->chunk * c->world;
+    CHK(dalloc(c, &c->X, rows_all * dim));
+    CHK(dalloc(c, &c->G, rows_all * dim));
+    CHK(dalloc(c, &c->xc, c->np * c->KP));
+    CHK(dalloc(c, &c->nrm, c->np));
+    CHK(dalloc(c, &c->cvec, c->np));
+    CHK(dalloc(c, &c->V, c->np * c->VW));
+    CHK(dalloc(c, &c->phi, std::max<int64_t>(1, c->nrows) * dim));
+    CHK(dalloc(c, &c->m, std::max<int64_t>(1, c->nrows) * dim));
+    CHK(dalloc(c, &c->v, std::max<int64_t>(1, c->nrows) * dim));
+    CHK(dalloc(c, &c->lower, dim));
+    CHK(dalloc(c, &c->upper, dim));
+    CHK(dalloc(c, &c->partial, (int64_t)c->nparts * dim));
+    CHK(dalloc(c, &c->scal, 2));
+    CHK(dalloc(c, &c->counts, 2048));
+    CHK(dalloc(c, &c->below, 2048));
+    CHK(dalloc(c, &c->cnt3, 4));
+    CHK(dalloc(c, &c->st, 1));
+    CHK(dalloc(c, &c->ghist, 2 * RADIX));
+    const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
+    HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_st, sizeof(SelState), hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_scal, 2 * sizeof(double), hipHostMallocDefault));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SVGD_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int svgd_get_unique_id(void *unique_id128)
+{
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return SVGD_ERR_RCCL;
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    std::memcpy(unique_id128, &id, sizeof(id));
+    return SVGD_OK;
+}
+
+int svgd_create(svgd_ctx **out, int dim, int64_t n, int dtype, int device)
+{
+    if (!out) return SVGD_ERR_ARG;
+    svgd_ctx *c = new svgd_ctx();
+    *out = c;
+    return init_ctx(c, dim, n, dtype, device);
+}
+
+int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, int world,
+                     int rank, const void *unique_id128)
+{
+    if (!out) return SVGD_ERR_ARG;
+    svgd_ctx *c = new svgd_ctx();
+    *out = c;
+    if (world < 1 || rank < 0 || rank >= world || (world > 1 && !unique_id128))
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid world/rank.");
+    c->world = world;
+    c->rank = rank;
+    CHK(init_ctx(c, dim, n, dtype, device));
+    if (world > 1) {
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id128, sizeof(id));
+        NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
+    }
+    return SVGD_OK;
+}
+
+int svgd_destroy(svgd_ctx *c)
+{
+    if (!c) return SVGD_OK;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    double *dbufs[] = {c->X, c->G, c->xc, c->nrm, c->cvec, c->V, c->phi, c->m, c->v,
+                       c->lower, c->upper, c->partial, c->scal};
+    for (double *p : dbufs)
+        if (p) (void)hipFree(p);
+    void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist};
+    for (void *p : obufs)
+        if (p) (void)hipFree(p);
+    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal};
+    for (void *p : hbufs)
+        if (p) (void)hipHostFree(p);
+    for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})
+        for (auto &e : *v) {
+            (void)hipEventDestroy(e.a);
+            (void)hipEventDestroy(e.b);
+        }
+    if (c->ev_x) (void)hipEventDestroy(c->ev_x);
+    if (c->ev_cnt) (void)hipEventDestroy(c->ev_cnt);
+    if (c->ev_scal) (void)hipEventDestroy(c->ev_scal);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SVGD_OK;
+}
+
+const char *svgd_last_error(const svgd_ctx *c) { return c ? c->err.c_str() : "SVGDCpp: null context"; }
+
+int svgd_shard(const svgd_ctx *c, int64_t *row0, int64_t *row1)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (row0) *row0 = c->row0;
+    if (row1) *row1 = c->row1;
+    return SVGD_OK;
+}
+
+int svgd_set_optimizer(svgd_ctx *c, int kind, double lr, double beta1, double beta2, double eps)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (kind == SVGD_OPT_ADAM && (beta1 >= 1.0 || beta1 < 0.0 || beta2 >= 1.0 || beta2 < 0.0))
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid value for decay parameter beta.");
+    if (kind == SVGD_OPT_RMSPROP && (beta1 > 1.0 || beta1 < 0.0))
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid value for decay parameter beta.");
+    if (kind < SVGD_OPT_ADAM || kind > SVGD_OPT_RMSPROP)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
+    c->opt_kind = kind;
+    c->lr = lr;
+    c->b1 = beta1;
+    c->b2 = beta2;
+    c->eps = eps;
+    return svgd_reset_optimizer(c);
+}
+
+int svgd_reset_optimizer(svgd_ctx *c)
+{
+    if (!c) return SVGD_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * c->dim;
+    HIPCHK(c, hipMemsetAsync(c->m, 0, bytes, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->v, 0, bytes, c->stream));
+    c->t = 0;
+    return SVGD_OK;
+}
+
+int svgd_set_bounds(svgd_ctx *c, const double *lower, const double *upper)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (!lower && !upper) {
+        c->bounded = false;
+        return SVGD_OK;
+    }
+    if (!lower || !upper)
+        return fail(c, SVGD_ERR_DIM, "[Dimension Error] The provided bounds have incorrect dimensions.");
+    HIPCHK(c, hipMemcpy(c->lower, lower, sizeof(double) * c->dim, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->upper, upper, sizeof(double) * c->dim, hipMemcpyHostToDevice));
+    c->bounded = true;
+    return SVGD_OK;
+}
+
+int svgd_set_scale(svgd_ctx *c, int method, double fixed_a)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (method != SVGD_SCALE_MEDIAN && method != SVGD_SCALE_FIXED)
+        return fail(c, SVGD_ERR_ARG, "[Argument error] Invalid scale method Enum provided.");
+    c->scale_method = method;
+    c->fixed_a = fixed_a;
+    return SVGD_OK;
+}
+
+int svgd_set_particles(svgd_ctx *c, const double *X)
+{
+    if (!c || !X) return SVGD_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(c->X, X, sizeof(double) * (size_t)c->n * c->dim,
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->have_particles = true;
+    return SVGD_OK;
+}
+
+int svgd_get_particles(svgd_ctx *c, double *X)
+{
+    CHK(check_ready(c));
+    if (!X) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null output buffer.");
+    HIPCHK(c, hipMemcpyAsync(X, c->X, sizeof(double) * (size_t)c->n * c->dim,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SVGD_OK;
+}
+
+int svgd_get_shard(svgd_ctx *c, double *X_shard)
+{
+    CHK(check_ready(c));
+    if (c->nrows == 0) return SVGD_OK;
+    HIPCHK(c, hipMemcpyAsync(X_shard, c->X + (size_t)c->row0 * c->dim,
+                             sizeof(double) * (size_t)c->nrows * c->dim, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SVGD_OK;
+}
+
+int svgd_median_scale(svgd_ctx *c, double *a_out, double *med_out)
+{
+    CHK(check_ready(c));
+    const int keep = c->scale_method;
+    c->scale_method = SVGD_SCALE_MEDIAN;
+    int rc = scale_begin(c);
+    if (rc == SVGD_OK) rc = scale_finish(c);
+    c->scale_method = keep;
+    CHK(rc);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (a_out) *a_out = c->h_scal[0];
+    if (med_out) *med_out = c->h_scal[1];
+    return SVGD_OK;
+}
+
+int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
+{
+    CHK(check_ready(c));
+    CHK(center(c));
+    c->h_scal[0] = a;
+    HIPCHK(c, hipMemcpyAsync(c->scal, c->h_scal, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    CHK(upload_g(c, G_shard));
+    CHK(run_phi(c));
+    if (phi_out && c->nrows > 0) {
+        HIPCHK(c, hipMemcpyAsync(phi_out, c->phi, sizeof(double) * (size_t)c->nrows * c->dim,
+                                 hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SVGD_OK;
+}
+
+int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
+{
+    CHK(check_ready(c));
+    if (c->opt_kind < 0)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
+    const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
+    if (X_shard_out && c->nrows > 0) {
+        HIPCHK(c, hipMemcpyAsync(c->h_x, c->X + (size_t)c->row0 * c->dim, bytes,
+                                 hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_x, c->stream));
+    }
+    CHK(scale_begin(c));
+    if (X_shard_out && c->nrows > 0) {
+        HIPCHK(c, hipEventSynchronize(c->ev_x));
+        if (X_shard_out != c->h_x) std::memcpy(X_shard_out, c->h_x, bytes);
+    }
+    return SVGD_OK;
+}
+
+int svgd_finish_step(svgd_ctx *c, const double *G_shard)
+{
+    CHK(check_ready(c));
+    CHK(upload_g(c, G_shard));
+    CHK(scale_finish(c));
+    CHK(run_phi(c));
+    CHK(run_opt(c));
+    return SVGD_OK;
+}
+
+int svgd_step(svgd_ctx *c, const double *G_shard)
+{
+    CHK(svgd_begin_step(c, nullptr));
+    return svgd_finish_step(c, G_shard);
+}
+
+int svgd_host_buffers(svgd_ctx *c, double **x_shard, double **g_shard)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (x_shard) *x_shard = c->h_x;
+    if (g_shard) *g_shard = c->h_g;
+    return SVGD_OK;
+}
+
+int svgd_sync(svgd_ctx *c)
+{
+    if (!c) return SVGD_ERR_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SVGD_OK;
+}
+
+int svgd_last_scale(const svgd_ctx *c, double *a_out, double *med_out, int *path)
+{
+    if (!c) return SVGD_ERR_ARG;
+    svgd_ctx *m = const_cast<svgd_ctx *>(c);
+    if (m->ev_scal) (void)hipEventSynchronize(m->ev_scal);
+    if (a_out) *a_out = c->h_scal[0];
+    if (med_out) *med_out = c->h_scal[1];
+    if (path) *path = c->last_path;
+    return SVGD_OK;
+}
+
+int svgd_set_timing(svgd_ctx *c, int enable)
+{
+    if (!c) return SVGD_ERR_ARG;
+    c->timing = enable != 0;
+    return SVGD_OK;
+}
+
+int svgd_get_timing(svgd_ctx *c, double *phi_ms, double *median_ms, int64_t *count)
+{
+    if (!c) return SVGD_ERR_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (auto &e : c->ev_phi) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, e.a, e.b));
+        c->phi_ms += ms;
+        c->tcount += 1;
+        c->ev_pool.push_back(e);
+    }
+    c->ev_phi.clear();
+    for (auto &e : c->ev_med) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, e.a, e.b));
+        c->med_ms += ms;
+        c->ev_pool.push_back(e);
+    }
+    c->ev_med.clear();
+    if (phi_ms) *phi_ms = c->phi_ms;
+    if (median_ms) *median_ms = c->med_ms;
+    if (count) *count = c->tcount;
+    c->phi_ms = c->med_ms = 0;
+    c->tcount = 0;
+    return SVGD_OK;
+}
+
+int svgd_set_median_tuning(svgd_ctx *c, int64_t direct_max_pairs, int64_t sample_size,
+                           int64_t candidate_capacity)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (direct_max_pairs >= 0) c->direct_max_pairs = direct_max_pairs;
+    if (sample_size > 0) c->sample_size = sample_size;
+    if (candidate_capacity >= 0) c->cand_capacity = candidate_capacity;
+    return SVGD_OK;
+}
+
+int svgd_debug_pair_keys(svgd_ctx *c, double *out, int64_t capacity)
+{
+    CHK(check_ready(c));
+    const int64_t M = upper_pairs(c->n);
+    if (capacity < M) return fail(c, SVGD_ERR_ARG, "[Argument Error] Output buffer too small.");
+    if (c->world != 1)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Debug keys are single-GPU only.");
+    CHK(center(c));
+    double *d = nullptr;
+    HIPCHK(c, hipMalloc((void **)&d, sizeof(double) * (size_t)std::max<int64_t>(1, M)));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 1024));
+    hipError_t e = launch_pair_tiles(c->KP, 2, grid, c->xc, c->nrm, c->n, c->nb, 0, c->own_tiles,
+                                     nullptr, 0, nullptr, nullptr, nullptr, nullptr, d, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(out, d, sizeof(double) * (size_t)M, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    HIPCHK(c, e);
+    return SVGD_OK;
+}
+
+} // extern "C"

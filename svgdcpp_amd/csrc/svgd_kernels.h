@@ -1,0 +1,61 @@
+// svgd_kernels.h -- host-callable launchers of the gfx950 kernels (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace svgd_amd {
+
+constexpr int RADIX_BITS = 11;
+constexpr int RADIX = 1 << RADIX_BITS;
+
+// Device-resident state of the (dual) radix select over 63-bit keys
+// (non-negative doubles as uint64).  Digits from the top: bits 62..52,
+// 51..41, 40..30, 29..19, 18..8, 7..0.
+struct SelState {
+    uint64_t prefix[2];   // resolved high bits of the two selected keys
+    uint64_t rank[2];     // remaining rank within the current prefix
+    uint64_t lo_key;      // candidate bracket [lo_key, hi_key)
+    uint64_t hi_key;
+    int32_t nsel;         // 1 or 2 active selections
+    int32_t shift;        // shift of the current digit
+    int32_t width;        // width of the current digit
+    int32_t pass;         // digits resolved so far
+    int32_t error;        // rank outside the histogram (should not happen)
+    int32_t pad_;
+};
+
+hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
+                              double *partial, int nparts, double *xc, double *nrm,
+                              hipStream_t stream);
+hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
+                         int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
+                         hipStream_t stream);
+hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
+                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
+                      double inv_n, double *phi, hipStream_t stream);
+hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
+                             int64_t cnt, int d, double lr, double b1, double b2, double eps,
+                             double c1, double c2, const double *lower, const double *upper,
+                             hipStream_t stream);
+// mode 0: collect keys in [st->lo_key, st->hi_key) into per-block regions and count
+// keys below lo_key; mode 1: radix histogram pass over all pairs (fallback);
+// mode 2: debug dump of every key in (i<j) row-major order.
+hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
+                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                             int64_t cap, uint32_t *counts, unsigned long long *below,
+                             const SelState *st, uint32_t *ghist, double *dbg_out,
+                             hipStream_t stream);
+hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int KP, int64_t S,
+                              uint64_t *keys, hipStream_t stream);
+hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
+                               int64_t cap, int parts, const SelState *st, uint32_t *ghist,
+                               hipStream_t stream);
+hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream);
+hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
+                                int64_t nblk, int64_t cap, unsigned long long *cnt,
+                                hipStream_t stream);
+hipError_t launch_bracket(SelState *st, hipStream_t stream);
+hipError_t launch_finalize(const SelState *st, int navg, int zero_lo, int zero_hi, double logn,
+                           double *a_out, double *med_out, hipStream_t stream);
+
+} // namespace svgd_amd

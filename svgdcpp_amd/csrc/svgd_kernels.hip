@@ -1,0 +1,757 @@
+// svgd_kernels.hip -- CDNA4 (gfx950) kernels of the SVGD inner step.
+//
+// Reference hot path (khaiyichin/SVGDCpp, paths relative to its root):
+//   GaussianRBFKernel::ComputeScale (Median) + ComputeMedian
+//       include/SVGDCpp/Kernel/GaussianRBFKernel.hpp:164-188, 222-254
+//   SVGD::ComputePhi (K, Kg, (1/N)(G K + [I..I] Kg))   include/SVGDCpp/SVGD.hpp:407-454
+//   RBF lambda exp(-(x-x')^T M (x-x'))                 GaussianRBFKernel.hpp:75-81
+//   Adam / AdaGrad / RMSProp Step                       Optimizer/*.hpp
+//   X += Step(phi); clamp                               SVGD.hpp:393-399
+//
+// Device data layout (HBM): particle-major, i.e. the reference's d x n
+// column-major Eigen matrix: particle j at X[j*d .. j*d+d-1].  The working
+// copies are padded: xc[j*KP + k] holds the mean-centred coordinates with
+// k padded to KP (multiple of 4, the f64 MFMA K), V[j*16*NCB + c] holds
+// [G_j - 2a xc_j, 1, 0 ...] (the phi contraction operand), rows padded to a
+// multiple of 64 with zeros.
+//
+// f64 MFMA: v_mfma_f64_16x16x4_f64.  A/B lane maps: A[i = l&15][k = l>>4],
+// B[k = l>>4][j = l&15]; C/D: col = l&15, row = (l>>4) + 4*reg.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "svgd_kernels.h"
+
+namespace svgd_amd {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int TB = 64;   // particles per tile (rows and columns)
+constexpr int LDP = TB + 16; // padded LDS row stride (doubles) of the k-major X tiles
+
+__device__ __forceinline__ d4 mfma64(double a, double b, d4 c)
+{
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// 2^t for t <= 0 (t = -a*log2(e)*s).  Range reduction t = k + f, |f| <= 1/2,
+// degree-12 Taylor polynomial of 2^f (max error 1.9 ulp on [-1/2, 1/2]),
+// v_ldexp_f64 for 2^k.  Results below 2^-1075 flush to 0 like exp() does.
+__device__ __forceinline__ double exp2_neg(double t)
+{
+    t = fmax(t, -1075.0);
+    const double k = __builtin_rint(t);
+    const double f = t - k;
+    double p = 0x1.c3bd650fc2986p-36;
+    p = fma(p, f, 0x1.e8cac7351bb25p-32);
+    p = fma(p, f, 0x1.e4cf5158b8ecap-28);
+    p = fma(p, f, 0x1.b5253d395e7c4p-24);
+    p = fma(p, f, 0x1.62c0223a5c824p-20);
+    p = fma(p, f, 0x1.ffcbfc588b0c7p-17);
+    p = fma(p, f, 0x1.430912f86c787p-13);
+    p = fma(p, f, 0x1.5d87fe78a6731p-10);
+    p = fma(p, f, 0x1.3b2ab6fba4e77p-7);
+    p = fma(p, f, 0x1.c6b08d704a0c0p-5);
+    p = fma(p, f, 0x1.ebfbdff82c58fp-3);
+    p = fma(p, f, 0x1.62e42fefa39efp-1);
+    p = fma(p, f, 1.0);
+    return __builtin_ldexp(p, (int)k);
+}
+
+constexpr double LOG2E = 0x1.71547652b82fep+0;
+
+// ------------------------------------------------------------ centering --
+
+// Per-block partial column sums of X (n x d) -> partial[b*d + k].
+__global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
+                               double *__restrict__ partial)
+{
+    __shared__ double red[256];
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t j0 = per * blockIdx.x, j1 = min(n, j0 + per);
+    for (int k = 0; k < d; ++k) {
+        double s = 0.0;
+        for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) s += X[j * d + k];
+        red[threadIdx.x] = s;
+        __syncthreads();
+        for (int o = 128; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) partial[blockIdx.x * d + k] = red[0];
+        __syncthreads();
+    }
+}
+
+// xc = X - mean (padded to KP columns, rows [n, np) zero), nrm = |xc|^2.
+// The mean is re-derived by every block from the partials in a fixed order,
+// so it is bit-identical on every rank and block.
+__global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
+                         const double *__restrict__ partial, int nparts, int64_t np,
+                         double *__restrict__ xc, double *__restrict__ nrm)
+{
+    __shared__ double mu[256];
+    for (int k = threadIdx.x; k < d; k += blockDim.x) {
+        double s = 0.0;
+        for (int b = 0; b < nparts; ++b) s += partial[b * d + k];
+        mu[k] = s / (double)n;
+    }
+    __syncthreads();
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        double s = 0.0;
+        for (int k = 0; k < KP; ++k) {
+            double v = (j < n && k < d) ? X[j * d + k] - mu[k] : 0.0;
+            xc[j * KP + k] = v;
+            s = fma(v, v, s);
+        }
+        nrm[j] = s;
+    }
+}
+
+// V_j = [G_j - 2a xc_j, 1, 0...] (row stride 16*NCB), c_j = -a log2e |xc_j|^2.
+__global__ void k_prep_v(const double *__restrict__ xc, const double *__restrict__ G,
+                         const double *__restrict__ nrm, const double *__restrict__ a_ptr,
+                         int64_t n, int64_t np, int d, int KP, int VW,
+                         double *__restrict__ V, double *__restrict__ cvec)
+{
+    const double a = *a_ptr;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const bool live = j < n;
+        for (int c = 0; c < VW; ++c) {
+            double v = 0.0;
+            if (live) {
+                if (c < d) v = G[j * d + c] - 2.0 * a * xc[j * KP + c];
+                else if (c == d) v = 1.0;
+            }
+            V[j * VW + c] = v;
+        }
+        cvec[j] = live ? -a * LOG2E * nrm[j] : 0.0;
+    }
+}
+
+// ------------------------------------------------------------------ phi --
+//
+// One workgroup = 4 waves = 64 rows i (wave w: rows 16w..16w+15).  The
+// workgroup sweeps all column tiles of 64 particles j staged through LDS.
+// Per 16(j) x 16(i) sub-tile:
+//   Gram   dot[j][i] = xc_j . xc_i     KP/4 MFMAs (A = X_J from LDS, B = X_I regs)
+//   VALU   t = c_i + c_j + 2a log2e dot  ( = -a log2e |x_i - x_j|^2 )
+//          P = 2^t                      (lane l: i = l&15, j = (l>>4) + 4r)
+//   MFMA   acc[i][c] += sum_j P[i][j] V[j][c]   (P is already the A-operand map)
+// Epilogue: phi_i = (acc[i][0:d] + 2a xc_i acc[i][d]) / N.
+template <int KP, int NCB>
+__global__ __launch_bounds__(256) void k_phi(const double *__restrict__ xc,
+                                            const double *__restrict__ cvec,
+                                            const double *__restrict__ V,
+                                            const double *__restrict__ a_ptr, int64_t row0,
+                                            int64_t nrows, int64_t ntiles_j, int d,
+                                            double inv_n, double *__restrict__ phi)
+{
+    constexpr int VW = 16 * NCB;
+    __shared__ double sX[KP * LDP];
+    __shared__ double sV[TB * VW];
+    __shared__ double sC[TB];
+    __shared__ double sAcc[4][16][VW + 1];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lo = lane & 15, hi = lane >> 4;
+    const double a = *a_ptr;
+    const double alpha = 2.0 * a * LOG2E;
+
+    const int64_t ibase = row0 + (int64_t)blockIdx.x * TB + w * 16;
+    // B operand of the Gram MFMA: X_I^T, lane holds xc[i = lo][k = 4kk + hi]
+    double bI[KP / 4];
+#pragma unroll
+    for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = xc[(ibase + lo) * KP + 4 * kk + hi];
+    const double ci = cvec[ibase + lo];
+
+    d4 acc[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
+
+    for (int64_t jt = 0; jt < ntiles_j; ++jt) {
+        const int64_t j0 = jt * TB;
+        __syncthreads();
+        // stage X_J (k-major, padded rows) and V_J, c_J
+        for (int e = tid; e < TB * KP; e += 256) {
+            const int jl = e / KP, k = e - jl * KP;
+            sX[k * LDP + jl] = xc[(j0 + jl) * KP + k];
+        }
+        for (int e = tid; e < TB * VW / 2; e += 256)
+            reinterpret_cast<double2 *>(sV)[e] = reinterpret_cast<const double2 *>(V + j0 * VW)[e];
+        if (tid < TB) sC[tid] = cvec[j0 + tid];
+        __syncthreads();
+
+#pragma unroll
+        for (int js = 0; js < 4; ++js) {
+            d4 dot = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kk = 0; kk < KP / 4; ++kk)
+                dot = mfma64(sX[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jl = js * 16 + 4 * r + hi;
+                double t = fma(alpha, dot[r], ci + sC[jl]);
+                const double p = exp2_neg(fmin(t, 0.0));
+#pragma unroll
+                for (int cb = 0; cb < NCB; ++cb)
+                    acc[cb] = mfma64(p, sV[jl * VW + cb * 16 + lo], acc[cb]);
+            }
+        }
+    }
+
+    // epilogue: acc lane map row i = hi + 4q, col c = lo (+16cb)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sAcc[w][hi + 4 * q][cb * 16 + lo] = acc[cb][q];
+    __syncthreads();
+    const double two_a = 2.0 * a;
+    for (int e = lane; e < 16 * d; e += 64) {
+        const int il = e / d, c = e - il * d;
+        const int64_t i = ibase + il;
+        if (i - row0 < nrows) {
+            const double s1 = sAcc[w][il][d];
+            phi[(i - row0) * d + c] = inv_n * (sAcc[w][il][c] + two_a * xc[i * KP + c] * s1);
+        }
+    }
+}
+
+// ----------------------------------------------------------- optimizers --
+// Elementwise, bit-exact with the reference expressions (no FMA contraction).
+
+__global__ void k_opt_update(int kind, const double *__restrict__ g, double *__restrict__ m,
+                             double *__restrict__ v, double *__restrict__ X, int64_t cnt, int d,
+                             double lr, double b1, double b2, double eps, double c1, double c2,
+                             const double *__restrict__ lower, const double *__restrict__ upper)
+{
+#pragma clang fp contract(off)
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cnt;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const double ge = g[e];
+        double delta;
+        if (kind == 0) { // Adam.hpp:75-83
+            const double me = b1 * m[e] + (1 - b1) * ge;
+            const double ve = b2 * v[e] + (1 - b2) * (ge * ge);
+            m[e] = me;
+            v[e] = ve;
+            delta = (lr * (1.0 / (eps + sqrt(ve / c2)))) * (me / c1);
+        } else if (kind == 1) { // AdaGrad.hpp:60-65
+            const double ve = v[e] + ge * ge;
+            v[e] = ve;
+            delta = (lr * (1.0 / (eps + sqrt(ve)))) * ge;
+        } else { // RMSProp.hpp:69-74 (beta passed as b1)
+            const double ve = b1 * v[e] + (1 - b1) * (ge * ge);
+            v[e] = ve;
+            delta = (lr * (1.0 / (eps + sqrt(ve)))) * ge;
+        }
+        double x = X[e] + delta; // SVGD.hpp:393
+        if (lower) {             // SVGD.hpp:396-399: min(upper) then max(lower)
+            const int k = (int)(e % d);
+            x = x < upper[k] ? x : upper[k];
+            x = x > lower[k] ? x : lower[k];
+        }
+        X[e] = x;
+    }
+}
+
+// --------------------------------------------------------------- median --
+//
+// Keys: squared distances s = max((|xc_i|^2 + |xc_j|^2) - 2 xc_i.xc_j, 0)
+// (the reference's Gram form, GaussianRBFKernel.hpp:179-183, on centred
+// coordinates) as the IEEE bit pattern, which orders like uint64 for s >= 0.
+// Every unordered pair i<j is visited once by the tile sweep of plan.h.
+
+__device__ __forceinline__ uint64_t key_of(double s) { return (uint64_t)__double_as_longlong(s); }
+
+// Device copy of plan_pair_tile (plan.cpp): tile index -> (row block, col block).
+__device__ __forceinline__ void tile_coords(int64_t nb, int64_t t, int64_t *I, int64_t *J)
+{
+    const int64_t H = (nb - 1) / 2;
+    int64_t slot;
+    if ((nb & 1) == 0) {
+        const int64_t c1 = H + 2, c2 = H + 1, half = nb / 2;
+        if (t < half * c1) {
+            *I = t / c1;
+            slot = t - *I * c1;
+        } else {
+            const int64_t u = t - half * c1;
+            *I = half + u / c2;
+            slot = u - (*I - half) * c2;
+        }
+    } else {
+        const int64_t c = H + 1;
+        *I = t / c;
+        slot = t - *I * c;
+    }
+    *J = slot == 0 ? *I : (*I + slot) % nb;
+}
+
+struct SinkCollect {
+    const SelState *st; // bracket [st->lo_key, st->hi_key)
+    uint64_t *region; // this block's region (capacity cap)
+    int64_t cap;
+    uint32_t *count_out;
+    unsigned long long *below_out;
+};
+
+struct SinkHist {
+    const SelState *st;
+    uint32_t *ghist; // [2][RADIX]
+};
+
+struct SinkDebug {
+    double *out;
+    int64_t n;
+};
+
+template <int KP, int MODE>
+__global__ __launch_bounds__(256) void k_pair_tiles(const double *__restrict__ xc,
+                                                   const double *__restrict__ nrm, int64_t n,
+                                                   int64_t nb, int64_t t0, int64_t t1,
+                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
+{
+    __shared__ double sXI[KP * LDP];
+    __shared__ double sXJ[KP * LDP];
+    __shared__ double sNI[TB], sNJ[TB];
+    __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
+    __shared__ uint32_t sCnt;
+    __shared__ unsigned long long sBelow[4];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lo = lane & 15, hi = lane >> 4;
+
+    const int64_t ntiles = t1 - t0;
+    const int64_t tb = t0 + ntiles * blockIdx.x / gridDim.x;
+    const int64_t te = t0 + ntiles * (blockIdx.x + 1) / gridDim.x;
+
+    // MODE 1 (histogram) selection state
+    int nsel = 0, shift = 0;
+    uint64_t pfx[2] = {0, 0};
+    int hsh = 63;
+    if (MODE == 1) {
+        nsel = sh.st->nsel;
+        shift = sh.st->shift;
+        hsh = shift + sh.st->width;
+        pfx[0] = sh.st->prefix[0];
+        pfx[1] = sh.st->prefix[1];
+        for (int e = tid; e < 2 * RADIX; e += 256) sHist[e] = 0;
+    }
+    uint64_t lo_key = 0, hi_key = 0;
+    if (MODE == 0) {
+        lo_key = sc.st->lo_key;
+        hi_key = sc.st->hi_key;
+        if (tid == 0) sCnt = 0;
+    }
+    uint32_t below = 0;
+
+    int64_t curI = -1;
+    for (int64_t t = tb; t < te; ++t) {
+        int64_t I, J;
+        tile_coords(nb, t, &I, &J);
+        __syncthreads();
+        if (I != curI) {
+            for (int e = tid; e < TB * KP; e += 256) {
+                const int il = e / KP, k = e - il * KP;
+                sXI[k * LDP + il] = xc[(I * TB + il) * KP + k];
+            }
+            if (tid < TB) sNI[tid] = nrm[I * TB + tid];
+        }
+        for (int e = tid; e < TB * KP; e += 256) {
+            const int jl = e / KP, k = e - jl * KP;
+            sXJ[k * LDP + jl] = xc[(J * TB + jl) * KP + k];
+        }
+        if (tid < TB) sNJ[tid] = nrm[J * TB + tid];
+        __syncthreads();
+        curI = I;
+
+        double bI[KP / 4];
+#pragma unroll
+        for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = sXI[(4 * kk + hi) * LDP + w * 16 + lo];
+        const int il = w * 16 + lo;
+        const int64_t i = I * TB + il;
+        const double ni = sNI[il];
+
+#pragma unroll
+        for (int js = 0; js < 4; ++js) {
+            d4 dot = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kk = 0; kk < KP / 4; ++kk)
+                dot = mfma64(sXJ[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int jl = js * 16 + 4 * r + hi;
+                const int64_t j = J * TB + jl;
+                const bool valid = (i < n) && (j < n) && (I != J || il < jl);
+                const double s = fmax(fma(-2.0, dot[r], ni + sNJ[jl]), 0.0);
+                const uint64_t key = key_of(s);
+                if (MODE == 0) {
+                    const bool in = valid && key >= lo_key && key < hi_key;
+                    below += (valid && key < lo_key) ? 1u : 0u;
+                    const unsigned long long mask = __ballot(in);
+                    if (mask) {
+                        uint32_t base = 0;
+                        if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mask));
+                        base = __shfl(base, 0);
+                        if (in) {
+                            const int64_t pos =
+                                base + __popcll(mask & ((1ull << lane) - 1ull));
+                            if (pos < sc.cap) sc.region[blockIdx.x * sc.cap + pos] = key;
+                        }
+                    }
+                } else if (MODE == 1) {
+                    if (valid) {
+                        for (int s2 = 0; s2 < nsel; ++s2) {
+                            const bool match = hsh >= 64 || (key >> hsh) == (pfx[s2] >> hsh);
+                            if (match)
+                                atomicAdd(&sHist[s2 * RADIX + ((key >> shift) & (RADIX - 1))], 1u);
+                        }
+                    }
+                } else {
+                    if (valid) {
+                        const int64_t a = i < j ? i : j, b = i < j ? j : i;
+                        const int64_t idx = a * (2 * sd.n - a - 1) / 2 + (b - a - 1);
+                        sd.out[idx] = s;
+                    }
+                }
+            }
+        }
+    }
+
+    if (MODE == 0) {
+        // block reduce `below`
+        unsigned long long bl = below;
+        for (int o = 32; o > 0; o >>= 1) bl += __shfl_down(bl, o);
+        if (lane == 0) sBelow[w] = bl;
+        __syncthreads();
+        if (tid == 0) {
+            sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
+            sc.count_out[blockIdx.x] = sCnt;
+        }
+    } else if (MODE == 1) {
+        __syncthreads();
+        for (int e = tid; e < 2 * RADIX; e += 256)
+            if (sHist[e]) atomicAdd(&sh.ghist[e], sHist[e]);
+    }
+}
+
+// Sampled keys: pair (i, j != i) from a splitmix hash of the sample index;
+// region b holds keys [b*per, (b+1)*per).
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+__global__ void k_sample_keys(const double *__restrict__ xc, const double *__restrict__ nrm,
+                              int64_t n, int KP, int64_t S, uint64_t *__restrict__ keys)
+{
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = mix64((uint64_t)g * 2 + 1);
+        const int64_t i = (int64_t)(h % (uint64_t)n);
+        const int64_t j = (i + 1 + (int64_t)((h >> 32) % (uint64_t)(n - 1))) % n;
+        double dot = 0.0;
+        for (int k = 0; k < KP; ++k) dot = fma(xc[i * KP + k], xc[j * KP + k], dot);
+        keys[g] = key_of(fmax(fma(-2.0, dot, nrm[i] + nrm[j]), 0.0));
+    }
+}
+
+// Histogram of keys in `nreg` regions (region r: keys[r*cap .. r*cap+cnt_r)),
+// cnt_r = counts ? min(counts[r], cap) : cap.  Grid = nreg * parts.
+__global__ __launch_bounds__(256) void k_hist_regions(const uint64_t *__restrict__ keys,
+                                                     const uint32_t *__restrict__ counts,
+                                                     int64_t nreg, int64_t cap, int parts,
+                                                     const SelState *__restrict__ st,
+                                                     uint32_t *__restrict__ ghist)
+{
+    __shared__ uint32_t sHist[2 * RADIX];
+    for (int e = threadIdx.x; e < 2 * RADIX; e += 256) sHist[e] = 0;
+    __syncthreads();
+    const int nsel = st->nsel, shift = st->shift, hsh = shift + st->width;
+    const uint64_t p0 = st->prefix[0], p1 = st->prefix[1];
+    const int64_t r = blockIdx.x / parts, part = blockIdx.x - r * parts;
+    int64_t cnt = counts ? (int64_t)counts[r] : cap;
+    if (cnt > cap) cnt = cap;
+    const uint64_t *kr = keys + r * cap;
+    for (int64_t e = part * 256 + threadIdx.x; e < cnt; e += (int64_t)parts * 256) {
+        const uint64_t key = kr[e];
+        const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
+        if (hsh >= 64 || (key >> hsh) == (p0 >> hsh)) atomicAdd(&sHist[dg], 1u);
+        if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (p1 >> hsh)))
+            atomicAdd(&sHist[RADIX + dg], 1u);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 2 * RADIX; e += 256)
+        if (sHist[e]) atomicAdd(&ghist[e], sHist[e]);
+}
+
+// One radix-select step: for each active selection find the digit holding
+// its remaining rank, append it to the prefix, subtract the count below,
+// zero the histogram and advance to the next digit.
+__global__ __launch_bounds__(256) void k_select_scan(SelState *st, uint32_t *ghist)
+{
+    __shared__ unsigned long long sPart[256];
+    __shared__ int sDigit;
+    __shared__ unsigned long long sBelowD;
+    const int tid = threadIdx.x;
+    const int nsel = st->nsel, shift = st->shift, width = st->width;
+    constexpr int PER = RADIX / 256;
+    for (int s = 0; s < nsel; ++s) {
+        const uint32_t *h = ghist + s * RADIX;
+        unsigned long long loc = 0;
+        for (int q = 0; q < PER; ++q) loc += h[tid * PER + q];
+        sPart[tid] = loc;
+        if (tid == 0) sDigit = -1;
+        __syncthreads();
+        // inclusive scan over 256 partials (Hillis-Steele)
+        for (int o = 1; o < 256; o <<= 1) {
+            unsigned long long v = tid >= o ? sPart[tid - o] : 0ull;
+            __syncthreads();
+            sPart[tid] += v;
+            __syncthreads();
+        }
+        const unsigned long long rank = st->rank[s];
+        const unsigned long long excl = tid ? sPart[tid - 1] : 0ull;
+        if (rank >= excl && rank < sPart[tid]) {
+            unsigned long long c = excl;
+            for (int q = 0; q < PER; ++q) {
+                const unsigned long long hv = h[tid * PER + q];
+                if (rank < c + hv) {
+                    sDigit = tid * PER + q;
+                    sBelowD = c;
+                    break;
+                }
+                c += hv;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            if (sDigit < 0) {
+                st->error = 1;
+            } else {
+                st->prefix[s] |= (uint64_t)sDigit << shift;
+                st->rank[s] = rank - sBelowD;
+            }
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < 2 * RADIX; e += 256) ghist[e] = 0;
+    if (tid == 0) {
+        st->pass += 1;
+        const int nshift = shift - RADIX_BITS;
+        st->shift = nshift >= 0 ? nshift : 0;
+        st->width = nshift >= 0 ? RADIX_BITS : shift;
+        (void)width;
+    }
+}
+
+// Sum per-block collect outputs: counts and below -> cnt[0] = below,
+// cnt[1] = candidates (true count), cnt[2] = 1 if any region overflowed.
+__global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
+                                const uint32_t *__restrict__ counts, int64_t nblk, int64_t cap,
+                                unsigned long long *__restrict__ cnt)
+{
+    __shared__ unsigned long long s0[256], s1[256], s2[256];
+    unsigned long long b = 0, c = 0, o = 0;
+    for (int64_t e = threadIdx.x; e < nblk; e += 256) {
+        b += below[e];
+        c += counts[e];
+        o |= (counts[e] > cap) ? 1ull : 0ull;
+    }
+    s0[threadIdx.x] = b;
+    s1[threadIdx.x] = c;
+    s2[threadIdx.x] = o;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) {
+            s0[threadIdx.x] += s0[threadIdx.x + k];
+            s1[threadIdx.x] += s1[threadIdx.x + k];
+            s2[threadIdx.x] |= s2[threadIdx.x + k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        cnt[0] = s0[0];
+        cnt[1] = s1[0];
+        cnt[2] = s2[0];
+    }
+}
+
+// After the truncated sample select: bracket [lo_key, hi_key) from the
+// bucket of selection 0 (lower edge) and of selection 1 (upper edge).
+__global__ void k_bracket(SelState *st)
+{
+    const int sh = st->shift + st->width; // bits below the resolved digits
+    st->lo_key = st->prefix[0];
+    const uint64_t top = st->prefix[1] + (sh >= 64 ? 0ull : (1ull << sh));
+    st->hi_key = (top < st->prefix[1]) ? ~0ull : top;
+}
+
+// med = (sqrt(u_lo) + sqrt(u_hi)) / 2 (or the single middle value);
+// a = ln(n) / med^2  (GaussianRBFKernel.hpp:187, ComputeMedian :222-254).
+__global__ void k_finalize(const SelState *st, int navg, int zero_lo, int zero_hi, double logn,
+                           double *a_out, double *med_out)
+{
+    const double u0 = zero_lo ? 0.0 : sqrt(__longlong_as_double((long long)st->prefix[0]));
+    double med;
+    if (navg == 2) {
+        const double u1 = zero_hi ? 0.0 : sqrt(__longlong_as_double((long long)st->prefix[1]));
+        med = (u0 + u1) / 2.0;
+    } else {
+        med = u0;
+    }
+    *med_out = med;
+    *a_out = logn / (med * med);
+}
+
+// ============================================================ launchers ==
+
+#define SVGD_PHI_CASE(KPv, NCBv)                                                             \
+    if (KP == KPv && NCB == NCBv) {                                                          \
+        hipLaunchKernelGGL((k_phi<KPv, NCBv>), dim3(grid), dim3(256), 0, stream, xc, cvec, V, \
+                           a_ptr, row0, nrows, ntiles_j, d, inv_n, phi);                     \
+        return hipGetLastError();                                                            \
+    }
+
+hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
+                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
+                      double inv_n, double *phi, hipStream_t stream)
+{
+    const int64_t grid = (nrows + TB - 1) / TB;
+    if (grid == 0) return hipSuccess;
+    SVGD_PHI_CASE(4, 1)
+    SVGD_PHI_CASE(8, 1)
+    SVGD_PHI_CASE(12, 1)
+    SVGD_PHI_CASE(16, 1)
+    SVGD_PHI_CASE(16, 2)
+    SVGD_PHI_CASE(32, 2)
+    SVGD_PHI_CASE(32, 3)
+    SVGD_PHI_CASE(64, 4)
+    SVGD_PHI_CASE(64, 5)
+    return hipErrorInvalidValue;
+}
+
+#define SVGD_TILE_CASE(KPv)                                                                  \
+    if (KP == KPv) {                                                                         \
+        if (mode == 0)                                                                       \
+            hipLaunchKernelGGL((k_pair_tiles<KPv, 0>), dim3(grid), dim3(256), 0, stream, xc, \
+                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+        else if (mode == 1)                                                                  \
+            hipLaunchKernelGGL((k_pair_tiles<KPv, 1>), dim3(grid), dim3(256), 0, stream, xc, \
+                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+        else                                                                                 \
+            hipLaunchKernelGGL((k_pair_tiles<KPv, 2>), dim3(grid), dim3(256), 0, stream, xc, \
+                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+        return hipGetLastError();                                                            \
+    }
+
+hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
+                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                             int64_t cap, uint32_t *counts, unsigned long long *below,
+                             const SelState *st, uint32_t *ghist, double *dbg_out,
+                             hipStream_t stream)
+{
+    if (grid <= 0 || t1 <= t0) return hipSuccess;
+    SinkCollect sc{st, regions, cap, counts, below};
+    SinkHist sh{st, ghist};
+    SinkDebug sd{dbg_out, n};
+    (void)sc;
+    SVGD_TILE_CASE(4)
+    SVGD_TILE_CASE(8)
+    SVGD_TILE_CASE(12)
+    SVGD_TILE_CASE(16)
+    SVGD_TILE_CASE(32)
+    SVGD_TILE_CASE(64)
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
+                              double *partial, int nparts, double *xc, double *nrm,
+                              hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial);
+    int64_t g = (np + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_center, dim3(g), dim3(256), 0, stream, X, n, d, KP, partial, nparts, np,
+                       xc, nrm);
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
+                         int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
+                         hipStream_t stream)
+{
+    int64_t g = (np + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_prep_v, dim3(g), dim3(256), 0, stream, xc, G, nrm, a_ptr, n, np, d, KP,
+                       VW, V, cvec);
+    return hipGetLastError();
+}
+
+hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
+                             int64_t cnt, int d, double lr, double b1, double b2, double eps,
+                             double c1, double c2, const double *lower, const double *upper,
+                             hipStream_t stream)
+{
+    if (cnt <= 0) return hipSuccess;
+    int64_t grid = (cnt + 255) / 256;
+    if (grid > 8192) grid = 8192;
+    hipLaunchKernelGGL(k_opt_update, dim3(grid), dim3(256), 0, stream, kind, g, m, v, X, cnt, d,
+                       lr, b1, b2, eps, c1, c2, lower, upper);
+    return hipGetLastError();
+}
+
+hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int KP, int64_t S,
+                              uint64_t *keys, hipStream_t stream)
+{
+    int64_t g = (S + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, KP, S, keys);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
+                               int64_t cap, int parts, const SelState *st, uint32_t *ghist,
+                               hipStream_t stream)
+{
+    if (nreg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_hist_regions, dim3(nreg * parts), dim3(256), 0, stream, keys, counts,
+                       nreg, cap, parts, st, ghist);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_select_scan, dim3(1), dim3(256), 0, stream, st, ghist);
+    return hipGetLastError();
+}
+
+hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
+                                int64_t nblk, int64_t cap, unsigned long long *cnt,
+                                hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_counts_reduce, dim3(1), dim3(256), 0, stream, below, counts, nblk, cap,
+                       cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_bracket(SelState *st, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_bracket, dim3(1), dim3(1), 0, stream, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const SelState *st, int navg, int zero_lo, int zero_hi, double logn,
+                           double *a_out, double *med_out, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, stream, st, navg, zero_lo, zero_hi, logn,
+                       a_out, med_out);
+    return hipGetLastError();
+}
+
+} // namespace svgd_amd

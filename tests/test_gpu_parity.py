@@ -1,0 +1,272 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle.  GPU only.
+
+Tolerances (fp64, north star: <= 1e-10 max-abs on phi_hat):
+  * phi_hat from identical (X, G, a):            max-abs <= 1e-10 (observed ~1e-15)
+  * median / scale a:                            rel <= 1e-12 (ulp-level: the device
+    computes the Gram form on mean-centred coordinates, the oracle on raw ones)
+  * median selection:                            BIT-EXACT against the exact order
+    statistics of the device's own keys (svgd_debug_pair_keys)
+  * optimizer + clamp on identical phi:          BIT-EXACT
+  * 1000-iteration notebook trajectories:        the published 6 significant digits
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import svgdcpp_amd as S
+from svgdcpp_amd import _capi as C
+
+pytestmark = pytest.mark.gpu
+
+PHI_TOL = 1e-10
+
+
+def _ctx(X, **kw):
+    n, d = X.shape
+    c = S.Context(d, n, **kw)
+    c.set_particles(X)
+    return c
+
+
+def _gmm(oracle, d, k, seed):
+    mus = oracle.splitmix((k, d), 3.0, seed)
+    covs = np.stack([np.eye(d) * (1.0 + 0.25 * c) for c in range(k)])
+    return mus, covs
+
+
+@pytest.mark.parametrize("name", ["n256_d2", "n1000_d8", "n300_d64", "n77_d3"])
+def test_phi_and_scale_match_golden(golden_dir, name):
+    z = np.load(os.path.join(golden_dir, f"phi_{name}.npz"))
+    c = _ctx(z["X"])
+    a, med = c.median_scale()
+    assert med == pytest.approx(float(z["med"]), rel=1e-12)
+    assert a == pytest.approx(float(z["a"]), rel=1e-12)
+    ph = c.phi(z["G"], float(z["a"]))
+    assert np.max(np.abs(ph - z["phi"])) <= PHI_TOL
+
+
+@pytest.mark.parametrize("n,d", [(1, 2), (2, 1), (3, 3), (63, 2), (64, 4), (65, 5), (130, 7),
+                                 (200, 8), (129, 12), (97, 13), (70, 16), (50, 17), (40, 32),
+                                 (33, 33), (31, 63), (20, 64)])
+def test_phi_random_shapes(oracle, n, d):
+    X = oracle.splitmix((n, d), 2.0, 100 + n + d)
+    G = oracle.splitmix((n, d), 1.0, 200 + n + d)
+    a = 0.37
+    c = _ctx(X)
+    ph = c.phi(G, a)
+    ref = oracle.phi(X, G, a)
+    assert np.max(np.abs(ph - ref)) <= PHI_TOL
+
+
+def test_phi_far_from_origin(oracle):
+    """Translation: particles around 1e3 (mean-centring keeps the x_i*sum K -
+    sum K x_j assembly accurate)."""
+    n, d = 300, 4
+    X = 1000.0 + oracle.splitmix((n, d), 1.0, 9)
+    G = oracle.splitmix((n, d), 1.0, 10)
+    a = 1.3
+    ref = oracle.phi(X, G, a)
+    ph = _ctx(X).phi(G, a)
+    assert np.max(np.abs(ph - ref)) <= PHI_TOL
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 9, 64, 65, 127, 400, 777])
+def test_median_exact_selection_direct(oracle, n):
+    d = 3
+    X = oracle.splitmix((n, d), 1.0, 3 * n)
+    c = _ctx(X)
+    a, med = c.median_scale()
+    keys = np.empty(n * (n - 1) // 2)
+    c.check(c.lib.svgd_debug_pair_keys(c.h, C.dptr(keys), keys.size))
+    # device keys agree with the direct-form distances to rounding
+    iu = np.triu_indices(n, 1)
+    ref_keys = ((X[iu[0]] - X[iu[1]]) ** 2).sum(-1)
+    np.testing.assert_allclose(keys, ref_keys, rtol=1e-12, atol=1e-13)
+    # exact order statistics of the device's own keys
+    u = np.sort(keys)
+    tot = n * n
+
+    def at(k):
+        return 0.0 if k < n else np.sqrt(u[(k - n) // 2])
+    exp = (at(tot // 2 - 1) + at(tot // 2)) / 2 if tot % 2 == 0 else at(tot // 2)
+    assert med == exp  # bit-exact selection
+    assert med == pytest.approx(oracle.median_scale(X)[1], rel=1e-12)
+    assert a == pytest.approx(np.log(n) / (exp * exp), rel=1e-15)
+    assert c.last_scale()[2] == C.SVGD_MEDIAN_DIRECT
+
+
+def _median_with_tuning(X, direct_max, sample, cap):
+    c = _ctx(X)
+    c.check(c.lib.svgd_set_median_tuning(c.h, direct_max, sample, cap))
+    a, med = c.median_scale()
+    return c, a, med
+
+
+@pytest.mark.parametrize("n", [700, 1501])
+def test_median_bracket_path_exact(oracle, n):
+    X = oracle.splitmix((n, 5), 1.0, n)
+    ref_c = _ctx(X)
+    a0, m0 = ref_c.median_scale()  # direct path
+    c, a, med = _median_with_tuning(X, 0, 1 << 14, -1)
+    assert c.last_scale()[2] == C.SVGD_MEDIAN_BRACKET
+    assert med == m0 and a == a0
+
+
+def test_median_fallback_path_exact(oracle):
+    n = 900
+    X = oracle.splitmix((n, 4), 1.0, 42)
+    a0, m0 = _ctx(X).median_scale()
+    # a 1-key candidate capacity forces the overflow -> streamed radix select
+    c, a, med = _median_with_tuning(X, 0, 1 << 12, 1)
+    assert c.last_scale()[2] == C.SVGD_MEDIAN_FALLBACK
+    assert med == m0 and a == a0
+
+
+def test_median_ties_and_duplicates(oracle):
+    """Many coincident particles: heavy ties and zero distances."""
+    base = oracle.splitmix((5, 2), 1.0, 1)
+    X = np.repeat(base, 40, axis=0)  # 200 particles, 5 distinct points
+    c = _ctx(X)
+    a, med = c.median_scale()
+    assert med == pytest.approx(oracle.median_scale(X)[1], rel=1e-12)
+    c2, a2, med2 = _median_with_tuning(X, 0, 1 << 10, -1)
+    assert med2 == med
+
+
+def _run_device(X0, model, iters, kind, params, scale=None, bounds=None):
+    n, d = X0.shape
+    c = _ctx(X0)
+    c.set_optimizer(kind, *params)
+    if bounds is not None:
+        c.set_bounds(*bounds)
+    if scale is not None:
+        c.set_scale(C.SVGD_SCALE_FIXED, scale)
+    for _ in range(iters):
+        c.step_with_model(model)
+    return c.get_particles()
+
+
+@pytest.mark.parametrize("case", ["mvn", "gmm"])
+def test_published_notebook_trajectory(oracle, golden_dir, case):
+    with open(os.path.join(golden_dir, "notebooks.json")) as f:
+        nb = json.load(f)[case]
+    n, d = nb["n"], nb["d"]
+    X0 = oracle.eigen_random(d, n, nb["init_scale"], nb["seed"])
+    model = S.GaussianSum(nb["means"], nb["covs"])
+    opt = nb["optimizer"]
+    if opt["kind"] == "adam":
+        X = _run_device(X0, model, nb["iters"], C.SVGD_OPT_ADAM,
+                        (opt["lr"], opt["beta1"], opt["beta2"], 1e-8))
+    else:
+        X = _run_device(X0, model, nb["iters"], C.SVGD_OPT_ADAGRAD, (opt["lr"], 0.0, 0.0, 1e-8))
+    np.testing.assert_allclose(X, np.array(nb["final"]), rtol=5e-6, atol=1e-6)
+
+
+def test_reference_test_svgd_scenario(oracle, golden_dir):
+    """tests/test_svgd.cpp: fixed exp(-|x-x'|^2), user model, Adam, bounds [-1,1]^2."""
+    from golden.make_golden import test_svgd_model_grad
+
+    class CosModel(S.Model):
+        def __init__(self):
+            super().__init__(2)
+
+        def log_model_grad(self, X):
+            return test_svgd_model_grad(np.asarray(X))
+
+    with open(os.path.join(golden_dir, "test_svgd_n10.json")) as f:
+        g = json.load(f)
+    X0 = np.array(g["initial"])
+    X = _run_device(X0, CosModel(), g["iters"], C.SVGD_OPT_ADAM, (0.1, 0.9, 0.999, 1e-8),
+                    scale=1.0, bounds=(np.array(g["lower"]), np.array(g["upper"])))
+    np.testing.assert_allclose(X, np.array(g["final"]), rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["adam", "adagrad", "rmsprop"])
+def test_step_matches_oracle_per_step(oracle, kind):
+    """Per-step parity on a GMM (n=333, d=6): each device step vs the oracle step
+    started from the device's own X_t (so differences do not accumulate)."""
+    n, d = 333, 6
+    X = oracle.splitmix((n, d), 3.0, 5)
+    mus, covs = _gmm(oracle, d, 3, 6)
+    model = S.GaussianSum(list(mus), list(covs))
+    c = _ctx(X)
+    if kind == "adam":
+        c.set_optimizer(C.SVGD_OPT_ADAM, 0.05, 0.9, 0.999, 1e-8)
+        o_opt = oracle.Adam((n, d), 0.05, 0.9, 0.999)
+    elif kind == "adagrad":
+        c.set_optimizer(C.SVGD_OPT_ADAGRAD, 0.05, 0.0, 0.0, 1e-8)
+        o_opt = oracle.AdaGrad((n, d), 0.05)
+    else:
+        c.set_optimizer(C.SVGD_OPT_RMSPROP, 0.05, 0.9, 0.0, 1e-8)
+        o_opt = oracle.RMSProp((n, d), 0.05, 0.9)
+    lo, up = -np.full(d, 2.5), np.full(d, 2.5)
+    c.set_bounds(lo, up)
+    for _ in range(5):
+        Xt = c.get_particles()
+        a_ref, _ = oracle.median_scale(Xt)
+        G = oracle.logp_grad_gmm(Xt, mus, covs)
+        ph_ref = oracle.phi(Xt, G, a_ref)
+        c.step_with_model(model)
+        a_dev, _, _ = c.last_scale()
+        assert a_dev == pytest.approx(a_ref, rel=1e-12)
+        Xref = Xt.copy()
+        oracle.apply_update(Xref, o_opt.step(ph_ref), lo, up)
+        Xdev = c.get_particles()
+        # increments are lr * O(1) -> compare positions with the phi tolerance
+        assert np.max(np.abs(Xdev - Xref)) <= 1e-9
+
+
+def test_optimizer_bit_exact(oracle):
+    """Same phi in -> bit-identical optimizer increments and clamp."""
+    n, d = 100, 3
+    X = oracle.splitmix((n, d), 1.0, 7)
+    G = oracle.splitmix((n, d), 1.0, 8)
+    c = _ctx(X)
+    c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+    c.set_scale(C.SVGD_SCALE_FIXED, 0.5)
+    c.set_bounds(np.full(d, -0.9), np.full(d, 0.9))
+    o_opt = oracle.Adam((n, d), 0.1, 0.9, 0.999)
+    Xo = X.copy()
+    for _ in range(3):
+        ph = c.phi(G, 0.5)  # the device's own phi for this X
+        c.check(c.lib.svgd_step(c.h, C.dptr(np.ascontiguousarray(G))))
+        oracle.apply_update(Xo, o_opt.step(ph), np.full(d, -0.9), np.full(d, 0.9))
+        np.testing.assert_array_equal(c.get_particles(), Xo)
+
+
+def test_api_errors():
+    with pytest.raises(ValueError, match=r"SVGDCpp: \[Argument Error\] Invalid value for decay"):
+        S.Adam(2, 10, 0.1, 1.0, 0.9)
+    X = np.zeros((2, 10))
+    k = S.GaussianRBFKernel(X)
+    m = S.MultivariateNormal([0.0, 0.0], np.eye(2))
+    with pytest.raises(S.DimensionMismatchException, match=r"SVGDCpp: \[Dimension Error\]"):
+        S.SVGD(3, 10, X, k, m, S.Adam(2, 10, 0.1, 0.9, 0.999))
+    with pytest.raises(ValueError, match="Invalid Model object pointer"):
+        S.SVGD(2, 10, X, k, None, S.Adam(2, 10, 0.1, 0.9, 0.999))
+    c = S.Context(2, 10)
+    with pytest.raises(S.UnsetException):
+        c.median_scale()  # particles unset
+    rc = c.lib.svgd_set_optimizer(c.h, C.SVGD_OPT_ADAM, 0.1, 1.5, 0.9, 1e-8)
+    assert rc == C.SVGD_ERR_ARG and b"decay parameter beta" in c.lib.svgd_last_error(c.h)
+
+
+def test_svgd_class_matches_manual_loop(oracle):
+    """test_svgd.cpp structure: the SVGD class vs a manual loop on the same
+    device primitives (median, phi, optimizer) -- here the manual loop is the
+    oracle, the class is the Python mirror over the C ABI."""
+    n, d = 50, 2
+    X0 = oracle.eigen_random(d, n, 3.0, 1)
+    mvn = S.MultivariateNormal([-0.6871, 0.8010], 5 * np.array([[0.2260, 0.1652], [0.1652, 0.6779]]))
+    coord = np.ascontiguousarray(X0.T)  # (d, n) like Eigen
+    kern = S.GaussianRBFKernel(coord, S.GaussianRBFKernel.ScaleMethod.Median, mvn)
+    opt = S.Adam(d, n, 0.1, 0.9, 0.999)
+    svgd = S.SVGD(d, 30, coord, kern, mvn, opt)
+    svgd.Initialize()
+    svgd.Run()
+    Xo = oracle.run_svgd(X0, lambda X: oracle.logp_grad_gmm(X, np.array([[-0.6871, 0.8010]]),
+                                                            5 * np.array([[[0.2260, 0.1652], [0.1652, 0.6779]]])),
+                         30, oracle.Adam((n, d), 0.1, 0.9, 0.999))
+    np.testing.assert_allclose(coord.T, Xo, rtol=0, atol=1e-8)
