@@ -335,7 +335,7 @@ int median_finish(svgd_ctx *c)
         // every averaged order statistic is a diagonal zero
         uint64_t z[2] = {0, 0};
         CHK(upload_state(c, 1, z, 0, 0));
-        HIPCHK(c, launch_finalize(c->st, c->navg, 1, 1, logn, c->scal, c->scal + 1, c->stream));
+        HIPCHK(c, launch_finalize(c->st, c->navg, -1, -1, logn, c->scal, c->scal + 1, c->stream));
         c->last_path = SVGD_MEDIAN_DIRECT;
         return SVGD_OK;
     }
@@ -367,9 +367,8 @@ int median_finish(svgd_ctx *c)
         CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
         HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
     }
-    HIPCHK(c, launch_finalize(c->st, c->navg, c->src_lo < 0 ? 1 : 0, c->src_hi < 0 ? 1 : 0, logn,
-                              c->scal, c->scal + 1, c->stream));
-    (void)c->src_lo;
+    HIPCHK(c, launch_finalize(c->st, c->navg, c->src_lo, c->src_hi, logn, c->scal, c->scal + 1,
+                              c->stream));
     c->last_path = path;
     return SVGD_OK;
 }

@@ -55,7 +55,7 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
                                 int64_t nblk, int64_t cap, unsigned long long *cnt,
                                 hipStream_t stream);
 hipError_t launch_bracket(SelState *st, hipStream_t stream);
-hipError_t launch_finalize(const SelState *st, int navg, int zero_lo, int zero_hi, double logn,
+hipError_t launch_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
                            double *a_out, double *med_out, hipStream_t stream);
 
 } // namespace svgd_amd

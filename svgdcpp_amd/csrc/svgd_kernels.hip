@@ -594,13 +594,17 @@ __global__ void k_bracket(SelState *st)
 
 // med = (sqrt(u_lo) + sqrt(u_hi)) / 2 (or the single middle value);
 // a = ln(n) / med^2  (GaussianRBFKernel.hpp:187, ComputeMedian :222-254).
-__global__ void k_finalize(const SelState *st, int navg, int zero_lo, int zero_hi, double logn,
+// src_lo / src_hi: selection slot holding each order statistic, -1 for a
+// diagonal zero of the full n^2 list.
+__global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
                            double *a_out, double *med_out)
 {
-    const double u0 = zero_lo ? 0.0 : sqrt(__longlong_as_double((long long)st->prefix[0]));
+    const double u0 =
+        src_lo < 0 ? 0.0 : sqrt(__longlong_as_double((long long)st->prefix[src_lo]));
     double med;
     if (navg == 2) {
-        const double u1 = zero_hi ? 0.0 : sqrt(__longlong_as_double((long long)st->prefix[1]));
+        const double u1 =
+            src_hi < 0 ? 0.0 : sqrt(__longlong_as_double((long long)st->prefix[src_hi]));
         med = (u0 + u1) / 2.0;
     } else {
         med = u0;
@@ -746,10 +750,10 @@ hipError_t launch_bracket(SelState *st, hipStream_t stream)
     return hipGetLastError();
 }
 
-hipError_t launch_finalize(const SelState *st, int navg, int zero_lo, int zero_hi, double logn,
+hipError_t launch_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
                            double *a_out, double *med_out, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, stream, st, navg, zero_lo, zero_hi, logn,
+    hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, stream, st, navg, src_lo, src_hi, logn,
                        a_out, med_out);
     return hipGetLastError();
 }
