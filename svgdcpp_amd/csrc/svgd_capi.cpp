@@ -57,6 +57,14 @@ struct svgd_ctx {
     int nparts = 64;
     double *scal = nullptr; // [0] a, [1] med
 
+    // row-stream path (d <= ROWS_MAX_D)
+    bool rowpath = false;
+    int RS = 0;             // record stride 2d+2
+    double *rec = nullptr;  // np x RS particle records
+    double *part = nullptr; // S x ldp x (d+1) phi partials
+    int S = 1;
+    int64_t ldp = 0;
+
     // median
     int64_t direct_max_pairs = int64_t(1) << 24;
     int64_t sample_size = int64_t(1) << 22;
@@ -233,6 +241,19 @@ int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, 
     return SVGD_OK;
 }
 
+// One sweep over this rank's median pair tiles (mode 0 collect, 1 radix
+// histogram, 2 debug dump) on the row-stream (d <= 16) or MFMA tile kernel.
+hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t cap, double *dbg)
+{
+    if (c->rowpath)
+        return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->n, c->nb, c->tile0,
+                                c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
+                                c->ghist, dbg, c->stream);
+    return launch_pair_tiles(c->KP, mode, grid, c->xc, c->nrm, c->n, c->nb, c->tile0,
+                             c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
+                             c->ghist, dbg, c->stream);
+}
+
 // Phase 1 of the median: candidate bracket + collect pass + counts.
 // Leaves the reduced counts in c->h_cnt (ready at c->ev_cnt).
 int median_begin(svgd_ctx *c)
@@ -313,9 +334,7 @@ int median_begin(svgd_ctx *c)
         CHK(dalloc(c, &c->regions, need));
         c->regions_alloc = need;
     }
-    HIPCHK(c, launch_pair_tiles(c->KP, 0, c->collect_grid, c->xc, c->nrm, n, c->nb, c->tile0,
-                                c->tile0 + tiles, c->regions, c->reg_cap, c->counts, c->below,
-                                c->st, nullptr, nullptr, c->stream));
+    HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->collect_grid, c->reg_cap, c->cnt3,
                                    c->stream));
     CHK(allreduce_cnt3(c));
@@ -357,9 +376,7 @@ int median_finish(svgd_ctx *c)
     for (int p = 0; p < 6; ++p) {
         if (path == SVGD_MEDIAN_FALLBACK) {
             const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 2048));
-            HIPCHK(c, launch_pair_tiles(c->KP, 1, grid, c->xc, c->nrm, c->n, c->nb, c->tile0,
-                                        c->tile0 + c->own_tiles, nullptr, 0, nullptr, nullptr,
-                                        c->st, c->ghist, nullptr, c->stream));
+            HIPCHK(c, pair_pass(c, 1, grid, nullptr, 0, nullptr));
         } else {
             HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->collect_grid, c->reg_cap, 1,
                                           c->st, c->ghist, c->stream));
@@ -396,15 +413,23 @@ int upload_g(svgd_ctx *c, const double *G_shard)
 
 int run_phi(svgd_ctx *c)
 {
-    HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW, c->V,
-                            c->cvec, c->stream));
+    if (c->rowpath)
+        HIPCHK(c, launch_prep_rec(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->RS,
+                                  c->rec, c->stream));
+    else
+        HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
+                                c->V, c->cvec, c->stream));
     EvPair ev{};
     if (c->timing) {
         ev = take_pair(c);
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
     }
-    HIPCHK(c, launch_phi(c->KP, c->NCB, c->xc, c->cvec, c->V, c->scal, c->row0, c->nrows,
-                         (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n, c->phi, c->stream));
+    if (c->rowpath)
+        HIPCHK(c, launch_phi_rows(c->dim, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
+                                  c->ldp, 1.0 / (double)c->n, c->phi, c->stream));
+    else
+        HIPCHK(c, launch_phi(c->KP, c->NCB, c->xc, c->cvec, c->V, c->scal, c->row0, c->nrows,
+                             (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n, c->phi, c->stream));
     if (c->timing) {
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         c->ev_phi.push_back(ev);
@@ -492,7 +517,24 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->xc, c->np * c->KP));
     CHK(dalloc(c, &c->nrm, c->np));
     CHK(dalloc(c, &c->cvec, c->np));
-    CHK(dalloc(c, &c->V, c->np * c->VW));
+    c->rowpath = dim <= ROWS_MAX_D;
+    if (c->rowpath) {
+        // column splits: enough workgroups to fill every CU at the kernel's occupancy
+        int ncu = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) ncu = prop.multiProcessorCount;
+        const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim) * ncu;
+        const int64_t iblocks = std::max<int64_t>(1, (c->nrows + 511) / 512);
+        int64_t S = std::max<int64_t>(1, (resident + iblocks - 1) / iblocks);
+        S = std::min<int64_t>(S, std::max<int64_t>(1, n / 256));
+        c->S = (int)S;
+        c->RS = 2 * dim + 2;
+        c->ldp = std::max<int64_t>(1, c->nrows);
+        CHK(dalloc(c, &c->rec, c->np * c->RS));
+        CHK(dalloc(c, &c->part, (int64_t)c->S * c->ldp * (dim + 1)));
+    } else {
+        CHK(dalloc(c, &c->V, c->np * c->VW));
+    }
     CHK(dalloc(c, &c->phi, std::max<int64_t>(1, c->nrows) * dim));
     CHK(dalloc(c, &c->m, std::max<int64_t>(1, c->nrows) * dim));
     CHK(dalloc(c, &c->v, std::max<int64_t>(1, c->nrows) * dim));
@@ -563,8 +605,9 @@ int svgd_destroy(svgd_ctx *c)
     if (!c) return SVGD_OK;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
-    double *dbufs[] = {c->X, c->G, c->xc, c->nrm, c->cvec, c->V, c->phi, c->m, c->v,
-                       c->lower, c->upper, c->partial, c->scal};
+    double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
+                       c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
+                       c->part};
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist};
@@ -828,8 +871,7 @@ int svgd_debug_pair_keys(svgd_ctx *c, double *out, int64_t capacity)
     double *d = nullptr;
     HIPCHK(c, hipMalloc((void **)&d, sizeof(double) * (size_t)std::max<int64_t>(1, M)));
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 1024));
-    hipError_t e = launch_pair_tiles(c->KP, 2, grid, c->xc, c->nrm, c->n, c->nb, 0, c->own_tiles,
-                                     nullptr, 0, nullptr, nullptr, nullptr, nullptr, d, c->stream);
+    hipError_t e = pair_pass(c, 2, grid, nullptr, 0, d);
     if (e == hipSuccess)
         e = hipMemcpyAsync(out, d, sizeof(double) * (size_t)M, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

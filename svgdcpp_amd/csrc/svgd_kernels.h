@@ -55,6 +55,22 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
                                 int64_t nblk, int64_t cap, unsigned long long *cnt,
                                 hipStream_t stream);
 hipError_t launch_bracket(SelState *st, hipStream_t stream);
+
+// Row-stream path (d <= 16): particle records rec_j = [xc_j, c_j, G_j - 2a xc_j, pad],
+// stride 2d+2.  phi partials over S column splits -> part[S][ldp][d+1].
+constexpr int ROWS_MAX_D = 16;
+hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
+                           const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
+                           double *rec, hipStream_t stream);
+hipError_t launch_phi_rows(int d, const double *rec, const double *a_ptr, int64_t row0,
+                           int64_t nrows, int64_t n, int S, double *part, int64_t ldp,
+                           double inv_n, double *phi, hipStream_t stream);
+hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc, const double *nrm,
+                            int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                            int64_t cap, uint32_t *counts, unsigned long long *below,
+                            const SelState *st, uint32_t *ghist, double *dbg_out,
+                            hipStream_t stream);
+int phi_rows_blocks_per_cu(int d);
 hipError_t launch_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
                            double *a_out, double *med_out, hipStream_t stream);
 

@@ -613,7 +613,365 @@ __global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi,
     *a_out = logn / (med * med);
 }
 
+// ===================================================== row-stream kernels ==
+//
+// gfx950 runs f64 MFMA and f64 VALU on one shared pipeline (tools/ubench_f64:
+// ~64 TF MFMA alone, ~68 TF VALU alone, ~70 TF mixed), so for small d the
+// phi pass minimises f64 instructions per pair instead of using MFMA:
+//
+//   lane = particle i (2 rows per lane), column particle j wave-uniform:
+//   x_j, c_j, V_j arrive through scalar loads (SGPR operands, no LDS, no
+//   barriers) and are broadcast into the VALU FMAs.
+//   per (i, j):  dot  d FMA      (Gram form on centred coordinates)
+//                u    add + FMA  (u = 32 * (-a log2e) |x_i - x_j|^2)
+//                2^(u/32)        32-entry LDS table 2^(k/32) x degree-6 poly, ldexp
+//                acc  d FMA + 1  (sum_j K_ij V_j, sum_j K_ij)
+//   ~3d + 14 f64 ops per ordered pair (d = 8: 38, was 54 with MFMA padding).
+// Columns are split over S workgroups (partials reduced by k_phi_reduce in a
+// fixed order, so results are deterministic).
+
+__constant__ double EXP2_TAB32[32] = {
+    0x1.0000000000000p+0, 0x1.059b0d3158574p+0, 0x1.0b5586cf9890fp+0, 0x1.11301d0125b51p+0,
+    0x1.172b83c7d517bp+0, 0x1.1d4873168b9aap+0, 0x1.2387a6e756238p+0, 0x1.29e9df51fdee1p+0,
+    0x1.306fe0a31b715p+0, 0x1.371a7373aa9cbp+0, 0x1.3dea64c123422p+0, 0x1.44e086061892dp+0,
+    0x1.4bfdad5362a27p+0, 0x1.5342b569d4f82p+0, 0x1.5ab07dd485429p+0, 0x1.6247eb03a5585p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.71f75e8ec5f74p+0, 0x1.7a11473eb0187p+0, 0x1.82589994cce13p+0,
+    0x1.8ace5422aa0dbp+0, 0x1.93737b0cdc5e5p+0, 0x1.9c49182a3f090p+0, 0x1.a5503b23e255dp+0,
+    0x1.ae89f995ad3adp+0, 0x1.b7f76f2fb5e47p+0, 0x1.c199bdd85529cp+0, 0x1.cb720dcef9069p+0,
+    0x1.d5818dcfba487p+0, 0x1.dfc97337b9b5fp+0, 0x1.ea4afa2a490dap+0, 0x1.f50765b6e4540p+0};
+
+// 2^(u/32) for u <= ~0: u = k + f, |f| <= 1/2, 2^(u/32) = 2^(k>>5) 2^((k&31)/32) 2^(f/32);
+// 2^(f/32) by its degree-6 Taylor polynomial (|f/32| <= 1/64: 1.3 ulp overall).
+__device__ __forceinline__ double exp2_32(double u, const double *tab)
+{
+    const double k = __builtin_rint(u);
+    const double f = u - k;
+    const int ki = (int)k;
+    double p = 0x1.430912f86c787p-43;
+    p = fma(p, f, 0x1.5d87fe78a6731p-35);
+    p = fma(p, f, 0x1.3b2ab6fba4e77p-27);
+    p = fma(p, f, 0x1.c6b08d704a0c0p-20);
+    p = fma(p, f, 0x1.ebfbdff82c58fp-13);
+    p = fma(p, f, 0x1.62e42fefa39efp-6);
+    p = fma(p, f, 1.0);
+    return __builtin_ldexp(p * tab[ki & 31], ki >> 5);
+}
+
+// rec_j = [xc_j (D), c_j = -32 a log2e |xc_j|^2, V_j = G_j - 2a xc_j (D), pad]
+template <int D> struct RecLayout {
+    static constexpr int RS = 2 * D + 2;
+};
+
+__global__ void k_prep_rec(const double *__restrict__ xc, const double *__restrict__ G,
+                           const double *__restrict__ nrm, const double *__restrict__ a_ptr,
+                           int64_t n, int64_t np, int d, int KP, int RS, double *__restrict__ rec)
+{
+    const double a = *a_ptr;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const bool live = j < n;
+        double *r = rec + j * RS;
+        for (int k = 0; k < d; ++k) {
+            const double x = live ? xc[j * KP + k] : 0.0;
+            r[k] = x;
+            r[d + 1 + k] = live ? G[j * d + k] - 2.0 * a * x : 0.0;
+        }
+        r[d] = live ? -32.0 * a * LOG2E * nrm[j] : 0.0;
+        r[RS - 1] = 0.0;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec,
+                                                 const double *__restrict__ a_ptr, int64_t row0,
+                                                 int64_t nrows, int64_t n, int S,
+                                                 double *__restrict__ part, int64_t ldp)
+{
+    constexpr int RS = RecLayout<D>::RS;
+    __shared__ double tab[32];
+    if (threadIdx.x < 32) tab[threadIdx.x] = EXP2_TAB32[threadIdx.x];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t iblk = blockIdx.x / S;
+    const int s = (int)(blockIdx.x - iblk * S);
+    const int64_t rbase = iblk * 512 + w * 128; // local row of this wave's first lane
+    const double alpha = 64.0 * LOG2E * (*a_ptr);
+
+    double xi[2][D], ci[2], acc[2][D], acc1[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        int64_t li = rbase + 64 * r + lane;
+        if (li >= nrows) li = nrows - 1; // padding lanes recompute a valid row
+        const double *ri = rec + (row0 + li) * RS;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            xi[r][k] = ri[k];
+            acc[r][k] = 0.0;
+        }
+        ci[r] = ri[D];
+        acc1[r] = 0.0;
+    }
+
+    const int64_t j0 = n * s / S, j1 = n * (s + 1) / S;
+    for (int64_t j = j0; j < j1; ++j) {
+        const double *rj = rec + j * RS; // wave-uniform: scalar loads
+        double xj[D], vj[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            xj[k] = rj[k];
+            vj[k] = rj[D + 1 + k];
+        }
+        const double cj = rj[D];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            double dot = xi[r][0] * xj[0];
+#pragma unroll
+            for (int k = 1; k < D; ++k) dot = fma(xi[r][k], xj[k], dot);
+            const double K = exp2_32(fma(alpha, dot, ci[r] + cj), tab);
+#pragma unroll
+            for (int k = 0; k < D; ++k) acc[r][k] = fma(K, vj[k], acc[r][k]);
+            acc1[r] += K;
+        }
+    }
+
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const int64_t li = rbase + 64 * r + lane;
+        if (li < nrows) {
+            double *o = part + ((int64_t)s * ldp + li) * (D + 1);
+#pragma unroll
+            for (int k = 0; k < D; ++k) o[k] = acc[r][k];
+            o[D] = acc1[r];
+        }
+    }
+}
+
+// phi_i = (sum_s acc_s + 2a xc_i sum_s acc1_s) / N, partials summed in s order.
+__global__ void k_phi_reduce(const double *__restrict__ part, const double *__restrict__ rec,
+                             const double *__restrict__ a_ptr, int64_t row0, int64_t nrows,
+                             int d, int RS, int S, int64_t ldp, double inv_n,
+                             double *__restrict__ phi)
+{
+    const double two_a = 2.0 * (*a_ptr);
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nrows;
+         li += (int64_t)gridDim.x * blockDim.x) {
+        double s1 = 0.0;
+        for (int s = 0; s < S; ++s) s1 += part[((int64_t)s * ldp + li) * (d + 1) + d];
+        const double *ri = rec + (row0 + li) * RS;
+        for (int k = 0; k < d; ++k) {
+            double sk = 0.0;
+            for (int s = 0; s < S; ++s) sk += part[((int64_t)s * ldp + li) * (d + 1) + k];
+            phi[li * d + k] = inv_n * (sk + two_a * ri[k] * s1);
+        }
+    }
+}
+
+// Median pair sweep, row-stream form: each wave walks a contiguous run of the
+// rank's block tiles (plan.cpp); lane = particle i of the row block, j of the
+// column block wave-uniform (scalar loads).  Key = max(|xc_i|^2 + |xc_j|^2 -
+// 2 xc_i.xc_j, 0) with the dot as an FMA chain in k order (bit-identical to
+// k_sample_keys).  MODE 0 collect, 1 histogram (fallback), 2 debug dump.
+template <int D, int MODE>
+__global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc, int KP,
+                                                  const double *__restrict__ nrm, int64_t n,
+                                                  int64_t nb, int64_t t0, int64_t t1,
+                                                  SinkCollect sc, SinkHist sh, SinkDebug sd)
+{
+    __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
+    __shared__ uint32_t sCnt;
+    __shared__ unsigned long long sBelow[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+
+    int nsel = 0, shift = 0, hsh = 63;
+    uint64_t pfx0 = 0, pfx1 = 0, lo_key = 0, hi_key = 0;
+    if (MODE == 0) {
+        lo_key = sc.st->lo_key;
+        hi_key = sc.st->hi_key;
+        if (tid == 0) sCnt = 0;
+    } else if (MODE == 1) {
+        nsel = sh.st->nsel;
+        shift = sh.st->shift;
+        hsh = shift + sh.st->width;
+        pfx0 = sh.st->prefix[0];
+        pfx1 = sh.st->prefix[1];
+        for (int e = tid; e < 2 * RADIX; e += 256) sHist[e] = 0;
+    }
+    __syncthreads();
+
+    const int64_t W = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + w;
+    const int64_t T = t1 - t0;
+    const int64_t tb = t0 + T * gw / W, te = t0 + T * (gw + 1) / W;
+    uint32_t below = 0;
+
+    if (tb < te) {
+        const int64_t H = (nb - 1) / 2;
+        int64_t I, J;
+        tile_coords(nb, tb, &I, &J);
+        int64_t slot = (J - I + nb) % nb;
+        int64_t curI = -1;
+        double xi[D], ni = 0.0;
+        int64_t i = 0;
+        for (int64_t t = tb; t < te; ++t) {
+            if (I != curI) {
+                i = I * TB + lane;
+                const int64_t ic = i < n ? i : n - 1;
+#pragma unroll
+                for (int k = 0; k < D; ++k) xi[k] = xc[ic * KP + k];
+                ni = nrm[ic];
+                curI = I;
+            }
+            const int64_t jb = J * TB, je = min(jb + TB, n);
+            for (int64_t j = jb; j < je; ++j) {
+                const double *xj = xc + j * KP; // wave-uniform
+                double dot = xi[0] * xj[0];
+#pragma unroll
+                for (int k = 1; k < D; ++k) dot = fma(xi[k], xj[k], dot);
+                const double s = fmax(fma(-2.0, dot, ni + nrm[j]), 0.0);
+                const uint64_t key = key_of(s);
+                const bool valid = (i < n) && (I != J || i < j);
+                if (MODE == 0) {
+                    const bool in = valid && key >= lo_key && key < hi_key;
+                    below += (valid && key < lo_key) ? 1u : 0u;
+                    const unsigned long long mask = __ballot(in);
+                    if (mask) {
+                        uint32_t base = 0;
+                        if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mask));
+                        base = __shfl(base, 0);
+                        if (in) {
+                            const int64_t pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+                            if (pos < sc.cap) sc.region[blockIdx.x * sc.cap + pos] = key;
+                        }
+                    }
+                } else if (MODE == 1) {
+                    if (valid) {
+                        const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
+                        if (hsh >= 64 || (key >> hsh) == (pfx0 >> hsh)) atomicAdd(&sHist[dg], 1u);
+                        if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (pfx1 >> hsh)))
+                            atomicAdd(&sHist[RADIX + dg], 1u);
+                    }
+                } else {
+                    if (valid) {
+                        const int64_t a = i < j ? i : j, b = i < j ? j : i;
+                        sd.out[a * (2 * sd.n - a - 1) / 2 + (b - a - 1)] = s;
+                    }
+                }
+            }
+            // next tile of the plan (incremental tile_coords)
+            ++slot;
+            const int64_t cntI = ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
+            if (slot == cntI) {
+                ++I;
+                slot = 0;
+            }
+            J = slot == 0 ? I : (I + slot) % nb;
+        }
+    }
+
+    if (MODE == 0) {
+        unsigned long long bl = below;
+        for (int o = 32; o > 0; o >>= 1) bl += __shfl_down(bl, o);
+        if (lane == 0) sBelow[w] = bl;
+        __syncthreads();
+        if (tid == 0) {
+            sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
+            sc.count_out[blockIdx.x] = sCnt;
+        }
+    } else if (MODE == 1) {
+        __syncthreads();
+        for (int e = tid; e < 2 * RADIX; e += 256)
+            if (sHist[e]) atomicAdd(&sh.ghist[e], sHist[e]);
+    }
+}
+
 // ============================================================ launchers ==
+
+#define SVGD_ROWS_CASE(Dv)                                                                   \
+    case Dv:                                                                                 \
+        if (kind == 0)                                                                       \
+            hipLaunchKernelGGL((k_phi_rows<Dv>), dim3(grid), dim3(256), 0, stream, rec, a_ptr, \
+                               row0, nrows, n, S, part, ldp);                                \
+        else if (kind == 10)                                                                 \
+            hipLaunchKernelGGL((k_pair_rows<Dv, 0>), dim3(grid), dim3(256), 0, stream, xc, KP, \
+                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+        else if (kind == 11)                                                                 \
+            hipLaunchKernelGGL((k_pair_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream, xc, KP, \
+                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+        else                                                                                 \
+            hipLaunchKernelGGL((k_pair_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream, xc, KP, \
+                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+        break;
+
+static hipError_t launch_rows_kernel(int kind, int D, int grid, const double *rec,
+                                     const double *a_ptr, int64_t row0, int64_t nrows, int64_t n,
+                                     int S, double *part, int64_t ldp, const double *xc, int KP,
+                                     const double *nrm, int64_t nb, int64_t t0, int64_t t1,
+                                     SinkCollect sc, SinkHist sh, SinkDebug sd, hipStream_t stream)
+{
+    switch (D) {
+        SVGD_ROWS_CASE(1)
+        SVGD_ROWS_CASE(2)
+        SVGD_ROWS_CASE(3)
+        SVGD_ROWS_CASE(4)
+        SVGD_ROWS_CASE(5)
+        SVGD_ROWS_CASE(6)
+        SVGD_ROWS_CASE(7)
+        SVGD_ROWS_CASE(8)
+        SVGD_ROWS_CASE(9)
+        SVGD_ROWS_CASE(10)
+        SVGD_ROWS_CASE(11)
+        SVGD_ROWS_CASE(12)
+        SVGD_ROWS_CASE(13)
+        SVGD_ROWS_CASE(14)
+        SVGD_ROWS_CASE(15)
+        SVGD_ROWS_CASE(16)
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
+                           const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
+                           double *rec, hipStream_t stream)
+{
+    int64_t g = (np + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_prep_rec, dim3(g), dim3(256), 0, stream, xc, G, nrm, a_ptr, n, np, d, KP,
+                       RS, rec);
+    return hipGetLastError();
+}
+
+hipError_t launch_phi_rows(int d, const double *rec, const double *a_ptr, int64_t row0,
+                           int64_t nrows, int64_t n, int S, double *part, int64_t ldp,
+                           double inv_n, double *phi, hipStream_t stream)
+{
+    if (nrows <= 0) return hipSuccess;
+    const int grid = (int)(((nrows + 511) / 512) * S);
+    hipError_t e = launch_rows_kernel(0, d, grid, rec, a_ptr, row0, nrows, n, S, part, ldp,
+                                      nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
+                                      SinkDebug{}, stream);
+    if (e != hipSuccess) return e;
+    int64_t g = (nrows + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
+                       d, 2 * d + 2, S, ldp, inv_n, phi);
+    return hipGetLastError();
+}
+
+hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc, const double *nrm,
+                            int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                            int64_t cap, uint32_t *counts, unsigned long long *below,
+                            const SelState *st, uint32_t *ghist, double *dbg_out,
+                            hipStream_t stream)
+{
+    if (grid <= 0 || t1 <= t0) return hipSuccess;
+    SinkCollect sc{st, regions, cap, counts, below};
+    SinkHist sh{st, ghist};
+    SinkDebug sd{dbg_out, n};
+    return launch_rows_kernel(10 + mode, d, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, xc,
+                              KP, nrm, nb, t0, t1, sc, sh, sd, stream);
+}
 
 #define SVGD_PHI_CASE(KPv, NCBv)                                                             \
     if (KP == KPv && NCB == NCBv) {                                                          \
@@ -756,6 +1114,30 @@ hipError_t launch_finalize(const SelState *st, int navg, int src_lo, int src_hi,
     hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1), 0, stream, st, navg, src_lo, src_hi, logn,
                        a_out, med_out);
     return hipGetLastError();
+}
+
+} // namespace svgd_amd
+
+namespace svgd_amd {
+
+#define SVGD_OCC_CASE(Dv)                                                                    \
+    case Dv:                                                                                 \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<Dv>, 256, 0);       \
+        break;
+
+int phi_rows_blocks_per_cu(int d)
+{
+    int nb = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (d) {
+        SVGD_OCC_CASE(1) SVGD_OCC_CASE(2) SVGD_OCC_CASE(3) SVGD_OCC_CASE(4)
+        SVGD_OCC_CASE(5) SVGD_OCC_CASE(6) SVGD_OCC_CASE(7) SVGD_OCC_CASE(8)
+        SVGD_OCC_CASE(9) SVGD_OCC_CASE(10) SVGD_OCC_CASE(11) SVGD_OCC_CASE(12)
+        SVGD_OCC_CASE(13) SVGD_OCC_CASE(14) SVGD_OCC_CASE(15) SVGD_OCC_CASE(16)
+    default:
+        break;
+    }
+    return (e == hipSuccess && nb > 0) ? nb : 1;
 }
 
 } // namespace svgd_amd
