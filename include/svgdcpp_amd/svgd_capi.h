@@ -182,11 +182,13 @@ void svgd_plan_rows(int64_t n, int world, int rank, int64_t *row0, int64_t *row1
  * (2 for even n^2, 1 for odd). */
 int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi);
 /* Number of block-level tiles of the median pair sweep owned by rank r
- * (row blocks of 64; each unordered pair of particles is visited by exactly
- * one rank), and the (row block, column block) of tile t of that rank. */
-int64_t svgd_plan_pair_tiles(int64_t n, int world, int rank);
-void svgd_plan_pair_tile(int64_t n, int world, int rank, int64_t t, int64_t *row_block,
-                         int64_t *col_block);
+ * (row blocks of `block` particles; each unordered pair of particles is
+ * visited by exactly one rank), and the (row block, column block) of tile t
+ * of that rank.  The device uses block = SVGD_PAIR_BLOCK(dim). */
+#define SVGD_PAIR_BLOCK(dim) ((dim) <= 16 ? 256 : 64)
+int64_t svgd_plan_pair_tiles(int64_t n, int block, int world, int rank);
+void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
+                         int64_t *row_block, int64_t *col_block);
 
 #ifdef __cplusplus
 }

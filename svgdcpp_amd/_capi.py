@@ -67,8 +67,8 @@ SIGNATURES = {
     "svgd_debug_pair_keys": (ctypes.c_int, [_P, _D, _I64]),
     "svgd_plan_rows": (None, [_I64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "svgd_plan_median_ranks": (ctypes.c_int, [_I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
-    "svgd_plan_pair_tiles": (_I64, [_I64, ctypes.c_int, ctypes.c_int]),
-    "svgd_plan_pair_tile": (None, [_I64, ctypes.c_int, ctypes.c_int, _I64, ctypes.POINTER(_I64),
+    "svgd_plan_pair_tiles": (_I64, [_I64, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "svgd_plan_pair_tile": (None, [_I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _I64, ctypes.POINTER(_I64),
                                    ctypes.POINTER(_I64)]),
     "svgd_model_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.c_int, _D, _D]),
     "svgd_model_destroy": (ctypes.c_int, [_P]),

@@ -7,7 +7,8 @@
 // Median pairs: the reference takes the median over all n^2 distances
 // (GaussianRBFKernel.hpp:185, 222-254): n diagonal zeros plus every
 // off-diagonal distance twice.  Only the n(n-1)/2 upper-triangle values are
-// visited, as 64x64 block tiles: row block I pairs with itself (upper
+// visited, as block x block tiles (block = 256 on the row-stream path, 64 on
+// the MFMA tile path): row block I pairs with itself (upper
 // triangle inside the tile) and with column blocks I+1 .. I+H (mod nb),
 // H = floor((nb-1)/2), plus I + nb/2 when nb is even and I < nb/2.  Every
 // unordered pair of blocks then appears exactly once and every row block
@@ -47,18 +48,18 @@ int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi)
 
 static int64_t tiles_total(int64_t nb) { return nb * (nb + 1) / 2; }
 
-int64_t svgd_plan_pair_tiles(int64_t n, int world, int rank)
+int64_t svgd_plan_pair_tiles(int64_t n, int block, int world, int rank)
 {
-    const int64_t nb = (n + 63) / 64;
+    const int64_t nb = (n + block - 1) / block;
     const int64_t T = tiles_total(nb);
     if (world < 1) world = 1;
     return T * (rank + 1) / world - T * rank / world;
 }
 
-void svgd_plan_pair_tile(int64_t n, int world, int rank, int64_t t, int64_t *row_block,
-                         int64_t *col_block)
+void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
+                         int64_t *row_block, int64_t *col_block)
 {
-    const int64_t nb = (n + 63) / 64;
+    const int64_t nb = (n + block - 1) / block;
     if (world < 1) world = 1;
     t += tiles_total(nb) * rank / world;
     const int64_t H = (nb - 1) / 2;

@@ -12,6 +12,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -63,6 +64,7 @@ struct svgd_ctx {
     double *rec = nullptr;  // np x RS particle records
     double *part = nullptr; // S x ldp x (d+1) phi partials
     int S = 1;
+    int R = 2; // rows per lane of k_phi_rows
     int64_t ldp = 0;
 
     // median
@@ -79,7 +81,9 @@ struct svgd_ctx {
     unsigned long long *cnt3 = nullptr;
     SelState *st = nullptr;
     uint32_t *ghist = nullptr;
-    int64_t own_tiles = 0, tile0 = 0;
+    int64_t own_tiles = 0, tile0 = 0; // this rank's range of the median tile plan
+    int pblock = 64;                  // median tile block (SVGD_PAIR_BLOCK)
+    int64_t pnb = 0;                  // median row blocks
 
     // per-step median plan (set in begin, consumed in finish)
     int med_path = SVGD_MEDIAN_DIRECT;
@@ -246,10 +250,10 @@ int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, 
 hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t cap, double *dbg)
 {
     if (c->rowpath)
-        return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->n, c->nb, c->tile0,
+        return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->n, c->pnb, c->tile0,
                                 c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
                                 c->ghist, dbg, c->stream);
-    return launch_pair_tiles(c->KP, mode, grid, c->xc, c->nrm, c->n, c->nb, c->tile0,
+    return launch_pair_tiles(c->KP, mode, grid, c->xc, c->nrm, c->n, c->pnb, c->tile0,
                              c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
                              c->ghist, dbg, c->stream);
 }
@@ -291,7 +295,7 @@ int median_begin(svgd_ctx *c)
     if (M <= c->direct_max_pairs) {
         // every key is a candidate: bracket [0, ~0)
         c->med_path = SVGD_MEDIAN_DIRECT;
-        c->reg_cap = tiles_per_blk * TB * TB;
+        c->reg_cap = tiles_per_blk * c->pblock * c->pblock;
         uint64_t z[2] = {0, 0};
         CHK(upload_state(c, 1, z, 0, ~0ull));
     } else {
@@ -321,7 +325,7 @@ int median_begin(svgd_ctx *c)
         }
         // bracket [lo_key, hi_key) stays on the device (read by the collect pass)
         HIPCHK(c, launch_bracket(c->st, c->stream));
-        int64_t pairs_own = tiles * TB * TB;
+        int64_t pairs_own = tiles * c->pblock * c->pblock;
         int64_t total = c->cand_capacity;
         if (total <= 0) {
             const double frac = (qhi - qlo) + 16.0 / std::sqrt((double)S) + 0.004;
@@ -425,7 +429,7 @@ int run_phi(svgd_ctx *c)
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
     }
     if (c->rowpath)
-        HIPCHK(c, launch_phi_rows(c->dim, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
+        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, c->phi, c->stream));
     else
         HIPCHK(c, launch_phi(c->KP, c->NCB, c->xc, c->cvec, c->V, c->scal, c->row0, c->nrows,
@@ -504,9 +508,11 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     c->chunk = (n + c->world - 1) / c->world;
     svgd_plan_rows(n, c->world, c->rank, &c->row0, &c->row1);
     c->nrows = c->row1 - c->row0;
-    c->own_tiles = svgd_plan_pair_tiles(n, c->world, c->rank);
+    c->pblock = SVGD_PAIR_BLOCK(dim);
+    c->pnb = (n + c->pblock - 1) / c->pblock;
+    c->own_tiles = svgd_plan_pair_tiles(n, c->pblock, c->world, c->rank);
     {
-        const int64_t nbv = c->nb, T = nbv * (nbv + 1) / 2;
+        const int64_t T = c->pnb * (c->pnb + 1) / 2;
         c->tile0 = T * c->rank / c->world;
     }
     HIPCHK(c, hipSetDevice(device));
@@ -523,8 +529,13 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         int ncu = 256;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) ncu = prop.multiProcessorCount;
-        const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim) * ncu;
-        const int64_t iblocks = std::max<int64_t>(1, (c->nrows + 511) / 512);
+        c->R = dim <= 8 ? 4 : 2; // rows per lane (register budget)
+        if (const char *e = std::getenv("SVGD_PHI_R")) {
+            const int r = std::atoi(e);
+            if (r == 1 || r == 2 || r == 4) c->R = r;
+        }
+        const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim, c->R) * ncu;
+        const int64_t iblocks = std::max<int64_t>(1, (c->nrows + 256 * c->R - 1) / (256 * c->R));
         int64_t S = std::max<int64_t>(1, (resident + iblocks - 1) / iblocks);
         S = std::min<int64_t>(S, std::max<int64_t>(1, n / 256));
         c->S = (int)S;

@@ -62,7 +62,7 @@ constexpr int ROWS_MAX_D = 16;
 hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
                            double *rec, hipStream_t stream);
-hipError_t launch_phi_rows(int d, const double *rec, const double *a_ptr, int64_t row0,
+hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr, int64_t row0,
                            int64_t nrows, int64_t n, int S, double *part, int64_t ldp,
                            double inv_n, double *phi, hipStream_t stream);
 hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc, const double *nrm,
@@ -70,7 +70,7 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
                             const SelState *st, uint32_t *ghist, double *dbg_out,
                             hipStream_t stream);
-int phi_rows_blocks_per_cu(int d);
+int phi_rows_blocks_per_cu(int d, int R);
 hipError_t launch_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
                            double *a_out, double *med_out, hipStream_t stream);
 

@@ -264,7 +264,10 @@ __global__ void k_opt_update(int kind, const double *__restrict__ g, double *__r
 // coordinates) as the IEEE bit pattern, which orders like uint64 for s >= 0.
 // Every unordered pair i<j is visited once by the tile sweep of plan.h.
 
-__device__ __forceinline__ uint64_t key_of(double s) { return (uint64_t)__double_as_longlong(s); }
+__device__ __forceinline__ uint64_t key_of(double s)
+{
+    return (uint64_t)__double_as_longlong(s) & 0x7fffffffffffffffull; // s >= 0 (+0, never -0)
+}
 
 // Device copy of plan_pair_tile (plan.cpp): tile index -> (row block, col block).
 __device__ __forceinline__ void tile_coords(int64_t nb, int64_t t, int64_t *I, int64_t *J)
@@ -681,7 +684,7 @@ __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restri
     }
 }
 
-template <int D>
+template <int D, int R>
 __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec,
                                                  const double *__restrict__ a_ptr, int64_t row0,
                                                  int64_t nrows, int64_t n, int S,
@@ -695,12 +698,12 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int64_t iblk = blockIdx.x / S;
     const int s = (int)(blockIdx.x - iblk * S);
-    const int64_t rbase = iblk * 512 + w * 128; // local row of this wave's first lane
+    const int64_t rbase = iblk * (256 * R) + w * (64 * R); // local row of this wave's lane 0
     const double alpha = 64.0 * LOG2E * (*a_ptr);
 
-    double xi[2][D], ci[2], acc[2][D], acc1[2];
+    double xi[R][D], ci[R], acc[R][D], acc1[R];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < R; ++r) {
         int64_t li = rbase + 64 * r + lane;
         if (li >= nrows) li = nrows - 1; // padding lanes recompute a valid row
         const double *ri = rec + (row0 + li) * RS;
@@ -714,17 +717,37 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     }
 
     const int64_t j0 = n * s / S, j1 = n * (s + 1) / S;
+    // software pipeline: the record of column j+1 is loaded (scalar loads,
+    // wave-uniform) while column j is computed
+    double xn[D], vn[D], cn;
+    {
+        const double *rj = rec + j0 * RS;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            xn[k] = rj[k];
+            vn[k] = rj[D + 1 + k];
+        }
+        cn = rj[D];
+    }
     for (int64_t j = j0; j < j1; ++j) {
-        const double *rj = rec + j * RS; // wave-uniform: scalar loads
         double xj[D], vj[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            xj[k] = rj[k];
-            vj[k] = rj[D + 1 + k];
+            xj[k] = xn[k];
+            vj[k] = vn[k];
         }
-        const double cj = rj[D];
+        const double cj = cn;
+        {
+            const double *rj = rec + (j + 1 < j1 ? j + 1 : j) * RS;
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
+            for (int k = 0; k < D; ++k) {
+                xn[k] = rj[k];
+                vn[k] = rj[D + 1 + k];
+            }
+            cn = rj[D];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
             double dot = xi[r][0] * xj[0];
 #pragma unroll
             for (int k = 1; k < D; ++k) dot = fma(xi[r][k], xj[k], dot);
@@ -736,7 +759,7 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     }
 
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < R; ++r) {
         const int64_t li = rbase + 64 * r + lane;
         if (li < nrows) {
             double *o = part + ((int64_t)s * ldp + li) * (D + 1);
@@ -772,6 +795,9 @@ __global__ void k_phi_reduce(const double *__restrict__ part, const double *__re
 // column block wave-uniform (scalar loads).  Key = max(|xc_i|^2 + |xc_j|^2 -
 // 2 xc_i.xc_j, 0) with the dot as an FMA chain in k order (bit-identical to
 // k_sample_keys).  MODE 0 collect, 1 histogram (fallback), 2 debug dump.
+constexpr int PR = 4;     // rows per lane of the median sweep
+constexpr int PBLK = 256; // = 64 * PR: tile block of the row-stream median plan
+
 template <int D, int MODE>
 __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc, int KP,
                                                   const double *__restrict__ nrm, int64_t n,
@@ -781,7 +807,9 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
     __shared__ uint32_t sCnt;
     __shared__ unsigned long long sBelow[4];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    // wave index made provably uniform so the column stream uses scalar loads
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     int nsel = 0, shift = 0, hsh = 63;
     uint64_t pfx0 = 0, pfx1 = 0, lo_key = 0, hi_key = 0;
@@ -799,10 +827,15 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     }
     __syncthreads();
 
+    // keys of non-negative doubles order like the doubles themselves
+    const double lo_d = __longlong_as_double((long long)lo_key);
+    const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
+                                                        : __longlong_as_double((long long)hi_key);
+
     const int64_t W = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + w;
     const int64_t T = t1 - t0;
     const int64_t tb = t0 + T * gw / W, te = t0 + T * (gw + 1) / W;
-    uint32_t below = 0;
+    unsigned long long below = 0; // wave-uniform (scalar) count
 
     if (tb < te) {
         const int64_t H = (nb - 1) / 2;
@@ -810,50 +843,81 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
         tile_coords(nb, tb, &I, &J);
         int64_t slot = (J - I + nb) % nb;
         int64_t curI = -1;
-        double xi[D], ni = 0.0;
-        int64_t i = 0;
+        double xi[PR][D], ni[PR];
+        int64_t irow[PR];
+        bool ivalid[PR];
+        unsigned long long vmask[PR];
         for (int64_t t = tb; t < te; ++t) {
             if (I != curI) {
-                i = I * TB + lane;
-                const int64_t ic = i < n ? i : n - 1;
 #pragma unroll
-                for (int k = 0; k < D; ++k) xi[k] = xc[ic * KP + k];
-                ni = nrm[ic];
+                for (int r = 0; r < PR; ++r) {
+                    irow[r] = I * PBLK + 64 * r + lane;
+                    ivalid[r] = irow[r] < n;
+                    vmask[r] = __ballot(ivalid[r]);
+                    const int64_t ic = ivalid[r] ? irow[r] : n - 1;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) xi[r][k] = xc[ic * KP + k];
+                    ni[r] = nrm[ic];
+                }
                 curI = I;
             }
-            const int64_t jb = J * TB, je = min(jb + TB, n);
-            for (int64_t j = jb; j < je; ++j) {
-                const double *xj = xc + j * KP; // wave-uniform
-                double dot = xi[0] * xj[0];
+            const bool diag = I == J;
+            const int64_t jb = J * PBLK, je = min(jb + PBLK, n);
+            // prefetched wave-uniform column record (scalar loads)
+            double xn[D], nn;
 #pragma unroll
-                for (int k = 1; k < D; ++k) dot = fma(xi[k], xj[k], dot);
-                const double s = fmax(fma(-2.0, dot, ni + nrm[j]), 0.0);
-                const uint64_t key = key_of(s);
-                const bool valid = (i < n) && (I != J || i < j);
-                if (MODE == 0) {
-                    const bool in = valid && key >= lo_key && key < hi_key;
-                    below += (valid && key < lo_key) ? 1u : 0u;
-                    const unsigned long long mask = __ballot(in);
-                    if (mask) {
-                        uint32_t base = 0;
-                        if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mask));
-                        base = __shfl(base, 0);
-                        if (in) {
-                            const int64_t pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-                            if (pos < sc.cap) sc.region[blockIdx.x * sc.cap + pos] = key;
+            for (int k = 0; k < D; ++k) xn[k] = xc[jb * KP + k];
+            nn = nrm[jb];
+            for (int64_t j = jb; j < je; ++j) {
+                double xj[D];
+#pragma unroll
+                for (int k = 0; k < D; ++k) xj[k] = xn[k];
+                const double nj = nn;
+                {
+                    const int64_t jn = j + 1 < je ? j + 1 : j;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) xn[k] = xc[jn * KP + k];
+                    nn = nrm[jn];
+                }
+#pragma unroll
+                for (int r = 0; r < PR; ++r) {
+                    double dot = xi[r][0] * xj[0];
+#pragma unroll
+                    for (int k = 1; k < D; ++k) dot = fma(xi[r][k], xj[k], dot);
+                    const double s = fmax(fma(-2.0, dot, ni[r] + nj), 0.0);
+                    const bool valid = ivalid[r] && (!diag || irow[r] < j);
+                    if (MODE == 0) {
+                        // masks live in SGPRs: two f64 compares per pair
+                        const unsigned long long vm = diag ? __ballot(valid) : vmask[r];
+                        const unsigned long long mb = __ballot(s < lo_d) & vm;
+                        below += __popcll(mb);
+                        const unsigned long long mask = __ballot(s < hi_d) & vm & ~mb;
+                        const bool in = (mask >> lane) & 1ull;
+                        if (mask) {
+                            uint32_t base = 0;
+                            if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mask));
+                            base = __shfl(base, 0);
+                            if (in) {
+                                const int64_t pos =
+                                    base + __popcll(mask & ((1ull << lane) - 1ull));
+                                if (pos < sc.cap) sc.region[blockIdx.x * sc.cap + pos] = key_of(s);
+                            }
                         }
-                    }
-                } else if (MODE == 1) {
-                    if (valid) {
-                        const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
-                        if (hsh >= 64 || (key >> hsh) == (pfx0 >> hsh)) atomicAdd(&sHist[dg], 1u);
-                        if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (pfx1 >> hsh)))
-                            atomicAdd(&sHist[RADIX + dg], 1u);
-                    }
-                } else {
-                    if (valid) {
-                        const int64_t a = i < j ? i : j, b = i < j ? j : i;
-                        sd.out[a * (2 * sd.n - a - 1) / 2 + (b - a - 1)] = s;
+                    } else if (MODE == 1) {
+                        if (valid) {
+                            const uint64_t key = key_of(s);
+                            const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
+                            if (hsh >= 64 || (key >> hsh) == (pfx0 >> hsh))
+                                atomicAdd(&sHist[dg], 1u);
+                            if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (pfx1 >> hsh)))
+                                atomicAdd(&sHist[RADIX + dg], 1u);
+                        }
+                    } else {
+                        if (valid) {
+                            const int64_t i = irow[r];
+                            const int64_t a = i < j ? i : j, b = i < j ? j : i;
+                            sd.out[a * (2 * sd.n - a - 1) / 2 + (b - a - 1)] = s;
+                        }
                     }
                 }
             }
@@ -869,9 +933,7 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     }
 
     if (MODE == 0) {
-        unsigned long long bl = below;
-        for (int o = 32; o > 0; o >>= 1) bl += __shfl_down(bl, o);
-        if (lane == 0) sBelow[w] = bl;
+        if (lane == 0) sBelow[w] = below;
         __syncthreads();
         if (tid == 0) {
             sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
@@ -888,9 +950,15 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
 
 #define SVGD_ROWS_CASE(Dv)                                                                   \
     case Dv:                                                                                 \
-        if (kind == 0)                                                                       \
-            hipLaunchKernelGGL((k_phi_rows<Dv>), dim3(grid), dim3(256), 0, stream, rec, a_ptr, \
-                               row0, nrows, n, S, part, ldp);                                \
+        if (kind == 0 && R == 1)                                                             \
+            hipLaunchKernelGGL((k_phi_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream, rec,     \
+                               a_ptr, row0, nrows, n, S, part, ldp);                         \
+        else if (kind == 0 && R == 2)                                                        \
+            hipLaunchKernelGGL((k_phi_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream, rec,     \
+                               a_ptr, row0, nrows, n, S, part, ldp);                         \
+        else if (kind == 0)                                                                  \
+            hipLaunchKernelGGL((k_phi_rows<Dv, 4>), dim3(grid), dim3(256), 0, stream, rec,     \
+                               a_ptr, row0, nrows, n, S, part, ldp);                         \
         else if (kind == 10)                                                                 \
             hipLaunchKernelGGL((k_pair_rows<Dv, 0>), dim3(grid), dim3(256), 0, stream, xc, KP, \
                                nrm, n, nb, t0, t1, sc, sh, sd);                              \
@@ -902,7 +970,7 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
                                nrm, n, nb, t0, t1, sc, sh, sd);                              \
         break;
 
-static hipError_t launch_rows_kernel(int kind, int D, int grid, const double *rec,
+static hipError_t launch_rows_kernel(int kind, int D, int R, int grid, const double *rec,
                                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t n,
                                      int S, double *part, int64_t ldp, const double *xc, int KP,
                                      const double *nrm, int64_t nb, int64_t t0, int64_t t1,
@@ -942,13 +1010,13 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
     return hipGetLastError();
 }
 
-hipError_t launch_phi_rows(int d, const double *rec, const double *a_ptr, int64_t row0,
+hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr, int64_t row0,
                            int64_t nrows, int64_t n, int S, double *part, int64_t ldp,
                            double inv_n, double *phi, hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
-    const int grid = (int)(((nrows + 511) / 512) * S);
-    hipError_t e = launch_rows_kernel(0, d, grid, rec, a_ptr, row0, nrows, n, S, part, ldp,
+    const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
+    hipError_t e = launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp,
                                       nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
                                       SinkDebug{}, stream);
     if (e != hipSuccess) return e;
@@ -969,7 +1037,7 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
     SinkCollect sc{st, regions, cap, counts, below};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n};
-    return launch_rows_kernel(10 + mode, d, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, xc,
+    return launch_rows_kernel(10 + mode, d, 1, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, xc,
                               KP, nrm, nb, t0, t1, sc, sh, sd, stream);
 }
 
@@ -1122,10 +1190,12 @@ namespace svgd_amd {
 
 #define SVGD_OCC_CASE(Dv)                                                                    \
     case Dv:                                                                                 \
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<Dv>, 256, 0);       \
+        e = R == 1   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<Dv, 1>, 256, 0) \
+            : R == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<Dv, 2>, 256, 0) \
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<Dv, 4>, 256, 0); \
         break;
 
-int phi_rows_blocks_per_cu(int d)
+int phi_rows_blocks_per_cu(int d, int R)
 {
     int nb = 0;
     hipError_t e = hipErrorInvalidValue;

@@ -47,26 +47,27 @@ def test_plan_rows_partition(n, world):
     assert all(r1 - r0 <= chunk for r0, r1 in spans)
 
 
-def _tiles(n, world, rank):
+def _tiles(n, world, rank, block=64):
     lib = C.lib()
-    T = lib.svgd_plan_pair_tiles(n, world, rank)
+    T = lib.svgd_plan_pair_tiles(n, block, world, rank)
     out = []
     I, J = ctypes.c_int64(), ctypes.c_int64()
     for t in range(T):
-        lib.svgd_plan_pair_tile(n, world, rank, t, ctypes.byref(I), ctypes.byref(J))
+        lib.svgd_plan_pair_tile(n, block, world, rank, t, ctypes.byref(I), ctypes.byref(J))
         out.append((I.value, J.value))
     return out
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 128, 129, 300, 640, 1000])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 128, 129, 300, 640, 1000, 3000])
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_plan_pair_tiles_cover_each_pair_once(n, world):
+@pytest.mark.parametrize("block", [64, 256])
+def test_plan_pair_tiles_cover_each_pair_once(n, world, block):
     """Every unordered particle pair i<j is in exactly one tile of one rank."""
-    nb = -(-n // 64)
+    nb = -(-n // block)
     seen = np.zeros((nb, nb), dtype=int)
     counts = []
     for r in range(world):
-        t = _tiles(n, world, r)
+        t = _tiles(n, world, r, block)
         counts.append(len(t))
         for I, J in t:
             if I == J:
