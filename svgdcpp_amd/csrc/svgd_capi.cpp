@@ -225,7 +225,7 @@ int allreduce_cnt3(svgd_ctx *c)
 int center(svgd_ctx *c)
 {
     HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
-                                 c->nrm, c->stream));
+                                 c->nrm, c->rowpath ? 1 : 0, c->stream));
     return SVGD_OK;
 }
 
@@ -305,7 +305,8 @@ int median_begin(svgd_ctx *c)
             CHK(dalloc(c, &c->sample_keys, S));
             c->sample_alloc = S;
         }
-        HIPCHK(c, launch_sample_keys(c->xc, c->nrm, n, c->KP, S, c->sample_keys, c->stream));
+        HIPCHK(c, launch_sample_keys(c->xc, c->nrm, n, c->dim, c->KP, S, c->sample_keys,
+                                     c->stream));
         // sample ranks bracketing the target quantiles (6 sigma)
         const double qlo = (double)c->sel_rank[0] / (double)M;
         const double qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;
@@ -498,6 +499,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Only the F64 device path is built.");
     if (!pick_tiles(dim, &c->KP, &c->NCB))
         return fail(c, SVGD_ERR_DIM, "[Dimension Error] Device path supports dimension <= 64.");
+    // row-stream path: xc rows are the median records [xc | |xc|^2 | 0..]
+    if (dim <= ROWS_MAX_D) c->KP = med_rec_stride(dim);
     c->dim = dim;
     c->n = n;
     c->dtype = dtype;
@@ -539,7 +542,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         int64_t S = std::max<int64_t>(1, (resident + iblocks - 1) / iblocks);
         S = std::min<int64_t>(S, std::max<int64_t>(1, n / 256));
         c->S = (int)S;
-        c->RS = 2 * dim + 2;
+        c->RS = phi_rec_stride(dim);
         c->ldp = std::max<int64_t>(1, c->nrows);
         CHK(dalloc(c, &c->rec, c->np * c->RS));
         CHK(dalloc(c, &c->part, (int64_t)c->S * c->ldp * (dim + 1)));

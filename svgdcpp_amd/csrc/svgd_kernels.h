@@ -24,9 +24,11 @@ struct SelState {
     int32_t pad_;
 };
 
+// xc = X - mean (stride KP, zero padded), nrm = |xc|^2; nrm_in_slot also
+// stores |xc|^2 at xc[j*KP + d] (the row-stream median record).
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
-                              hipStream_t stream);
+                              int nrm_in_slot, hipStream_t stream);
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);
@@ -45,8 +47,8 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
                              int64_t cap, uint32_t *counts, unsigned long long *below,
                              const SelState *st, uint32_t *ghist, double *dbg_out,
                              hipStream_t stream);
-hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int KP, int64_t S,
-                              uint64_t *keys, hipStream_t stream);
+hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int d, int KP,
+                              int64_t S, uint64_t *keys, hipStream_t stream);
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                int64_t cap, int parts, const SelState *st, uint32_t *ghist,
                                hipStream_t stream);
@@ -56,9 +58,13 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
                                 hipStream_t stream);
 hipError_t launch_bracket(SelState *st, hipStream_t stream);
 
-// Row-stream path (d <= 16): particle records rec_j = [xc_j, c_j, G_j - 2a xc_j, pad],
-// stride 2d+2.  phi partials over S column splits -> part[S][ldp][d+1].
+// Row-stream path (d <= 16): particle records rec_j = [xc_j | G_j - 2a xc_j | c_j | 0..],
+// stride phi_rec_stride(d).  phi partials over S column splits -> part[S][ldp][d+1].
 constexpr int ROWS_MAX_D = 16;
+// record strides (doubles) of the row-stream path: phi records
+// [xc | G - 2a xc | c | 0..] and median records [xc | |xc|^2 | 0..]
+constexpr int phi_rec_stride(int d) { return ((2 * d + 1 + 7) / 8) * 8; }
+constexpr int med_rec_stride(int d) { return ((d + 1 + 3) / 4) * 4; }
 hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
                            double *rec, hipStream_t stream);

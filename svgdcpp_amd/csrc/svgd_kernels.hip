@@ -88,7 +88,7 @@ __global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
 // so it is bit-identical on every rank and block.
 __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
                          const double *__restrict__ partial, int nparts, int64_t np,
-                         double *__restrict__ xc, double *__restrict__ nrm)
+                         double *__restrict__ xc, double *__restrict__ nrm, int nrm_in_slot)
 {
     __shared__ double mu[256];
     for (int k = threadIdx.x; k < d; k += blockDim.x) {
@@ -106,6 +106,7 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
             s = fma(v, v, s);
         }
         nrm[j] = s;
+        if (KP > d && nrm_in_slot) xc[j * KP + d] = s; // median record [xc | |xc|^2 | 0..]
     }
 }
 
@@ -451,7 +452,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
 }
 
 __global__ void k_sample_keys(const double *__restrict__ xc, const double *__restrict__ nrm,
-                              int64_t n, int KP, int64_t S, uint64_t *__restrict__ keys)
+                              int64_t n, int d, int KP, int64_t S, uint64_t *__restrict__ keys)
 {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S;
          g += (int64_t)gridDim.x * blockDim.x) {
@@ -459,7 +460,7 @@ __global__ void k_sample_keys(const double *__restrict__ xc, const double *__res
         const int64_t i = (int64_t)(h % (uint64_t)n);
         const int64_t j = (i + 1 + (int64_t)((h >> 32) % (uint64_t)(n - 1))) % n;
         double dot = 0.0;
-        for (int k = 0; k < KP; ++k) dot = fma(xc[i * KP + k], xc[j * KP + k], dot);
+        for (int k = 0; k < d; ++k) dot = fma(xc[i * KP + k], xc[j * KP + k], dot);
         keys[g] = key_of(fmax(fma(-2.0, dot, nrm[i] + nrm[j]), 0.0));
     }
 }
@@ -660,10 +661,34 @@ __device__ __forceinline__ double exp2_32(double u, const double *tab)
     return __builtin_ldexp(p * tab[ki & 31], ki >> 5);
 }
 
-// rec_j = [xc_j (D), c_j = -32 a log2e |xc_j|^2, V_j = G_j - 2a xc_j (D), pad]
+constexpr int CH_PHI = 16; // columns per LDS chunk of the phi row stream
+
+// rec_j = [xc_j (D) | V_j = G_j - 2a xc_j (D) | c_j = -32 a log2e |xc_j|^2 | 0 ...],
+// stride phi_rec_stride(D) = roundup(2D+1, 8) doubles, so CH_PHI records are
+// a whole number of 1 KiB LDS-DMA pieces.
 template <int D> struct RecLayout {
-    static constexpr int RS = 2 * D + 2;
+    static constexpr int RS = phi_rec_stride(D);
 };
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+// Copy BYTES (multiple of 1 KiB) from global to this wave's LDS buffer with
+// global_load_lds_dwordx4 (one 1 KiB piece per wave instruction; counted by
+// vmcnt, no VGPR destination).
+template <int BYTES>
+__device__ __forceinline__ void dma_to_lds(const char *gsrc, char *ldst, int lane)
+{
+#pragma unroll
+    for (int p = 0; p < BYTES / 1024; ++p)
+        __builtin_amdgcn_global_load_lds((gbl_void *)(gsrc + p * 1024 + lane * 16),
+                                         (lds_void *)(ldst + p * 1024), 16, 0, 0);
+}
+
+template <int N> __device__ __forceinline__ void wait_vmcnt()
+{
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restrict__ G,
                            const double *__restrict__ nrm, const double *__restrict__ a_ptr,
@@ -677,10 +702,10 @@ __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restri
         for (int k = 0; k < d; ++k) {
             const double x = live ? xc[j * KP + k] : 0.0;
             r[k] = x;
-            r[d + 1 + k] = live ? G[j * d + k] - 2.0 * a * x : 0.0;
+            r[d + k] = live ? G[j * d + k] - 2.0 * a * x : 0.0;
         }
-        r[d] = live ? -32.0 * a * LOG2E * nrm[j] : 0.0;
-        r[RS - 1] = 0.0;
+        r[2 * d] = live ? -32.0 * a * LOG2E * nrm[j] : 0.0;
+        for (int k = 2 * d + 1; k < RS; ++k) r[k] = 0.0;
     }
 }
 
@@ -691,11 +716,16 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
                                                  double *__restrict__ part, int64_t ldp)
 {
     constexpr int RS = RecLayout<D>::RS;
-    __shared__ double tab[32];
+    constexpr int CHB = CH_PHI * RS * 8; // bytes per column chunk (multiple of 1 KiB)
+    // per-wave double-buffered column chunks, then the 2^(k/32) table
+    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + 32 * 8];
+    double *tab = reinterpret_cast<double *>(smem + 4 * 2 * CHB);
     if (threadIdx.x < 32) tab[threadIdx.x] = EXP2_TAB32[threadIdx.x];
     __syncthreads();
 
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    char *wbuf = smem + w * 2 * CHB;
     const int64_t iblk = blockIdx.x / S;
     const int s = (int)(blockIdx.x - iblk * S);
     const int64_t rbase = iblk * (256 * R) + w * (64 * R); // local row of this wave's lane 0
@@ -712,49 +742,46 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
             xi[r][k] = ri[k];
             acc[r][k] = 0.0;
         }
-        ci[r] = ri[D];
+        ci[r] = ri[2 * D];
         acc1[r] = 0.0;
     }
 
+    // Column records stream through two LDS chunk buffers: the DMA of chunk
+    // c+1 is in flight (vmcnt) while chunk c is computed; every lane reads the
+    // same record (LDS broadcast).  rec has >= 64 padded rows past n, so whole
+    // chunks may be copied.
     const int64_t j0 = n * s / S, j1 = n * (s + 1) / S;
-    // software pipeline: the record of column j+1 is loaded (scalar loads,
-    // wave-uniform) while column j is computed
-    double xn[D], vn[D], cn;
-    {
-        const double *rj = rec + j0 * RS;
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            xn[k] = rj[k];
-            vn[k] = rj[D + 1 + k];
+    const int64_t nch = (j1 - j0 + CH_PHI - 1) / CH_PHI;
+    const char *gcol = reinterpret_cast<const char *>(rec + j0 * RS);
+    if (nch > 0) dma_to_lds<CHB>(gcol, wbuf, lane);
+    for (int64_t c = 0; c < nch; ++c) {
+        if (c + 1 < nch) {
+            dma_to_lds<CHB>(gcol + (c + 1) * CHB, wbuf + ((c + 1) & 1) * CHB, lane);
+            wait_vmcnt<CHB / 1024>();
+        } else {
+            wait_vmcnt<0>();
         }
-        cn = rj[D];
-    }
-    for (int64_t j = j0; j < j1; ++j) {
-        double xj[D], vj[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            xj[k] = xn[k];
-            vj[k] = vn[k];
-        }
-        const double cj = cn;
-        {
-            const double *rj = rec + (j + 1 < j1 ? j + 1 : j) * RS;
+        const double *cb = reinterpret_cast<const double *>(wbuf + (c & 1) * CHB);
+        const int cnt = (int)min<int64_t>(CH_PHI, j1 - j0 - c * CH_PHI);
+        for (int jj = 0; jj < cnt; ++jj) {
+            const double *rj = cb + jj * RS;
+            double xj[D], vj[D];
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                xn[k] = rj[k];
-                vn[k] = rj[D + 1 + k];
+                xj[k] = rj[k];
+                vj[k] = rj[D + k];
             }
-            cn = rj[D];
-        }
+            const double cj = rj[2 * D];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            double dot = xi[r][0] * xj[0];
+            for (int r = 0; r < R; ++r) {
+                double dot = xi[r][0] * xj[0];
 #pragma unroll
-            for (int k = 1; k < D; ++k) dot = fma(xi[r][k], xj[k], dot);
-            const double K = exp2_32(fma(alpha, dot, ci[r] + cj), tab);
+                for (int k = 1; k < D; ++k) dot = fma(xi[r][k], xj[k], dot);
+                const double K = exp2_32(fma(alpha, dot, ci[r] + cj), tab);
 #pragma unroll
-            for (int k = 0; k < D; ++k) acc[r][k] = fma(K, vj[k], acc[r][k]);
-            acc1[r] += K;
+                for (int k = 0; k < D; ++k) acc[r][k] = fma(K, vj[k], acc[r][k]);
+                acc1[r] += K;
+            }
         }
     }
 
@@ -797,19 +824,31 @@ __global__ void k_phi_reduce(const double *__restrict__ part, const double *__re
 // k_sample_keys).  MODE 0 collect, 1 histogram (fallback), 2 debug dump.
 constexpr int PR = 4;     // rows per lane of the median sweep
 constexpr int PBLK = 256; // = 64 * PR: tile block of the row-stream median plan
+constexpr int CH_MED = 32; // columns per LDS chunk of the median stream
+
+struct TileIt {
+    int64_t t, I, J, slot;
+    int c;
+};
 
 template <int D, int MODE>
-__global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc, int KP,
+__global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
                                                   const double *__restrict__ nrm, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
 {
+    constexpr int KPM = med_rec_stride(D);
+    constexpr int CHB = CH_MED * KPM * 8; // bytes per column chunk (multiple of 1 KiB)
+    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB];
     __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
     __shared__ uint32_t sCnt;
     __shared__ unsigned long long sBelow[4];
     const int tid = threadIdx.x, lane = tid & 63;
-    // wave index made provably uniform so the column stream uses scalar loads
+    // wave index made provably uniform (wave-uniform tile walk)
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    char *wbuf = smem + w * 2 * CHB;
+    (void)kp_arg;           // == KPM: median records [xc | |xc|^2 | 0..]
+    constexpr int KP = KPM; // record stride (doubles)
 
     int nsel = 0, shift = 0, hsh = 63;
     uint64_t pfx0 = 0, pfx1 = 0, lo_key = 0, hi_key = 0;
@@ -839,15 +878,45 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
 
     if (tb < te) {
         const int64_t H = (nb - 1) / 2;
-        int64_t I, J;
-        tile_coords(nb, tb, &I, &J);
-        int64_t slot = (J - I + nb) % nb;
+        // flat stream of (tile, 32-column chunk) items; the DMA of item q+1
+        // into this wave's other LDS buffer overlaps the compute of item q
+        TileIt it;
+        tile_coords(nb, tb, &it.I, &it.J);
+        it.t = tb;
+        it.slot = (it.J - it.I + nb) % nb;
+        it.c = 0;
+        auto advance = [&](TileIt &x) {
+            const int64_t jb = x.J * PBLK, je = min(jb + PBLK, n);
+            if (++x.c * CH_MED < je - jb) return;
+            x.c = 0;
+            ++x.t;
+            ++x.slot;
+            const int64_t cntI = ((nb & 1) == 0 && x.I < nb / 2) ? H + 2 : H + 1;
+            if (x.slot == cntI) {
+                ++x.I;
+                x.slot = 0;
+            }
+            x.J = x.slot == 0 ? x.I : (x.I + x.slot) % nb;
+        };
+        auto src = [&](const TileIt &x) {
+            return reinterpret_cast<const char *>(xc + (x.J * PBLK + x.c * CH_MED) * KP);
+        };
+        dma_to_lds<CHB>(src(it), wbuf, lane);
         int64_t curI = -1;
         double xi[PR][D], ni[PR];
         int64_t irow[PR];
         bool ivalid[PR];
         unsigned long long vmask[PR];
-        for (int64_t t = tb; t < te; ++t) {
+        for (int q = 0; it.t < te; ++q) {
+            TileIt nx = it;
+            advance(nx);
+            if (nx.t < te) {
+                dma_to_lds<CHB>(src(nx), wbuf + ((q + 1) & 1) * CHB, lane);
+                wait_vmcnt<CHB / 1024>();
+            } else {
+                wait_vmcnt<0>();
+            }
+            const int64_t I = it.I, J = it.J;
             if (I != curI) {
 #pragma unroll
                 for (int r = 0; r < PR; ++r) {
@@ -857,28 +926,20 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
                     const int64_t ic = ivalid[r] ? irow[r] : n - 1;
 #pragma unroll
                     for (int k = 0; k < D; ++k) xi[r][k] = xc[ic * KP + k];
-                    ni[r] = nrm[ic];
+                    ni[r] = xc[ic * KP + D];
                 }
                 curI = I;
             }
             const bool diag = I == J;
-            const int64_t jb = J * PBLK, je = min(jb + PBLK, n);
-            // prefetched wave-uniform column record (scalar loads)
-            double xn[D], nn;
-#pragma unroll
-            for (int k = 0; k < D; ++k) xn[k] = xc[jb * KP + k];
-            nn = nrm[jb];
-            for (int64_t j = jb; j < je; ++j) {
+            const int64_t jb = J * PBLK + it.c * CH_MED;
+            const int cnt = (int)min<int64_t>(CH_MED, n - jb);
+            const double *cb = reinterpret_cast<const double *>(wbuf + (q & 1) * CHB);
+            for (int jj = 0; jj < cnt; ++jj) {
+                const int64_t j = jb + jj;
                 double xj[D];
 #pragma unroll
-                for (int k = 0; k < D; ++k) xj[k] = xn[k];
-                const double nj = nn;
-                {
-                    const int64_t jn = j + 1 < je ? j + 1 : j;
-#pragma unroll
-                    for (int k = 0; k < D; ++k) xn[k] = xc[jn * KP + k];
-                    nn = nrm[jn];
-                }
+                for (int k = 0; k < D; ++k) xj[k] = cb[jj * KP + k]; // LDS broadcast
+                const double nj = cb[jj * KP + D];
 #pragma unroll
                 for (int r = 0; r < PR; ++r) {
                     double dot = xi[r][0] * xj[0];
@@ -921,14 +982,7 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
                     }
                 }
             }
-            // next tile of the plan (incremental tile_coords)
-            ++slot;
-            const int64_t cntI = ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
-            if (slot == cntI) {
-                ++I;
-                slot = 0;
-            }
-            J = slot == 0 ? I : (I + slot) % nb;
+            it = nx;
         }
     }
 
@@ -1023,7 +1077,7 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
     int64_t g = (nrows + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
-                       d, 2 * d + 2, S, ldp, inv_n, phi);
+                       d, phi_rec_stride(d), S, ldp, inv_n, phi);
     return hipGetLastError();
 }
 
@@ -1102,13 +1156,13 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
 
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
-                              hipStream_t stream)
+                              int nrm_in_slot, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial);
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_center, dim3(g), dim3(256), 0, stream, X, n, d, KP, partial, nparts, np,
-                       xc, nrm);
+                       xc, nrm, nrm_in_slot);
     return hipGetLastError();
 }
 
@@ -1136,12 +1190,12 @@ hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, do
     return hipGetLastError();
 }
 
-hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int KP, int64_t S,
-                              uint64_t *keys, hipStream_t stream)
+hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int d, int KP,
+                              int64_t S, uint64_t *keys, hipStream_t stream)
 {
     int64_t g = (S + 255) / 256;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, KP, S, keys);
+    hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, d, KP, S, keys);
     return hipGetLastError();
 }
 
