@@ -1,6 +1,7 @@
 # Top-level build of the MI355X (gfx950) SVGD library and test/bench helpers.
 #   make            -> svgdcpp_amd/libsvgdcpp_amd.so (HIP kernels + C ABI, links RCCL)
 #   make oracle     -> oracle/liboracle.so (CPU restatement; test infrastructure)
+#   make cpp        -> build/{mvn_example,gmm_example,test_api} (SVGDCpp-compatible C++ API)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
@@ -30,8 +31,24 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# C++ programs over the SVGDCpp-compatible headers (include/Core, Model, Kernel, Optimizer)
+CPP_FLAGS := -O2 -std=c++17 -Wall -Iinclude
+CPP_LINK := -Lsvgdcpp_amd -lsvgdcpp_amd -Wl,-rpath,'$$ORIGIN/../svgdcpp_amd' -Wl,--allow-shlib-undefined
+CPP_HDRS := $(wildcard include/SVGDCpp/*.hpp include/SVGDCpp/*/*.hpp) include/Core include/Model include/Kernel include/Optimizer
+CPP_BINS := build/mvn_example build/gmm_example build/test_api
+
+cpp: $(CPP_BINS)
+
+build/%: examples/%.cpp $(CPP_HDRS) $(LIB)
+	@mkdir -p build
+	$(CXX) $(CPP_FLAGS) $< -o $@ $(CPP_LINK)
+
+build/test_api: tests/cpp/test_api.cpp $(CPP_HDRS) $(LIB)
+	@mkdir -p build
+	$(CXX) $(CPP_FLAGS) $< -o $@ $(CPP_LINK)
+
 clean:
-	rm -f $(OBJS) $(LIB)
+	rm -f $(OBJS) $(LIB) $(CPP_BINS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle cpp clean

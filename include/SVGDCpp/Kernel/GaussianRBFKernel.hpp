@@ -1,0 +1,131 @@
+/**
+ * @file GaussianRBFKernel.hpp
+ * @brief Gaussian RBF kernel (reference: include/SVGDCpp/Kernel/GaussianRBFKernel.hpp:22-270).
+ *
+ * k(x, x') = exp(-(x - x')^T M (x - x')) with M = a I (:75-81).
+ *   ScaleMethod::Median   a = ln(N) / med^2, med = median of all N^2 pairwise
+ *                         distances of the coordinate matrix (:168-188) --
+ *                         recomputed every step ON THE DEVICE by the SVGD driver.
+ *   ScaleMethod::Hessian  (:189-210) not on the device path (throws).
+ *   ScaleMethod::Constant extension (the reference's "TODO: constant scale"):
+ *                         a fixed M = a I set by UpdateParameters({a * I}).
+ * The host methods below (ComputeScale, EvaluateKernel/Grad) restate the
+ * kernel for callers that use it directly; SVGD does not call them.
+ */
+#ifndef SVGDCPP_AMD_GAUSSIAN_RBF_KERNEL_HPP
+#define SVGDCPP_AMD_GAUSSIAN_RBF_KERNEL_HPP
+
+#include "../Core.hpp"
+#include "../Model/Model.hpp"
+#include "Kernel.hpp"
+
+class GaussianRBFKernel : public Kernel
+{
+public:
+    enum class ScaleMethod
+    {
+        Median = 0,
+        Hessian = 1,
+        Constant = 2
+    };
+
+    GaussianRBFKernel() {}
+
+    /** :47-88 */
+    GaussianRBFKernel(const std::shared_ptr<Eigen::MatrixXd> &coord_mat_ptr, const ScaleMethod &method = ScaleMethod::Median,
+                      const std::shared_ptr<Model> &model_ptr = nullptr)
+        : Kernel((size_t)coord_mat_ptr->rows()), scale_method_(method), coord_matrix_ptr_(coord_mat_ptr),
+          target_model_ptr_(model_ptr)
+    {
+        if (scale_method_ == ScaleMethod::Hessian && !model_ptr)
+            throw UnsetException("Hessian-based scale requires a model.");
+        if (scale_method_ == ScaleMethod::Hessian)
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
+                                        "[Argument error] Hessian scale method is not on the device path.");
+        // The reference computes the median scale here (:84) and again in every
+        // Step() before it is used (SVGD.hpp:389); the device recomputes it per
+        // step, so no O(N^2) host work happens at construction.
+        kernel_parameters_ = {Eigen::MatrixXd::Identity(dimension_, dimension_)};
+    }
+
+    std::unique_ptr<Kernel> CloneUniquePointer() const override { return std::make_unique<GaussianRBFKernel>(*this); }
+    std::shared_ptr<Kernel> CloneSharedPointer() const override { return std::make_shared<GaussianRBFKernel>(*this); }
+
+    ScaleMethod GetScaleMethod() const { return scale_method_; }
+
+    /** a of M = a I (the device path supports isotropic scales only). */
+    double GetScale() const
+    {
+        const Eigen::MatrixXd &M = kernel_parameters_.at(0);
+        return M(0, 0);
+    }
+
+    void UpdateParameters(const std::vector<Eigen::MatrixXd> &params) override
+    {
+        const Eigen::MatrixXd &M = params.at(0);
+        if (M.rows() != dimension_ || M.cols() != dimension_)
+            throw DimensionMismatchException("Kernel scale matrix has incorrect dimensions.");
+        for (long r = 0; r < M.rows(); ++r)
+            for (long c = 0; c < M.cols(); ++c)
+                if (M(r, c) != (r == c ? M(0, 0) : 0.0))
+                    throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
+                                                "[Argument Error] Only isotropic scales M = a I are supported.");
+        kernel_parameters_ = {M};
+    }
+
+    /** exp(-a |x - location|^2) */
+    double EvaluateKernel(const Eigen::VectorXd &x) override
+    {
+        const double a = GetScale();
+        double s = 0.0;
+        for (long k = 0; k < dimension_; ++k)
+            s += (-(x(k) - location_(k)) * a) * (x(k) - location_(k));
+        return std::exp(s);
+    }
+
+    /** -2 a (x - location) k(x, location) */
+    Eigen::VectorXd EvaluateKernelGrad(const Eigen::VectorXd &x) override
+    {
+        const double a = GetScale(), kv = EvaluateKernel(x);
+        Eigen::VectorXd g(dimension_);
+        for (long k = 0; k < dimension_; ++k)
+            g(k) = -2.0 * a * (x(k) - location_(k)) * kv;
+        return g;
+    }
+
+    /** :141-156 -- host restatement; the SVGD driver computes the scale on the device. */
+    void Step() override
+    {
+        if (scale_method_ == ScaleMethod::Median)
+            kernel_parameters_[0] = ComputeScale();
+    }
+
+    /** :164-188 Median heuristic on the host (O(N^2) memory, small N only). */
+    Eigen::MatrixXd ComputeScale()
+    {
+        const Eigen::MatrixXd &X = *coord_matrix_ptr_;
+        const long n = X.cols(), d = X.rows();
+        std::vector<double> dist((size_t)(n * n));
+        for (long j = 0; j < n; ++j)
+            for (long i = 0; i < n; ++i)
+            {
+                double s = 0.0;
+                for (long k = 0; k < d; ++k)
+                    s += (X(k, i) - X(k, j)) * (X(k, i) - X(k, j));
+                dist[(size_t)(j * n + i)] = std::sqrt(s);
+            }
+        const size_t h = dist.size() / 2;
+        std::nth_element(dist.begin(), dist.begin() + (long)h, dist.end());
+        double med = dist[h];
+        if (dist.size() % 2 == 0)
+            med = (med + *std::max_element(dist.begin(), dist.begin() + (long)h)) / 2.0;
+        return std::log((double)n) / std::pow(med, 2) * Eigen::MatrixXd::Identity(d, d);
+    }
+
+protected:
+    ScaleMethod scale_method_ = ScaleMethod::Median;
+    std::shared_ptr<Eigen::MatrixXd> coord_matrix_ptr_;
+    std::shared_ptr<Model> target_model_ptr_;
+};
+
+#endif

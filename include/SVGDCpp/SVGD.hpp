@@ -1,0 +1,281 @@
+/**
+ * @file SVGD.hpp
+ * @brief SVGD driver on the MI355X path (reference: include/SVGDCpp/SVGD.hpp:27-511).
+ *
+ * Same options struct, constructors, checks, messages and Initialize/Run
+ * flow as the reference.  Each Step() (SVGD.hpp:373-400) runs on the GPU
+ * through the C ABI (svgdcpp_amd/svgd_capi.h):
+ *
+ *   svgd_begin_step    median-heuristic scale of X_t (GaussianRBFKernel.hpp:141-188)
+ *                      while X_t is copied to the host
+ *   host               G = grad log p(X_t) from the Model plugin (Model.hpp:335)
+ *   svgd_finish_step   phi_hat (SVGD.hpp:407-454), optimizer increment, clamp (:393-399)
+ *
+ * The coordinate matrix stays on the device during Run() and is written back
+ * to *CoordinateMatrixPtr at the end (the reference mutates it every step).
+ * Requirements of the device path: the kernel is a GaussianRBFKernel
+ * (Median or Constant scale) and the optimizer is Adam, AdaGrad or RMSProp.
+ * LogIntermediateMatrices re-evaluates K and Kg on the host from the step's
+ * scale (debug aid for small N, same text format as SVGD.hpp:345-365).
+ */
+#ifndef SVGDCPP_AMD_SVGD_HPP
+#define SVGDCPP_AMD_SVGD_HPP
+
+#include <fstream>
+#include <sstream>
+
+#include "Core.hpp"
+#include "Kernel/GaussianRBFKernel.hpp"
+#include "Kernel/Kernel.hpp"
+#include "Model/Model.hpp"
+#include "Optimizer/Optimizer.hpp"
+
+/** SVGD.hpp:27-52 (+ Device: HIP device index of the context). */
+struct SVGDOptions
+{
+    size_t Dimension;
+    size_t NumIterations;
+    std::shared_ptr<Eigen::MatrixXd> CoordinateMatrixPtr = nullptr;
+    std::shared_ptr<Kernel> KernelPtr = nullptr;
+    std::shared_ptr<Model> ModelPtr = nullptr;
+    std::shared_ptr<Optimizer> OptimizerPtr = nullptr;
+    Eigen::VectorXd LowerBound = Eigen::VectorXd::Constant(1, -INFINITY);
+    Eigen::VectorXd UpperBound = Eigen::VectorXd::Constant(1, INFINITY);
+    std::string IntermediateMatricesOutputPath = "log.txt";
+    bool Parallel = false;
+    bool LogIntermediateMatrices = false;
+    int Device = 0;
+    SVGDOptions() {}
+};
+
+class SVGD
+{
+public:
+    SVGD(const SVGDOptions &o)
+        : SVGD(o.Dimension, o.NumIterations, o.CoordinateMatrixPtr, o.KernelPtr, o.ModelPtr, o.OptimizerPtr,
+               o.LowerBound, o.UpperBound, o.Parallel, o.LogIntermediateMatrices, o.IntermediateMatricesOutputPath,
+               o.Device)
+    {
+    }
+
+    SVGD(const size_t &dim, const size_t &iter, const std::shared_ptr<Eigen::MatrixXd> &coord_mat_ptr,
+         const std::shared_ptr<Kernel> &kernel_ptr, const std::shared_ptr<Model> &model_ptr,
+         const std::shared_ptr<Optimizer> &optimizer_ptr, const bool &parallel = false)
+        : SVGD(dim, iter, coord_mat_ptr, kernel_ptr, model_ptr, optimizer_ptr, Eigen::VectorXd::Constant(1, -INFINITY),
+               Eigen::VectorXd::Constant(1, INFINITY), parallel)
+    {
+    }
+
+    SVGD(const size_t &dim, const size_t &iter, const std::shared_ptr<Eigen::MatrixXd> &coord_mat_ptr,
+         const std::shared_ptr<Kernel> &kernel_ptr, const std::shared_ptr<Model> &model_ptr,
+         const std::shared_ptr<Optimizer> &optimizer_ptr, const Eigen::VectorXd &bound_lower,
+         const Eigen::VectorXd &bound_upper, const bool &parallel = false, const bool &log_intermediate_matrices = false,
+         const std::string &intermediate_matrices_output_path = "log.txt", int device = 0)
+        : dimension_((int)coord_mat_ptr->rows()), num_iterations_(iter), parallel_(parallel),
+          log_intermediate_matrices_(log_intermediate_matrices),
+          intermediate_matrices_output_path_(intermediate_matrices_output_path)
+    {
+        if ((size_t)dimension_ != dim) // SVGD.hpp:170-173
+            throw DimensionMismatchException("Specified dimension does not match the particle coordinate matrix.");
+        coord_matrix_ptr_ = coord_mat_ptr;
+        num_particles_ = coord_mat_ptr->cols();
+
+        // SVGD.hpp:184-216: bounds enabled unless both are the default 1-row +-inf
+        if (bound_lower.rows() == 1 && bound_lower(0) == -INFINITY && bound_upper.rows() == 1 &&
+            bound_upper(0) == INFINITY)
+        {
+            check_bounds_ = false;
+        }
+        else
+        {
+            if (bound_lower.rows() != dimension_ && bound_lower.rows() != 1)
+                throw DimensionMismatchException("The provided lower bounds have incorrect dimensions.");
+            std::cout << SVGDCPP_LOG_PREFIX + "Bound checking enabled, lower bound set to " << bound_lower.transpose()
+                      << "." << std::endl;
+            if (bound_upper.rows() != dimension_ && bound_upper.rows() != 1)
+                throw DimensionMismatchException("The provided upper bounds have incorrect dimensions.");
+            std::cout << SVGDCPP_LOG_PREFIX + "Bound checking enabled, upper bound set to " << bound_upper.transpose()
+                      << "." << std::endl;
+            check_bounds_ = true;
+            lower_.assign((size_t)dimension_, 0.0);
+            upper_.assign((size_t)dimension_, 0.0);
+            for (int k = 0; k < dimension_; ++k)
+            {
+                lower_[(size_t)k] = bound_lower(bound_lower.rows() == 1 ? 0 : k);
+                upper_[(size_t)k] = bound_upper(bound_upper.rows() == 1 ? 0 : k);
+            }
+        }
+
+        kernel_ptr_ = kernel_ptr;
+        model_ptr_ = model_ptr;
+        optimizer_ptr_ = optimizer_ptr;
+        if (kernel_ptr_ == nullptr) // SVGD.hpp:223-236
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX + "[Argument Error] Invalid Kernel object pointer.");
+        if (model_ptr_ == nullptr)
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX + "[Argument Error] Invalid Model object pointer.");
+        if (optimizer_ptr_ == nullptr)
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX + "[Argument Error] Invalid Optimizer object pointer.");
+        rbf_ptr_ = std::dynamic_pointer_cast<GaussianRBFKernel>(kernel_ptr_);
+        if (!rbf_ptr_)
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
+                                        "[Argument Error] The device path requires a GaussianRBFKernel.");
+        if (optimizer_ptr_->Kind() < 0)
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
+                                        "[Argument Error] The device path requires Adam, AdaGrad or RMSProp.");
+
+        svgd_ctx *c = nullptr;
+        const int rc = svgd_create(&c, dimension_, (int64_t)num_particles_, SVGD_F64, device);
+        ctx_.reset(c, [](svgd_ctx *p) { svgd_destroy(p); });
+        Check(rc);
+    }
+
+    SVGD(const SVGD &) = delete;
+    ~SVGD() {}
+
+    /** SVGD.hpp:268-296 */
+    void Initialize()
+    {
+        model_ptr_->Initialize();
+        kernel_ptr_->Initialize();
+        optimizer_ptr_->Initialize();
+        ConfigureDevice();
+        if (log_intermediate_matrices_)
+        {
+            intermediate_matrices_sstream_vector_.clear();
+            intermediate_matrices_sstream_vector_.resize(num_iterations_);
+        }
+        initialized_ = true;
+    }
+
+    /** SVGD.hpp:304-320 */
+    void UpdateKernelParameters(const std::vector<Eigen::MatrixXd> &params)
+    {
+        kernel_ptr_->UpdateParameters(params);
+        kernel_ptr_->Initialize();
+        ConfigureScale();
+    }
+
+    /** SVGD.hpp:328-332 */
+    void UpdateModelParameters(const std::vector<Eigen::MatrixXd> &params)
+    {
+        model_ptr_->UpdateParameters(params);
+        model_ptr_->Initialize();
+    }
+
+    /** SVGD.hpp:338-366 */
+    void Run()
+    {
+        if (!initialized_)
+            throw UnsetException("SVGD::Initialize must be called before Run.");
+        svgd_ctx *c = ctx_.get();
+        Check(svgd_set_particles(c, coord_matrix_ptr_->data()));
+        double *hx = nullptr, *hg = nullptr;
+        Check(svgd_host_buffers(c, &hx, &hg));
+        for (size_t iter = 0; iter < num_iterations_; ++iter)
+        {
+            Step(hx, hg);
+            if (log_intermediate_matrices_)
+                LogStep(iter, hx, hg);
+        }
+        Check(svgd_get_particles(c, coord_matrix_ptr_->data()));
+        double a = 0.0;
+        Check(svgd_last_scale(c, &a, nullptr, nullptr));
+        if (rbf_ptr_->GetScaleMethod() == GaussianRBFKernel::ScaleMethod::Median && num_iterations_ > 0)
+            rbf_ptr_->UpdateParameters({a * Eigen::MatrixXd::Identity(dimension_, dimension_)});
+        if (log_intermediate_matrices_)
+            WriteIntermediateMatricesToFile();
+    }
+
+    /** The context (for callers that need the C ABI directly). */
+    svgd_ctx *Context() const { return ctx_.get(); }
+
+protected:
+    /** SVGD.hpp:373-400 on the device; the model gradient stays on the host. */
+    void Step(double *hx, double *hg)
+    {
+        svgd_ctx *c = ctx_.get();
+        model_ptr_->Step();
+        Check(svgd_begin_step(c, hx));
+        model_ptr_->LogModelGradBatch(hx, (int64_t)num_particles_, hg);
+        Check(svgd_finish_step(c, hg));
+    }
+
+    void ConfigureDevice()
+    {
+        svgd_ctx *c = ctx_.get();
+        double p[4];
+        optimizer_ptr_->Params(p);
+        Check(svgd_set_optimizer(c, optimizer_ptr_->Kind(), p[0], p[1], p[2], p[3]));
+        Check(check_bounds_ ? svgd_set_bounds(c, lower_.data(), upper_.data()) : svgd_set_bounds(c, nullptr, nullptr));
+        ConfigureScale();
+    }
+
+    void ConfigureScale()
+    {
+        if (rbf_ptr_->GetScaleMethod() == GaussianRBFKernel::ScaleMethod::Constant)
+            Check(svgd_set_scale(ctx_.get(), SVGD_SCALE_FIXED, rbf_ptr_->GetScale()));
+        else
+            Check(svgd_set_scale(ctx_.get(), SVGD_SCALE_MEDIAN, 0.0));
+    }
+
+    /** SVGD.hpp:345-358 text format; K and Kg re-evaluated on the host. */
+    void LogStep(size_t iter, const double *hx, const double *hg)
+    {
+        const long n = (long)num_particles_, d = dimension_;
+        double a = 0.0;
+        Check(svgd_last_scale(ctx_.get(), &a, nullptr, nullptr));
+        Eigen::MatrixXd G(d, n), K(n, n), Kg(d * n, n), X(d, n);
+        std::copy(hg, hg + n * d, G.data());
+        for (long i = 0; i < n; ++i)
+            for (long j = 0; j < n; ++j)
+            {
+                double u = 0.0;
+                for (long k = 0; k < d; ++k)
+                    u += (-(hx[j * d + k] - hx[i * d + k]) * a) * (hx[j * d + k] - hx[i * d + k]);
+                const double kv = std::exp(u);
+                K(j, i) = kv;
+                for (long k = 0; k < d; ++k)
+                    Kg(j * d + k, i) = -2.0 * a * (hx[j * d + k] - hx[i * d + k]) * kv;
+            }
+        Check(svgd_get_particles(ctx_.get(), X.data()));
+        intermediate_matrices_sstream_vector_[iter] << "========== Step " << iter + 1 << " =========="
+                                                    << "\nLogModelGrad=\n" << G << "\n\nKernel=\n" << K
+                                                    << "\n\nKernelGrad=\n" << Kg << "\n\nCoordMat=\n" << X << "\n\n";
+    }
+
+    /** SVGD.hpp:460-476 */
+    void WriteIntermediateMatricesToFile()
+    {
+        std::ofstream output_file(intermediate_matrices_output_path_);
+        if (!output_file)
+            throw std::runtime_error(SVGDCPP_LOG_PREFIX + "[Runtime Error] Cannot open " +
+                                     intermediate_matrices_output_path_ + " for writing.");
+        for (const auto &ss : intermediate_matrices_sstream_vector_)
+            output_file << ss.str();
+    }
+
+    void Check(int rc) const
+    {
+        if (rc != SVGD_OK)
+            svgdcpp::ThrowFromCode(rc, svgd_last_error(ctx_.get()));
+    }
+
+    int dimension_ = -1;
+    size_t num_iterations_;
+    size_t num_particles_ = 0;
+    const bool parallel_ = false;
+    bool check_bounds_ = false;
+    bool log_intermediate_matrices_ = false;
+    bool initialized_ = false;
+    std::vector<double> lower_, upper_;
+    std::shared_ptr<Kernel> kernel_ptr_;
+    std::shared_ptr<GaussianRBFKernel> rbf_ptr_;
+    std::shared_ptr<Model> model_ptr_;
+    std::shared_ptr<Optimizer> optimizer_ptr_;
+    std::shared_ptr<Eigen::MatrixXd> coord_matrix_ptr_;
+    std::shared_ptr<svgd_ctx> ctx_;
+    std::vector<std::stringstream> intermediate_matrices_sstream_vector_;
+    std::string intermediate_matrices_output_path_ = "log.txt";
+};
+
+#endif
