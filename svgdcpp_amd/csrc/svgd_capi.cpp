@@ -63,6 +63,8 @@ struct svgd_ctx {
     int RS = 0;             // record stride 2d+2
     double *rec = nullptr;  // np x RS particle records
     double *part = nullptr; // S x ldp x (d+1) phi partials
+    float *xf = nullptr;    // np x med_f32_stride(d) fp32 median records
+    unsigned long long *nmax = nullptr; // max |xc|^2 (double bits)
     int S = 1;
     int R = 2; // rows per lane of k_phi_rows
     int64_t ldp = 0;
@@ -78,6 +80,7 @@ struct svgd_ctx {
     uint32_t *counts = nullptr;
     unsigned long long *below = nullptr;
     int collect_grid = 0;
+    int64_t nregions = 0; // candidate regions: one per wave (row-stream) or per block (tiles)
     unsigned long long *cnt3 = nullptr;
     SelState *st = nullptr;
     uint32_t *ghist = nullptr;
@@ -225,7 +228,7 @@ int allreduce_cnt3(svgd_ctx *c)
 int center(svgd_ctx *c)
 {
     HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
-                                 c->nrm, c->rowpath ? 1 : 0, c->stream));
+                                 c->nrm, c->rowpath ? 1 : 0, c->xf, c->nmax, c->stream));
     return SVGD_OK;
 }
 
@@ -250,7 +253,8 @@ int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, 
 hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t cap, double *dbg)
 {
     if (c->rowpath)
-        return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->n, c->pnb, c->tile0,
+        return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->xf, c->nmax, c->n,
+                                c->pnb, c->tile0,
                                 c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
                                 c->ghist, dbg, c->stream);
     return launch_pair_tiles(c->KP, mode, grid, c->xc, c->nrm, c->n, c->pnb, c->tile0,
@@ -290,7 +294,8 @@ int median_begin(svgd_ctx *c)
     const int64_t M = upper_pairs(n);
     const int64_t tiles = c->own_tiles;
     c->collect_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, 1024));
-    const int64_t tiles_per_blk = (tiles + c->collect_grid - 1) / c->collect_grid;
+    c->nregions = c->rowpath ? 4 * (int64_t)c->collect_grid : c->collect_grid;
+    const int64_t tiles_per_blk = (tiles + c->nregions - 1) / c->nregions;
 
     if (M <= c->direct_max_pairs) {
         // every key is a candidate: bracket [0, ~0)
@@ -305,7 +310,7 @@ int median_begin(svgd_ctx *c)
             CHK(dalloc(c, &c->sample_keys, S));
             c->sample_alloc = S;
         }
-        HIPCHK(c, launch_sample_keys(c->xc, c->nrm, n, c->dim, c->KP, S, c->sample_keys,
+        HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, S, c->sample_keys,
                                      c->stream));
         // sample ranks bracketing the target quantiles (6 sigma)
         const double qlo = (double)c->sel_rank[0] / (double)M;
@@ -330,17 +335,17 @@ int median_begin(svgd_ctx *c)
         int64_t total = c->cand_capacity;
         if (total <= 0) {
             const double frac = (qhi - qlo) + 16.0 / std::sqrt((double)S) + 0.004;
-            total = (int64_t)(2.0 * frac * (double)pairs_own) + 8192 * (int64_t)c->collect_grid;
+            total = (int64_t)(2.0 * frac * (double)pairs_own) + 2048 * c->nregions;
         }
-        c->reg_cap = std::max<int64_t>(1, total / c->collect_grid);
+        c->reg_cap = std::max<int64_t>(1, total / c->nregions);
     }
-    const int64_t need = c->reg_cap * c->collect_grid;
+    const int64_t need = c->reg_cap * c->nregions;
     if (c->regions_alloc < need) {
         CHK(dalloc(c, &c->regions, need));
         c->regions_alloc = need;
     }
     HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
-    HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->collect_grid, c->reg_cap, c->cnt3,
+    HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->cnt3,
                                    c->stream));
     CHK(allreduce_cnt3(c));
     HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, 3 * sizeof(unsigned long long),
@@ -383,7 +388,7 @@ int median_finish(svgd_ctx *c)
             const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 2048));
             HIPCHK(c, pair_pass(c, 1, grid, nullptr, 0, nullptr));
         } else {
-            HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->collect_grid, c->reg_cap, 1,
+            HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->nregions, c->reg_cap, 1,
                                           c->st, c->ghist, c->stream));
         }
         CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
@@ -545,6 +550,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         c->RS = phi_rec_stride(dim);
         c->ldp = std::max<int64_t>(1, c->nrows);
         CHK(dalloc(c, &c->rec, c->np * c->RS));
+        CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
+        CHK(dalloc(c, &c->nmax, 1));
         CHK(dalloc(c, &c->part, (int64_t)c->S * c->ldp * (dim + 1)));
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
@@ -556,8 +563,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->upper, dim));
     CHK(dalloc(c, &c->partial, (int64_t)c->nparts * dim));
     CHK(dalloc(c, &c->scal, 2));
-    CHK(dalloc(c, &c->counts, 2048));
-    CHK(dalloc(c, &c->below, 2048));
+    CHK(dalloc(c, &c->counts, 4096)); // <= 4 regions per collect block, <= 1024 blocks
+    CHK(dalloc(c, &c->below, 4096));
     CHK(dalloc(c, &c->cnt3, 4));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
@@ -624,7 +631,8 @@ int svgd_destroy(svgd_ctx *c)
                        c->part};
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
-    void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist};
+    void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
+                     c->xf,          c->nmax};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal};

@@ -26,9 +26,12 @@ struct SelState {
 
 // xc = X - mean (stride KP, zero padded), nrm = |xc|^2; nrm_in_slot also
 // stores |xc|^2 at xc[j*KP + d] (the row-stream median record).
+// xf (optional, d <= 16): fp32 median records [xc | -|xc|^2/2 | 0..] of stride
+// med_f32_stride(d); nmax_bits: max |xc|^2 as double bits (atomicMax).
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
-                              int nrm_in_slot, hipStream_t stream);
+                              int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
+                              hipStream_t stream);
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);
@@ -47,8 +50,9 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
                              int64_t cap, uint32_t *counts, unsigned long long *below,
                              const SelState *st, uint32_t *ghist, double *dbg_out,
                              hipStream_t stream);
-hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int d, int KP,
-                              int64_t S, uint64_t *keys, hipStream_t stream);
+// xf != nullptr (d <= 16): keys from the fp32 records (a bracket estimate only)
+hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
+                              int d, int KP, int64_t S, uint64_t *keys, hipStream_t stream);
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                int64_t cap, int parts, const SelState *st, uint32_t *ghist,
                                hipStream_t stream);
@@ -65,13 +69,16 @@ constexpr int ROWS_MAX_D = 16;
 // [xc | G - 2a xc | c | 0..] and median records [xc | |xc|^2 | 0..]
 constexpr int phi_rec_stride(int d) { return ((2 * d + 1 + 7) / 8) * 8; }
 constexpr int med_rec_stride(int d) { return ((d + 1 + 3) / 4) * 4; }
+constexpr int med_f32_stride(int d) { return ((d + 1 + 7) / 8) * 8; }
 hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
                            double *rec, hipStream_t stream);
-hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr, int64_t row0,
-                           int64_t nrows, int64_t n, int S, double *part, int64_t ldp,
-                           double inv_n, double *phi, hipStream_t stream);
+hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
+                           int64_t row0, int64_t nrows, int64_t n, int S, double *part,
+                           int64_t ldp, double inv_n, double *phi, hipStream_t stream);
+// mode 0 (collect) needs nmax_bits from launch_mean_center (classification margin).
 hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc, const double *nrm,
+                            const float *xf, const unsigned long long *nmax_bits,
                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
                             const SelState *st, uint32_t *ghist, double *dbg_out,

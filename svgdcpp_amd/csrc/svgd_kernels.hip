@@ -18,6 +18,7 @@
 // f64 MFMA: v_mfma_f64_16x16x4_f64.  A/B lane maps: A[i = l&15][k = l>>4],
 // B[k = l>>4][j = l&15]; C/D: col = l&15, row = (l>>4) + 4*reg.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 #include "svgd_kernels.h"
@@ -64,9 +65,10 @@ constexpr double LOG2E = 0x1.71547652b82fep+0;
 
 // Per-block partial column sums of X (n x d) -> partial[b*d + k].
 __global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
-                               double *__restrict__ partial)
+                               double *__restrict__ partial, unsigned long long *nmax_bits)
 {
     __shared__ double red[256];
+    if (nmax_bits && blockIdx.x == 0 && threadIdx.x == 0) *nmax_bits = 0; // k_center's atomicMax target
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t j0 = per * blockIdx.x, j1 = min(n, j0 + per);
     for (int k = 0; k < d; ++k) {
@@ -86,9 +88,13 @@ __global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
 // xc = X - mean (padded to KP columns, rows [n, np) zero), nrm = |xc|^2.
 // The mean is re-derived by every block from the partials in a fixed order,
 // so it is bit-identical on every rank and block.
+// With xf: also the fp32 median record [fl(xc) | fl(-|xc|^2/2) | 0..] (stride
+// KF = med_f32_stride(d)) and max_j |xc_j|^2 into *nmax_bits (non-negative
+// doubles order like their bit patterns).
 __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
                          const double *__restrict__ partial, int nparts, int64_t np,
-                         double *__restrict__ xc, double *__restrict__ nrm, int nrm_in_slot)
+                         double *__restrict__ xc, double *__restrict__ nrm, int nrm_in_slot,
+                         float *__restrict__ xf, int KF, unsigned long long *nmax_bits)
 {
     __shared__ double mu[256];
     for (int k = threadIdx.x; k < d; k += blockDim.x) {
@@ -106,7 +112,17 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
             s = fma(v, v, s);
         }
         nrm[j] = s;
-        if (KP > d && nrm_in_slot) xc[j * KP + d] = s; // median record [xc | |xc|^2 | 0..]
+        if (KP > d && nrm_in_slot) xc[j * KP + d] = -0.5 * s; // median record [xc | -|xc|^2/2 | 0..]
+        if (xf) {
+            for (int k = 0; k < KF; ++k)
+                xf[j * KF + k] = k < d ? (float)xc[j * KP + k] : (k == d ? (float)(-0.5 * s) : 0.0f);
+            unsigned long long m = (unsigned long long)__double_as_longlong(s);
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long t = __shfl_xor(m, o);
+                m = t > m ? t : m;
+            }
+            if ((threadIdx.x & 63) == 0) atomicMax(nmax_bits, m);
+        }
     }
 }
 
@@ -299,6 +315,8 @@ struct SinkCollect {
     int64_t cap;
     uint32_t *count_out;
     unsigned long long *below_out;
+    const float *xf;                     // fp32 records (unused by the collect pass)
+    const unsigned long long *nmax_bits; // max |xc|^2 (double bits): classification margin
 };
 
 struct SinkHist {
@@ -462,6 +480,41 @@ __global__ void k_sample_keys(const double *__restrict__ xc, const double *__res
         double dot = 0.0;
         for (int k = 0; k < d; ++k) dot = fma(xc[i * KP + k], xc[j * KP + k], dot);
         keys[g] = key_of(fmax(fma(-2.0, dot, nrm[i] + nrm[j]), 0.0));
+    }
+}
+
+// Sampled keys from the fp32 records (d <= 16): one random upper-triangle
+// pair per thread, each record read with KF/4 16-byte loads.  The keys only
+// place the bracket, whose exactness the collect pass checks.
+__device__ __forceinline__ int64_t mulhi_index(uint32_t r, int64_t n)
+{
+    return (int64_t)(((uint64_t)r * (uint64_t)n) >> 32);
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict__ xf, int64_t n,
+                                                         int64_t S, uint64_t *__restrict__ keys)
+{
+    constexpr int KF = med_f32_stride(D);
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = mix64((uint64_t)g * 2 + 1);
+        const int64_t i = mulhi_index((uint32_t)(h >> 32), n);
+        int64_t j = i + 1 + mulhi_index((uint32_t)h, n - 1);
+        if (j >= n) j -= n;
+        float a[KF], b[KF];
+        const float4 *ri = reinterpret_cast<const float4 *>(xf + i * KF);
+        const float4 *rj = reinterpret_cast<const float4 *>(xf + j * KF);
+#pragma unroll
+        for (int q = 0; q < KF / 4; ++q) {
+            const float4 u = ri[q], v = rj[q];
+            a[4 * q] = u.x, a[4 * q + 1] = u.y, a[4 * q + 2] = u.z, a[4 * q + 3] = u.w;
+            b[4 * q] = v.x, b[4 * q + 1] = v.y, b[4 * q + 2] = v.z, b[4 * q + 3] = v.w;
+        }
+        float e = a[D] + b[D]; // -(n_i + n_j) / 2
+#pragma unroll
+        for (int k = 0; k < D; ++k) e = fmaf(a[k], b[k], e);
+        keys[g] = key_of(fmax(-2.0 * (double)e, 0.0));
     }
 }
 
@@ -634,36 +687,92 @@ __global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi,
 // Columns are split over S workgroups (partials reduced by k_phi_reduce in a
 // fixed order, so results are deterministic).
 
-__constant__ double EXP2_TAB32[32] = {
-    0x1.0000000000000p+0, 0x1.059b0d3158574p+0, 0x1.0b5586cf9890fp+0, 0x1.11301d0125b51p+0,
-    0x1.172b83c7d517bp+0, 0x1.1d4873168b9aap+0, 0x1.2387a6e756238p+0, 0x1.29e9df51fdee1p+0,
-    0x1.306fe0a31b715p+0, 0x1.371a7373aa9cbp+0, 0x1.3dea64c123422p+0, 0x1.44e086061892dp+0,
-    0x1.4bfdad5362a27p+0, 0x1.5342b569d4f82p+0, 0x1.5ab07dd485429p+0, 0x1.6247eb03a5585p+0,
-    0x1.6a09e667f3bcdp+0, 0x1.71f75e8ec5f74p+0, 0x1.7a11473eb0187p+0, 0x1.82589994cce13p+0,
-    0x1.8ace5422aa0dbp+0, 0x1.93737b0cdc5e5p+0, 0x1.9c49182a3f090p+0, 0x1.a5503b23e255dp+0,
-    0x1.ae89f995ad3adp+0, 0x1.b7f76f2fb5e47p+0, 0x1.c199bdd85529cp+0, 0x1.cb720dcef9069p+0,
-    0x1.d5818dcfba487p+0, 0x1.dfc97337b9b5fp+0, 0x1.ea4afa2a490dap+0, 0x1.f50765b6e4540p+0};
+// 2^(i/256), i = 0..255, correctly rounded (tests/golden/make_tables.py)
+__constant__ double EXP2_TAB256[256] = {
+    0x1.0000000000000p+0, 0x1.00b1afa5abcbfp+0, 0x1.0163da9fb3335p+0, 0x1.02168143b0281p+0,
+    0x1.02c9a3e778061p+0, 0x1.037d42e11bbccp+0, 0x1.04315e86e7f85p+0, 0x1.04e5f72f654b1p+0,
+    0x1.059b0d3158574p+0, 0x1.0650a0e3c1f89p+0, 0x1.0706b29ddf6dep+0, 0x1.07bd42b72a836p+0,
+    0x1.0874518759bc8p+0, 0x1.092bdf66607e0p+0, 0x1.09e3ecac6f383p+0, 0x1.0a9c79b1f3919p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0c0f145e46c85p+0, 0x1.0cc922b7247f7p+0, 0x1.0d83b23395decp+0,
+    0x1.0e3ec32d3d1a2p+0, 0x1.0efa55fdfa9c5p+0, 0x1.0fb66affed31bp+0, 0x1.1073028d7233ep+0,
+    0x1.11301d0125b51p+0, 0x1.11edbab5e2ab6p+0, 0x1.12abdc06c31ccp+0, 0x1.136a814f204abp+0,
+    0x1.1429aaea92de0p+0, 0x1.14e95934f312ep+0, 0x1.15a98c8a58e51p+0, 0x1.166a45471c3c2p+0,
+    0x1.172b83c7d517bp+0, 0x1.17ed48695bbc0p+0, 0x1.18af9388c8deap+0, 0x1.1972658375d2fp+0,
+    0x1.1a35beb6fcb75p+0, 0x1.1af99f8138a1cp+0, 0x1.1bbe084045cd4p+0, 0x1.1c82f95281c6bp+0,
+    0x1.1d4873168b9aap+0, 0x1.1e0e75eb44027p+0, 0x1.1ed5022fcd91dp+0, 0x1.1f9c18438ce4dp+0,
+    0x1.2063b88628cd6p+0, 0x1.212be3578a819p+0, 0x1.21f49917ddc96p+0, 0x1.22bdda27912d1p+0,
+    0x1.2387a6e756238p+0, 0x1.2451ffb82140ap+0, 0x1.251ce4fb2a63fp+0, 0x1.25e85711ece75p+0,
+    0x1.26b4565e27cddp+0, 0x1.2780e341ddf29p+0, 0x1.284dfe1f56381p+0, 0x1.291ba7591bb70p+0,
+    0x1.29e9df51fdee1p+0, 0x1.2ab8a66d10f13p+0, 0x1.2b87fd0dad990p+0, 0x1.2c57e39771b2fp+0,
+    0x1.2d285a6e4030bp+0, 0x1.2df961f641589p+0, 0x1.2ecafa93e2f56p+0, 0x1.2f9d24abd886bp+0,
+    0x1.306fe0a31b715p+0, 0x1.31432edeeb2fdp+0, 0x1.32170fc4cd831p+0, 0x1.32eb83ba8ea32p+0,
+    0x1.33c08b26416ffp+0, 0x1.3496266e3fa2dp+0, 0x1.356c55f929ff1p+0, 0x1.36431a2de883bp+0,
+    0x1.371a7373aa9cbp+0, 0x1.37f26231e754ap+0, 0x1.38cae6d05d866p+0, 0x1.39a401b7140efp+0,
+    0x1.3a7db34e59ff7p+0, 0x1.3b57fbfec6cf4p+0, 0x1.3c32dc313a8e5p+0, 0x1.3d0e544ede173p+0,
+    0x1.3dea64c123422p+0, 0x1.3ec70df1c5175p+0, 0x1.3fa4504ac801cp+0, 0x1.40822c367a024p+0,
+    0x1.4160a21f72e2ap+0, 0x1.423fb2709468ap+0, 0x1.431f5d950a897p+0, 0x1.43ffa3f84b9d4p+0,
+    0x1.44e086061892dp+0, 0x1.45c2042a7d232p+0, 0x1.46a41ed1d0057p+0, 0x1.4786d668b3237p+0,
+    0x1.486a2b5c13cd0p+0, 0x1.494e1e192aed2p+0, 0x1.4a32af0d7d3dep+0, 0x1.4b17dea6db7d7p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4ce41b817c114p+0, 0x1.4dcb299fddd0dp+0, 0x1.4eb2d81d8abffp+0,
+    0x1.4f9b2769d2ca7p+0, 0x1.508417f4531eep+0, 0x1.516daa2cf6642p+0, 0x1.5257de83f4eefp+0,
+    0x1.5342b569d4f82p+0, 0x1.542e2f4f6ad27p+0, 0x1.551a4ca5d920fp+0, 0x1.56070dde910d2p+0,
+    0x1.56f4736b527dap+0, 0x1.57e27dbe2c4cfp+0, 0x1.58d12d497c7fdp+0, 0x1.59c0827ff07ccp+0,
+    0x1.5ab07dd485429p+0, 0x1.5ba11fba87a03p+0, 0x1.5c9268a5946b7p+0, 0x1.5d84590998b93p+0,
+    0x1.5e76f15ad2148p+0, 0x1.5f6a320dceb71p+0, 0x1.605e1b976dc09p+0, 0x1.6152ae6cdf6f4p+0,
+    0x1.6247eb03a5585p+0, 0x1.633dd1d1929fdp+0, 0x1.6434634ccc320p+0, 0x1.652b9febc8fb7p+0,
+    0x1.6623882552225p+0, 0x1.671c1c70833f6p+0, 0x1.68155d44ca973p+0, 0x1.690f4b19e9538p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6b052fa75173ep+0, 0x1.6c012750bdabfp+0, 0x1.6cfdcddd47645p+0,
+    0x1.6dfb23c651a2fp+0, 0x1.6ef9298593ae5p+0, 0x1.6ff7df9519484p+0, 0x1.70f7466f42e87p+0,
+    0x1.71f75e8ec5f74p+0, 0x1.72f8286ead08ap+0, 0x1.73f9a48a58174p+0, 0x1.74fbd35d7cbfdp+0,
+    0x1.75feb564267c9p+0, 0x1.77024b1ab6e09p+0, 0x1.780694fde5d3fp+0, 0x1.790b938ac1cf6p+0,
+    0x1.7a11473eb0187p+0, 0x1.7b17b0976cfdbp+0, 0x1.7c1ed0130c132p+0, 0x1.7d26a62ff86f0p+0,
+    0x1.7e2f336cf4e62p+0, 0x1.7f3878491c491p+0, 0x1.80427543e1a12p+0, 0x1.814d2add106d9p+0,
+    0x1.82589994cce13p+0, 0x1.8364c1eb941f7p+0, 0x1.8471a4623c7adp+0, 0x1.857f4179f5b21p+0,
+    0x1.868d99b4492edp+0, 0x1.879cad931a436p+0, 0x1.88ac7d98a6699p+0, 0x1.89bd0a478580fp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8be05bad61778p+0, 0x1.8cf3216b5448cp+0, 0x1.8e06a5e0866d9p+0,
+    0x1.8f1ae99157736p+0, 0x1.902fed0282c8ap+0, 0x1.9145b0b91ffc6p+0, 0x1.925c353aa2fe2p+0,
+    0x1.93737b0cdc5e5p+0, 0x1.948b82b5f98e5p+0, 0x1.95a44cbc8520fp+0, 0x1.96bdd9a7670b3p+0,
+    0x1.97d829fde4e50p+0, 0x1.98f33e47a22a2p+0, 0x1.9a0f170ca07bap+0, 0x1.9b2bb4d53fe0dp+0,
+    0x1.9c49182a3f090p+0, 0x1.9d674194bb8d5p+0, 0x1.9e86319e32323p+0, 0x1.9fa5e8d07f29ep+0,
+    0x1.a0c667b5de565p+0, 0x1.a1e7aed8eb8bbp+0, 0x1.a309bec4a2d33p+0, 0x1.a42c980460ad8p+0,
+    0x1.a5503b23e255dp+0, 0x1.a674a8af46052p+0, 0x1.a799e1330b358p+0, 0x1.a8bfe53c12e59p+0,
+    0x1.a9e6b5579fdbfp+0, 0x1.ab0e521356ebap+0, 0x1.ac36bbfd3f37ap+0, 0x1.ad5ff3a3c2774p+0,
+    0x1.ae89f995ad3adp+0, 0x1.afb4ce622f2ffp+0, 0x1.b0e07298db666p+0, 0x1.b20ce6c9a8952p+0,
+    0x1.b33a2b84f15fbp+0, 0x1.b468415b749b1p+0, 0x1.b59728de5593ap+0, 0x1.b6c6e29f1c52ap+0,
+    0x1.b7f76f2fb5e47p+0, 0x1.b928cf22749e4p+0, 0x1.ba5b030a1064ap+0, 0x1.bb8e0b79a6f1fp+0,
+    0x1.bcc1e904bc1d2p+0, 0x1.bdf69c3f3a207p+0, 0x1.bf2c25bd71e09p+0, 0x1.c06286141b33dp+0,
+    0x1.c199bdd85529cp+0, 0x1.c2d1cd9fa652cp+0, 0x1.c40ab5fffd07ap+0, 0x1.c544778fafb22p+0,
+    0x1.c67f12e57d14bp+0, 0x1.c7ba88988c933p+0, 0x1.c8f6d9406e7b5p+0, 0x1.ca3405751c4dbp+0,
+    0x1.cb720dcef9069p+0, 0x1.ccb0f2e6d1675p+0, 0x1.cdf0b555dc3fap+0, 0x1.cf3155b5bab74p+0,
+    0x1.d072d4a07897cp+0, 0x1.d1b532b08c968p+0, 0x1.d2f87080d89f2p+0, 0x1.d43c8eacaa1d6p+0,
+    0x1.d5818dcfba487p+0, 0x1.d6c76e862e6d3p+0, 0x1.d80e316c98398p+0, 0x1.d955d71ff6075p+0,
+    0x1.da9e603db3285p+0, 0x1.dbe7cd63a8315p+0, 0x1.dd321f301b460p+0, 0x1.de7d5641c0658p+0,
+    0x1.dfc97337b9b5fp+0, 0x1.e11676b197d17p+0, 0x1.e264614f5a129p+0, 0x1.e3b333b16ee12p+0,
+    0x1.e502ee78b3ff6p+0, 0x1.e653924676d76p+0, 0x1.e7a51fbc74c83p+0, 0x1.e8f7977cdb740p+0,
+    0x1.ea4afa2a490dap+0, 0x1.eb9f4867cca6ep+0, 0x1.ecf482d8e67f1p+0, 0x1.ee4aaa2188510p+0,
+    0x1.efa1bee615a27p+0, 0x1.f0f9c1cb6412ap+0, 0x1.f252b376bba97p+0, 0x1.f3ac948dd7274p+0,
+    0x1.f50765b6e4540p+0, 0x1.f6632798844f8p+0, 0x1.f7bfdad9cbe14p+0, 0x1.f91d802243c89p+0,
+    0x1.fa7c1819e90d8p+0, 0x1.fbdba3692d514p+0, 0x1.fd3c22b8f71f1p+0, 0x1.fe9d96b2a23d9p+0};
 
-// 2^(u/32) for u <= ~0: u = k + f, |f| <= 1/2, 2^(u/32) = 2^(k>>5) 2^((k&31)/32) 2^(f/32);
-// 2^(f/32) by its degree-6 Taylor polynomial (|f/32| <= 1/64: 1.3 ulp overall).
-__device__ __forceinline__ double exp2_32(double u, const double *tab)
+// 2^(u/256) for u <= ~0: u = k + f, |f| <= 1/2, 2^(u/256) = 2^(k>>8) 2^((k&255)/256) 2^(f/256);
+// 2^(f/256) = e^r, r = f ln2/256, |r| <= 1.36e-3, by its degree-4 Taylor
+// polynomial (remainder r^5/5! < 0.35 ulp; <= ~2 ulp overall).  9 fp64 ops.
+__device__ __forceinline__ double exp2_256(double u, const double *tab)
 {
     const double k = __builtin_rint(u);
     const double f = u - k;
     const int ki = (int)k;
-    double p = 0x1.430912f86c787p-43;
-    p = fma(p, f, 0x1.5d87fe78a6731p-35);
-    p = fma(p, f, 0x1.3b2ab6fba4e77p-27);
-    p = fma(p, f, 0x1.c6b08d704a0c0p-20);
-    p = fma(p, f, 0x1.ebfbdff82c58fp-13);
-    p = fma(p, f, 0x1.62e42fefa39efp-6);
+    double p = 0x1.3b2ab6fba4e77p-39;
+    p = fma(p, f, 0x1.c6b08d704a0c0p-29);
+    p = fma(p, f, 0x1.ebfbdff82c58fp-19);
+    p = fma(p, f, 0x1.62e42fefa39efp-9);
     p = fma(p, f, 1.0);
-    return __builtin_ldexp(p * tab[ki & 31], ki >> 5);
+    return __builtin_ldexp(p * tab[ki & 255], ki >> 8);
 }
 
 constexpr int CH_PHI = 16; // columns per LDS chunk of the phi row stream
 
-// rec_j = [xc_j (D) | V_j = G_j - 2a xc_j (D) | c_j = -32 a log2e |xc_j|^2 | 0 ...],
+// rec_j = [xc_j (D) | V_j = G_j - 2a xc_j (D) | c_j = -256 a log2e |xc_j|^2 | 0 ...],
 // stride phi_rec_stride(D) = roundup(2D+1, 8) doubles, so CH_PHI records are
 // a whole number of 1 KiB LDS-DMA pieces.
 template <int D> struct RecLayout {
@@ -685,10 +794,33 @@ __device__ __forceinline__ void dma_to_lds(const char *gsrc, char *ldst, int lan
                                          (lds_void *)(ldst + p * 1024), 16, 0, 0);
 }
 
+// s_waitcnt vmcnt(N) through the intrinsic (gfx9 encoding: vmcnt[3:0] in bits
+// 3:0, vmcnt[5:4] in 15:14, expcnt/lgkmcnt left at their maxima), so the
+// compiler's own wait insertion sees it and does not add a vmcnt(0) of its own
+// at the first use of registers loaded before the wait.
 template <int N> __device__ __forceinline__ void wait_vmcnt()
 {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
 }
+
+// LDS accesses the compiler does not see: used for the collect pass's key
+// staging area, which no LDS DMA ever targets.  A compiler-visible LDS store
+// there would make it drain every in-flight column DMA first (it cannot prove
+// the two do not alias).  The caller waits (lgkm_wait) before reading back.
+__device__ __forceinline__ void lds_store_u64(const uint64_t *p, uint64_t v)
+{
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint64_t *)p;
+    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint64_t lds_load_u64(const uint64_t *p)
+{
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint64_t *)p;
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restrict__ G,
                            const double *__restrict__ nrm, const double *__restrict__ a_ptr,
@@ -704,7 +836,7 @@ __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restri
             r[k] = x;
             r[d + k] = live ? G[j * d + k] - 2.0 * a * x : 0.0;
         }
-        r[2 * d] = live ? -32.0 * a * LOG2E * nrm[j] : 0.0;
+        r[2 * d] = live ? -256.0 * a * LOG2E * nrm[j] : 0.0;
         for (int k = 2 * d + 1; k < RS; ++k) r[k] = 0.0;
     }
 }
@@ -717,10 +849,10 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
 {
     constexpr int RS = RecLayout<D>::RS;
     constexpr int CHB = CH_PHI * RS * 8; // bytes per column chunk (multiple of 1 KiB)
-    // per-wave double-buffered column chunks, then the 2^(k/32) table
-    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + 32 * 8];
+    // per-wave double-buffered column chunks, then the 2^(i/256) table
+    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + 256 * 8];
     double *tab = reinterpret_cast<double *>(smem + 4 * 2 * CHB);
-    if (threadIdx.x < 32) tab[threadIdx.x] = EXP2_TAB32[threadIdx.x];
+    tab[threadIdx.x] = EXP2_TAB256[threadIdx.x];
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -729,9 +861,11 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     const int64_t iblk = blockIdx.x / S;
     const int s = (int)(blockIdx.x - iblk * S);
     const int64_t rbase = iblk * (256 * R) + w * (64 * R); // local row of this wave's lane 0
-    const double alpha = 64.0 * LOG2E * (*a_ptr);
+    // u_ij = c_i + c_j + 512 a log2e xc_i.xc_j = -256 a log2e |xc_i - xc_j|^2;
+    // the row coordinates are pre-scaled by 512 a log2e
+    const double alpha = 512.0 * LOG2E * (*a_ptr);
 
-    double xi[R][D], ci[R], acc[R][D], acc1[R];
+    double xs[R][D], ci[R], acc[R][D], acc1[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int64_t li = rbase + 64 * r + lane;
@@ -739,7 +873,7 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
         const double *ri = rec + (row0 + li) * RS;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            xi[r][k] = ri[k];
+            xs[r][k] = alpha * ri[k];
             acc[r][k] = 0.0;
         }
         ci[r] = ri[2 * D];
@@ -748,8 +882,10 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
 
     // Column records stream through two LDS chunk buffers: the DMA of chunk
     // c+1 is in flight (vmcnt) while chunk c is computed; every lane reads the
-    // same record (LDS broadcast).  rec has >= 64 padded rows past n, so whole
-    // chunks may be copied.
+    // same record (LDS broadcast), one column ahead of its use so the LDS
+    // latency overlaps the previous column's arithmetic.  rec has >= 64 padded
+    // rows past n, so whole chunks may be copied; the look-ahead read past a
+    // chunk stays inside smem and is discarded.
     const int64_t j0 = n * s / S, j1 = n * (s + 1) / S;
     const int64_t nch = (j1 - j0 + CH_PHI - 1) / CH_PHI;
     const char *gcol = reinterpret_cast<const char *>(rec + j0 * RS);
@@ -774,10 +910,10 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
             const double cj = rj[2 * D];
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                double dot = xi[r][0] * xj[0];
+                double u = ci[r] + cj;
 #pragma unroll
-                for (int k = 1; k < D; ++k) dot = fma(xi[r][k], xj[k], dot);
-                const double K = exp2_32(fma(alpha, dot, ci[r] + cj), tab);
+                for (int k = 0; k < D; ++k) u = fma(xs[r][k], xj[k], u);
+                const double K = exp2_256(u, tab);
 #pragma unroll
                 for (int k = 0; k < D; ++k) acc[r][k] = fma(K, vj[k], acc[r][k]);
                 acc1[r] += K;
@@ -837,25 +973,58 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
 {
-    constexpr int KPM = med_rec_stride(D);
-    constexpr int CHB = CH_MED * KPM * 8; // bytes per column chunk (multiple of 1 KiB)
-    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB];
+    // Median records (k_center): [xc (D) | h = -|xc|^2 / 2 | 0..], stride KP.
+    // The pair key of rows i, j (every mode, so all passes agree bit for bit):
+    //   e_ij = h_j + sum_k xc_ik xc_jk   (fma chain, k ascending)
+    //   s_ij = max(fl(-2 h_i - 2 e_ij), 0) = |xc_i - xc_j|^2 up to rounding.
+    constexpr int KP = med_rec_stride(D);
+    constexpr int CHB = CH_MED * KP * 8; // bytes per column chunk (multiple of 1 KiB)
+    constexpr int STG = MODE == 0 ? 512 : 1; // staged keys per wave (MODE 0)
+    // per-wave double-buffered column chunks, then (MODE 0) per-wave key
+    // staging.  The staging lives inside smem on purpose: a separate
+    // __shared__ array makes the compiler drain the in-flight column DMA
+    // before every LDS read of the loop.
+    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + (MODE == 0 ? 4 * STG * 8 : 0)];
     __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
-    __shared__ uint32_t sCnt;
-    __shared__ unsigned long long sBelow[4];
     const int tid = threadIdx.x, lane = tid & 63;
     // wave index made provably uniform (wave-uniform tile walk)
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     char *wbuf = smem + w * 2 * CHB;
-    (void)kp_arg;           // == KPM: median records [xc | |xc|^2 | 0..]
-    constexpr int KP = KPM; // record stride (doubles)
+    (void)kp_arg;
+    (void)nrm;
+
+    // MODE 0: each wave appends the keys in [lo, hi) to its own region.  Keys
+    // are staged in LDS (asm stores, see lds_store_u64) and flushed right
+    // after each column-DMA wait, so the global stores drain during a whole
+    // chunk instead of stalling the next vmcnt wait; no LDS atomics.
+    uint64_t(*sStage)[STG] = reinterpret_cast<uint64_t(*)[STG]>(smem + 4 * 2 * CHB);
+    const int64_t wreg = (int64_t)blockIdx.x * 4 + w;
+    int64_t wcnt = 0; // keys written to the region
+    int scnt = 0;     // keys staged in sStage[w]
+    uint64_t *wregion = MODE == 0 ? sc.region + wreg * sc.cap : nullptr;
+    auto flush = [&]() {
+        if (scnt == 0) return;
+        uint64_t v[STG / 64 > 0 ? STG / 64 : 1];
+#pragma unroll
+        for (int t = 0; t < STG / 64; ++t)
+            if (t * 64 < scnt) v[t] = lds_load_u64(&sStage[w][t * 64 + lane]);
+        lgkm_wait();
+#pragma unroll
+        for (int t = 0; t < STG / 64; ++t) {
+            const int64_t pos = wcnt + t * 64 + lane;
+            if (t * 64 + lane < scnt && pos < sc.cap) wregion[pos] = v[t];
+        }
+        wcnt += scnt;
+        scnt = 0;
+    };
 
     int nsel = 0, shift = 0, hsh = 63;
     uint64_t pfx0 = 0, pfx1 = 0, lo_key = 0, hi_key = 0;
+    double nmax = 0.0;
     if (MODE == 0) {
         lo_key = sc.st->lo_key;
         hi_key = sc.st->hi_key;
-        if (tid == 0) sCnt = 0;
+        nmax = __longlong_as_double((long long)*sc.nmax_bits);
     } else if (MODE == 1) {
         nsel = sh.st->nsel;
         shift = sh.st->shift;
@@ -870,11 +1039,18 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     const double lo_d = __longlong_as_double((long long)lo_key);
     const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
                                                         : __longlong_as_double((long long)hi_key);
+    // MODE 0 classifies on e directly.  s = fl(n_i - 2e) is monotone in e and
+    // within 2^-53 (n_i + 2|e|) <= 2^-51 (n_i + nmax) of n_i - 2e, so with
+    // m_i = 2^-48 (n_i + nmax)
+    //   e >  TL_i = (n_i - lo + m_i) / 2   =>  s <  lo   (counted)
+    //   e <= TH_i = (n_i - hi - m_i) / 2   =>  s >= hi   (ignored)
+    // and only the thin band between (the bracket itself) forms s.
 
     const int64_t W = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + w;
     const int64_t T = t1 - t0;
     const int64_t tb = t0 + T * gw / W, te = t0 + T * (gw + 1) / W;
     unsigned long long below = 0; // wave-uniform (scalar) count
+    uint32_t wbelow = 0;          // 32-bit scalar count, flushed per chunk (MODE 0)
 
     if (tb < te) {
         const int64_t H = (nb - 1) / 2;
@@ -903,7 +1079,7 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
         };
         dma_to_lds<CHB>(src(it), wbuf, lane);
         int64_t curI = -1;
-        double xi[PR][D], ni[PR];
+        double xi[PR][D], ni[PR], TL[PR], TH[PR];
         int64_t irow[PR];
         bool ivalid[PR];
         unsigned long long vmask[PR];
@@ -916,6 +1092,11 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
             } else {
                 wait_vmcnt<0>();
             }
+            if constexpr (MODE == 0) {
+                flush();
+                below += wbelow; // a chunk adds < 2^14 to the 32-bit count
+                wbelow = 0;
+            }
             const int64_t I = it.I, J = it.J;
             if (I != curI) {
 #pragma unroll
@@ -926,72 +1107,125 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
                     const int64_t ic = ivalid[r] ? irow[r] : n - 1;
 #pragma unroll
                     for (int k = 0; k < D; ++k) xi[r][k] = xc[ic * KP + k];
-                    ni[r] = xc[ic * KP + D];
+                    ni[r] = -2.0 * xc[ic * KP + D];
+                    if constexpr (MODE == 0) {
+                        const double m = 0x1p-48 * (ni[r] + nmax);
+                        TL[r] = lo_key == 0 ? __builtin_inf() : 0.5 * (ni[r] - lo_d + m);
+                        TH[r] = 0.5 * (ni[r] - hi_d - m); // -inf when hi is +inf
+                        if (!ivalid[r]) TL[r] = TH[r] = __builtin_inf(); // never counted
+                    }
                 }
+                // row registers complete here (rare: once per row block), not
+                // at their first use inside the column loop
+                wait_vmcnt<0>();
                 curI = I;
             }
             const bool diag = I == J;
             const int64_t jb = J * PBLK + it.c * CH_MED;
             const int cnt = (int)min<int64_t>(CH_MED, n - jb);
             const double *cb = reinterpret_cast<const double *>(wbuf + (q & 1) * CHB);
-            for (int jj = 0; jj < cnt; ++jj) {
-                const int64_t j = jb + jj;
-                double xj[D];
+            // off-diagonal tiles (all but 1 in H+1): every valid row counts
+            auto columns = [&](auto diag_tag) {
+                constexpr bool DIAG = decltype(diag_tag)::value;
+                for (int jj = 0; jj < cnt; ++jj) {
+                    const int64_t j = jb + jj;
+                    double xj[D];
 #pragma unroll
-                for (int k = 0; k < D; ++k) xj[k] = cb[jj * KP + k]; // LDS broadcast
-                const double nj = cb[jj * KP + D];
+                    for (int k = 0; k < D; ++k) xj[k] = cb[jj * KP + k]; // LDS broadcast
+                    const double hj = cb[jj * KP + D];
+                    // all rows' chains first (independent, interleaved), then
+                    // the classification: no branch between the FMA chains
+                    double ev[PR];
 #pragma unroll
-                for (int r = 0; r < PR; ++r) {
-                    double dot = xi[r][0] * xj[0];
+                    for (int r = 0; r < PR; ++r) {
+                        ev[r] = hj;
 #pragma unroll
-                    for (int k = 1; k < D; ++k) dot = fma(xi[r][k], xj[k], dot);
-                    const double s = fmax(fma(-2.0, dot, ni[r] + nj), 0.0);
-                    const bool valid = ivalid[r] && (!diag || irow[r] < j);
-                    if (MODE == 0) {
-                        // masks live in SGPRs: two f64 compares per pair
-                        const unsigned long long vm = diag ? __ballot(valid) : vmask[r];
-                        const unsigned long long mb = __ballot(s < lo_d) & vm;
-                        below += __popcll(mb);
-                        const unsigned long long mask = __ballot(s < hi_d) & vm & ~mb;
-                        const bool in = (mask >> lane) & 1ull;
-                        if (mask) {
-                            uint32_t base = 0;
-                            if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mask));
-                            base = __shfl(base, 0);
-                            if (in) {
-                                const int64_t pos =
-                                    base + __popcll(mask & ((1ull << lane) - 1ull));
-                                if (pos < sc.cap) sc.region[blockIdx.x * sc.cap + pos] = key_of(s);
+                        for (int k = 0; k < D; ++k) ev[r] = fma(xi[r][k], xj[k], ev[r]);
+                    }
+                    if constexpr (MODE == 0) {
+                        // two f64 compares per pair.  Off-diagonal tiles count
+                        // per lane (invalid rows have TL = TH = +inf) and take
+                        // one wave-uniform branch per column; diagonal tiles
+                        // (1 in H+1) use SGPR masks for the i < j condition.
+                        unsigned long long mcs[PR];
+#pragma unroll
+                        for (int r = 0; r < PR; ++r) {
+                            const unsigned long long ml = __ballot(ev[r] > TL[r]);
+                            const unsigned long long mh = __ballot(ev[r] > TH[r]);
+                            if constexpr (DIAG) {
+                                const unsigned long long vm = __ballot(ivalid[r] && irow[r] < j);
+                                below += __popcll(ml & vm);
+                                mcs[r] = mh & ~ml & vm;
+                            } else {
+                                // invalid rows: TL = TH = +inf, so no mask
+                                wbelow += (uint32_t)__popcll(ml);
+                                mcs[r] = mh & ~ml;
                             }
                         }
-                    } else if (MODE == 1) {
-                        if (valid) {
-                            const uint64_t key = key_of(s);
-                            const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
-                            if (hsh >= 64 || (key >> hsh) == (pfx0 >> hsh))
-                                atomicAdd(&sHist[dg], 1u);
-                            if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (pfx1 >> hsh)))
-                                atomicAdd(&sHist[RADIX + dg], 1u);
+                        if ((mcs[0] | mcs[1] | mcs[2] | mcs[3]) != 0) {
+#pragma unroll
+                            for (int r = 0; r < PR; ++r) {
+                                const unsigned long long mc = mcs[r];
+                                if (!mc) continue;
+                                // the bracket band: form the key
+                                const double sx = fmax(fma(-2.0, ev[r], ni[r]), 0.0);
+                                const unsigned long long mb = __ballot(sx < lo_d) & mc;
+                                below += __popcll(mb);
+                                const unsigned long long mask = __ballot(sx < hi_d) & mc & ~mb;
+                                if (mask) {
+                                    if (scnt + 64 > STG) flush(); // rare: > STG-64 keys in a chunk
+                                    if ((mask >> lane) & 1ull)
+                                        lds_store_u64(&sStage[w][scnt + __popcll(mask & ((1ull << lane) -
+                                                                                         1ull))],
+                                                      key_of(sx));
+                                    scnt += __popcll(mask);
+                                }
+                            }
                         }
-                    } else {
-                        if (valid) {
-                            const int64_t i = irow[r];
-                            const int64_t a = i < j ? i : j, b = i < j ? j : i;
-                            sd.out[a * (2 * sd.n - a - 1) / 2 + (b - a - 1)] = s;
+                    }
+#pragma unroll
+                    for (int r = 0; r < PR; ++r) {
+                        const double e = ev[r];
+                        const bool valid = ivalid[r] && (!DIAG || irow[r] < j);
+                        if constexpr (MODE == 0) {
+                            (void)e;
+                            (void)valid;
+                        } else {
+                            const double sk = fmax(fma(-2.0, e, ni[r]), 0.0);
+                            if (MODE == 1) {
+                                if (valid) {
+                                    const uint64_t key = key_of(sk);
+                                    const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
+                                    if (hsh >= 64 || (key >> hsh) == (pfx0 >> hsh))
+                                        atomicAdd(&sHist[dg], 1u);
+                                    if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (pfx1 >> hsh)))
+                                        atomicAdd(&sHist[RADIX + dg], 1u);
+                                }
+                            } else {
+                                if (valid) {
+                                    const int64_t i = irow[r];
+                                    const int64_t a = i < j ? i : j, b = i < j ? j : i;
+                                    sd.out[a * (2 * sd.n - a - 1) / 2 + (b - a - 1)] = sk;
+                                }
+                            }
                         }
                     }
                 }
-            }
+            };
+            if (diag)
+                columns(std::true_type{});
+            else
+                columns(std::false_type{});
             it = nx;
         }
     }
 
-    if (MODE == 0) {
-        if (lane == 0) sBelow[w] = below;
-        __syncthreads();
-        if (tid == 0) {
-            sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
-            sc.count_out[blockIdx.x] = sCnt;
+    if constexpr (MODE == 0) {
+        flush();
+        below += wbelow;
+        if (lane == 0) {
+            sc.below_out[wreg] = below;
+            sc.count_out[wreg] = (uint32_t)min<int64_t>(wcnt, 0xffffffffll);
         }
     } else if (MODE == 1) {
         __syncthreads();
@@ -1005,14 +1239,14 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
 #define SVGD_ROWS_CASE(Dv)                                                                   \
     case Dv:                                                                                 \
         if (kind == 0 && R == 1)                                                             \
-            hipLaunchKernelGGL((k_phi_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream, rec,     \
-                               a_ptr, row0, nrows, n, S, part, ldp);                         \
+            hipLaunchKernelGGL((k_phi_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream,   \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp);                    \
         else if (kind == 0 && R == 2)                                                        \
-            hipLaunchKernelGGL((k_phi_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream, rec,     \
-                               a_ptr, row0, nrows, n, S, part, ldp);                         \
+            hipLaunchKernelGGL((k_phi_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream,   \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp);                    \
         else if (kind == 0)                                                                  \
-            hipLaunchKernelGGL((k_phi_rows<Dv, 4>), dim3(grid), dim3(256), 0, stream, rec,     \
-                               a_ptr, row0, nrows, n, S, part, ldp);                         \
+            hipLaunchKernelGGL((k_phi_rows<Dv, 4>), dim3(grid), dim3(256), 0, stream,   \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp);                    \
         else if (kind == 10)                                                                 \
             hipLaunchKernelGGL((k_pair_rows<Dv, 0>), dim3(grid), dim3(256), 0, stream, xc, KP, \
                                nrm, n, nb, t0, t1, sc, sh, sd);                              \
@@ -1064,9 +1298,9 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
     return hipGetLastError();
 }
 
-hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr, int64_t row0,
-                           int64_t nrows, int64_t n, int S, double *part, int64_t ldp,
-                           double inv_n, double *phi, hipStream_t stream)
+hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
+                           int64_t row0, int64_t nrows, int64_t n, int S, double *part,
+                           int64_t ldp, double inv_n, double *phi, hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
     const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
@@ -1082,13 +1316,15 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
 }
 
 hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc, const double *nrm,
+                            const float *xf, const unsigned long long *nmax_bits,
                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
                             const SelState *st, uint32_t *ghist, double *dbg_out,
                             hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
-    SinkCollect sc{st, regions, cap, counts, below};
+    if (mode == 0 && !nmax_bits) return hipErrorInvalidValue;
+    SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n};
     return launch_rows_kernel(10 + mode, d, 1, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, xc,
@@ -1156,13 +1392,15 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
 
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
-                              int nrm_in_slot, hipStream_t stream)
+                              int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
+                              hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial);
+    hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial,
+                       xf ? nmax_bits : nullptr);
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_center, dim3(g), dim3(256), 0, stream, X, n, d, KP, partial, nparts, np,
-                       xc, nrm, nrm_in_slot);
+                       xc, nrm, nrm_in_slot, xf, med_f32_stride(d), nmax_bits);
     return hipGetLastError();
 }
 
@@ -1190,12 +1428,28 @@ hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, do
     return hipGetLastError();
 }
 
-hipError_t launch_sample_keys(const double *xc, const double *nrm, int64_t n, int d, int KP,
-                              int64_t S, uint64_t *keys, hipStream_t stream)
+#define SVGD_SAMPLE_CASE(Dv)                                                                 \
+    case Dv:                                                                                 \
+        hipLaunchKernelGGL((k_sample_keys_f32<Dv>), dim3(g), dim3(256), 0, stream, xf, n, S, keys); \
+        break;
+
+hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
+                              int d, int KP, int64_t S, uint64_t *keys, hipStream_t stream)
 {
     int64_t g = (S + 255) / 256;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, d, KP, S, keys);
+    if (!xf) {
+        hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, d, KP, S, keys);
+        return hipGetLastError();
+    }
+    switch (d) {
+        SVGD_SAMPLE_CASE(1) SVGD_SAMPLE_CASE(2) SVGD_SAMPLE_CASE(3) SVGD_SAMPLE_CASE(4)
+        SVGD_SAMPLE_CASE(5) SVGD_SAMPLE_CASE(6) SVGD_SAMPLE_CASE(7) SVGD_SAMPLE_CASE(8)
+        SVGD_SAMPLE_CASE(9) SVGD_SAMPLE_CASE(10) SVGD_SAMPLE_CASE(11) SVGD_SAMPLE_CASE(12)
+        SVGD_SAMPLE_CASE(13) SVGD_SAMPLE_CASE(14) SVGD_SAMPLE_CASE(15) SVGD_SAMPLE_CASE(16)
+    default:
+        return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
