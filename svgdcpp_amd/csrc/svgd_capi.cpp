@@ -216,10 +216,9 @@ int allreduce_u32(svgd_ctx *c, uint32_t *buf, size_t cnt)
 int allreduce_cnt3(svgd_ctx *c)
 {
     if (c->world == 1) return SVGD_OK;
-    // below and candidate totals are sums, the overflow flag a max
-    NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 2, ncclUint64, ncclSum, c->comm, c->stream));
-    NCCLCHK(c, ncclAllReduce(c->cnt3 + 2, c->cnt3 + 2, 1, ncclUint64, ncclMax, c->comm,
-                             c->stream));
+    // below, candidate and overflowed-region totals are sums; [3..4] (the
+    // bracket) is identical on every rank and stays local
+    NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 3, ncclUint64, ncclSum, c->comm, c->stream));
     return SVGD_OK;
 }
 
@@ -232,15 +231,20 @@ int center(svgd_ctx *c)
     return SVGD_OK;
 }
 
-// Upload a fresh select state (ranks, digit 0) from the host.
-int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key)
+// Upload a fresh select state from the host.  Bits >= known_from of every
+// selected key are already known to equal those of `prefix` (64: nothing
+// known; keys are < 2^63); the first digit is the RADIX_BITS below them.
+int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key,
+                 int known_from = 63, uint64_t prefix = 0)
 {
     SelState s{};
     s.nsel = nsel;
     s.rank[0] = ranks[0];
     s.rank[1] = nsel > 1 ? ranks[1] : 0;
-    s.shift = 63 - RADIX_BITS;
-    s.width = RADIX_BITS;
+    const uint64_t pm = known_from >= 64 ? 0ull : ~((1ull << known_from) - 1ull);
+    s.prefix[0] = s.prefix[1] = prefix & pm;
+    s.shift = known_from > RADIX_BITS ? known_from - RADIX_BITS : 0;
+    s.width = known_from > RADIX_BITS ? RADIX_BITS : known_from;
     s.lo_key = lo_key;
     s.hi_key = hi_key;
     *c->h_st = s;
@@ -345,10 +349,10 @@ int median_begin(svgd_ctx *c)
         c->regions_alloc = need;
     }
     HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
-    HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->cnt3,
+    HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->cnt3,
                                    c->stream));
     CHK(allreduce_cnt3(c));
-    HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, 3 * sizeof(unsigned long long),
+    HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, 5 * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_cnt, c->stream));
     return SVGD_OK;
@@ -370,6 +374,7 @@ int median_finish(svgd_ctx *c)
     }
     HIPCHK(c, hipEventSynchronize(c->ev_cnt));
     const unsigned long long below = c->h_cnt[0], cand = c->h_cnt[1], ovf = c->h_cnt[2];
+    const uint64_t lo_key = c->h_cnt[3], hi_key = c->h_cnt[4];
     const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
     bool ok = !ovf && r0 >= below && r1 < below + cand;
     int path = c->med_path;
@@ -382,8 +387,17 @@ int median_finish(svgd_ctx *c)
         ranks[0] = c->sel_rank[0];
         ranks[1] = c->sel_rank[c->nsel - 1];
     }
-    CHK(upload_state(c, c->nsel, ranks, 0, ~0ull));
-    for (int p = 0; p < 6; ++p) {
+    // every candidate key lies in [lo_key, hi_key): their common leading bits
+    // are known, so the radix passes start below them (bracket path only)
+    int known_from = 63;
+    if (path == SVGD_MEDIAN_BRACKET && hi_key > lo_key) {
+        const uint64_t diff = lo_key ^ (hi_key - 1);
+        known_from = diff ? 64 - __builtin_clzll(diff) : 0;
+        if (known_from > 63) known_from = 63;
+    }
+    CHK(upload_state(c, c->nsel, ranks, 0, ~0ull, known_from, lo_key));
+    const int passes = (known_from + RADIX_BITS - 1) / RADIX_BITS;
+    for (int p = 0; p < passes; ++p) {
         if (path == SVGD_MEDIAN_FALLBACK) {
             const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 2048));
             HIPCHK(c, pair_pass(c, 1, grid, nullptr, 0, nullptr));
@@ -565,13 +579,13 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->scal, 2));
     CHK(dalloc(c, &c->counts, 4096)); // <= 4 regions per collect block, <= 1024 blocks
     CHK(dalloc(c, &c->below, 4096));
-    CHK(dalloc(c, &c->cnt3, 4));
+    CHK(dalloc(c, &c->cnt3, 8));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
     const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
     HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, 4 * sizeof(unsigned long long), hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_st, sizeof(SelState), hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_scal, 2 * sizeof(double), hipHostMallocDefault));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));

@@ -58,8 +58,8 @@ hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int
                                hipStream_t stream);
 hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream);
 hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
-                                int64_t nblk, int64_t cap, unsigned long long *cnt,
-                                hipStream_t stream);
+                                int64_t nblk, int64_t cap, const SelState *st,
+                                unsigned long long *cnt, hipStream_t stream);
 hipError_t launch_bracket(SelState *st, hipStream_t stream);
 
 // Row-stream path (d <= 16): particle records rec_j = [xc_j | G_j - 2a xc_j | c_j | 0..],

@@ -607,10 +607,12 @@ __global__ __launch_bounds__(256) void k_select_scan(SelState *st, uint32_t *ghi
     }
 }
 
-// Sum per-block collect outputs: counts and below -> cnt[0] = below,
-// cnt[1] = candidates (true count), cnt[2] = 1 if any region overflowed.
+// Sum per-region collect outputs: cnt[0] = below, cnt[1] = candidates (true
+// count), cnt[2] = number of overflowed regions (all sums, so one all-reduce
+// serves every rank); cnt[3..4] = the bracket [lo_key, hi_key) for the host.
 __global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
                                 const uint32_t *__restrict__ counts, int64_t nblk, int64_t cap,
+                                const SelState *__restrict__ st,
                                 unsigned long long *__restrict__ cnt)
 {
     __shared__ unsigned long long s0[256], s1[256], s2[256];
@@ -618,7 +620,7 @@ __global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
     for (int64_t e = threadIdx.x; e < nblk; e += 256) {
         b += below[e];
         c += counts[e];
-        o |= (counts[e] > cap) ? 1ull : 0ull;
+        o += (counts[e] > cap) ? 1ull : 0ull;
     }
     s0[threadIdx.x] = b;
     s1[threadIdx.x] = c;
@@ -628,7 +630,7 @@ __global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
         if ((int)threadIdx.x < k) {
             s0[threadIdx.x] += s0[threadIdx.x + k];
             s1[threadIdx.x] += s1[threadIdx.x + k];
-            s2[threadIdx.x] |= s2[threadIdx.x + k];
+            s2[threadIdx.x] += s2[threadIdx.x + k];
         }
         __syncthreads();
     }
@@ -636,6 +638,8 @@ __global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
         cnt[0] = s0[0];
         cnt[1] = s1[0];
         cnt[2] = s2[0];
+        cnt[3] = st->lo_key;
+        cnt[4] = st->hi_key;
     }
 }
 
@@ -673,21 +677,22 @@ __global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi,
 // ===================================================== row-stream kernels ==
 //
 // gfx950 runs f64 MFMA and f64 VALU on one shared pipeline (tools/ubench_f64:
-// ~64 TF MFMA alone, ~68 TF VALU alone, ~70 TF mixed), so for small d the
-// phi pass minimises f64 instructions per pair instead of using MFMA:
+// ~64 TF MFMA alone, ~68 TF VALU alone, ~70 TF mixed), and these loops are
+// instruction-issue bound (rocprof: one instruction per SIMD per 4 cycles,
+// whatever its type), so for small d the phi pass minimises instructions
+// per pair instead of using MFMA:
 //
-//   lane = particle i (2 rows per lane), column particle j wave-uniform:
-//   x_j, c_j, V_j arrive through scalar loads (SGPR operands, no LDS, no
-//   barriers) and are broadcast into the VALU FMAs.
-//   per (i, j):  dot  d FMA      (Gram form on centred coordinates)
-//                u    add + FMA  (u = 32 * (-a log2e) |x_i - x_j|^2)
-//                2^(u/32)        32-entry LDS table 2^(k/32) x degree-6 poly, ldexp
-//                acc  d FMA + 1  (sum_j K_ij V_j, sum_j K_ij)
-//   ~3d + 14 f64 ops per ordered pair (d = 8: 38, was 54 with MFMA padding).
+//   lane = R particle rows i (pre-scaled by 512 a log2e), column particle j
+//   wave-uniform: its record arrives in LDS by DMA (per-wave double-buffered
+//   chunks) and is read with broadcast ds_read_b128.
+//   per (i, j):  u    add + d FMA    (u = 256 log2 K_ij, Gram form on centred x)
+//                2^(u/256)           256-entry LDS table x degree-4 poly, ldexp
+//                acc  d FMA + 1      (sum_j K_ij V_j, sum_j K_ij)
+//   3d + 11 f64 ops per ordered pair (d = 8: 35 incl. the integer ops).
 // Columns are split over S workgroups (partials reduced by k_phi_reduce in a
 // fixed order, so results are deterministic).
 
-// 2^(i/256), i = 0..255, correctly rounded (tests/golden/make_tables.py)
+// 2^(i/256), i = 0..255, correctly rounded (tools/make_exp_table.py)
 __constant__ double EXP2_TAB256[256] = {
     0x1.0000000000000p+0, 0x1.00b1afa5abcbfp+0, 0x1.0163da9fb3335p+0, 0x1.02168143b0281p+0,
     0x1.02c9a3e778061p+0, 0x1.037d42e11bbccp+0, 0x1.04315e86e7f85p+0, 0x1.04e5f72f654b1p+0,
@@ -1470,11 +1475,11 @@ hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream)
 }
 
 hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
-                                int64_t nblk, int64_t cap, unsigned long long *cnt,
-                                hipStream_t stream)
+                                int64_t nblk, int64_t cap, const SelState *st,
+                                unsigned long long *cnt, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_counts_reduce, dim3(1), dim3(256), 0, stream, below, counts, nblk, cap,
-                       cnt);
+                       st, cnt);
     return hipGetLastError();
 }
 

@@ -119,3 +119,25 @@ def test_python_api_host_side(oracle):
     ref = oracle.logp_grad_gmm(X, np.array([[0.0, 1.0], [1.0, -1.0]]),
                                np.array([[[2.0, 0.3], [0.3, 1.0]], [[1.0, 0.0], [0.0, 1.0]]]))
     np.testing.assert_allclose(m.log_model_grad(X), ref, rtol=1e-12, atol=1e-14)
+
+
+def test_exp2_table_and_coefficients_match_generator():
+    """The kernel's 2^(i/256) table and Taylor coefficients (exp2_256) are the
+    correctly rounded values tools/make_exp_table.py derives at 60 digits."""
+    import importlib.util
+    import os
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("mk", os.path.join(root, "tools", "make_exp_table.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    src = open(os.path.join(root, "svgdcpp_amd", "csrc", "svgd_kernels.hip")).read()
+    body = src[src.index("EXP2_TAB256[256] = {"):]
+    body = body[body.index("{") + 1:body.index("}")]
+    vals = [float.fromhex(v.strip()) for v in body.replace("\n", " ").split(",") if v.strip()]
+    assert vals == mk.table()
+    fn = src[src.index("double exp2_256("):]
+    fn = fn[:fn.index("return")]
+    lits = [float.fromhex(t) for t in re.findall(r"0x1\.[0-9a-f]+p[-+]\d+", fn)]
+    c = mk.coeffs()
+    assert lits == [c[4], c[3], c[2], c[1]]
