@@ -102,6 +102,11 @@ struct svgd_ctx {
     SelState *h_st = nullptr;
     double *h_scal = nullptr;
     hipEvent_t ev_x = nullptr, ev_cnt = nullptr, ev_scal = nullptr;
+    // host<->device copies of the X / G shards run on their own stream so
+    // they overlap the median kernels; RCCL calls stay on `stream` (one
+    // communicator, one issue order on every rank)
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_xready = nullptr, ev_g = nullptr;
 
     // optimizer
     int opt_kind = -1;
@@ -422,17 +427,35 @@ int check_ready(svgd_ctx *c)
     return SVGD_OK;
 }
 
-int upload_g(svgd_ctx *c, const double *G_shard)
+// G shard -> device on the copy stream (ready at ev_g) ...
+int upload_g_begin(svgd_ctx *c, const double *G_shard)
 {
     const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
     if (!G_shard) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null log-gradient buffer.");
     if (c->nrows > 0) {
-        if (G_shard != c->h_g) std::memcpy(c->h_g, G_shard, bytes);
+        if (G_shard != c->h_g) {
+            HIPCHK(c, hipEventSynchronize(c->ev_g)); // the previous upload left h_g
+            std::memcpy(c->h_g, G_shard, bytes);
+        }
         HIPCHK(c, hipMemcpyAsync(c->G + (size_t)c->row0 * c->dim, c->h_g, bytes,
-                                 hipMemcpyHostToDevice, c->stream));
+                                 hipMemcpyHostToDevice, c->cstream));
     }
+    HIPCHK(c, hipEventRecord(c->ev_g, c->cstream));
+    return SVGD_OK;
+}
+
+// ... and, on the compute stream once it needs G, the all-gather of the shards.
+int upload_g_finish(svgd_ctx *c)
+{
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_g, 0));
     CHK(allgather_rows(c, c->G));
     return SVGD_OK;
+}
+
+int upload_g(svgd_ctx *c, const double *G_shard)
+{
+    CHK(upload_g_begin(c, G_shard));
+    return upload_g_finish(c);
 }
 
 int run_phi(svgd_ctx *c)
@@ -477,6 +500,7 @@ int run_opt(svgd_ctx *c)
                                 c->bounded ? c->lower : nullptr, c->bounded ? c->upper : nullptr,
                                 c->stream));
     CHK(allgather_rows(c, c->X));
+    HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
     return SVGD_OK;
 }
 
@@ -539,6 +563,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     }
     HIPCHK(c, hipSetDevice(device));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     const int64_t rows_all = c->chunk * c->world;
     CHK(dalloc(c, &c->X, rows_all * dim));
     CHK(dalloc(c, &c->G, rows_all * dim));
@@ -589,6 +614,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     HIPCHK(c, hipHostMalloc((void **)&c->h_st, sizeof(SelState), hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_scal, 2 * sizeof(double), hipHostMallocDefault));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_xready, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_g, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -639,6 +666,7 @@ int svgd_destroy(svgd_ctx *c)
 {
     if (!c) return SVGD_OK;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
@@ -658,9 +686,12 @@ int svgd_destroy(svgd_ctx *c)
             (void)hipEventDestroy(e.b);
         }
     if (c->ev_x) (void)hipEventDestroy(c->ev_x);
+    if (c->ev_xready) (void)hipEventDestroy(c->ev_xready);
+    if (c->ev_g) (void)hipEventDestroy(c->ev_g);
     if (c->ev_cnt) (void)hipEventDestroy(c->ev_cnt);
     if (c->ev_scal) (void)hipEventDestroy(c->ev_scal);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     delete c;
     return SVGD_OK;
 }
@@ -734,6 +765,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(c->X, X, sizeof(double) * (size_t)c->n * c->dim,
                              hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_particles = true;
     return SVGD_OK;
@@ -798,9 +830,11 @@ int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
     const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
     if (X_shard_out && c->nrows > 0) {
+        // X_t is final once the previous step's update (and all-gather) ran
+        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_xready, 0));
         HIPCHK(c, hipMemcpyAsync(c->h_x, c->X + (size_t)c->row0 * c->dim, bytes,
-                                 hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipEventRecord(c->ev_x, c->stream));
+                                 hipMemcpyDeviceToHost, c->cstream));
+        HIPCHK(c, hipEventRecord(c->ev_x, c->cstream));
     }
     CHK(scale_begin(c));
     if (X_shard_out && c->nrows > 0) {
@@ -813,8 +847,9 @@ int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
 int svgd_finish_step(svgd_ctx *c, const double *G_shard)
 {
     CHK(check_ready(c));
-    CHK(upload_g(c, G_shard));
+    CHK(upload_g_begin(c, G_shard)); // overlaps the median's selection passes
     CHK(scale_finish(c));
+    CHK(upload_g_finish(c));
     CHK(run_phi(c));
     CHK(run_opt(c));
     return SVGD_OK;
