@@ -7,7 +7,8 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 SRC_DIR := svgdcpp_amd/csrc
 LIB := svgdcpp_amd/libsvgdcpp_amd.so
-OBJS := $(SRC_DIR)/svgd_kernels.o $(SRC_DIR)/svgd_capi.o $(SRC_DIR)/plan.o $(SRC_DIR)/host_models.o
+OBJS := $(SRC_DIR)/svgd_kernels.o $(SRC_DIR)/svgd_capi.o $(SRC_DIR)/plan.o $(SRC_DIR)/host_models.o \
+        $(SRC_DIR)/hostcomm.o
 HDRS := $(SRC_DIR)/svgd_kernels.h include/svgdcpp_amd/svgd_capi.h
 
 all: $(LIB)
@@ -21,6 +22,9 @@ $(SRC_DIR)/svgd_capi.o: $(SRC_DIR)/svgd_capi.cpp $(HDRS)
 # host-only translation units (no device code)
 $(SRC_DIR)/plan.o: $(SRC_DIR)/plan.cpp $(HDRS)
 	$(CXX) -O3 -std=c++17 -fPIC -Wall -c $< -o $@
+
+$(SRC_DIR)/hostcomm.o: $(SRC_DIR)/hostcomm.cpp $(SRC_DIR)/hostcomm.h
+	$(HIPCC) -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
 $(SRC_DIR)/host_models.o: $(SRC_DIR)/host_models.cpp $(HDRS)
 	$(CXX) -O3 -std=c++17 -fPIC -fopenmp -Wall -c $< -o $@

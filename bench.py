@@ -101,6 +101,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal only: every rank on one device (SVGD_BENCH_DEVICE=0)
+    if os.environ.get("SVGD_BENCH_DEVICE") is not None:
+        local_rank = int(os.environ["SVGD_BENCH_DEVICE"])
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -19,6 +19,7 @@
 
 #include "../../include/svgdcpp_amd/svgd_capi.h"
 #include "svgd_kernels.h"
+#include "hostcomm.h"
 
 using namespace svgd_amd;
 
@@ -39,6 +40,7 @@ struct svgd_ctx {
     int device = 0;
     int world = 1, rank = 0;
     ncclComm_t comm = nullptr;
+    HostComm *hcomm = nullptr; // SVGD_HOSTCOMM rehearsal backend (ranks sharing one GPU)
     int64_t row0 = 0, row1 = 0, nrows = 0, chunk = 0;
     int KP = 0, NCB = 0, VW = 0;
     int64_t nb = 0, np = 0; // row blocks; padded rows of the work arrays
@@ -206,6 +208,12 @@ int allgather_rows(svgd_ctx *c, double *buf)
 {
     if (c->world == 1) return SVGD_OK;
     const size_t cnt = (size_t)c->chunk * c->dim;
+    if (c->hcomm) {
+        if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(double),
+                               c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-gather failed.");
+        return SVGD_OK;
+    }
     NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclDouble, c->comm,
                              c->stream));
     return SVGD_OK;
@@ -214,6 +222,11 @@ int allgather_rows(svgd_ctx *c, double *buf)
 int allreduce_u32(svgd_ctx *c, uint32_t *buf, size_t cnt)
 {
     if (c->world == 1) return SVGD_OK;
+    if (c->hcomm) {
+        if (hostcomm_allreduce_u32(c->hcomm, buf, cnt, c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
+        return SVGD_OK;
+    }
     NCCLCHK(c, ncclAllReduce(buf, buf, cnt, ncclUint32, ncclSum, c->comm, c->stream));
     return SVGD_OK;
 }
@@ -223,6 +236,11 @@ int allreduce_cnt3(svgd_ctx *c)
     if (c->world == 1) return SVGD_OK;
     // below, candidate and overflowed-region totals are sums; [3..4] (the
     // bracket) is identical on every rank and stays local
+    if (c->hcomm) {
+        if (hostcomm_allreduce_u64(c->hcomm, c->cnt3, 3, c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
+        return SVGD_OK;
+    }
     NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 3, ncclUint64, ncclSum, c->comm, c->stream));
     return SVGD_OK;
 }
@@ -649,11 +667,20 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
     if (!out) return SVGD_ERR_ARG;
     svgd_ctx *c = new svgd_ctx();
     *out = c;
-    if (world < 1 || rank < 0 || rank >= world || (world > 1 && !unique_id128))
+    if (world < 1 || rank < 0 || rank >= world ||
+        (world > 1 && !unique_id128 && !std::getenv("SVGD_HOSTCOMM")))
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid world/rank.");
     c->world = world;
     c->rank = rank;
     CHK(init_ctx(c, dim, n, dtype, device));
+    if (world > 1 && std::getenv("SVGD_HOSTCOMM")) {
+        // rehearsal backend: ranks sharing one GPU, collectives through host shm
+        const size_t slot = std::max<size_t>((size_t)c->chunk * c->dim * sizeof(double),
+                                             2 * RADIX * sizeof(uint32_t));
+        if (hostcomm_create(&c->hcomm, std::getenv("SVGD_HOSTCOMM"), world, rank, slot))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host communicator setup failed.");
+        return SVGD_OK;
+    }
     if (world > 1) {
         ncclUniqueId id;
         std::memcpy(&id, unique_id128, sizeof(id));
@@ -668,6 +695,7 @@ int svgd_destroy(svgd_ctx *c)
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->hcomm) hostcomm_destroy(c->hcomm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part};

@@ -1,0 +1,42 @@
+"""Rank body of tests/test_gpu_multirank.py: one process per rank, all ranks
+on cuda device 0, collectives through the SVGD_HOSTCOMM host backend (RCCL
+refuses two ranks on one device).  Exercises the library's sharded step --
+row shards, pair-tile median with all-reduced counts/histograms, all-gathers
+of G and X -- on the real kernels."""
+import os
+import sys
+import traceback
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def run(rank, world, name, n, d, steps, q):
+    try:
+        os.environ["SVGD_HOSTCOMM"] = name
+        import oracle as O
+        import svgdcpp_amd as S
+        from svgdcpp_amd import _capi as C
+
+        X0 = O.splitmix((n, d), 3.0, 41)
+        mus = O.splitmix((3, d), 3.0, 42)
+        covs = [np.eye(d) * (1.0 + 0.25 * c) for c in range(3)]
+        ctx = S.Context(d, n, device=0, world=world, rank=rank)
+        ctx.set_particles(X0)
+        ctx.set_optimizer(C.SVGD_OPT_ADAM, 0.05, 0.9, 0.999, 1e-8)
+        ctx.set_bounds(-np.full(d, 2.5), np.full(d, 2.5))
+        model = S.GaussianSum(list(mus), list(covs))
+        scales = []
+        for _ in range(steps):
+            ctx.step_with_model(model)
+            scales.append(ctx.last_scale()[:3])
+        X = ctx.get_particles()
+        shard = (ctx.row0, ctx.row1)
+        ctx.close()
+        q.put(("ok", rank, X, scales, shard))
+    except Exception:
+        q.put(("err", rank, traceback.format_exc(), None, None))

@@ -1,0 +1,54 @@
+"""Sharded step rehearsal on one GPU: world = 2 and 3 ranks on device 0 with
+the host shared-memory collective backend (SVGD_HOSTCOMM) vs the same
+problem on one rank.  The median is an exact order statistic, so the scale
+must agree bit for bit; phi sums columns in a different split, so positions
+agree to fp64 rounding (1e-12).  The RCCL calls themselves are the same
+in-place all-gather / sum all-reduce at the same call sites."""
+import multiprocessing as mp
+import os
+import uuid
+
+import numpy as np
+import pytest
+
+import _gpu_rank_worker as W
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_ranks(world, n, d, steps):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = "svgd_" + uuid.uuid4().hex[:12]
+    procs = [ctx.Process(target=W.run, args=(r, world, name, n, d, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            status, rank, X, scales, shard = q.get(timeout=300)
+            assert status == "ok", X
+            out[rank] = (X, scales, shard)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+@pytest.mark.parametrize("world,n", [(2, 3001), (3, 6007)])
+def test_sharded_step_matches_single_rank(world, n):
+    d, steps = 5, 4
+    multi = _run_ranks(world, n, d, steps)
+    single = _run_ranks(1, n, d, steps)[0]
+    X1, s1, _ = single
+    shards = sorted(v[2] for v in multi.values())
+    assert shards[0][0] == 0 and shards[-1][1] == n  # rows partition [0, n)
+    for (a0, a1), (b0, b1) in zip(shards, shards[1:]):
+        assert a1 == b0
+    for rank, (X, scales, _) in multi.items():
+        # every rank holds the all-gathered particles and the same exact scale
+        assert [s[0] for s in scales] == [s[0] for s in s1], (rank, scales, s1)
+        assert [s[2] for s in scales] == [s[2] for s in s1]
+        np.testing.assert_allclose(X, X1, rtol=0, atol=1e-12)
