@@ -49,10 +49,31 @@ def splitmix(shape, scale, seed):
 
 
 def workload(n, d, k):
+    """cfg3 (and cfg4): GMM with k unweighted unnormalised components."""
     X0 = splitmix((n, d), 3.0, 0x5EED)
     mus = splitmix((k, d), 3.0, 0x5EEE)
     covs = np.stack([np.eye(d) * (1.0 + 0.25 * c) for c in range(k)])
     return X0, mus, covs
+
+
+# SURVEY §8(d) configurations (the default cfg3 is the headline metric; the
+# others are reported on request: --config cfg2 / cfg5)
+CONFIGS = {
+    "cfg2": dict(n=16384, d=2, desc="N=16384 d=2 multivariate normal (mvn_example parameters)"),
+    "cfg3": dict(n=65536, d=8, desc="N=65536 d=8 GMM(k=4)"),
+    "cfg4": dict(n=262144, d=8, desc="N=262144 d=8 GMM(k=4)"),
+    "cfg5": dict(n=65536, d=64, desc="N=65536 d=64 multivariate normal (computed in fp64)"),
+}
+
+
+def config_workload(name, n, d, k):
+    if name == "cfg2":
+        mu = np.array([[-0.6871, 0.8010]])
+        cov = 5.0 * np.array([[[0.2260, 0.1652], [0.1652, 0.6779]]])
+        return splitmix((n, d), 3.0, 0x5EED), mu, cov
+    if name == "cfg5":
+        return splitmix((n, d), 3.0, 0x5EED), splitmix((1, d), 0.5, 0x5EEE), np.eye(d)[None]
+    return workload(n, d, k)
 
 
 def cpu_baseline(X0, mus, covs, rows):
@@ -76,7 +97,7 @@ def cpu_baseline(X0, mus, covs, rows):
         "unit": "particle-updates/s",
         "cores": int(o.num_threads()),
         "kind": "port",
-        "sample": f"one step of the N={n} d={d} GMM(k=4) workload restricted to {rows} particle rows "
+        "sample": f"one step of the N={n} d={d} Gaussian-sum(k={len(mus)}) workload restricted to {rows} particle rows "
                   f"(their median pair share, grad log p of all N, phi_hat of {rows} rows against all N, "
                   f"Adam); {dt:.2f} s, OpenMP threads={o.num_threads()}",
     }
@@ -87,11 +108,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=65536)
-    ap.add_argument("--d", type=int, default=8)
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--cpu-rows", type=int, default=8192)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--device-model", action="store_true",
+                    help="grad log p on the device (SURVEY 8(f) rank 1) instead of the host; "
+                         "not the north-star configuration")
     args = ap.parse_args()
 
     import torch
@@ -112,8 +137,12 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local_rank)
 
-    n, d, k = args.n, args.d, args.k
-    X0, mus, covs = workload(n, d, k)
+    cfg = CONFIGS[args.config]
+    n = args.n or cfg["n"]
+    d = args.d or cfg["d"]
+    k = args.k
+    X0, mus, covs = config_workload(args.config, n, d, k)
+    k = len(mus)
 
     uid = None
     if world > 1:
@@ -124,13 +153,21 @@ def main():
     ctx.set_particles(X0)
     ctx.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
     model = S.GaussianSum(list(mus), list(covs))
+    if args.device_model:
+        ctx.set_device_model(model)
+
+    def step():
+        if args.device_model:
+            ctx.step_device()
+        else:
+            ctx.step_with_model(model)
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
     for _ in range(args.warmup):
-        ctx.step_with_model(model)
+        step()
     ctx.sync()
     ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))  # drop warmup events
     ctx.check(ctx.lib.svgd_set_timing(ctx.h, 1))
@@ -139,7 +176,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ctx.step_with_model(model)
+        step()
     ctx.sync()
     torch.cuda.synchronize()
     barrier()
@@ -179,8 +216,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 X0 = 3*U[-1,1]^d, GMM means 3*U[-1,1]^d, cov_k = (1+0.25k) I)",
             "config": {
-                "workload": f"cfg3: N={n} d={d} GMM(k={k}) RBF-median + Adam(0.1,0.9,0.999), fp64, "
-                            f"host grad log p per step",
+                "workload": f"{args.config}: N={n} d={d} {'GMM(k=%d)' % k if k > 1 else 'MVN'} "
+                            f"RBF-median + Adam(0.1,0.9,0.999), fp64, "
+                            f"{'device' if args.device_model else 'host'} grad log p per step",
                 "n": n, "d": d, "k": k, "parallelism": f"rows{world}",
             },
             "roofline": {
@@ -199,6 +237,9 @@ def main():
             "median_path": ["direct", "bracket", "fallback"][path],
             "scale_a": a,
         }
+        if args.config != "cfg3" or args.device_model:
+            out["metric"] = (f"particle-updates/s, {cfg['desc']}"
+                             f"{', device grad log p' if args.device_model else ''} (not the headline config)")
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows)
         print(json.dumps(out), flush=True)

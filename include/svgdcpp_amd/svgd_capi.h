@@ -170,6 +170,15 @@ int svgd_model_destroy(void *model);
 /* G[i] = grad log p(X[i]) for nrows particles (OpenMP over rows). */
 int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G);
 
+/* Mirror a built-in Gaussian-sum model (svgd_model_create) on the device
+ * (MultivariateNormal.hpp:56-61, Model.hpp:55-92):
+ * afterwards svgd_step(ctx, NULL) evaluates grad log p on the device and the
+ * whole step stays in HBM.  NULL removes it.  d <= 64. */
+int svgd_set_device_model(svgd_ctx *ctx, const void *model);
+/* grad log p of the device model at the current particles, this rank's rows
+ * (shard layout like svgd_get_shard). */
+int svgd_device_logp_grad(svgd_ctx *ctx, double *G_shard_out);
+
 /* ---- host-only planning helpers (no GPU needed) ------------------------ */
 
 /* Row shard of rank r among `world` for n particles: equal chunks of

@@ -65,6 +65,8 @@ SIGNATURES = {
     "svgd_get_timing": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(_I64)]),
     "svgd_set_median_tuning": (ctypes.c_int, [_P, _I64, _I64, _I64]),
     "svgd_debug_pair_keys": (ctypes.c_int, [_P, _D, _I64]),
+    "svgd_set_device_model": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "svgd_device_logp_grad": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "svgd_plan_rows": (None, [_I64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "svgd_plan_median_ranks": (ctypes.c_int, [_I64, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "svgd_plan_pair_tiles": (_I64, [_I64, ctypes.c_int, ctypes.c_int, ctypes.c_int]),

@@ -429,6 +429,22 @@ class Context:
             self.g_host[:nr] = model.log_model_grad(self.x_host[:nr])
         self.check(self.lib.svgd_finish_step(self.h, self.g_host_ptr))
 
+    def set_device_model(self, model):
+        """Mirror a GaussianSum on the device; then
+        step_device() runs the whole step, grad log p included, in HBM."""
+        if model is not None and not isinstance(model, GaussianSum):
+            raise TypeError("only the built-in Gaussian-sum models have a device form")
+        self.check(self.lib.svgd_set_device_model(self.h, model._handle if model is not None else None))
+        self._device_model = model  # keep the host handle alive
+
+    def device_logp_grad(self):
+        out = np.empty((self.row1 - self.row0, self.dim), dtype=np.float64)
+        self.check(self.lib.svgd_device_logp_grad(self.h, C.dptr(out)))
+        return out
+
+    def step_device(self):
+        self.check(self.lib.svgd_step(self.h, None))
+
     def sync(self):
         self.check(self.lib.svgd_sync(self.h))
 

@@ -20,14 +20,11 @@
 #include <vector>
 
 #include "../../include/svgdcpp_amd/svgd_capi.h"
+#include "host_models.h"
+
+using svgd_amd::HostModel;
 
 namespace {
-
-struct HostModel {
-    int d = 0, k = 0;
-    std::vector<double> mu;   // k x d
-    std::vector<double> prec; // k x d x d (row-major)
-};
 
 // Gauss-Jordan inverse with partial pivoting; false if singular.
 bool invert(const double *A, int d, double *out)

@@ -20,6 +20,7 @@
 #include "../../include/svgdcpp_amd/svgd_capi.h"
 #include "svgd_kernels.h"
 #include "hostcomm.h"
+#include "host_models.h"
 
 using namespace svgd_amd;
 
@@ -41,6 +42,9 @@ struct svgd_ctx {
     int world = 1, rank = 0;
     ncclComm_t comm = nullptr;
     HostComm *hcomm = nullptr; // SVGD_HOSTCOMM rehearsal backend (ranks sharing one GPU)
+    // device mirror of a built-in Gaussian-sum model (svgd_set_device_model)
+    int dm_k = 0;
+    double *dm_mu = nullptr, *dm_prec = nullptr;
     int64_t row0 = 0, row1 = 0, nrows = 0, chunk = 0;
     int KP = 0, NCB = 0, VW = 0;
     int64_t nb = 0, np = 0; // row blocks; padded rows of the work arrays
@@ -698,7 +702,7 @@ int svgd_destroy(svgd_ctx *c)
     if (c->hcomm) hostcomm_destroy(c->hcomm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
-                       c->part};
+                       c->part,  c->dm_mu, c->dm_prec};
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
@@ -885,8 +889,59 @@ int svgd_finish_step(svgd_ctx *c, const double *G_shard)
 
 int svgd_step(svgd_ctx *c, const double *G_shard)
 {
+    if (G_shard) {
+        CHK(svgd_begin_step(c, nullptr));
+        return svgd_finish_step(c, G_shard);
+    }
+    // fully device-resident step: grad log p from the device model
+    CHK(check_ready(c));
+    if (c->dm_k == 0)
+        return fail(c, SVGD_ERR_ARG,
+                    "[Argument Error] Null log-gradient buffer and no device model set.");
     CHK(svgd_begin_step(c, nullptr));
-    return svgd_finish_step(c, G_shard);
+    HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
+                                c->dm_mu, c->dm_prec, c->G + (size_t)c->row0 * c->dim, c->stream));
+    CHK(scale_finish(c));
+    CHK(allgather_rows(c, c->G));
+    CHK(run_phi(c));
+    CHK(run_opt(c));
+    return SVGD_OK;
+}
+
+int svgd_set_device_model(svgd_ctx *c, const void *model)
+{
+    if (!c) return SVGD_ERR_ARG;
+    if (!model) {
+        c->dm_k = 0;
+        return SVGD_OK;
+    }
+    const HostModel *m = static_cast<const HostModel *>(model);
+    if (m->d != c->dim)
+        return fail(c, SVGD_ERR_DIM, "[Dimension Error] Model dimension does not match the particles.");
+    if (m->d > 64)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Device model supports d <= 64.");
+    CHK(dalloc(c, &c->dm_mu, (int64_t)m->k * m->d));
+    CHK(dalloc(c, &c->dm_prec, (int64_t)m->k * m->d * m->d));
+    HIPCHK(c, hipMemcpyAsync(c->dm_mu, m->mu.data(), sizeof(double) * m->mu.size(),
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->dm_prec, m->prec.data(), sizeof(double) * m->prec.size(),
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->dm_k = m->k;
+    return SVGD_OK;
+}
+
+int svgd_device_logp_grad(svgd_ctx *c, double *G_shard_out)
+{
+    CHK(check_ready(c));
+    if (c->dm_k == 0) return fail(c, SVGD_ERR_UNSET, "[Unset Error] No device model set.");
+    if (!G_shard_out) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null output buffer.");
+    HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
+                                c->dm_mu, c->dm_prec, c->phi, c->stream));
+    HIPCHK(c, hipMemcpyAsync(G_shard_out, c->phi, sizeof(double) * (size_t)c->nrows * c->dim,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SVGD_OK;
 }
 
 int svgd_host_buffers(svgd_ctx *c, double **x_shard, double **g_shard)

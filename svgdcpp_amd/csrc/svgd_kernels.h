@@ -84,6 +84,9 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                             const SelState *st, uint32_t *ghist, double *dbg_out,
                             hipStream_t stream);
 int phi_rows_blocks_per_cu(int d, int R);
+// G = grad log p of the Gaussian-sum model for `rows` particle rows (d <= 64)
+hipError_t launch_gauss_grad(const double *X, int64_t rows, int d, int k, const double *mu,
+                             const double *prec, double *G, hipStream_t stream);
 hipError_t launch_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
                            double *a_out, double *med_out, hipStream_t stream);
 

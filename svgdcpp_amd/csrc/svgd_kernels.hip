@@ -1239,6 +1239,60 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     }
 }
 
+// ================================================ device log-gradient ==
+// grad log p for the built-in Gaussian-sum model (MultivariateNormal.hpp:56-61,
+// Model::operator+ Model.hpp:55-92): p = sum_c exp(-q_c / 2), q_c = (x-mu_c)^T
+// P_c (x-mu_c); grad = sum_c w_c (-P_c (x - mu_c)) / sum_c w_c with
+// w_c = exp(-(q_c - q_min) / 2).  Same operation order as host_models.cpp.
+// One thread per particle row; mu and P are read through the cache.
+template <int D>
+__global__ __launch_bounds__(256) void k_gauss_grad(const double *__restrict__ X, int64_t rows,
+                                                    int d_rt, int k, const double *__restrict__ mu,
+                                                    const double *__restrict__ prec,
+                                                    double *__restrict__ G)
+{
+    constexpr int DM = D > 0 ? D : 64;
+    const int d = D > 0 ? D : d_rt;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= rows) return;
+    double x[DM], acc[DM], diff[DM];
+    for (int r = 0; r < d; ++r) {
+        x[r] = X[i * d + r];
+        acc[r] = 0.0;
+    }
+    // pass 1: q_c and q_min (the host keeps every g_c; here g_c is recomputed
+    // in pass 2 to keep registers bounded -- identical arithmetic)
+    double qmin = __builtin_inf();
+    for (int c = 0; c < k; ++c) {
+        const double *P = prec + (size_t)c * d * d, *m = mu + (size_t)c * d;
+        for (int r = 0; r < d; ++r) diff[r] = x[r] - m[r];
+        double qq = 0.0;
+        for (int r = 0; r < d; ++r) {
+            double s = 0.0;
+            for (int l = 0; l < d; ++l) s += P[r * d + l] * diff[l];
+            qq += diff[r] * s;
+        }
+        qmin = fmin(qmin, 0.5 * qq);
+    }
+    double wsum = 0.0;
+    for (int c = 0; c < k; ++c) {
+        const double *P = prec + (size_t)c * d * d, *m = mu + (size_t)c * d;
+        for (int r = 0; r < d; ++r) diff[r] = x[r] - m[r];
+        double qq = 0.0;
+        double g[DM];
+        for (int r = 0; r < d; ++r) {
+            double s = 0.0;
+            for (int l = 0; l < d; ++l) s += P[r * d + l] * diff[l];
+            g[r] = -s;
+            qq += diff[r] * s;
+        }
+        const double w = exp(-(0.5 * qq - qmin));
+        wsum += w;
+        for (int r = 0; r < d; ++r) acc[r] += w * g[r];
+    }
+    for (int r = 0; r < d; ++r) G[i * d + r] = acc[r] / wsum;
+}
+
 // ============================================================ launchers ==
 
 #define SVGD_ROWS_CASE(Dv)                                                                   \
@@ -1486,6 +1540,29 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
 hipError_t launch_bracket(SelState *st, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_bracket, dim3(1), dim3(1), 0, stream, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_gauss_grad(const double *X, int64_t rows, int d, int k, const double *mu,
+                             const double *prec, double *G, hipStream_t stream)
+{
+    if (rows <= 0) return hipSuccess;
+    const int64_t g = (rows + 255) / 256;
+#define SVGD_GG_CASE(Dv)                                                                     \
+    case Dv:                                                                                 \
+        hipLaunchKernelGGL((k_gauss_grad<Dv>), dim3(g), dim3(256), 0, stream, X, rows, d, k, mu, \
+                           prec, G);                                                         \
+        break;
+    switch (d) {
+        SVGD_GG_CASE(1) SVGD_GG_CASE(2) SVGD_GG_CASE(3) SVGD_GG_CASE(4)
+        SVGD_GG_CASE(5) SVGD_GG_CASE(6) SVGD_GG_CASE(7) SVGD_GG_CASE(8)
+        SVGD_GG_CASE(12) SVGD_GG_CASE(16)
+    default:
+        if (d > 64) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_gauss_grad<0>), dim3(g), dim3(256), 0, stream, X, rows, d, k, mu,
+                           prec, G);
+    }
+#undef SVGD_GG_CASE
     return hipGetLastError();
 }
 
