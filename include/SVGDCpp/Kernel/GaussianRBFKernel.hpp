@@ -2,13 +2,16 @@
  * @file GaussianRBFKernel.hpp
  * @brief Gaussian RBF kernel (reference: include/SVGDCpp/Kernel/GaussianRBFKernel.hpp:22-270).
  *
- * k(x, x') = exp(-(x - x')^T M (x - x')) with M = a I (:75-81).
- *   ScaleMethod::Median   a = ln(N) / med^2, med = median of all N^2 pairwise
- *                         distances of the coordinate matrix (:168-188) --
- *                         recomputed every step ON THE DEVICE by the SVGD driver.
- *   ScaleMethod::Hessian  (:189-210) not on the device path (throws).
+ * k(x, x') = exp(-(x - x')^T M (x - x')) (:75-81).
+ *   ScaleMethod::Median   M = a I, a = ln(N) / med^2, med = median of all N^2
+ *                         pairwise distances of the coordinate matrix (:168-188)
+ *                         -- recomputed every step ON THE DEVICE by the SVGD driver.
+ *   ScaleMethod::Hessian  M = sum_i -hess log p(x_i) / (2 d N) (:189-210) --
+ *                         the model's Hessians summed on the host, M and its
+ *                         Cholesky factor formed on the device each step.
  *   ScaleMethod::Constant extension (the reference's "TODO: constant scale"):
- *                         a fixed M = a I set by UpdateParameters({a * I}).
+ *                         a fixed M set by UpdateParameters({M}), isotropic
+ *                         a I or any symmetric positive-definite matrix.
  * The host methods below (ComputeScale, EvaluateKernel/Grad) restate the
  * kernel for callers that use it directly; SVGD does not call them.
  */
@@ -37,11 +40,8 @@ public:
         : Kernel((size_t)coord_mat_ptr->rows()), scale_method_(method), coord_matrix_ptr_(coord_mat_ptr),
           target_model_ptr_(model_ptr)
     {
-        if (scale_method_ == ScaleMethod::Hessian && !model_ptr)
+        if (scale_method_ == ScaleMethod::Hessian && !model_ptr) // :55-58
             throw UnsetException("Hessian-based scale requires a model.");
-        if (scale_method_ == ScaleMethod::Hessian)
-            throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
-                                        "[Argument error] Hessian scale method is not on the device path.");
         // The reference computes the median scale here (:84) and again in every
         // Step() before it is used (SVGD.hpp:389); the device recomputes it per
         // step, so no O(N^2) host work happens at construction.
@@ -52,12 +52,23 @@ public:
     std::shared_ptr<Kernel> CloneSharedPointer() const override { return std::make_shared<GaussianRBFKernel>(*this); }
 
     ScaleMethod GetScaleMethod() const { return scale_method_; }
+    std::shared_ptr<Model> GetTargetModel() const { return target_model_ptr_; }
 
-    /** a of M = a I (the device path supports isotropic scales only). */
-    double GetScale() const
+    /** The scale matrix M (kernel_parameters_[0]). */
+    const Eigen::MatrixXd &GetScaleMatrix() const { return kernel_parameters_.at(0); }
+
+    /** a of M = a I (M(0,0) for a full matrix). */
+    double GetScale() const { return GetScaleMatrix()(0, 0); }
+
+    /** True when M = a I. */
+    bool IsIsotropic() const
     {
-        const Eigen::MatrixXd &M = kernel_parameters_.at(0);
-        return M(0, 0);
+        const Eigen::MatrixXd &M = GetScaleMatrix();
+        for (long r = 0; r < M.rows(); ++r)
+            for (long c = 0; c < M.cols(); ++c)
+                if (M(r, c) != (r == c ? M(0, 0) : 0.0))
+                    return false;
+        return true;
     }
 
     void UpdateParameters(const std::vector<Eigen::MatrixXd> &params) override
@@ -65,45 +76,64 @@ public:
         const Eigen::MatrixXd &M = params.at(0);
         if (M.rows() != dimension_ || M.cols() != dimension_)
             throw DimensionMismatchException("Kernel scale matrix has incorrect dimensions.");
-        for (long r = 0; r < M.rows(); ++r)
-            for (long c = 0; c < M.cols(); ++c)
-                if (M(r, c) != (r == c ? M(0, 0) : 0.0))
-                    throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
-                                                "[Argument Error] Only isotropic scales M = a I are supported.");
         kernel_parameters_ = {M};
     }
 
-    /** exp(-a |x - location|^2) */
+    /** exp(-(x - location)^T M (x - location)) */
     double EvaluateKernel(const Eigen::VectorXd &x) override
     {
-        const double a = GetScale();
+        const Eigen::MatrixXd &M = GetScaleMatrix();
         double s = 0.0;
-        for (long k = 0; k < dimension_; ++k)
-            s += (-(x(k) - location_(k)) * a) * (x(k) - location_(k));
-        return std::exp(s);
+        for (long r = 0; r < dimension_; ++r)
+        {
+            double t = 0.0;
+            for (long c = 0; c < dimension_; ++c)
+                t += M(r, c) * (x(c) - location_(c));
+            s += (x(r) - location_(r)) * t;
+        }
+        return std::exp(-s);
     }
 
-    /** -2 a (x - location) k(x, location) */
+    /** -2 M (x - location) k(x, location) */
     Eigen::VectorXd EvaluateKernelGrad(const Eigen::VectorXd &x) override
     {
-        const double a = GetScale(), kv = EvaluateKernel(x);
+        const Eigen::MatrixXd &M = GetScaleMatrix();
+        const double kv = EvaluateKernel(x);
         Eigen::VectorXd g(dimension_);
-        for (long k = 0; k < dimension_; ++k)
-            g(k) = -2.0 * a * (x(k) - location_(k)) * kv;
+        for (long r = 0; r < dimension_; ++r)
+        {
+            double t = 0.0;
+            for (long c = 0; c < dimension_; ++c)
+                t += M(r, c) * (x(c) - location_(c));
+            g(r) = -2.0 * t * kv;
+        }
         return g;
     }
 
     /** :141-156 -- host restatement; the SVGD driver computes the scale on the device. */
     void Step() override
     {
-        if (scale_method_ == ScaleMethod::Median)
+        if (scale_method_ != ScaleMethod::Constant)
             kernel_parameters_[0] = ComputeScale();
     }
 
-    /** :164-188 Median heuristic on the host (O(N^2) memory, small N only). */
+    /** :164-210 on the host: the median heuristic (O(N^2) memory, small N
+     *  only) or the Hessian heuristic. */
     Eigen::MatrixXd ComputeScale()
     {
         const Eigen::MatrixXd &X = *coord_matrix_ptr_;
+        if (scale_method_ == ScaleMethod::Hessian)
+        {
+            const long n = X.cols(), d = X.rows();
+            Eigen::MatrixXd H(d, d), M(d, d);
+            std::vector<double> rows((size_t)(n * d)), Hs((size_t)(d * d));
+            std::copy(X.data(), X.data() + n * d, rows.data());
+            target_model_ptr_->NegHessSumBatch(rows.data(), n, Hs.data());
+            for (long r = 0; r < d; ++r)
+                for (long c = 0; c < d; ++c)
+                    M(r, c) = Hs[(size_t)(r * d + c)] / (2.0 * (double)d * (double)n);
+            return M;
+        }
         const long n = X.cols(), d = X.rows();
         std::vector<double> dist((size_t)(n * n));
         for (long j = 0; j < n; ++j)

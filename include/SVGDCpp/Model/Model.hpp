@@ -127,6 +127,46 @@ public:
         }
     }
 
+    /** hess log p at one particle (Model.hpp:366-370).  Gaussian models use
+     *  the closed form; other models override it to use the Hessian scale. */
+    virtual Eigen::MatrixXd EvaluateLogModelHessian(const Eigen::VectorXd &x)
+    {
+        RequireGaussian();
+        Eigen::MatrixXd H((long)dimension_, (long)dimension_);
+        NegHessSumBatch(x.data(), 1, H.data());
+        for (long e = 0; e < H.size(); ++e)
+            H(e) = -H(e);
+        return H;
+    }
+
+    /**
+     * sum_i -hess log p(x_i) over n particles (row-major d x d; symmetric) --
+     * the sum inside the Hessian kernel scale (GaussianRBFKernel.hpp:197-205).
+     */
+    virtual void NegHessSumBatch(const double *X, int64_t n, double *H)
+    {
+        const long d = dimension_;
+        if (!means_.empty())
+        {
+            if (!handle_)
+                Build();
+            const int rc = svgd_model_neg_hess_sum(handle_.get(), X, n, H);
+            if (rc != SVGD_OK)
+                svgdcpp::ThrowFromCode(rc, SVGDCPP_LOG_PREFIX + "[Runtime Error] host model evaluation failed.");
+            return;
+        }
+        std::fill(H, H + d * d, 0.0);
+        Eigen::VectorXd x(d);
+        for (int64_t i = 0; i < n; ++i)
+        {
+            std::copy(X + i * d, X + (i + 1) * d, x.data());
+            const Eigen::MatrixXd h = EvaluateLogModelHessian(x);
+            for (long r = 0; r < d; ++r)
+                for (long c = 0; c < d; ++c)
+                    H[r * d + c] -= h(r, c);
+        }
+    }
+
     /** Model.hpp:377-388: replace the parameter matrices (Gaussian terms: mean0, cov0, mean1, cov1, ...). */
     virtual void UpdateParameters(const std::vector<Eigen::MatrixXd> &params)
     {

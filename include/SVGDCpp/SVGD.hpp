@@ -14,7 +14,9 @@
  * The coordinate matrix stays on the device during Run() and is written back
  * to *CoordinateMatrixPtr at the end (the reference mutates it every step).
  * Requirements of the device path: the kernel is a GaussianRBFKernel
- * (Median or Constant scale) and the optimizer is Adam, AdaGrad or RMSProp.
+ * (Median, Hessian or Constant scale) and the optimizer is Adam, AdaGrad or
+ * RMSProp.  With the Hessian scale, the kernel's model sums -hess log p(X_t)
+ * on the host between the two device calls (GaussianRBFKernel.hpp:189-210).
  * LogIntermediateMatrices re-evaluates K and Kg on the host from the step's
  * scale (debug aid for small N, same text format as SVGD.hpp:345-365).
  */
@@ -178,10 +180,8 @@ public:
                 LogStep(iter, hx, hg);
         }
         Check(svgd_get_particles(c, coord_matrix_ptr_->data()));
-        double a = 0.0;
-        Check(svgd_last_scale(c, &a, nullptr, nullptr));
-        if (rbf_ptr_->GetScaleMethod() == GaussianRBFKernel::ScaleMethod::Median && num_iterations_ > 0)
-            rbf_ptr_->UpdateParameters({a * Eigen::MatrixXd::Identity(dimension_, dimension_)});
+        if (rbf_ptr_->GetScaleMethod() != GaussianRBFKernel::ScaleMethod::Constant && num_iterations_ > 0)
+            rbf_ptr_->UpdateParameters({LastScaleMatrix()});
         if (log_intermediate_matrices_)
             WriteIntermediateMatricesToFile();
     }
@@ -196,6 +196,12 @@ protected:
         svgd_ctx *c = ctx_.get();
         model_ptr_->Step();
         Check(svgd_begin_step(c, hx));
+        if (rbf_ptr_->GetScaleMethod() == GaussianRBFKernel::ScaleMethod::Hessian)
+        {
+            std::vector<double> H((size_t)dimension_ * dimension_);
+            rbf_ptr_->GetTargetModel()->NegHessSumBatch(hx, (int64_t)num_particles_, H.data());
+            Check(svgd_set_step_hessian_sum(c, H.data()));
+        }
         model_ptr_->LogModelGradBatch(hx, (int64_t)num_particles_, hg);
         Check(svgd_finish_step(c, hg));
     }
@@ -212,30 +218,67 @@ protected:
 
     void ConfigureScale()
     {
-        if (rbf_ptr_->GetScaleMethod() == GaussianRBFKernel::ScaleMethod::Constant)
-            Check(svgd_set_scale(ctx_.get(), SVGD_SCALE_FIXED, rbf_ptr_->GetScale()));
-        else
+        switch (rbf_ptr_->GetScaleMethod())
+        {
+        case GaussianRBFKernel::ScaleMethod::Constant:
+            if (rbf_ptr_->IsIsotropic())
+                Check(svgd_set_scale(ctx_.get(), SVGD_SCALE_FIXED, rbf_ptr_->GetScale()));
+            else
+            {
+                const Eigen::MatrixXd &M = rbf_ptr_->GetScaleMatrix();
+                std::vector<double> m((size_t)dimension_ * dimension_);
+                for (int r = 0; r < dimension_; ++r)
+                    for (int q = 0; q < dimension_; ++q)
+                        m[(size_t)r * dimension_ + q] = M(r, q);
+                Check(svgd_set_scale_matrix(ctx_.get(), m.data()));
+            }
+            break;
+        case GaussianRBFKernel::ScaleMethod::Hessian:
+            Check(svgd_set_scale(ctx_.get(), SVGD_SCALE_HESSIAN, 0.0));
+            break;
+        default:
             Check(svgd_set_scale(ctx_.get(), SVGD_SCALE_MEDIAN, 0.0));
+        }
+    }
+
+    /** M of the last step (svgd_get_scale_matrix; row-major -> matrix). */
+    Eigen::MatrixXd LastScaleMatrix()
+    {
+        std::vector<double> m((size_t)dimension_ * dimension_);
+        Check(svgd_get_scale_matrix(ctx_.get(), m.data()));
+        Eigen::MatrixXd M(dimension_, dimension_);
+        for (int r = 0; r < dimension_; ++r)
+            for (int q = 0; q < dimension_; ++q)
+                M(r, q) = m[(size_t)r * dimension_ + q];
+        return M;
     }
 
     /** SVGD.hpp:345-358 text format; K and Kg re-evaluated on the host. */
     void LogStep(size_t iter, const double *hx, const double *hg)
     {
         const long n = (long)num_particles_, d = dimension_;
-        double a = 0.0;
-        Check(svgd_last_scale(ctx_.get(), &a, nullptr, nullptr));
+        const Eigen::MatrixXd M = LastScaleMatrix();
         Eigen::MatrixXd G(d, n), K(n, n), Kg(d * n, n), X(d, n);
         std::copy(hg, hg + n * d, G.data());
+        std::vector<double> diff((size_t)d), Md((size_t)d);
         for (long i = 0; i < n; ++i)
             for (long j = 0; j < n; ++j)
             {
-                double u = 0.0;
                 for (long k = 0; k < d; ++k)
-                    u += (-(hx[j * d + k] - hx[i * d + k]) * a) * (hx[j * d + k] - hx[i * d + k]);
-                const double kv = std::exp(u);
+                    diff[(size_t)k] = hx[j * d + k] - hx[i * d + k];
+                double u = 0.0;
+                for (long r = 0; r < d; ++r)
+                {
+                    double t = 0.0;
+                    for (long q = 0; q < d; ++q)
+                        t += M(r, q) * diff[(size_t)q];
+                    Md[(size_t)r] = t;
+                    u += diff[(size_t)r] * t;
+                }
+                const double kv = std::exp(-u);
                 K(j, i) = kv;
                 for (long k = 0; k < d; ++k)
-                    Kg(j * d + k, i) = -2.0 * a * (hx[j * d + k] - hx[i * d + k]) * kv;
+                    Kg(j * d + k, i) = -2.0 * Md[(size_t)k] * kv;
             }
         Check(svgd_get_particles(ctx_.get(), X.data()));
         intermediate_matrices_sstream_vector_[iter] << "========== Step " << iter + 1 << " =========="

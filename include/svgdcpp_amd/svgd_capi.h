@@ -63,7 +63,9 @@ extern "C" {
  * SVGD_SCALE_FIXED is an extension: M = a*I with a user-set a (the
  * reference's "TODO: constant scale"; used by the test_svgd scenario). */
 #define SVGD_SCALE_MEDIAN 0
+#define SVGD_SCALE_HESSIAN 1 /* M = sum_i -hess log p(x_i) / (2 d N), GaussianRBFKernel.hpp:189-210 */
 #define SVGD_SCALE_FIXED 2
+#define SVGD_SCALE_MATRIX 3  /* extension: a fixed full (SPD) scale matrix M */
 
 /* median path taken by the last svgd_median_scale / step (diagnostics) */
 #define SVGD_MEDIAN_DIRECT 0   /* all pair keys stored and selected exactly */
@@ -102,6 +104,21 @@ int svgd_reset_optimizer(svgd_ctx *ctx);
 int svgd_set_bounds(svgd_ctx *ctx, const double *lower_d, const double *upper_d);
 /* SVGD_SCALE_MEDIAN (default) or SVGD_SCALE_FIXED with M = fixed_a * I. */
 int svgd_set_scale(svgd_ctx *ctx, int method, double fixed_a);
+
+/* Full-matrix kernel scale k(x, x') = exp(-(x-x')^T M (x-x')) (the
+ * reference's M = kernel_parameters_[0], GaussianRBFKernel.hpp:75-81):
+ *  - svgd_set_scale_matrix: a fixed symmetric positive-definite M (d x d,
+ *    row-major); selects SVGD_SCALE_MATRIX.
+ *  - SVGD_SCALE_HESSIAN (svgd_set_scale): every step, between
+ *    svgd_begin_step and svgd_finish_step, the caller passes
+ *    sum_{i in its shard} -hess log p(x_i) (d x d); the context sums it over
+ *    ranks and uses M = sum / (2 d N) for that step (:189-210).
+ *  The phi kernels run on z = L^T x (M = L L^T) with V_j = G_j - 2 M x_j.
+ *  svgd_get_scale_matrix returns the M of the last step (a I for the
+ *  isotropic methods); SVGD_ERR_RUNTIME if M was not positive definite. */
+int svgd_set_scale_matrix(svgd_ctx *ctx, const double *M);
+int svgd_set_step_hessian_sum(svgd_ctx *ctx, const double *H_shard_sum);
+int svgd_get_scale_matrix(svgd_ctx *ctx, double *M_out);
 
 /* ---- particles ---------------------------------------------------------- */
 
@@ -169,6 +186,9 @@ int svgd_model_create(void **model, int dim, int ncomp, const double *mus, const
 int svgd_model_destroy(void *model);
 /* G[i] = grad log p(X[i]) for nrows particles (OpenMP over rows). */
 int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G);
+/* H = sum_i -hess log p(x_i) over nrows particles (d x d, row-major): the sum
+ * of the Hessian scale (GaussianRBFKernel.hpp:197-205, Model.hpp:366-370). */
+int svgd_model_neg_hess_sum(void *model, const double *X, int64_t nrows, double *H);
 
 /* Mirror a built-in Gaussian-sum model (svgd_model_create) on the device
  * (MultivariateNormal.hpp:56-61, Model.hpp:55-92):

@@ -57,6 +57,8 @@ def lib():
         l.or_median_rows_work.argtypes = [_D, ctypes.c_int, _L, _L, _L]
         l.or_median_rows_work.restype = ctypes.c_double
         l.or_num_threads.restype = ctypes.c_int
+        l.or_neg_hess_sum_gmm.argtypes = [_D, ctypes.c_int, _L, ctypes.c_int, _D, _D, _D]
+        l.or_phi_matrix_rows.argtypes = [_D, _D, ctypes.c_int, _L, _D, _L, _L, _D]
         _lib = l
     return _lib
 
@@ -188,6 +190,35 @@ def median_rows_work(X, i0, i1) -> float:
     timing a bounded sample of a large step."""
     n, d = X.shape
     return lib().or_median_rows_work(_p(np.ascontiguousarray(X)), d, n, i0, i1)
+
+
+def neg_hess_sum_gmm(X, mus, covs):
+    """-sum_i hess log p(x_i) for the Gaussian-sum model (d x d)."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    n, d = X.shape
+    mus = np.ascontiguousarray(mus, dtype=np.float64)
+    covs = np.ascontiguousarray(covs, dtype=np.float64)
+    H = np.empty((d, d))
+    lib().or_neg_hess_sum_gmm(_p(X), d, n, mus.shape[0], _p(mus), _p(covs), _p(H))
+    return H
+
+
+def hessian_scale(X, mus, covs):
+    """GaussianRBFKernel.hpp:189-210: M = sum_i -hess log p(x_i) / (2 d N)."""
+    n, d = np.asarray(X).shape
+    return neg_hess_sum_gmm(X, mus, covs) / (2.0 * d * n)
+
+
+def phi_matrix(X, G, M, rows=None):
+    """phi_hat with a full kernel scale matrix M (rows [i0, i1))."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    n, d = X.shape
+    i0, i1 = rows if rows is not None else (0, n)
+    out = np.empty((i1 - i0, d))
+    M = np.ascontiguousarray(M, dtype=np.float64)
+    lib().or_phi_matrix_rows(_p(X), _p(np.ascontiguousarray(G, dtype=np.float64)), d, n, _p(M),
+                             i0, i1, _p(out))
+    return out
 
 
 def num_threads() -> int:

@@ -365,6 +365,89 @@ void or_logp_grad_gmm(const double *X, int d, long n, int k, const double *mu,
     free(prec);
 }
 
+/* -∑_i ∇² log p(x_i) for the Gaussian-sum model over n particles, the sum
+ * inside the Hessian scale (GaussianRBFKernel.hpp:189-210 with
+ * Model::EvaluateLogModelHessian, Model.hpp:366-370).  With w = softmax(-q/2)
+ * and g_c = -P_c (x - μ_c):
+ *   ∇² log p = ∑_c w_c (g_c g_cᵀ - P_c) - (∑_c w_c g_c)(∑_c w_c g_c)ᵀ.
+ * H_out: d×d row-major (symmetric), accumulated serially in particle order. */
+void or_neg_hess_sum_gmm(const double *X, int d, long n, int k, const double *mu,
+                         const double *cov, double *H_out)
+{
+    double *prec = (double *)malloc(sizeof(double) * (size_t)k * d * d);
+    for (int c = 0; c < k; ++c) invert((double *)cov + (size_t)c * d * d, d, prec + (size_t)c * d * d);
+    double *H = (double *)calloc((size_t)d * d, sizeof(double));
+    double q[64], gc[64 * 64], diff[256], gbar[256];
+    for (long i = 0; i < n; ++i) {
+        const double *x = X + i * d;
+        double qmin = INFINITY;
+        for (int c = 0; c < k; ++c) {
+            const double *P = prec + (size_t)c * d * d;
+            for (int r = 0; r < d; ++r) diff[r] = x[r] - mu[c * d + r];
+            double qq = 0.0;
+            for (int r = 0; r < d; ++r) {
+                double s = 0.0;
+                for (int l = 0; l < d; ++l) s += P[r * d + l] * diff[l];
+                gc[c * d + r] = -s;
+                qq += diff[r] * s;
+            }
+            q[c] = 0.5 * qq;
+            if (q[c] < qmin) qmin = q[c];
+        }
+        double wsum = 0.0;
+        for (int c = 0; c < k; ++c) { q[c] = exp(-(q[c] - qmin)); wsum += q[c]; }
+        for (int c = 0; c < k; ++c) q[c] /= wsum;
+        for (int r = 0; r < d; ++r) {
+            double s = 0.0;
+            for (int c = 0; c < k; ++c) s += q[c] * gc[c * d + r];
+            gbar[r] = s;
+        }
+        for (int r = 0; r < d; ++r)
+            for (int l = 0; l < d; ++l) {
+                double h = 0.0;
+                for (int c = 0; c < k; ++c)
+                    h += q[c] * (gc[c * d + r] * gc[c * d + l] - prec[(size_t)c * d * d + r * d + l]);
+                h -= gbar[r] * gbar[l];
+                H[r * d + l] -= h;
+            }
+    }
+    memcpy(H_out, H, sizeof(double) * (size_t)d * d);
+    free(H);
+    free(prec);
+}
+
+/* φ̂ for a full (symmetric) kernel scale matrix M: k(x, x') = exp(-(x-x')ᵀ M (x-x')),
+ * ∇ₓ k = -2 M (x - x') k (GaussianRBFKernel.hpp:75-81 with M = kernel_parameters_[0],
+ * the Hessian scale of :189-210 or a user-set constant).  Rows [i0, i1). */
+void or_phi_matrix_rows(const double *X, const double *G, int d, long n, const double *M,
+                        long i0, long i1, double *phi)
+{
+    const double inv_n = 1.0 / (double)n;
+#pragma omp parallel for schedule(dynamic, 16)
+    for (long i = i0; i < i1; ++i) {
+        double accg[256], acck[256], diff[256], Md[256];
+        for (int k = 0; k < d; ++k) { accg[k] = 0.0; acck[k] = 0.0; }
+        const double *xi = X + i * d;
+        for (long j = 0; j < n; ++j) {
+            const double *xj = X + j * d;
+            for (int k = 0; k < d; ++k) diff[k] = xj[k] - xi[k];
+            double u = 0.0;
+            for (int r = 0; r < d; ++r) {
+                double s = 0.0;
+                for (int l = 0; l < d; ++l) s += M[r * d + l] * diff[l];
+                Md[r] = s;
+                u += diff[r] * s;
+            }
+            const double kv = exp(-u);
+            for (int k = 0; k < d; ++k) {
+                accg[k] += G[j * d + k] * kv;
+                acck[k] += -2.0 * Md[k] * kv;
+            }
+        }
+        for (int k = 0; k < d; ++k) phi[(i - i0) * d + k] = inv_n * (accg[k] + acck[k]);
+    }
+}
+
 int or_num_threads(void)
 {
 #ifdef _OPENMP

@@ -28,6 +28,8 @@ SVGD_OPT_ADAGRAD = 1
 SVGD_OPT_RMSPROP = 2
 SVGD_SCALE_MEDIAN = 0
 SVGD_SCALE_FIXED = 2
+SVGD_SCALE_MATRIX = 3
+SVGD_SCALE_HESSIAN = 1
 SVGD_MEDIAN_DIRECT = 0
 SVGD_MEDIAN_BRACKET = 1
 SVGD_MEDIAN_FALLBACK = 2
@@ -65,6 +67,9 @@ SIGNATURES = {
     "svgd_get_timing": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(_I64)]),
     "svgd_set_median_tuning": (ctypes.c_int, [_P, _I64, _I64, _I64]),
     "svgd_debug_pair_keys": (ctypes.c_int, [_P, _D, _I64]),
+    "svgd_set_scale_matrix": (ctypes.c_int, [_P, _D]),
+    "svgd_set_step_hessian_sum": (ctypes.c_int, [_P, _D]),
+    "svgd_get_scale_matrix": (ctypes.c_int, [_P, _D]),
     "svgd_set_device_model": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "svgd_device_logp_grad": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "svgd_plan_rows": (None, [_I64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
@@ -75,6 +80,7 @@ SIGNATURES = {
     "svgd_model_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.c_int, _D, _D]),
     "svgd_model_destroy": (ctypes.c_int, [_P]),
     "svgd_model_logp_grad": (ctypes.c_int, [_P, _D, _I64, _D]),
+    "svgd_model_neg_hess_sum": (ctypes.c_int, [_P, _D, _I64, _D]),
 }
 
 _lib = None

@@ -94,6 +94,17 @@ class Model:
         X = np.asarray(X, dtype=np.float64)
         return np.stack([np.asarray(self.EvaluateLogModelGrad(x), dtype=np.float64) for x in X])
 
+    def EvaluateLogModelHessian(self, x):  # Model.hpp:366-370
+        raise UnsetException("Model function is unset.")
+
+    def neg_hess_sum(self, X):
+        """sum_i -hess log p(x_i): the sum inside the Hessian kernel scale."""
+        X = np.asarray(X, dtype=np.float64)
+        H = np.zeros((self.dimension_, self.dimension_))
+        for x in X:
+            H -= np.asarray(self.EvaluateLogModelHessian(x), dtype=np.float64)
+        return H
+
     def __add__(self, other):  # Model.hpp:55-92
         if not isinstance(other, Model) or self.dimension_ != other.dimension_:
             raise DimensionMismatchException("Only models with the same variable dimensions can be added.")
@@ -156,6 +167,20 @@ class GaussianSum(Model):
     def EvaluateLogModelGrad(self, x):
         return self.log_model_grad(np.asarray(x, dtype=np.float64).reshape(1, -1))[0]
 
+    def neg_hess_sum(self, X):
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        H = np.empty((self.dimension_, self.dimension_))
+        C.lib().svgd_model_neg_hess_sum(self._handle, C.dptr(X), X.shape[0], C.dptr(H))
+        return H
+
+    def neg_hess_sum_ptr(self, x_ptr, n):
+        H = np.empty((self.dimension_, self.dimension_))
+        C.lib().svgd_model_neg_hess_sum(self._handle, x_ptr, n, C.dptr(H))
+        return H
+
+    def EvaluateLogModelHessian(self, x):
+        return -self.neg_hess_sum(np.asarray(x, dtype=np.float64).reshape(1, -1))
+
     def EvaluateLogModel(self, x):
         x = np.asarray(x, dtype=np.float64).reshape(-1)
         q = [0.5 * (x - m) @ np.linalg.solve(c, x - m) for m, c in zip(self.means_, self.covs_)]
@@ -214,11 +239,14 @@ class Kernel:
 
 
 class GaussianRBFKernel(Kernel):
-    """GaussianRBFKernel.hpp:22-270: k(x, x') = exp(-(x-x')ᵀ M (x-x')), M = a I.
+    """GaussianRBFKernel.hpp:22-270: k(x, x') = exp(-(x-x')ᵀ M (x-x')).
 
-    ScaleMethod.Median recomputes a = ln(N)/med² every step on the device;
+    ScaleMethod.Median recomputes M = a I, a = ln(N)/med², every step on the
+    device; ScaleMethod.Hessian recomputes M = Σ_i -∇²log p(x_i) / (2dN)
+    every step (:189-210; the model supplies the Hessian on the host);
     ScaleMethod.Constant (extension; the reference's "TODO: constant scale")
-    keeps a fixed a (UpdateParameters([a * I]))."""
+    keeps a fixed M set by UpdateParameters([M]) -- isotropic a I or any
+    symmetric positive-definite matrix."""
 
     class ScaleMethod(enum.IntEnum):
         Median = 0
@@ -230,21 +258,26 @@ class GaussianRBFKernel(Kernel):
         super().__init__(np.asarray(coord_matrix).shape[0])
         if method == GaussianRBFKernel.ScaleMethod.Hessian and model is None:
             raise UnsetException("Hessian-based scale requires a model.")
-        if method == GaussianRBFKernel.ScaleMethod.Hessian:
-            raise ValueError(PREFIX + "[Argument error] Hessian scale is not on the device path yet.")
-        if method not in (GaussianRBFKernel.ScaleMethod.Median, GaussianRBFKernel.ScaleMethod.Constant):
+        if method not in tuple(GaussianRBFKernel.ScaleMethod):
             raise ValueError(PREFIX + "[Argument error] Invalid scale method Enum provided.")
         self.scale_method_ = method
         self.coord_matrix_ = coord_matrix
         self.target_model_ = model
         self.scale_ = float(scale)
+        self.scale_matrix_ = None  # full M for ScaleMethod.Constant
 
     def UpdateParameters(self, params):
         M = np.asarray(params[0], dtype=np.float64)
-        a = float(M) if M.ndim == 0 else float(M[0, 0])
-        if M.ndim == 2 and not np.allclose(M, a * np.eye(M.shape[0])):
-            raise ValueError(PREFIX + "[Argument Error] Only isotropic M = a*I is supported.")
-        self.scale_ = a
+        if M.ndim == 0:
+            self.scale_, self.scale_matrix_ = float(M), None
+            return
+        if M.shape != (self.dimension_, self.dimension_):
+            raise DimensionMismatchException("Kernel scale matrix has incorrect dimensions.")
+        a = float(M[0, 0])
+        if np.array_equal(M, a * np.eye(M.shape[0])):
+            self.scale_, self.scale_matrix_ = a, None
+        else:
+            self.scale_matrix_ = M.copy()
 
 
 # -------------------------------------------------------------- optimizers --
@@ -418,16 +451,34 @@ class Context:
         self.check(self.lib.svgd_last_scale(self.h, ctypes.byref(a), ctypes.byref(m), ctypes.byref(p)))
         return a.value, m.value, p.value
 
-    def step_with_model(self, model):
+    def step_with_model(self, model, hessian=False):
         """One SVGD::Step with host gradients from `model` (overlapped with the
-        device median via begin/finish)."""
+        device median via begin/finish).  hessian=True: the Hessian kernel
+        scale, with this shard's sum of -hess log p supplied from `model`."""
         self.check(self.lib.svgd_begin_step(self.h, self.x_host_ptr))
         nr = self.row1 - self.row0
+        if hessian:
+            H = (model.neg_hess_sum_ptr(self.x_host_ptr, nr) if isinstance(model, GaussianSum)
+                 else model.neg_hess_sum(self.x_host[:nr]))
+            self.set_step_hessian_sum(H)
         if isinstance(model, GaussianSum):
             model.log_model_grad_ptr(self.x_host_ptr, nr, self.g_host_ptr)
         elif nr > 0:
             self.g_host[:nr] = model.log_model_grad(self.x_host[:nr])
         self.check(self.lib.svgd_finish_step(self.h, self.g_host_ptr))
+
+    def set_scale_matrix(self, M):
+        M = np.ascontiguousarray(M, dtype=np.float64)
+        self.check(self.lib.svgd_set_scale_matrix(self.h, C.dptr(M)))
+
+    def set_step_hessian_sum(self, H):
+        H = np.ascontiguousarray(H, dtype=np.float64)
+        self.check(self.lib.svgd_set_step_hessian_sum(self.h, C.dptr(H)))
+
+    def get_scale_matrix(self):
+        M = np.empty((self.dim, self.dim))
+        self.check(self.lib.svgd_get_scale_matrix(self.h, C.dptr(M)))
+        return M
 
     def set_device_model(self, model):
         """Mirror a GaussianSum on the device; then
@@ -515,7 +566,12 @@ class SVGD:
         c.set_bounds(*(self.bounds_ if self.bounds_ is not None else (None, None)))
         k = self.kernel_
         if k.scale_method_ == GaussianRBFKernel.ScaleMethod.Constant:
-            c.set_scale(C.SVGD_SCALE_FIXED, k.scale_)
+            if k.scale_matrix_ is not None:
+                c.set_scale_matrix(k.scale_matrix_)
+            else:
+                c.set_scale(C.SVGD_SCALE_FIXED, k.scale_)
+        elif k.scale_method_ == GaussianRBFKernel.ScaleMethod.Hessian:
+            c.set_scale(C.SVGD_SCALE_HESSIAN, 0.0)
         else:
             c.set_scale(C.SVGD_SCALE_MEDIAN, 0.0)
         self._initialized = True
@@ -527,9 +583,22 @@ class SVGD:
             raise UnsetException("SVGD::Initialize must be called before Run.")
         c = self.ctx
         c.set_particles(np.ascontiguousarray(self.coord_matrix_.T))
+        hess = self.kernel_.scale_method_ == GaussianRBFKernel.ScaleMethod.Hessian
+        hmodel = self.kernel_.target_model_ if hess else None
         for _ in range(self.num_iterations_):
             self.model_.Step()
-            c.step_with_model(self.model_)
+            if hess and hmodel is not self.model_:
+                # the kernel's own model supplies the Hessian (GaussianRBFKernel.hpp:202)
+                c.check(c.lib.svgd_begin_step(c.h, c.x_host_ptr))
+                nr = c.row1 - c.row0
+                c.set_step_hessian_sum(hmodel.neg_hess_sum(c.x_host[:nr]))
+                if isinstance(self.model_, GaussianSum):
+                    self.model_.log_model_grad_ptr(c.x_host_ptr, nr, c.g_host_ptr)
+                elif nr > 0:
+                    c.g_host[:nr] = self.model_.log_model_grad(c.x_host[:nr])
+                c.check(c.lib.svgd_finish_step(c.h, c.g_host_ptr))
+            else:
+                c.step_with_model(self.model_, hessian=hess)
         X = c.get_particles()
         self.coord_matrix_[...] = X.T
 

@@ -15,6 +15,7 @@
 // Rows are evaluated in parallel with OpenMP (the reference evaluates them
 // serially even in parallel mode, SVGD.hpp:412-416).
 #include <cmath>
+#include <omp.h>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -120,6 +121,69 @@ int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G)
             }
         }
     }
+    return SVGD_OK;
+}
+
+int svgd_model_neg_hess_sum(void *model, const double *X, int64_t nrows, double *H)
+{
+    // -sum_i hess log p(x_i) (GaussianRBFKernel.hpp:197-205 with
+    // Model::EvaluateLogModelHessian, Model.hpp:366-370), closed form:
+    //   hess log p = sum_c w_c (g_c g_c^T - P_c) - gbar gbar^T,  gbar = sum_c w_c g_c,
+    // w = softmax(-q/2), g_c = -P_c (x - mu_c).  Per-thread partial sums are
+    // added in thread order (deterministic for a fixed thread count).
+    const HostModel *m = static_cast<const HostModel *>(model);
+    if (!m || !H || (!X && nrows > 0)) return SVGD_ERR_ARG;
+    const int d = m->d, k = m->k;
+    const size_t dd = (size_t)d * d;
+    std::vector<std::vector<double>> part;
+#pragma omp parallel
+    {
+#pragma omp single
+        part.assign((size_t)omp_get_num_threads(), std::vector<double>(dd, 0.0));
+        std::vector<double> &Hp = part[(size_t)omp_get_thread_num()];
+        std::vector<double> diff(d), gc((size_t)k * d), q(k), gbar(d);
+#pragma omp for schedule(static)
+        for (int64_t i = 0; i < nrows; ++i) {
+            const double *x = X + i * d;
+            double qmin = INFINITY;
+            for (int c = 0; c < k; ++c) {
+                const double *P = m->prec.data() + (size_t)c * dd;
+                const double *mu = m->mu.data() + (size_t)c * d;
+                for (int r = 0; r < d; ++r) diff[r] = x[r] - mu[r];
+                double qq = 0.0;
+                for (int r = 0; r < d; ++r) {
+                    double s = 0.0;
+                    for (int l = 0; l < d; ++l) s += P[r * d + l] * diff[l];
+                    gc[(size_t)c * d + r] = -s;
+                    qq += diff[r] * s;
+                }
+                q[c] = 0.5 * qq;
+                qmin = q[c] < qmin ? q[c] : qmin;
+            }
+            double wsum = 0.0;
+            for (int c = 0; c < k; ++c) {
+                q[c] = std::exp(-(q[c] - qmin));
+                wsum += q[c];
+            }
+            for (int c = 0; c < k; ++c) q[c] /= wsum;
+            for (int r = 0; r < d; ++r) {
+                double s = 0.0;
+                for (int c = 0; c < k; ++c) s += q[c] * gc[(size_t)c * d + r];
+                gbar[r] = s;
+            }
+            for (int r = 0; r < d; ++r)
+                for (int l = 0; l < d; ++l) {
+                    double h = 0.0;
+                    for (int c = 0; c < k; ++c)
+                        h += q[c] * (gc[(size_t)c * d + r] * gc[(size_t)c * d + l] -
+                                     m->prec[(size_t)c * dd + (size_t)r * d + l]);
+                    Hp[(size_t)r * d + l] -= h - gbar[r] * gbar[l];
+                }
+        }
+    }
+    for (size_t e = 0; e < dd; ++e) H[e] = 0.0;
+    for (const auto &Hp : part)
+        for (size_t e = 0; e < dd; ++e) H[e] += Hp[e];
     return SVGD_OK;
 }
 

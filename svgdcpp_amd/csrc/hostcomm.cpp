@@ -162,6 +162,11 @@ int hostcomm_allreduce_u32(HostComm *c, uint32_t *dbuf, size_t cnt, hipStream_t 
     return allreduce_sum(c, dbuf, cnt, stream);
 }
 
+int hostcomm_allreduce_f64(HostComm *c, double *dbuf, size_t cnt, hipStream_t stream)
+{
+    return allreduce_sum(c, dbuf, cnt, stream);
+}
+
 int hostcomm_allreduce_u64(HostComm *c, unsigned long long *dbuf, size_t cnt, hipStream_t stream)
 {
     return allreduce_sum(c, dbuf, cnt, stream);

@@ -121,6 +121,12 @@ struct svgd_ctx {
     bool bounded = false;
     int scale_method = SVGD_SCALE_MEDIAN;
     double fixed_a = 1.0;
+    // full-matrix scale (SVGD_SCALE_MATRIX / SVGD_SCALE_HESSIAN): device M, its
+    // Cholesky factor L, the (rank-summed) Hessian sum, wv = 2 M xc, zc = L^T xc
+    double *sc_src = nullptr, *sc_M = nullptr, *sc_L = nullptr, *wv = nullptr, *zc = nullptr;
+    int *sc_err = nullptr, *h_err = nullptr;
+    bool hess_ready = false; // Hessian sum supplied for the current step
+    std::vector<double> h_mat;
     bool have_particles = false;
 
     // timing
@@ -246,6 +252,20 @@ int allreduce_cnt3(svgd_ctx *c)
         return SVGD_OK;
     }
     NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 3, ncclUint64, ncclSum, c->comm, c->stream));
+    return SVGD_OK;
+}
+
+bool matrix_scale(const svgd_ctx *c);
+
+int allreduce_f64(svgd_ctx *c, double *buf, size_t cnt)
+{
+    if (c->world == 1) return SVGD_OK;
+    if (c->hcomm) {
+        if (hostcomm_allreduce_f64(c->hcomm, buf, cnt, c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
+        return SVGD_OK;
+    }
+    NCCLCHK(c, ncclAllReduce(buf, buf, cnt, ncclDouble, ncclSum, c->comm, c->stream));
     return SVGD_OK;
 }
 
@@ -480,9 +500,29 @@ int upload_g(svgd_ctx *c, const double *G_shard)
     return upload_g_finish(c);
 }
 
+bool matrix_scale(const svgd_ctx *c)
+{
+    return c->scale_method == SVGD_SCALE_MATRIX || c->scale_method == SVGD_SCALE_HESSIAN;
+}
+
 int run_phi(svgd_ctx *c)
 {
-    if (c->rowpath)
+    const bool mat = matrix_scale(c);
+    if (mat) {
+        // M = factor * src, L = chol(M), a_eff = 1 (GaussianRBFKernel.hpp:189-210)
+        const double factor = c->scale_method == SVGD_SCALE_HESSIAN
+                                  ? 1.0 / (2.0 * (double)c->dim * (double)c->n)
+                                  : 1.0;
+        HIPCHK(c, launch_scale_chol(c->sc_src, factor, c->dim, c->sc_M, c->sc_L, c->scal, c->sc_err,
+                                    c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_err, c->sc_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        if (c->rowpath)
+            HIPCHK(c, launch_prep_rec_mat(c->xc, c->G, c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
+                                          c->RS, c->rec, c->wv, c->stream));
+        else
+            HIPCHK(c, launch_prep_v_mat(c->xc, c->G, c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
+                                        c->VW, c->zc, c->V, c->cvec, c->wv, c->stream));
+    } else if (c->rowpath)
         HIPCHK(c, launch_prep_rec(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->RS,
                                   c->rec, c->stream));
     else
@@ -495,10 +535,12 @@ int run_phi(svgd_ctx *c)
     }
     if (c->rowpath)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
-                                  c->ldp, 1.0 / (double)c->n, c->phi, c->stream));
+                                  c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr, c->phi,
+                                  c->stream));
     else
-        HIPCHK(c, launch_phi(c->KP, c->NCB, c->xc, c->cvec, c->V, c->scal, c->row0, c->nrows,
-                             (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n, c->phi, c->stream));
+        HIPCHK(c, launch_phi(c->KP, c->NCB, mat ? c->zc : c->xc, c->cvec, c->V, c->scal, c->row0,
+                             c->nrows, (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n,
+                             mat ? c->wv : nullptr, c->phi, c->stream));
     if (c->timing) {
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         c->ev_phi.push_back(ev);
@@ -529,7 +571,7 @@ int run_opt(svgd_ctx *c)
 int scale_begin(svgd_ctx *c)
 {
     CHK(center(c));
-    if (c->scale_method == SVGD_SCALE_FIXED) return SVGD_OK;
+    if (c->scale_method == SVGD_SCALE_FIXED || matrix_scale(c)) return SVGD_OK;
     EvPair ev{};
     if (c->timing) {
         ev = take_pair(c);
@@ -541,6 +583,13 @@ int scale_begin(svgd_ctx *c)
 
 int scale_finish(svgd_ctx *c)
 {
+    if (c->scale_method == SVGD_SCALE_HESSIAN && !c->hess_ready)
+        return fail(c, SVGD_ERR_UNSET,
+                    "[Unset Error] Hessian scale: svgd_set_step_hessian_sum was not called this step.");
+    if (matrix_scale(c)) {
+        c->hess_ready = false;
+        return SVGD_OK;
+    }
     if (c->scale_method == SVGD_SCALE_FIXED) {
         c->h_scal[0] = c->fixed_a;
         c->h_scal[1] = NAN;
@@ -679,8 +728,9 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
     CHK(init_ctx(c, dim, n, dtype, device));
     if (world > 1 && std::getenv("SVGD_HOSTCOMM")) {
         // rehearsal backend: ranks sharing one GPU, collectives through host shm
-        const size_t slot = std::max<size_t>((size_t)c->chunk * c->dim * sizeof(double),
-                                             2 * RADIX * sizeof(uint32_t));
+        const size_t slot = std::max<size_t>(
+            std::max<size_t>((size_t)c->chunk * c->dim, (size_t)c->dim * c->dim) * sizeof(double),
+            2 * RADIX * sizeof(uint32_t));
         if (hostcomm_create(&c->hcomm, std::getenv("SVGD_HOSTCOMM"), world, rank, slot))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host communicator setup failed.");
         return SVGD_OK;
@@ -702,14 +752,14 @@ int svgd_destroy(svgd_ctx *c)
     if (c->hcomm) hostcomm_destroy(c->hcomm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
-                       c->part,  c->dm_mu, c->dm_prec};
+                       c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc};
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
-                     c->xf,          c->nmax};
+                     c->xf,          c->nmax,    c->sc_err};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
-    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal};
+    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal, c->h_err};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
     for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})
@@ -781,13 +831,79 @@ int svgd_set_bounds(svgd_ctx *c, const double *lower, const double *upper)
     return SVGD_OK;
 }
 
+int alloc_matrix_scale(svgd_ctx *c)
+{
+    if (c->sc_M) return SVGD_OK;
+    const int64_t dd = (int64_t)c->dim * c->dim;
+    CHK(dalloc(c, &c->sc_src, dd));
+    CHK(dalloc(c, &c->sc_M, dd));
+    CHK(dalloc(c, &c->sc_L, dd));
+    CHK(dalloc(c, &c->wv, c->np * c->dim));
+    if (!c->rowpath) CHK(dalloc(c, &c->zc, c->np * c->KP));
+    CHK(dalloc(c, &c->sc_err, 1));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_err, sizeof(int), hipHostMallocDefault));
+    *c->h_err = 0;
+    return SVGD_OK;
+}
+
 int svgd_set_scale(svgd_ctx *c, int method, double fixed_a)
 {
     if (!c) return SVGD_ERR_ARG;
-    if (method != SVGD_SCALE_MEDIAN && method != SVGD_SCALE_FIXED)
+    if (method != SVGD_SCALE_MEDIAN && method != SVGD_SCALE_FIXED && method != SVGD_SCALE_HESSIAN)
         return fail(c, SVGD_ERR_ARG, "[Argument error] Invalid scale method Enum provided.");
+    if (method == SVGD_SCALE_HESSIAN) CHK(alloc_matrix_scale(c));
     c->scale_method = method;
     c->fixed_a = fixed_a;
+    c->hess_ready = false;
+    return SVGD_OK;
+}
+
+int svgd_set_scale_matrix(svgd_ctx *c, const double *M)
+{
+    if (!c || !M) return c ? fail(c, SVGD_ERR_ARG, "[Argument Error] Null scale matrix.") : SVGD_ERR_ARG;
+    const int d = c->dim;
+    for (int r = 0; r < d; ++r)
+        for (int q = 0; q < r; ++q)
+            if (M[r * d + q] != M[q * d + r])
+                return fail(c, SVGD_ERR_ARG, "[Argument Error] The kernel scale matrix must be symmetric.");
+    CHK(alloc_matrix_scale(c));
+    HIPCHK(c, hipMemcpyAsync(c->sc_src, M, sizeof(double) * (size_t)d * d, hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->scale_method = SVGD_SCALE_MATRIX;
+    return SVGD_OK;
+}
+
+int svgd_set_step_hessian_sum(svgd_ctx *c, const double *H_shard_sum)
+{
+    if (!c || !H_shard_sum) return c ? fail(c, SVGD_ERR_ARG, "[Argument Error] Null Hessian sum.") : SVGD_ERR_ARG;
+    if (c->scale_method != SVGD_SCALE_HESSIAN)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] The kernel scale method is not Hessian.");
+    const size_t dd = (size_t)c->dim * c->dim;
+    c->h_mat.assign(H_shard_sum, H_shard_sum + dd);
+    HIPCHK(c, hipMemcpyAsync(c->sc_src, c->h_mat.data(), sizeof(double) * dd, hipMemcpyHostToDevice,
+                             c->stream));
+    CHK(allreduce_f64(c, c->sc_src, dd));
+    HIPCHK(c, hipStreamSynchronize(c->stream)); // h_mat may be reused
+    c->hess_ready = true;
+    return SVGD_OK;
+}
+
+int svgd_get_scale_matrix(svgd_ctx *c, double *M_out)
+{
+    if (!c || !M_out) return SVGD_ERR_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int d = c->dim;
+    if (matrix_scale(c)) {
+        if (*c->h_err)
+            return fail(c, SVGD_ERR_RUNTIME,
+                        "[Runtime Error] The kernel scale matrix is not positive definite.");
+        HIPCHK(c, hipMemcpy(M_out, c->sc_M, sizeof(double) * (size_t)d * d, hipMemcpyDeviceToHost));
+        return SVGD_OK;
+    }
+    const double a = c->scale_method == SVGD_SCALE_FIXED ? c->fixed_a : c->h_scal[0];
+    for (int r = 0; r < d; ++r)
+        for (int q = 0; q < d; ++q) M_out[r * d + q] = r == q ? a : 0.0;
     return SVGD_OK;
 }
 

@@ -37,7 +37,7 @@ hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, c
                          hipStream_t stream);
 hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
                       const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
-                      double inv_n, double *phi, hipStream_t stream);
+                      double inv_n, const double *wv, double *phi, hipStream_t stream);
 hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
                              int64_t cnt, int d, double lr, double b1, double b2, double eps,
                              double c1, double c2, const double *lower, const double *upper,
@@ -75,7 +75,17 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            double *rec, hipStream_t stream);
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
-                           int64_t ldp, double inv_n, double *phi, hipStream_t stream);
+                           int64_t ldp, double inv_n, const double *wv, double *phi,
+                           hipStream_t stream);
+// full-matrix kernel scale (wv = 2 M xc replaces 2 a xc in the phi epilogue)
+hipError_t launch_scale_chol(const double *src, double factor, int d, double *M, double *L,
+                             double *scal, int *err, hipStream_t stream);
+hipError_t launch_prep_rec_mat(const double *xc, const double *G, const double *M, const double *L,
+                               int64_t n, int64_t np, int d, int KP, int RS, double *rec,
+                               double *wv, hipStream_t stream);
+hipError_t launch_prep_v_mat(const double *xc, const double *G, const double *M, const double *L,
+                             int64_t n, int64_t np, int d, int KP, int VW, double *zc, double *V,
+                             double *cvec, double *wv, hipStream_t stream);
 // mode 0 (collect) needs nmax_bits from launch_mean_center (classification margin).
 hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc, const double *nrm,
                             const float *xf, const unsigned long long *nmax_bits,

@@ -164,7 +164,8 @@ __global__ __launch_bounds__(256) void k_phi(const double *__restrict__ xc,
                                             const double *__restrict__ V,
                                             const double *__restrict__ a_ptr, int64_t row0,
                                             int64_t nrows, int64_t ntiles_j, int d,
-                                            double inv_n, double *__restrict__ phi)
+                                            double inv_n, const double *__restrict__ wv,
+                                            double *__restrict__ phi)
 {
     constexpr int VW = 16 * NCB;
     __shared__ double sX[KP * LDP];
@@ -231,7 +232,8 @@ __global__ __launch_bounds__(256) void k_phi(const double *__restrict__ xc,
         const int64_t i = ibase + il;
         if (i - row0 < nrows) {
             const double s1 = sAcc[w][il][d];
-            phi[(i - row0) * d + c] = inv_n * (sAcc[w][il][c] + two_a * xc[i * KP + c] * s1);
+            const double wgt = wv ? wv[i * d + c] : two_a * xc[i * KP + c];
+            phi[(i - row0) * d + c] = inv_n * (sAcc[w][il][c] + wgt * s1);
         }
     }
 }
@@ -939,10 +941,11 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
 }
 
 // phi_i = (sum_s acc_s + 2a xc_i sum_s acc1_s) / N, partials summed in s order.
+// wv (full-matrix scale): 2 M xc_i per particle, in place of 2 a xc_i.
 __global__ void k_phi_reduce(const double *__restrict__ part, const double *__restrict__ rec,
                              const double *__restrict__ a_ptr, int64_t row0, int64_t nrows,
                              int d, int RS, int S, int64_t ldp, double inv_n,
-                             double *__restrict__ phi)
+                             const double *__restrict__ wv, double *__restrict__ phi)
 {
     const double two_a = 2.0 * (*a_ptr);
     for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nrows;
@@ -953,7 +956,8 @@ __global__ void k_phi_reduce(const double *__restrict__ part, const double *__re
         for (int k = 0; k < d; ++k) {
             double sk = 0.0;
             for (int s = 0; s < S; ++s) sk += part[((int64_t)s * ldp + li) * (d + 1) + k];
-            phi[li * d + k] = inv_n * (sk + two_a * ri[k] * s1);
+            const double w = wv ? wv[(row0 + li) * d + k] : two_a * ri[k];
+            phi[li * d + k] = inv_n * (sk + w * s1);
         }
     }
 }
@@ -1239,6 +1243,105 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     }
 }
 
+// =========================================== full-matrix kernel scale ==
+// k(x, x') = exp(-(x-x')^T M (x-x')) with M = L L^T (GaussianRBFKernel.hpp:
+// 75-81; M from the Hessian heuristic :189-210 or a user constant).  The phi
+// kernels run unchanged on z = L^T xc with a = 1 (|z_i - z_j|^2 is the
+// M-distance); V_j = G_j - 2 M xc_j and the reduce adds 2 M xc_i sum_j K_ij.
+//
+// One thread: M = factor * src (symmetrised), its Cholesky factor L (lower),
+// a_eff = 1 for the phi kernels.  err = 1 if M is not positive definite.
+__global__ void k_scale_chol(const double *__restrict__ src, double factor, int d,
+                             double *__restrict__ M, double *__restrict__ L,
+                             double *__restrict__ scal, int *__restrict__ err)
+{
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    for (int r = 0; r < d; ++r)
+        for (int c = 0; c < d; ++c)
+            M[r * d + c] = factor * 0.5 * (src[r * d + c] + src[c * d + r]);
+    int bad = 0;
+    for (int j = 0; j < d; ++j) {
+        double s = M[j * d + j];
+        for (int k = 0; k < j; ++k) s -= L[j * d + k] * L[j * d + k];
+        if (!(s > 0.0)) {
+            bad = 1;
+            s = 1.0;
+        }
+        const double ljj = sqrt(s);
+        L[j * d + j] = ljj;
+        for (int i = j + 1; i < d; ++i) {
+            double t = M[i * d + j];
+            for (int k = 0; k < j; ++k) t -= L[i * d + k] * L[j * d + k];
+            L[i * d + j] = t / ljj;
+        }
+        for (int c = j + 1; c < d; ++c) L[j * d + c] = 0.0;
+    }
+    scal[0] = 1.0;
+    scal[1] = __builtin_nan("");
+    *err = bad;
+}
+
+// Row-stream records for the matrix scale: rec_j = [z_j | G_j - 2 M xc_j |
+// -256 log2e |z_j|^2 | 0..], wv_j = 2 M xc_j.
+__global__ void k_prep_rec_mat(const double *__restrict__ xc, const double *__restrict__ G,
+                               const double *__restrict__ M, const double *__restrict__ L,
+                               int64_t n, int64_t np, int d, int KP, int RS,
+                               double *__restrict__ rec, double *__restrict__ wv)
+{
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const bool live = j < n;
+        double *r = rec + j * RS;
+        double zz = 0.0;
+        for (int k = 0; k < d; ++k) {
+            double z = 0.0, mx = 0.0;
+            if (live)
+                for (int l = 0; l < d; ++l) {
+                    const double x = xc[j * KP + l];
+                    z = fma(L[l * d + k], x, z);
+                    mx = fma(M[k * d + l], x, mx);
+                }
+            r[k] = z;
+            r[d + k] = live ? G[j * d + k] - 2.0 * mx : 0.0;
+            wv[j * d + k] = 2.0 * mx;
+            zz = fma(z, z, zz);
+        }
+        r[2 * d] = live ? -256.0 * LOG2E * zz : 0.0;
+        for (int k = 2 * d + 1; k < RS; ++k) r[k] = 0.0;
+    }
+}
+
+// MFMA path (d > 16): zc = [z | 0..] (stride KP), V = [G - 2 M xc, 1, 0..],
+// cvec = -log2e |z|^2, wv = 2 M xc.
+__global__ void k_prep_v_mat(const double *__restrict__ xc, const double *__restrict__ G,
+                             const double *__restrict__ M, const double *__restrict__ L,
+                             int64_t n, int64_t np, int d, int KP, int VW,
+                             double *__restrict__ zc, double *__restrict__ V,
+                             double *__restrict__ cvec, double *__restrict__ wv)
+{
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const bool live = j < n;
+        double zz = 0.0;
+        for (int k = 0; k < KP; ++k) {
+            double z = 0.0, mx = 0.0;
+            if (live && k < d)
+                for (int l = 0; l < d; ++l) {
+                    const double x = xc[j * KP + l];
+                    z = fma(L[l * d + k], x, z);
+                    mx = fma(M[k * d + l], x, mx);
+                }
+            zc[j * KP + k] = z;
+            zz = fma(z, z, zz);
+            if (k < d) wv[j * d + k] = 2.0 * mx;
+            if (k < VW) V[j * VW + k] = live && k < d ? G[j * d + k] - 2.0 * mx : 0.0;
+        }
+        for (int k = KP; k < VW; ++k) V[j * VW + k] = 0.0;
+        if (d < VW) V[j * VW + d] = live ? 1.0 : 0.0;
+        cvec[j] = live ? -LOG2E * zz : 0.0;
+    }
+}
+
 // ================================================ device log-gradient ==
 // grad log p for the built-in Gaussian-sum model (MultivariateNormal.hpp:56-61,
 // Model::operator+ Model.hpp:55-92): p = sum_c exp(-q_c / 2), q_c = (x-mu_c)^T
@@ -1359,7 +1462,8 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
 
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
-                           int64_t ldp, double inv_n, double *phi, hipStream_t stream)
+                           int64_t ldp, double inv_n, const double *wv, double *phi,
+                           hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
     const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
@@ -1370,7 +1474,7 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
     int64_t g = (nrows + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
-                       d, phi_rec_stride(d), S, ldp, inv_n, phi);
+                       d, phi_rec_stride(d), S, ldp, inv_n, wv, phi);
     return hipGetLastError();
 }
 
@@ -1393,13 +1497,13 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
 #define SVGD_PHI_CASE(KPv, NCBv)                                                             \
     if (KP == KPv && NCB == NCBv) {                                                          \
         hipLaunchKernelGGL((k_phi<KPv, NCBv>), dim3(grid), dim3(256), 0, stream, xc, cvec, V, \
-                           a_ptr, row0, nrows, ntiles_j, d, inv_n, phi);                     \
+                           a_ptr, row0, nrows, ntiles_j, d, inv_n, wv, phi);                 \
         return hipGetLastError();                                                            \
     }
 
 hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
                       const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
-                      double inv_n, double *phi, hipStream_t stream)
+                      double inv_n, const double *wv, double *phi, hipStream_t stream)
 {
     const int64_t grid = (nrows + TB - 1) / TB;
     if (grid == 0) return hipSuccess;
@@ -1540,6 +1644,35 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
 hipError_t launch_bracket(SelState *st, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_bracket, dim3(1), dim3(1), 0, stream, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_chol(const double *src, double factor, int d, double *M, double *L,
+                             double *scal, int *err, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_scale_chol, dim3(1), dim3(64), 0, stream, src, factor, d, M, L, scal, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_rec_mat(const double *xc, const double *G, const double *M, const double *L,
+                               int64_t n, int64_t np, int d, int KP, int RS, double *rec,
+                               double *wv, hipStream_t stream)
+{
+    int64_t g = (np + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_prep_rec_mat, dim3(g), dim3(256), 0, stream, xc, G, M, L, n, np, d, KP, RS,
+                       rec, wv);
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_v_mat(const double *xc, const double *G, const double *M, const double *L,
+                             int64_t n, int64_t np, int d, int KP, int VW, double *zc, double *V,
+                             double *cvec, double *wv, hipStream_t stream)
+{
+    int64_t g = (np + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_prep_v_mat, dim3(g), dim3(256), 0, stream, xc, G, M, L, n, np, d, KP, VW,
+                       zc, V, cvec, wv);
     return hipGetLastError();
 }
 

@@ -264,6 +264,49 @@ static void TestSVGDMedianGMM(int which)
     CHECK(std::fabs(kernel->GetScale() - host_kernel.GetScale()) <= 1e-12 * host_kernel.GetScale());
 }
 
+// Hessian scale (GaussianRBFKernel.hpp:189-210) and a constant full-matrix
+// scale: SVGD class vs the manual loop with the host kernel's ComputeScale.
+static void TestSVGDMatrixScales(bool hessian)
+{
+    const size_t d = 2, n = 80, iters = 8;
+    std::srand(11);
+    auto x = std::make_shared<Eigen::MatrixXd>(4 * Eigen::MatrixXd::Random(d, n));
+    const Eigen::MatrixXd x0 = *x;
+    Eigen::Matrix2d c1, c2;
+    c1 << 0.5001, 0.2426, 0.2426, 0.8420;
+    c2 << 0.6779, -0.1652, -0.1652, 0.2260;
+    MultivariateNormal a(Eigen::Vector2d(1.6871, -0.801), 3 * c1), b(Eigen::Vector2d(-1.9802, 1.3387), 3 * c2);
+    auto model = std::make_shared<Model>(a + b);
+    Eigen::Matrix2d Mc;
+    Mc << 0.30, 0.12, 0.12, 0.55;
+    const auto method = hessian ? GaussianRBFKernel::ScaleMethod::Hessian : GaussianRBFKernel::ScaleMethod::Constant;
+    auto kernel = std::make_shared<GaussianRBFKernel>(x, method, model);
+    if (!hessian)
+        kernel->UpdateParameters({Mc});
+    auto opt = std::make_shared<Adam>(d, n, 5.0e-2, 0.9, 0.999);
+    SVGD svgd(d, iters, x, kernel, model, opt);
+    svgd.Initialize();
+    svgd.Run();
+
+    Model host_model = a + b;
+    host_model.Initialize();
+    auto xm = std::make_shared<Eigen::MatrixXd>(x0);
+    GaussianRBFKernel host_kernel(xm, method, std::make_shared<Model>(a + b));
+    if (!hessian)
+        host_kernel.UpdateParameters({Mc});
+    Adam host_opt(d, n, 5.0e-2, 0.9, 0.999);
+    host_opt.Initialize();
+    for (size_t t = 0; t < iters; ++t)
+    {
+        host_kernel.Step();
+        *xm = ManualStep(*xm, host_model, host_kernel, host_opt, nullptr, nullptr);
+    }
+    const double err = MaxAbsDiff(*x, *xm);
+    std::printf("%s-scale SVGD vs manual loop: max |dx| = %.3e\n", hessian ? "Hessian" : "matrix", err);
+    CHECK(err < 1e-10);
+    CHECK(MaxAbsDiff(kernel->GetScaleMatrix(), host_kernel.GetScaleMatrix()) < 1e-12);
+}
+
 int main(int argc, char **argv)
 {
     const bool cpu_only = argc > 1 && std::strcmp(argv[1], "cpu") == 0;
@@ -273,6 +316,8 @@ int main(int argc, char **argv)
         TestSVGDClassConstantScale();
         for (int w = 0; w < 3; ++w)
             TestSVGDMedianGMM(w);
+        TestSVGDMatrixScales(true);
+        TestSVGDMatrixScales(false);
     }
     std::printf("%d checks passed, %d failed\n", g_pass, g_fail);
     return g_fail == 0 ? 0 : 1;

@@ -141,3 +141,19 @@ def test_exp2_table_and_coefficients_match_generator():
     lits = [float.fromhex(t) for t in re.findall(r"0x1\.[0-9a-f]+p[-+]\d+", fn)]
     c = mk.coeffs()
     assert lits == [c[4], c[3], c[2], c[1]]
+
+
+def test_host_model_hessian_sum_matches_oracle(oracle):
+    import svgdcpp_amd as S
+
+    rng = np.random.default_rng(4)
+    d, k, n = 5, 3, 400
+    mus = rng.standard_normal((k, d))
+    covs = []
+    for _ in range(k):
+        A = rng.standard_normal((d, d)) * 0.3
+        covs.append(A @ A.T + np.eye(d))
+    X = rng.standard_normal((n, d)) * 2
+    m = S.GaussianSum(list(mus), covs)
+    np.testing.assert_allclose(m.neg_hess_sum(X), oracle.neg_hess_sum_gmm(X, mus, np.stack(covs)),
+                               rtol=1e-11, atol=1e-11)

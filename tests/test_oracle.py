@@ -142,3 +142,34 @@ def test_golden_phi_fixtures_consistent(oracle, golden_dir):
         a, med = oracle.median_scale(z["X"])
         assert a == z["a"] and med == z["med"]
         np.testing.assert_array_equal(oracle.phi(z["X"], z["G"], a), z["phi"])
+
+
+def test_hessian_sum_matches_finite_differences(oracle):
+    """oracle.neg_hess_sum_gmm (the Hessian scale's sum, GaussianRBFKernel.hpp:
+    197-205) against central differences of the oracle's own gradient."""
+    rng = np.random.default_rng(0)
+    d, n = 3, 40
+    X = rng.standard_normal((n, d))
+    mus = rng.standard_normal((2, d))
+    covs = np.stack([np.eye(d) * 1.5, np.eye(d) * 0.7 + 0.1])
+    H = oracle.neg_hess_sum_gmm(X, mus, covs)
+    Hfd = np.zeros((d, d))
+    h = 1e-5
+    for i in range(n):
+        for l in range(d):
+            e = np.zeros(d)
+            e[l] = h
+            gp = oracle.logp_grad_gmm((X[i] + e)[None], mus, covs)[0]
+            gm = oracle.logp_grad_gmm((X[i] - e)[None], mus, covs)[0]
+            Hfd[:, l] -= (gp - gm) / (2 * h)
+    assert np.max(np.abs(H - Hfd)) < 1e-7
+    np.testing.assert_array_equal(H, H.T)
+
+
+def test_phi_matrix_reduces_to_isotropic(oracle):
+    rng = np.random.default_rng(1)
+    X = rng.standard_normal((60, 4))
+    G = rng.standard_normal((60, 4))
+    a = 0.37
+    np.testing.assert_allclose(oracle.phi_matrix(X, G, a * np.eye(4)), oracle.phi(X, G, a),
+                               rtol=1e-13, atol=1e-15)
