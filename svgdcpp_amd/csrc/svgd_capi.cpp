@@ -70,6 +70,12 @@ struct svgd_ctx {
     double *rec = nullptr;  // np x RS particle records
     double *part = nullptr; // S x ldp x (d+1) phi partials
     float *xf = nullptr;    // np x med_f32_stride(d) fp32 median records
+    // symmetric phi pass (k_phi_sym): pair tiles of SYM_BLOCK particles
+    bool sym = false;
+    int64_t snb = 0, st0 = 0, st1 = 0; // blocks, this rank's tile range
+    int sgrid = 0, srslots = 0;
+    double *srec = nullptr, *colpart = nullptr, *rowpart = nullptr, *Ssum = nullptr;
+    int64_t *wgI = nullptr;
     unsigned long long *nmax = nullptr; // max |xc|^2 (double bits)
     int S = 1;
     int R = 2; // rows per lane of k_phi_rows
@@ -500,6 +506,49 @@ int upload_g(svgd_ctx *c, const double *G_shard)
     return upload_g_finish(c);
 }
 
+int run_phi_sym(svgd_ctx *c, bool mat)
+{
+    const int d = c->dim;
+    if (mat) {
+        const double factor = c->scale_method == SVGD_SCALE_HESSIAN
+                                  ? 1.0 / (2.0 * (double)d * (double)c->n)
+                                  : 1.0;
+        HIPCHK(c, launch_scale_chol(c->sc_src, factor, d, c->sc_M, c->sc_L, c->scal, c->sc_err,
+                                    c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->h_err, c->sc_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, launch_prep_srec(c->xc, c->G, c->nrm, c->scal, mat ? c->sc_M : nullptr,
+                               mat ? c->sc_L : nullptr, c->n, c->snb * SYM_BLOCK, d, c->KP, c->srec,
+                               c->wv, c->stream));
+    EvPair ev{};
+    if (c->timing) {
+        ev = take_pair(c);
+        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+    }
+    HIPCHK(c, launch_phi_sym(d, c->sgrid, c->srec, c->scal, c->snb, c->st0, c->st1, c->srslots,
+                             c->colpart, c->rowpart, c->wgI, c->stream));
+    if (c->timing) {
+        HIPCHK(c, hipEventRecord(ev.b, c->stream));
+        c->ev_phi.push_back(ev);
+    }
+    HIPCHK(c, launch_sym_reduce(c->colpart, c->rowpart, c->wgI, c->n, d, c->snb, c->st0, c->st1,
+                                c->sgrid, c->srslots, c->Ssum, c->stream));
+    if (c->world > 1) {
+        // every rank's tiles touch every particle: sum S over ranks onto the row owners
+        const size_t cnt = (size_t)c->chunk * (d + 1);
+        if (c->hcomm) {
+            if (hostcomm_allreduce_f64(c->hcomm, c->Ssum, cnt * c->world, c->stream))
+                return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
+        } else {
+            NCCLCHK(c, ncclReduceScatter(c->Ssum, c->Ssum + (size_t)c->rank * cnt, cnt, ncclDouble,
+                                         ncclSum, c->comm, c->stream));
+        }
+    }
+    HIPCHK(c, launch_sym_finish(c->Ssum, c->srec, c->scal, mat ? c->wv : nullptr, c->row0, c->nrows,
+                                d, 1.0 / (double)c->n, c->phi, c->stream));
+    return SVGD_OK;
+}
+
 bool matrix_scale(const svgd_ctx *c)
 {
     return c->scale_method == SVGD_SCALE_MATRIX || c->scale_method == SVGD_SCALE_HESSIAN;
@@ -508,6 +557,7 @@ bool matrix_scale(const svgd_ctx *c)
 int run_phi(svgd_ctx *c)
 {
     const bool mat = matrix_scale(c);
+    if (c->sym) return run_phi_sym(c, mat);
     if (mat) {
         // M = factor * src, L = chol(M), a_eff = 1 (GaussianRBFKernel.hpp:189-210)
         const double factor = c->scale_method == SVGD_SCALE_HESSIAN
@@ -663,6 +713,26 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
         CHK(dalloc(c, &c->nmax, 1));
         CHK(dalloc(c, &c->part, (int64_t)c->S * c->ldp * (dim + 1)));
+        // symmetric phi (each unordered pair's kernel value used for both rows)
+        c->sym = false; // opt-in until measured faster (SVGD_PHI_SYM=1)
+        if (const char *e = std::getenv("SVGD_PHI_SYM")) c->sym = std::atoi(e) != 0;
+        if (c->sym) {
+            c->snb = (n + SYM_BLOCK - 1) / SYM_BLOCK;
+            const int64_t T = c->snb * (c->snb + 1) / 2;
+            c->st0 = T * c->rank / c->world;
+            c->st1 = T * (c->rank + 1) / c->world;
+            const int64_t items = (c->st1 - c->st0) * SYM_SUBTILES;
+            c->sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(items, ncu));
+            // distinct row blocks a work group can meet: its items / (items per row block) + 2
+            const int64_t per_wg = (items + c->sgrid - 1) / c->sgrid;
+            const int64_t per_block = ((c->snb - 1) / 2 + 1) * SYM_SUBTILES;
+            c->srslots = (int)(per_wg / per_block + 2);
+            CHK(dalloc(c, &c->srec, c->snb * SYM_BLOCK * SYM_REC));
+            CHK(dalloc(c, &c->colpart, std::max<int64_t>(1, items) * 64 * (dim + 1)));
+            CHK(dalloc(c, &c->rowpart, (int64_t)c->sgrid * c->srslots * SYM_BLOCK * (dim + 1)));
+            CHK(dalloc(c, &c->wgI, c->sgrid));
+            CHK(dalloc(c, &c->Ssum, (int64_t)c->world * c->chunk * (dim + 1)));
+        }
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
     }
@@ -752,11 +822,12 @@ int svgd_destroy(svgd_ctx *c)
     if (c->hcomm) hostcomm_destroy(c->hcomm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
-                       c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc};
+                       c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
+                       c->srec,  c->colpart, c->rowpart, c->Ssum};
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
-                     c->xf,          c->nmax,    c->sc_err};
+                     c->xf,          c->nmax,    c->sc_err, c->wgI};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal, c->h_err};

@@ -77,6 +77,22 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, double *phi,
                            hipStream_t stream);
+// symmetric phi pass (k_phi_sym): blocks of SYM_BLOCK particles on the pair-tile plan
+constexpr int SYM_BLOCK = 768;
+constexpr int SYM_REC = 34;   // record stride (doubles)
+constexpr int SYM_SUBTILES = 12;
+hipError_t launch_prep_srec(const double *xc, const double *G, const double *nrm, const double *a_ptr,
+                            const double *M, const double *L, int64_t n, int64_t nsr, int d, int KP,
+                            double *srec, double *wv, hipStream_t stream);
+hipError_t launch_phi_sym(int d, int grid, const double *srec, const double *a_ptr, int64_t nb,
+                          int64_t t0, int64_t t1, int rslots, double *colpart, double *rowpart,
+                          int64_t *wg_first_I, hipStream_t stream);
+hipError_t launch_sym_reduce(const double *colpart, const double *rowpart, const int64_t *wg_first_I,
+                             int64_t n, int d, int64_t nb, int64_t t0, int64_t t1, int G, int rslots,
+                             double *S, hipStream_t stream);
+hipError_t launch_sym_finish(const double *S, const double *srec, const double *a_ptr,
+                             const double *wv, int64_t row0, int64_t nrows, int d, double inv_n,
+                             double *phi, hipStream_t stream);
 // full-matrix kernel scale (wv = 2 M xc replaces 2 a xc in the phi epilogue)
 hipError_t launch_scale_chol(const double *src, double factor, int d, double *M, double *L,
                              double *scal, int *err, hipStream_t stream);

@@ -1243,6 +1243,339 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     }
 }
 
+// ================================================= symmetric phi pass ==
+//
+// K_ij = K_ji, so each unordered pair's kernel value can feed both rows:
+//   row i:    sum_j K_ij [V_j, 1]        column j:  sum_i K_ij [V_i, 1]
+// Work is the pair-tile plan (plan.cpp) with square blocks of SYM_B = 768
+// particles: tile (I, J != I) covers all 768 x 768 unordered pairs of two
+// blocks once, the diagonal tile (I, I) is done in ordered form (row sums
+// only).  A workgroup (4 waves) holds the 768 rows of I in registers (3 per
+// lane) and streams J in 64-column LDS sub-tiles.  Within a sub-tile each
+// 16-lane row group walks a 16-column set in 16 steps on a skewed schedule:
+// at step s lane t pairs its rows with column (t + s) mod 16 (per-lane LDS
+// read; the record stride makes these conflict-free) and the column
+// accumulators rotate one lane per step (DPP row_ror:15), so both sums stay
+// in registers -- no cross-lane reductions.  After 16 steps each lane adds
+// its column's accumulator to the wave's LDS column slot; the 4 waves' slots
+// are summed in fixed order per sub-tile into colpart.  Rows are flushed to
+// rowpart whenever the workgroup's row block changes.  k_sym_reduce then adds
+// every partial of a particle in a fixed order (deterministic), for all N
+// particles (rank-summed by a reduce-scatter when sharded).
+//
+// Per unordered pair and row: 9 (u) + 13 (exp) + 9 (row acc) + 9 (col acc);
+// per step and lane: 5 LDS reads + 18 DPP moves, amortised over 3 rows.
+constexpr int SYM_R = 3;
+constexpr int SYM_B = 4 * 64 * SYM_R; // 768
+constexpr int SYM_SUB = 64;           // columns per LDS sub-tile
+constexpr int SYM_NSUB = SYM_B / SYM_SUB;
+constexpr int SYM_RS = 34;            // record stride (doubles): 2*34 = 4 (mod 64) dwords
+constexpr int SYM_SUB_BYTES = SYM_SUB * SYM_RS * 8; // 17 KiB
+static_assert(SYM_SUB_BYTES % 1024 == 0, "whole LDS-DMA pieces");
+
+__device__ __forceinline__ int64_t sym_cnt(int64_t nb, int64_t I)
+{
+    const int64_t H = (nb - 1) / 2;
+    return ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
+}
+
+__device__ __forceinline__ int64_t sym_base(int64_t nb, int64_t I)
+{
+    const int64_t H = (nb - 1) / 2;
+    if ((nb & 1) == 0) {
+        const int64_t half = nb / 2;
+        return I < half ? I * (H + 2) : half * (H + 2) + (I - half) * (H + 1);
+    }
+    return I * (H + 1);
+}
+
+__device__ __forceinline__ double dpp_ror15(double v)
+{
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x12F, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x12F, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Work-group item range (items = (tile, sub-tile) pairs of this rank).
+__device__ __forceinline__ int64_t sym_item_begin(int64_t i0, int64_t nitems, int64_t g, int64_t G)
+{
+    return i0 + nitems * g / G;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec,
+                                                const double *__restrict__ a_ptr, int64_t nb,
+                                                int64_t t0, int64_t t1, int rslots,
+                                                double *__restrict__ colpart,
+                                                double *__restrict__ rowpart,
+                                                int64_t *__restrict__ wg_first_I)
+{
+    constexpr int R = SYM_R, B = SYM_B, RSS = SYM_RS, DP = D + 1;
+    constexpr int SCOL = 4 * SYM_SUB * DP; // doubles: per-wave column slots
+    __shared__ __attribute__((aligned(16))) char smem[2 * SYM_SUB_BYTES + SCOL * 8 + 256 * 8];
+    double *sCol = reinterpret_cast<double *>(smem + 2 * SYM_SUB_BYTES);
+    double *tab = sCol + SCOL;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, tl = lane & 15;
+    tab[tid] = EXP2_TAB256[tid];
+    for (int e = tid; e < SCOL; e += 256) sCol[e] = 0.0;
+
+    const double alpha = 512.0 * LOG2E * (*a_ptr);
+    const int64_t i0 = t0 * SYM_NSUB, nitems = (t1 - t0) * SYM_NSUB;
+    const int64_t ib = sym_item_begin(i0, nitems, blockIdx.x, gridDim.x);
+    const int64_t ie = sym_item_begin(i0, nitems, blockIdx.x + 1, gridDim.x);
+
+    double xs[R][D], ci[R], vi[R][D], acc[R][D], acc1[R];
+    int64_t curI = -1, firstI = -1;
+    auto flush_rows = [&]() {
+        double *o = rowpart + ((int64_t)blockIdx.x * rslots + (curI - firstI)) * B * DP;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int lr = w * 64 * R + r * 64 + lane;
+#pragma unroll
+            for (int k = 0; k < D; ++k) o[lr * DP + k] = acc[r][k];
+            o[lr * DP + D] = acc1[r];
+        }
+    };
+    // DMA one 64-column sub-tile of block J into LDS buffer `buf` (17 pieces
+    // of 1 KiB over the 4 waves: wave 0 issues 5, the others 4)
+    auto issue = [&](int64_t item, int buf) {
+        int64_t I, J;
+        tile_coords(nb, item / SYM_NSUB, &I, &J);
+        const int q = (int)(item % SYM_NSUB);
+        const char *src = reinterpret_cast<const char *>(srec + (J * B + q * SYM_SUB) * RSS);
+        char *dst = smem + buf * SYM_SUB_BYTES;
+        for (int p = w; p < SYM_SUB_BYTES / 1024; p += 4)
+            __builtin_amdgcn_global_load_lds((gbl_void *)(src + p * 1024 + lane * 16),
+                                             (lds_void *)(dst + p * 1024), 16, 0, 0);
+    };
+    auto wait_issue = [&]() {
+        if (w == 0)
+            wait_vmcnt<(SYM_SUB_BYTES / 1024 + 3) / 4>();
+        else
+            wait_vmcnt<(SYM_SUB_BYTES / 1024) / 4>();
+    };
+
+    if (ib < ie) issue(ib, 0);
+    for (int64_t item = ib; item < ie; ++item) {
+        const int buf = (int)((item - ib) & 1);
+        if (item + 1 < ie) {
+            issue(item + 1, buf ^ 1);
+            wait_issue();
+        } else {
+            wait_vmcnt<0>();
+        }
+        __syncthreads(); // the sub-tile is in LDS for every wave
+        int64_t I, J;
+        const int64_t t = item / SYM_NSUB;
+        tile_coords(nb, t, &I, &J);
+        const int q = (int)(item % SYM_NSUB);
+        if (I != curI) {
+            if (curI >= 0) flush_rows();
+            else firstI = I;
+            curI = I;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double *ri = srec + (I * B + w * 64 * R + r * 64 + lane) * RSS;
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    xs[r][k] = alpha * ri[k];
+                    vi[r][k] = ri[D + k];
+                    acc[r][k] = 0.0;
+                }
+                ci[r] = ri[2 * D];
+                acc1[r] = 0.0;
+            }
+            wait_vmcnt<0>();
+        }
+        const double *cb = reinterpret_cast<const double *>(smem + buf * SYM_SUB_BYTES);
+        if (I == J) {
+            // diagonal block: ordered pairs, row sums only (uniform column)
+            for (int c = 0; c < SYM_SUB; ++c) {
+                const double *rj = cb + c * RSS;
+                double xj[D], vj[D];
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    xj[k] = rj[k];
+                    vj[k] = rj[D + k];
+                }
+                const double cj = rj[2 * D];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    double u = ci[r] + cj;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) u = fma(xs[r][k], xj[k], u);
+                    const double K = exp2_256(u, tab);
+#pragma unroll
+                    for (int k = 0; k < D; ++k) acc[r][k] = fma(K, vj[k], acc[r][k]);
+                    acc1[r] += K;
+                }
+            }
+        } else {
+            double *myCol = sCol + w * SYM_SUB * DP;
+            for (int ph = 0; ph < 4; ++ph) {
+                const int set = (g + ph) & 3;
+                double cacc[DP];
+#pragma unroll
+                for (int k = 0; k < DP; ++k) cacc[k] = 0.0;
+                for (int s = 0; s < 16; ++s) {
+                    const double *rj = cb + (set * 16 + ((tl + s) & 15)) * RSS; // per lane
+                    double xj[D], vj[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        xj[k] = rj[k];
+                        vj[k] = rj[D + k];
+                    }
+                    const double cj = rj[2 * D];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        double u = ci[r] + cj;
+#pragma unroll
+                        for (int k = 0; k < D; ++k) u = fma(xs[r][k], xj[k], u);
+                        const double K = exp2_256(u, tab);
+#pragma unroll
+                        for (int k = 0; k < D; ++k) {
+                            acc[r][k] = fma(K, vj[k], acc[r][k]);
+                            cacc[k] = fma(K, vi[r][k], cacc[k]);
+                        }
+                        acc1[r] += K;
+                        cacc[D] += K;
+                    }
+#pragma unroll
+                    for (int k = 0; k < DP; ++k) cacc[k] = dpp_ror15(cacc[k]);
+                }
+                // after 16 rotations lane tl holds column set*16 + tl
+                double *sc = myCol + (set * 16 + tl) * DP;
+#pragma unroll
+                for (int k = 0; k < DP; ++k) {
+                    const uint64_t *pk = reinterpret_cast<const uint64_t *>(sc + k);
+                    const double old = __longlong_as_double((long long)lds_load_u64(pk));
+                    lgkm_wait();
+                    lds_store_u64(pk, (uint64_t)__double_as_longlong(old + cacc[k]));
+                }
+            }
+            lgkm_wait();
+            __syncthreads(); // every wave's column slots for this sub-tile are final
+            double *o = colpart + (item - i0) * SYM_SUB * DP;
+            for (int e = tid; e < SYM_SUB * DP; e += 256) {
+                double v = 0.0;
+                for (int ww = 0; ww < 4; ++ww) {
+                    const uint64_t *pk = reinterpret_cast<const uint64_t *>(sCol + ww * SYM_SUB * DP + e);
+                    v += __longlong_as_double((long long)lds_load_u64(pk));
+                }
+                lgkm_wait();
+                o[e] = v;
+                for (int ww = 0; ww < 4; ++ww)
+                    lds_store_u64(reinterpret_cast<const uint64_t *>(sCol + ww * SYM_SUB * DP + e), 0ull);
+            }
+            lgkm_wait();
+        }
+        __syncthreads(); // buffer `buf` and the column slots are free again
+    }
+    if (curI >= 0) flush_rows();
+    if (tid == 0) wg_first_I[blockIdx.x] = firstI;
+}
+
+// Sum every partial of particle p (rows block P), in a fixed order, into
+// S[p][0..D] (= sum_j K_pj [V_j, 1] over this rank's tiles).
+__global__ void k_sym_reduce(const double *__restrict__ colpart, const double *__restrict__ rowpart,
+                             const int64_t *__restrict__ wg_first_I, int64_t n, int D, int64_t nb,
+                             int64_t t0, int64_t t1, int G, int rslots, double *__restrict__ S)
+{
+    const int DP = D + 1;
+    const int64_t i0 = t0 * SYM_NSUB, nitems = (t1 - t0) * SYM_NSUB;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
+         p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t P = p / SYM_B, pl = p - P * SYM_B;
+        const int q = (int)(pl / SYM_SUB), cl = (int)(pl % SYM_SUB);
+        double s[17];
+        for (int k = 0; k < DP; ++k) s[k] = 0.0;
+        // row role: work groups whose item range meets row block P
+        const int64_t tb = max(t0, sym_base(nb, P)), te = min(t1, sym_base(nb, P) + sym_cnt(nb, P));
+        if (tb < te) {
+            const int64_t first = tb * SYM_NSUB, last = te * SYM_NSUB - 1;
+            int64_t ga = (first - i0) * G / nitems;
+            while (ga > 0 && sym_item_begin(i0, nitems, ga, G) > first) --ga;
+            while (ga + 1 < G && sym_item_begin(i0, nitems, ga + 1, G) <= first) ++ga;
+            for (int64_t gg = ga; gg < G && sym_item_begin(i0, nitems, gg, G) <= last; ++gg) {
+                if (sym_item_begin(i0, nitems, gg + 1, G) <= first) continue;
+                const double *o = rowpart + ((gg * rslots + (P - wg_first_I[gg])) * SYM_B + pl) * DP;
+                for (int k = 0; k < DP; ++k) s[k] += o[k];
+            }
+        }
+        // column role: tiles (I, P) with slot >= 1
+        for (int64_t sl = 1; sl <= (nb - 1) / 2 + 1; ++sl) {
+            const int64_t I = ((P - sl) % nb + nb) % nb;
+            if (I == P || sl >= sym_cnt(nb, I)) continue;
+            const int64_t t = sym_base(nb, I) + sl;
+            if (t < t0 || t >= t1) continue;
+            const double *o = colpart + ((t * SYM_NSUB + q - i0) * SYM_SUB + cl) * DP;
+            for (int k = 0; k < DP; ++k) s[k] += o[k];
+        }
+        for (int k = 0; k < DP; ++k) S[p * DP + k] = s[k];
+    }
+}
+
+// phi_i = (S_i[0..d) + w_i S_i[d]) / N for this rank's rows; w_i = 2a xc_i
+// (srec holds xc) or the full-matrix 2 M xc_i (wv).
+__global__ void k_sym_finish(const double *__restrict__ S, const double *__restrict__ srec,
+                             const double *__restrict__ a_ptr, const double *__restrict__ wv,
+                             int64_t row0, int64_t nrows, int d, double inv_n,
+                             double *__restrict__ phi)
+{
+    const double two_a = 2.0 * (*a_ptr);
+    const int DP = d + 1;
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nrows;
+         li += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = row0 + li;
+        for (int k = 0; k < d; ++k) {
+            const double wgt = wv ? wv[i * d + k] : two_a * srec[i * SYM_RS + k];
+            phi[li * d + k] = inv_n * (S[i * DP + k] + wgt * S[i * DP + d]);
+        }
+    }
+}
+
+// Symmetric-path records (stride SYM_RS): [xc | G - 2a xc | -256 a log2e |xc|^2 | 0..];
+// rows >= n get c = -2^29 so every pair with them has K = 0 (u >= -2^31 keeps
+// exp2_256's integer conversion in range).  For the full-
+// matrix scale, xc is replaced by z = L^T xc and a by 1 (wv = 2 M xc).
+__global__ void k_prep_srec(const double *__restrict__ xc, const double *__restrict__ G,
+                            const double *__restrict__ nrm, const double *__restrict__ a_ptr,
+                            const double *__restrict__ M, const double *__restrict__ L,
+                            int64_t n, int64_t nsr, int d, int KP, double *__restrict__ srec,
+                            double *__restrict__ wv)
+{
+    const double a = M ? 1.0 : *a_ptr;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nsr;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const bool live = j < n;
+        double *r = srec + j * SYM_RS;
+        double zz = 0.0;
+        for (int k = 0; k < d; ++k) {
+            double z = 0.0, mx = 0.0;
+            if (live) {
+                if (M) {
+                    for (int l = 0; l < d; ++l) {
+                        const double x = xc[j * KP + l];
+                        z = fma(L[l * d + k], x, z);
+                        mx = fma(M[k * d + l], x, mx);
+                    }
+                    wv[j * d + k] = 2.0 * mx;
+                } else {
+                    z = xc[j * KP + k];
+                    mx = a * z;
+                }
+            }
+            r[k] = z;
+            r[d + k] = live ? G[j * d + k] - 2.0 * mx : 0.0;
+            zz = fma(z, z, zz);
+        }
+        r[2 * d] = live ? -256.0 * a * LOG2E * (M ? zz : nrm[j]) : -536870912.0;
+        for (int k = 2 * d + 1; k < SYM_RS; ++k) r[k] = 0.0;
+    }
+}
+
 // =========================================== full-matrix kernel scale ==
 // k(x, x') = exp(-(x-x')^T M (x-x')) with M = L L^T (GaussianRBFKernel.hpp:
 // 75-81; M from the Hessian heuristic :189-210 or a user constant).  The phi
@@ -1644,6 +1977,63 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
 hipError_t launch_bracket(SelState *st, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_bracket, dim3(1), dim3(1), 0, stream, st);
+    return hipGetLastError();
+}
+
+#define SVGD_SYM_CASE(Dv)                                                                    \
+    case Dv:                                                                                 \
+        hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(grid), dim3(256), 0, stream, srec, a_ptr, nb, t0, t1, \
+                           rslots, colpart, rowpart, wg_first_I);                            \
+        break;
+
+hipError_t launch_phi_sym(int d, int grid, const double *srec, const double *a_ptr, int64_t nb,
+                          int64_t t0, int64_t t1, int rslots, double *colpart, double *rowpart,
+                          int64_t *wg_first_I, hipStream_t stream)
+{
+    if (t1 <= t0 || grid <= 0) return hipSuccess;
+    switch (d) {
+        SVGD_SYM_CASE(1) SVGD_SYM_CASE(2) SVGD_SYM_CASE(3) SVGD_SYM_CASE(4)
+        SVGD_SYM_CASE(5) SVGD_SYM_CASE(6) SVGD_SYM_CASE(7) SVGD_SYM_CASE(8)
+        SVGD_SYM_CASE(9) SVGD_SYM_CASE(10) SVGD_SYM_CASE(11) SVGD_SYM_CASE(12)
+        SVGD_SYM_CASE(13) SVGD_SYM_CASE(14) SVGD_SYM_CASE(15) SVGD_SYM_CASE(16)
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#undef SVGD_SYM_CASE
+
+hipError_t launch_sym_reduce(const double *colpart, const double *rowpart, const int64_t *wg_first_I,
+                             int64_t n, int d, int64_t nb, int64_t t0, int64_t t1, int G, int rslots,
+                             double *S, hipStream_t stream)
+{
+    int64_t g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_sym_reduce, dim3(g), dim3(256), 0, stream, colpart, rowpart, wg_first_I, n, d,
+                       nb, t0, t1, G, rslots, S);
+    return hipGetLastError();
+}
+
+hipError_t launch_sym_finish(const double *S, const double *srec, const double *a_ptr,
+                             const double *wv, int64_t row0, int64_t nrows, int d, double inv_n,
+                             double *phi, hipStream_t stream)
+{
+    if (nrows <= 0) return hipSuccess;
+    int64_t g = (nrows + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_sym_finish, dim3(g), dim3(256), 0, stream, S, srec, a_ptr, wv, row0, nrows, d,
+                       inv_n, phi);
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_srec(const double *xc, const double *G, const double *nrm, const double *a_ptr,
+                            const double *M, const double *L, int64_t n, int64_t nsr, int d, int KP,
+                            double *srec, double *wv, hipStream_t stream)
+{
+    int64_t g = (nsr + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_prep_srec, dim3(g), dim3(256), 0, stream, xc, G, nrm, a_ptr, M, L, n, nsr, d,
+                       KP, srec, wv);
     return hipGetLastError();
 }
 

@@ -3,14 +3,18 @@
 # own time limit; anything other than "tests failed" (rc 1) stops the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+source tools/fault_guard.sh
 STEPS=${STEPS:-10}
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+fault_guard gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
+fault_guard gpurun_out/smoke.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 2 > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log
+fault_guard gpurun_out/bench.log
 exit $rc
