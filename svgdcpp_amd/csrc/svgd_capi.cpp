@@ -70,7 +70,7 @@ struct svgd_ctx {
     double *rec = nullptr;  // np x RS particle records
     double *part = nullptr; // S x ldp x (d+1) phi partials
     float *xf = nullptr;    // np x med_f32_stride(d) fp32 median records
-    // symmetric phi pass (k_phi_sym): pair tiles of SYM_BLOCK particles
+    // symmetric phi pass (k_phi_sym): pair tiles of sym_block(d) particles
     bool sym = false;
     int64_t snb = 0, st0 = 0, st1 = 0; // blocks, this rank's tile range
     int sgrid = 0, srslots = 0;
@@ -518,7 +518,7 @@ int run_phi_sym(svgd_ctx *c, bool mat)
         HIPCHK(c, hipMemcpyAsync(c->h_err, c->sc_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
     }
     HIPCHK(c, launch_prep_srec(c->xc, c->G, c->nrm, c->scal, mat ? c->sc_M : nullptr,
-                               mat ? c->sc_L : nullptr, c->n, c->snb * SYM_BLOCK, d, c->KP, c->srec,
+                               mat ? c->sc_L : nullptr, c->n, c->snb * sym_block(d), d, c->KP, c->srec,
                                c->wv, c->stream));
     EvPair ev{};
     if (c->timing) {
@@ -717,19 +717,19 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         c->sym = false; // opt-in until measured faster (SVGD_PHI_SYM=1)
         if (const char *e = std::getenv("SVGD_PHI_SYM")) c->sym = std::atoi(e) != 0;
         if (c->sym) {
-            c->snb = (n + SYM_BLOCK - 1) / SYM_BLOCK;
+            c->snb = (n + sym_block(dim) - 1) / sym_block(dim);
             const int64_t T = c->snb * (c->snb + 1) / 2;
             c->st0 = T * c->rank / c->world;
             c->st1 = T * (c->rank + 1) / c->world;
-            const int64_t items = (c->st1 - c->st0) * SYM_SUBTILES;
+            const int64_t items = (c->st1 - c->st0) * sym_subtiles(dim);
             c->sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(items, ncu));
             // distinct row blocks a work group can meet: its items / (items per row block) + 2
             const int64_t per_wg = (items + c->sgrid - 1) / c->sgrid;
-            const int64_t per_block = ((c->snb - 1) / 2 + 1) * SYM_SUBTILES;
+            const int64_t per_block = ((c->snb - 1) / 2 + 1) * sym_subtiles(dim);
             c->srslots = (int)(per_wg / per_block + 2);
-            CHK(dalloc(c, &c->srec, c->snb * SYM_BLOCK * SYM_REC));
+            CHK(dalloc(c, &c->srec, c->snb * sym_block(dim) * SYM_REC));
             CHK(dalloc(c, &c->colpart, std::max<int64_t>(1, items) * 64 * (dim + 1)));
-            CHK(dalloc(c, &c->rowpart, (int64_t)c->sgrid * c->srslots * SYM_BLOCK * (dim + 1)));
+            CHK(dalloc(c, &c->rowpart, (int64_t)c->sgrid * c->srslots * sym_block(dim) * (dim + 1)));
             CHK(dalloc(c, &c->wgI, c->sgrid));
             CHK(dalloc(c, &c->Ssum, (int64_t)c->world * c->chunk * (dim + 1)));
         }

@@ -77,10 +77,13 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, double *phi,
                            hipStream_t stream);
-// symmetric phi pass (k_phi_sym): blocks of SYM_BLOCK particles on the pair-tile plan
-constexpr int SYM_BLOCK = 768;
-constexpr int SYM_REC = 34;   // record stride (doubles)
-constexpr int SYM_SUBTILES = 12;
+// symmetric phi pass (k_phi_sym): blocks of sym_block(d) particles on the pair-tile plan
+// rows per lane (register budget: 2 waves/SIMD for every d)
+constexpr int sym_rows(int d) { return d <= 4 ? 4 : (d <= 8 ? 2 : 1); }
+// particles per block (4 waves x 64 lanes x rows); 64-column sub-tiles per block
+constexpr int sym_block(int d) { return 256 * sym_rows(d); }
+constexpr int sym_subtiles(int d) { return sym_block(d) / 64; }
+constexpr int SYM_REC = 34; // record stride (doubles)
 hipError_t launch_prep_srec(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                             const double *M, const double *L, int64_t n, int64_t nsr, int d, int KP,
                             double *srec, double *wv, hipStream_t stream);

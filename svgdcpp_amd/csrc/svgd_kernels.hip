@@ -820,12 +820,29 @@ __device__ __forceinline__ void lds_store_u64(const uint64_t *p, uint64_t v)
     const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint64_t *)p;
     asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
-__device__ __forceinline__ uint64_t lds_load_u64(const uint64_t *p)
+// Loads: the destination registers are only valid after lgkmcnt drains and the
+// compiler does not know that, so every load helper waits inside the same asm
+// statement (early-clobber outputs keep the address registers intact).
+__device__ __forceinline__ uint32_t lds_addr(const void *p)
 {
-    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint64_t *)p;
-    uint64_t v;
-    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a) : "memory");
-    return v;
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char *)p;
+}
+// v[t] = p[t * 64] for t < 8 (one wave's 512-key staging row)
+__device__ __forceinline__ void lds_load8_u64_sync(const uint64_t *p, uint64_t (&v)[8])
+{
+    asm volatile("ds_read_b64 %0, %8\n\t"
+                 "ds_read_b64 %1, %8 offset:512\n\t"
+                 "ds_read_b64 %2, %8 offset:1024\n\t"
+                 "ds_read_b64 %3, %8 offset:1536\n\t"
+                 "ds_read_b64 %4, %8 offset:2048\n\t"
+                 "ds_read_b64 %5, %8 offset:2560\n\t"
+                 "ds_read_b64 %6, %8 offset:3072\n\t"
+                 "ds_read_b64 %7, %8 offset:3584\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]),
+                   "=&v"(v[6]), "=&v"(v[7])
+                 : "v"(lds_addr(p))
+                 : "memory");
 }
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -1013,11 +1030,9 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
     uint64_t *wregion = MODE == 0 ? sc.region + wreg * sc.cap : nullptr;
     auto flush = [&]() {
         if (scnt == 0) return;
-        uint64_t v[STG / 64 > 0 ? STG / 64 : 1];
-#pragma unroll
-        for (int t = 0; t < STG / 64; ++t)
-            if (t * 64 < scnt) v[t] = lds_load_u64(&sStage[w][t * 64 + lane]);
-        lgkm_wait();
+        uint64_t v[8];
+        static_assert(MODE != 0 || STG == 512, "flush reads 8 x 64 staged keys");
+        lds_load8_u64_sync(&sStage[w][lane], v);
 #pragma unroll
         for (int t = 0; t < STG / 64; ++t) {
             const int64_t pos = wcnt + t * 64 + lane;
@@ -1247,11 +1262,12 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
 //
 // K_ij = K_ji, so each unordered pair's kernel value can feed both rows:
 //   row i:    sum_j K_ij [V_j, 1]        column j:  sum_i K_ij [V_i, 1]
-// Work is the pair-tile plan (plan.cpp) with square blocks of SYM_B = 768
-// particles: tile (I, J != I) covers all 768 x 768 unordered pairs of two
-// blocks once, the diagonal tile (I, I) is done in ordered form (row sums
-// only).  A workgroup (4 waves) holds the 768 rows of I in registers (3 per
-// lane) and streams J in 64-column LDS sub-tiles.  Within a sub-tile each
+// Work is the pair-tile plan (plan.cpp) with square blocks of B = 256 R
+// particles (R = sym_rows(d) rows per lane: 4, 2 or 1 by register budget):
+// tile (I, J != I) covers all B x B unordered pairs of two blocks once, the
+// diagonal tile (I, I) is done in ordered form (row sums only).  A workgroup
+// (4 waves) holds the B rows of I in registers (R per lane) and streams J in
+// 64-column LDS sub-tiles.  Within a sub-tile each
 // 16-lane row group walks a 16-column set in 16 steps on a skewed schedule:
 // at step s lane t pairs its rows with column (t + s) mod 16 (per-lane LDS
 // read; the record stride makes these conflict-free) and the column
@@ -1264,11 +1280,8 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
 // particles (rank-summed by a reduce-scatter when sharded).
 //
 // Per unordered pair and row: 9 (u) + 13 (exp) + 9 (row acc) + 9 (col acc);
-// per step and lane: 5 LDS reads + 18 DPP moves, amortised over 3 rows.
-constexpr int SYM_R = 3;
-constexpr int SYM_B = 4 * 64 * SYM_R; // 768
+// per step and lane: a few LDS reads + 2(d+1) DPP moves, amortised over R rows.
 constexpr int SYM_SUB = 64;           // columns per LDS sub-tile
-constexpr int SYM_NSUB = SYM_B / SYM_SUB;
 constexpr int SYM_RS = 34;            // record stride (doubles): 2*34 = 4 (mod 64) dwords
 constexpr int SYM_SUB_BYTES = SYM_SUB * SYM_RS * 8; // 17 KiB
 static_assert(SYM_SUB_BYTES % 1024 == 0, "whole LDS-DMA pieces");
@@ -1291,8 +1304,11 @@ __device__ __forceinline__ int64_t sym_base(int64_t nb, int64_t I)
 
 __device__ __forceinline__ double dpp_ror15(double v)
 {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x12F, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x12F, 0xF, 0xF, false);
+    // old = src: every lane has a source in a full-row rotation, and tying the
+    // two lets the move happen in place (no zeroed `old` register per move)
+    const int l = __double2loint(v), h = __double2hiint(v);
+    const int lo = __builtin_amdgcn_update_dpp(l, l, 0x12F, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(h, h, 0x12F, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
 
@@ -1300,6 +1316,14 @@ __device__ __forceinline__ double dpp_ror15(double v)
 __device__ __forceinline__ int64_t sym_item_begin(int64_t i0, int64_t nitems, int64_t g, int64_t G)
 {
     return i0 + nitems * g / G;
+}
+
+// Work-group barrier that only drains LDS operations: __syncthreads() would
+// also wait for the next sub-tile's in-flight DMA (vmcnt(0)); the DMA pieces
+// this barrier publishes were already waited for with a counted vmcnt.
+__device__ __forceinline__ void lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <int D>
@@ -1310,7 +1334,8 @@ __global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec
                                                 double *__restrict__ rowpart,
                                                 int64_t *__restrict__ wg_first_I)
 {
-    constexpr int R = SYM_R, B = SYM_B, RSS = SYM_RS, DP = D + 1;
+    constexpr int R = sym_rows(D), B = sym_block(D), NSUB = sym_subtiles(D), RSS = SYM_RS,
+                  DP = D + 1;
     constexpr int SCOL = 4 * SYM_SUB * DP; // doubles: per-wave column slots
     __shared__ __attribute__((aligned(16))) char smem[2 * SYM_SUB_BYTES + SCOL * 8 + 256 * 8];
     double *sCol = reinterpret_cast<double *>(smem + 2 * SYM_SUB_BYTES);
@@ -1322,7 +1347,7 @@ __global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec
     for (int e = tid; e < SCOL; e += 256) sCol[e] = 0.0;
 
     const double alpha = 512.0 * LOG2E * (*a_ptr);
-    const int64_t i0 = t0 * SYM_NSUB, nitems = (t1 - t0) * SYM_NSUB;
+    const int64_t i0 = t0 * NSUB, nitems = (t1 - t0) * NSUB;
     const int64_t ib = sym_item_begin(i0, nitems, blockIdx.x, gridDim.x);
     const int64_t ie = sym_item_begin(i0, nitems, blockIdx.x + 1, gridDim.x);
 
@@ -1342,8 +1367,8 @@ __global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec
     // of 1 KiB over the 4 waves: wave 0 issues 5, the others 4)
     auto issue = [&](int64_t item, int buf) {
         int64_t I, J;
-        tile_coords(nb, item / SYM_NSUB, &I, &J);
-        const int q = (int)(item % SYM_NSUB);
+        tile_coords(nb, item / NSUB, &I, &J);
+        const int q = (int)(item % NSUB);
         const char *src = reinterpret_cast<const char *>(srec + (J * B + q * SYM_SUB) * RSS);
         char *dst = smem + buf * SYM_SUB_BYTES;
         for (int p = w; p < SYM_SUB_BYTES / 1024; p += 4)
@@ -1366,11 +1391,11 @@ __global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec
         } else {
             wait_vmcnt<0>();
         }
-        __syncthreads(); // the sub-tile is in LDS for every wave
+        lds_barrier(); // the sub-tile is in LDS for every wave
         int64_t I, J;
-        const int64_t t = item / SYM_NSUB;
+        const int64_t t = item / NSUB;
         tile_coords(nb, t, &I, &J);
-        const int q = (int)(item % SYM_NSUB);
+        const int q = (int)(item % NSUB);
         if (I != curI) {
             if (curI >= 0) flush_rows();
             else firstI = I;
@@ -1445,33 +1470,24 @@ __global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec
 #pragma unroll
                     for (int k = 0; k < DP; ++k) cacc[k] = dpp_ror15(cacc[k]);
                 }
-                // after 16 rotations lane tl holds column set*16 + tl
+                // after 16 rotations lane tl holds column set*16 + tl (each
+                // phase a different group of the wave meets that column).
+                // Compiler-visible LDS: any wait it adds for the next sub-tile's
+                // DMA comes a whole phase after that DMA was issued.
                 double *sc = myCol + (set * 16 + tl) * DP;
 #pragma unroll
-                for (int k = 0; k < DP; ++k) {
-                    const uint64_t *pk = reinterpret_cast<const uint64_t *>(sc + k);
-                    const double old = __longlong_as_double((long long)lds_load_u64(pk));
-                    lgkm_wait();
-                    lds_store_u64(pk, (uint64_t)__double_as_longlong(old + cacc[k]));
-                }
+                for (int k = 0; k < DP; ++k) sc[k] += cacc[k];
             }
-            lgkm_wait();
-            __syncthreads(); // every wave's column slots for this sub-tile are final
+            lds_barrier(); // every wave's column slots for this sub-tile are final
             double *o = colpart + (item - i0) * SYM_SUB * DP;
             for (int e = tid; e < SYM_SUB * DP; e += 256) {
-                double v = 0.0;
-                for (int ww = 0; ww < 4; ++ww) {
-                    const uint64_t *pk = reinterpret_cast<const uint64_t *>(sCol + ww * SYM_SUB * DP + e);
-                    v += __longlong_as_double((long long)lds_load_u64(pk));
-                }
-                lgkm_wait();
+                double v = sCol[e];
+                for (int ww = 1; ww < 4; ++ww) v += sCol[ww * SYM_SUB * DP + e];
                 o[e] = v;
-                for (int ww = 0; ww < 4; ++ww)
-                    lds_store_u64(reinterpret_cast<const uint64_t *>(sCol + ww * SYM_SUB * DP + e), 0ull);
+                for (int ww = 0; ww < 4; ++ww) sCol[ww * SYM_SUB * DP + e] = 0.0;
             }
-            lgkm_wait();
         }
-        __syncthreads(); // buffer `buf` and the column slots are free again
+        lds_barrier(); // buffer `buf` and the column slots are free again
     }
     if (curI >= 0) flush_rows();
     if (tid == 0) wg_first_I[blockIdx.x] = firstI;
@@ -1484,23 +1500,24 @@ __global__ void k_sym_reduce(const double *__restrict__ colpart, const double *_
                              int64_t t0, int64_t t1, int G, int rslots, double *__restrict__ S)
 {
     const int DP = D + 1;
-    const int64_t i0 = t0 * SYM_NSUB, nitems = (t1 - t0) * SYM_NSUB;
+    const int B = sym_block(D), NSUB = sym_subtiles(D);
+    const int64_t i0 = t0 * NSUB, nitems = (t1 - t0) * NSUB;
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
          p += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t P = p / SYM_B, pl = p - P * SYM_B;
+        const int64_t P = p / B, pl = p - P * B;
         const int q = (int)(pl / SYM_SUB), cl = (int)(pl % SYM_SUB);
         double s[17];
         for (int k = 0; k < DP; ++k) s[k] = 0.0;
         // row role: work groups whose item range meets row block P
         const int64_t tb = max(t0, sym_base(nb, P)), te = min(t1, sym_base(nb, P) + sym_cnt(nb, P));
         if (tb < te) {
-            const int64_t first = tb * SYM_NSUB, last = te * SYM_NSUB - 1;
+            const int64_t first = tb * NSUB, last = te * NSUB - 1;
             int64_t ga = (first - i0) * G / nitems;
             while (ga > 0 && sym_item_begin(i0, nitems, ga, G) > first) --ga;
             while (ga + 1 < G && sym_item_begin(i0, nitems, ga + 1, G) <= first) ++ga;
             for (int64_t gg = ga; gg < G && sym_item_begin(i0, nitems, gg, G) <= last; ++gg) {
                 if (sym_item_begin(i0, nitems, gg + 1, G) <= first) continue;
-                const double *o = rowpart + ((gg * rslots + (P - wg_first_I[gg])) * SYM_B + pl) * DP;
+                const double *o = rowpart + ((gg * rslots + (P - wg_first_I[gg])) * B + pl) * DP;
                 for (int k = 0; k < DP; ++k) s[k] += o[k];
             }
         }
@@ -1510,7 +1527,7 @@ __global__ void k_sym_reduce(const double *__restrict__ colpart, const double *_
             if (I == P || sl >= sym_cnt(nb, I)) continue;
             const int64_t t = sym_base(nb, I) + sl;
             if (t < t0 || t >= t1) continue;
-            const double *o = colpart + ((t * SYM_NSUB + q - i0) * SYM_SUB + cl) * DP;
+            const double *o = colpart + ((t * NSUB + q - i0) * SYM_SUB + cl) * DP;
             for (int k = 0; k < DP; ++k) s[k] += o[k];
         }
         for (int k = 0; k < DP; ++k) S[p * DP + k] = s[k];
