@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "particle-updates/sec (N×iters/s) + per-step ms, N=65536 d=8, 1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6  # MI355X spec (not in MI355X_MICROARCH.md; vector = matrix for fp64)
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix = vector (v_mfma_f32_16x16x4_f32)
 
 
 def splitmix(shape, scale, seed):
@@ -62,7 +63,7 @@ CONFIGS = {
     "cfg2": dict(n=16384, d=2, desc="N=16384 d=2 multivariate normal (mvn_example parameters)"),
     "cfg3": dict(n=65536, d=8, desc="N=65536 d=8 GMM(k=4)"),
     "cfg4": dict(n=262144, d=8, desc="N=262144 d=8 GMM(k=4)"),
-    "cfg5": dict(n=65536, d=64, desc="N=65536 d=64 multivariate normal (computed in fp64)"),
+    "cfg5": dict(n=65536, d=64, dtype="f32", desc="N=65536 d=64 multivariate normal, fp32 compute"),
 }
 
 
@@ -114,6 +115,8 @@ def main():
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--cpu-rows", type=int, default=8192)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dtype", choices=["f64", "f32"], default=None,
+                    help="compute dtype of the O(N^2) work (default: the config's; cfg5 is f32)")
     ap.add_argument("--device-model", action="store_true",
                     help="grad log p on the device (SURVEY 8(f) rank 1) instead of the host; "
                          "not the north-star configuration")
@@ -141,6 +144,7 @@ def main():
     n = args.n or cfg["n"]
     d = args.d or cfg["d"]
     k = args.k
+    dtype = args.dtype or cfg.get("dtype", "f64")
     X0, mus, covs = config_workload(args.config, n, d, k)
     k = len(mus)
 
@@ -149,7 +153,8 @@ def main():
         box = [S.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
-    ctx = S.Context(d, n, device=local_rank, world=world, rank=rank, unique_id=uid)
+    ctx = S.Context(d, n, device=local_rank, world=world, rank=rank, unique_id=uid,
+                    dtype=C.SVGD_F32 if dtype == "f32" else C.SVGD_F64)
     ctx.set_particles(X0)
     ctx.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
     model = S.GaussianSum(list(mus), list(covs))
@@ -195,6 +200,7 @@ def main():
         phi_avg_s = phi_ms.value / max(1, cnt.value) / 1e3
         flops_launch = float(rows) * n * (5 * d + 4)
         achieved = flops_launch / phi_avg_s / 1e12 if phi_avg_s > 0 else None
+        peak = FP32_PEAK_TFLOPS if dtype == "f32" else FP64_PEAK_TFLOPS
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "phi_pmc_traffic.json")
         if os.path.exists(pmc_path):
@@ -213,11 +219,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": dtype,
             "data": "synthetic (splitmix64 X0 = 3*U[-1,1]^d, GMM means 3*U[-1,1]^d, cov_k = (1+0.25k) I)",
             "config": {
                 "workload": f"{args.config}: N={n} d={d} {'GMM(k=%d)' % k if k > 1 else 'MVN'} "
-                            f"RBF-median + Adam(0.1,0.9,0.999), fp64, "
+                            f"RBF-median + Adam(0.1,0.9,0.999), {dtype} compute, "
                             f"{'device' if args.device_model else 'host'} grad log p per step",
                 "n": n, "d": d, "k": k, "parallelism": f"rows{world}",
             },
@@ -225,9 +231,9 @@ def main():
                 "kernel": "k_phi (fused RBF + grad + phi contraction)",
                 "bound": "mfma",
                 "achieved": achieved,
-                "peak": FP64_PEAK_TFLOPS,
+                "peak": peak,
                 "unit": "TFLOP/s",
-                "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
+                "frac": (achieved / peak) if achieved else None,
                 "traffic": traffic,
                 "avg_launch_ms": phi_avg_s * 1e3,
                 "flop_per_launch": flops_launch,
@@ -237,7 +243,7 @@ def main():
             "median_path": ["direct", "bracket", "fallback"][path],
             "scale_a": a,
         }
-        if args.config != "cfg3" or args.device_model:
+        if args.config != "cfg3" or args.device_model or dtype != "f64":
             out["metric"] = (f"particle-updates/s, {cfg['desc']}"
                              f"{', device grad log p' if args.device_model else ''} (not the headline config)")
         if world == 1 and not args.no_cpu:

@@ -50,7 +50,11 @@ extern "C" {
 #define SVGD_ERR_RCCL -5    /* RCCL failure        -> std::runtime_error */
 #define SVGD_ERR_RUNTIME -6 /* other runtime error -> std::runtime_error */
 
-/* compute dtype of the device path (host I/O is always double) */
+/* compute dtype of the device path (host I/O is always double).  F32 runs the
+ * O(N^2) work -- median distances, kernel values, phi contraction -- on the
+ * fp32 MFMA tile kernels (v_mfma_f32_16x16x4f32, v_exp_f32) for every d; the
+ * O(N d) work (centring, phi epilogue, optimizer, clamp) stays fp64.  The
+ * median is the exact order statistic of the fp32 distances. */
 #define SVGD_F64 0
 #define SVGD_F32 1
 
@@ -213,8 +217,10 @@ int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi);
 /* Number of block-level tiles of the median pair sweep owned by rank r
  * (row blocks of `block` particles; each unordered pair of particles is
  * visited by exactly one rank), and the (row block, column block) of tile t
- * of that rank.  The device uses block = SVGD_PAIR_BLOCK(dim). */
+ * of that rank.  The device uses block = SVGD_PAIR_BLOCK(dim) for F64 and
+ * SVGD_PAIR_BLOCK_DT(dim, dtype) in general (F32: always the 64 tile). */
 #define SVGD_PAIR_BLOCK(dim) ((dim) <= 16 ? 256 : 64)
+#define SVGD_PAIR_BLOCK_DT(dim, dtype) ((dtype) == SVGD_F32 ? 64 : SVGD_PAIR_BLOCK(dim))
 int64_t svgd_plan_pair_tiles(int64_t n, int block, int world, int rank);
 void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
                          int64_t *row_block, int64_t *col_block);

@@ -363,13 +363,14 @@ class SVGDOptions:
 class Context:
     """Owns one svgd_ctx (one GPU).  Thin RAII wrapper used by SVGD and the bench."""
 
-    def __init__(self, dim, n, device=0, world=1, rank=0, unique_id=None):
+    def __init__(self, dim, n, device=0, world=1, rank=0, unique_id=None, dtype=None):
         self.lib = C.lib()
         h = ctypes.c_void_p()
+        dt = C.SVGD_F64 if dtype is None else int(dtype)
         if world == 1:
-            rc = self.lib.svgd_create(ctypes.byref(h), int(dim), int(n), C.SVGD_F64, int(device))
+            rc = self.lib.svgd_create(ctypes.byref(h), int(dim), int(n), dt, int(device))
         else:
-            rc = self.lib.svgd_create_dist(ctypes.byref(h), int(dim), int(n), C.SVGD_F64,
+            rc = self.lib.svgd_create_dist(ctypes.byref(h), int(dim), int(n), dt,
                                            int(device), int(world), int(rank), unique_id)
         self.h = h
         if rc != C.SVGD_OK:

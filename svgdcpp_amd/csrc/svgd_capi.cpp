@@ -63,6 +63,8 @@ struct svgd_ctx {
     double *partial = nullptr;
     int nparts = 64;
     double *scal = nullptr; // [0] a, [1] med
+    // SVGD_F32: fp32 copies feeding the tile kernels
+    float *xcf = nullptr, *nrmf = nullptr, *cvf = nullptr, *Vf = nullptr, *zcf = nullptr;
 
     // row-stream path (d <= ROWS_MAX_D)
     bool rowpath = false;
@@ -281,6 +283,10 @@ int center(svgd_ctx *c)
 {
     HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
                                  c->nrm, c->rowpath ? 1 : 0, c->xf, c->nmax, c->stream));
+    if (c->dtype == SVGD_F32) {
+        HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
+        HIPCHK(c, launch_cvt_f32(c->nrm, c->np, c->nrmf, c->stream));
+    }
     return SVGD_OK;
 }
 
@@ -314,6 +320,10 @@ hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t
                                 c->pnb, c->tile0,
                                 c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
                                 c->ghist, dbg, c->stream);
+    if (c->dtype == SVGD_F32)
+        return launch_pair_tiles_f32(c->KP, mode, grid, c->xcf, c->nrmf, c->n, c->pnb, c->tile0,
+                                     c->tile0 + c->own_tiles, regions, cap, c->counts, c->below,
+                                     c->st, c->ghist, dbg, c->stream);
     return launch_pair_tiles(c->KP, mode, grid, c->xc, c->nrm, c->n, c->pnb, c->tile0,
                              c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
                              c->ghist, dbg, c->stream);
@@ -578,6 +588,11 @@ int run_phi(svgd_ctx *c)
     else
         HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
                                 c->V, c->cvec, c->stream));
+    if (c->dtype == SVGD_F32) {
+        HIPCHK(c, launch_cvt_f32(c->V, c->np * c->VW, c->Vf, c->stream));
+        HIPCHK(c, launch_cvt_f32(c->cvec, c->np, c->cvf, c->stream));
+        if (mat) HIPCHK(c, launch_cvt_f32(c->zc, c->np * c->KP, c->zcf, c->stream));
+    }
     EvPair ev{};
     if (c->timing) {
         ev = take_pair(c);
@@ -587,6 +602,11 @@ int run_phi(svgd_ctx *c)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr, c->phi,
                                   c->stream));
+    else if (c->dtype == SVGD_F32)
+        HIPCHK(c, launch_phi_f32(c->KP, c->NCB, mat ? c->zcf : c->xcf, c->cvf, c->Vf, c->scal,
+                                 c->row0, c->nrows, (c->n + TB - 1) / TB, c->dim,
+                                 1.0 / (double)c->n, mat ? c->wv : nullptr, c->xc, c->phi,
+                                 c->stream));
     else
         HIPCHK(c, launch_phi(c->KP, c->NCB, mat ? c->zc : c->xc, c->cvec, c->V, c->scal, c->row0,
                              c->nrows, (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n,
@@ -659,12 +679,13 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
 {
     if (dim <= 0 || n <= 0)
         return fail(c, SVGD_ERR_DIM, "[Dimension Error] Particle count and dimension must be positive.");
-    if (dtype != SVGD_F64)
-        return fail(c, SVGD_ERR_ARG, "[Argument Error] Only the F64 device path is built.");
+    if (dtype != SVGD_F64 && dtype != SVGD_F32)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] dtype must be SVGD_F64 or SVGD_F32.");
+    const bool f32 = dtype == SVGD_F32;
     if (!pick_tiles(dim, &c->KP, &c->NCB))
         return fail(c, SVGD_ERR_DIM, "[Dimension Error] Device path supports dimension <= 64.");
-    // row-stream path: xc rows are the median records [xc | |xc|^2 | 0..]
-    if (dim <= ROWS_MAX_D) c->KP = med_rec_stride(dim);
+    // row-stream path (fp64, d <= 16): xc rows are the median records [xc | |xc|^2 | 0..]
+    if (dim <= ROWS_MAX_D && !f32) c->KP = med_rec_stride(dim);
     c->dim = dim;
     c->n = n;
     c->dtype = dtype;
@@ -675,7 +696,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     c->chunk = (n + c->world - 1) / c->world;
     svgd_plan_rows(n, c->world, c->rank, &c->row0, &c->row1);
     c->nrows = c->row1 - c->row0;
-    c->pblock = SVGD_PAIR_BLOCK(dim);
+    c->pblock = SVGD_PAIR_BLOCK_DT(dim, dtype);
     c->pnb = (n + c->pblock - 1) / c->pblock;
     c->own_tiles = svgd_plan_pair_tiles(n, c->pblock, c->world, c->rank);
     {
@@ -691,7 +712,12 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->xc, c->np * c->KP));
     CHK(dalloc(c, &c->nrm, c->np));
     CHK(dalloc(c, &c->cvec, c->np));
-    c->rowpath = dim <= ROWS_MAX_D;
+    c->rowpath = dim <= ROWS_MAX_D && !f32;
+    if (f32) {
+        CHK(dalloc(c, &c->xcf, c->np * c->KP));
+        CHK(dalloc(c, &c->nrmf, c->np));
+        CHK(dalloc(c, &c->cvf, c->np));
+    }
     if (c->rowpath) {
         // column splits: enough workgroups to fill every CU at the kernel's occupancy
         int ncu = 256;
@@ -735,6 +761,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         }
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
+        if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
     }
     CHK(dalloc(c, &c->phi, std::max<int64_t>(1, c->nrows) * dim));
     CHK(dalloc(c, &c->m, std::max<int64_t>(1, c->nrows) * dim));
@@ -824,6 +851,9 @@ int svgd_destroy(svgd_ctx *c)
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
                        c->srec,  c->colpart, c->rowpart, c->Ssum};
+    float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf};
+    for (float *p : fbufs)
+        if (p) (void)hipFree(p);
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
@@ -911,6 +941,7 @@ int alloc_matrix_scale(svgd_ctx *c)
     CHK(dalloc(c, &c->sc_L, dd));
     CHK(dalloc(c, &c->wv, c->np * c->dim));
     if (!c->rowpath) CHK(dalloc(c, &c->zc, c->np * c->KP));
+    if (c->dtype == SVGD_F32) CHK(dalloc(c, &c->zcf, c->np * c->KP));
     CHK(dalloc(c, &c->sc_err, 1));
     HIPCHK(c, hipHostMalloc((void **)&c->h_err, sizeof(int), hipHostMallocDefault));
     *c->h_err = 0;

@@ -38,6 +38,17 @@ hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, c
 hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
                       const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
                       double inv_n, const double *wv, double *phi, hipStream_t stream);
+// fp32 variants of the tile kernels (SVGD_F32); phi and the epilogue stay fp64
+hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, const float *V,
+                          const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j,
+                          int d, double inv_n, const double *wv, const double *xc, double *phi,
+                          hipStream_t stream);
+hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, const float *nrm,
+                                 int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                                 int64_t cap, uint32_t *counts, unsigned long long *below,
+                                 const SelState *st, uint32_t *ghist, double *dbg_out,
+                                 hipStream_t stream);
+hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream);
 hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
                              int64_t cnt, int d, double lr, double b1, double b2, double eps,
                              double c1, double c2, const double *lower, const double *upper,

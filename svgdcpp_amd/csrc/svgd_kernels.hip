@@ -30,10 +30,36 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int TB = 64;   // particles per tile (rows and columns)
 constexpr int LDP = TB + 16; // padded LDS row stride (doubles) of the k-major X tiles
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ d4 mfma64(double a, double b, d4 c)
 {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+
+// Same 16x16x4 lane maps for both precisions (the fp32 path, SVGD_F32, runs
+// the tile kernels on v_mfma_f32_16x16x4f32).
+template <class T> struct Acc4;
+template <> struct Acc4<double> {
+    typedef d4 type;
+};
+template <> struct Acc4<float> {
+    typedef f4 type;
+};
+__device__ __forceinline__ d4 mfma16(double a, double b, d4 c)
+{
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 mfma16(float a, float b, f4 c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// Row of accumulator register r in lane group hi = lane >> 4 (column = lane & 15):
+// f64 16x16x4 interleaves the groups (row = hi + 4r), f32 16x16x4 gives each
+// group 4 consecutive rows (row = 4hi + r).  A/B maps are the same for both.
+template <class T> __device__ __forceinline__ int acc_row(int hi, int r);
+template <> __device__ __forceinline__ int acc_row<double>(int hi, int r) { return hi + 4 * r; }
+template <> __device__ __forceinline__ int acc_row<float>(int hi, int r) { return 4 * hi + r; }
 
 // 2^t for t <= 0 (t = -a*log2(e)*s).  Range reduction t = k + f, |f| <= 1/2,
 // degree-12 Taylor polynomial of 2^f (max error 1.9 ulp on [-1/2, 1/2]),
@@ -60,6 +86,18 @@ __device__ __forceinline__ double exp2_neg(double t)
 }
 
 constexpr double LOG2E = 0x1.71547652b82fep+0;
+
+// 2^t for t <= 0 in the tile kernels' precision (fp32: v_exp_f32, 1 ulp)
+__device__ __forceinline__ double exp2_nonpos(double t) { return exp2_neg(fmin(t, 0.0)); }
+__device__ __forceinline__ float exp2_nonpos(float t) { return __builtin_amdgcn_exp2f(fminf(t, 0.0f)); }
+
+// fp32 working copies for the SVGD_F32 path (rows of padded arrays)
+__global__ void k_cvt_f32(const double *__restrict__ src, int64_t cnt, float *__restrict__ dst)
+{
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cnt;
+         e += (int64_t)gridDim.x * blockDim.x)
+        dst[e] = (float)src[e];
+}
 
 // ------------------------------------------------------------ centering --
 
@@ -155,39 +193,42 @@ __global__ void k_prep_v(const double *__restrict__ xc, const double *__restrict
 // Per 16(j) x 16(i) sub-tile:
 //   Gram   dot[j][i] = xc_j . xc_i     KP/4 MFMAs (A = X_J from LDS, B = X_I regs)
 //   VALU   t = c_i + c_j + 2a log2e dot  ( = -a log2e |x_i - x_j|^2 )
-//          P = 2^t                      (lane l: i = l&15, j = (l>>4) + 4r)
+//          P = 2^t                      (lane l: i = l&15, j = acc_row(l>>4, r))
 //   MFMA   acc[i][c] += sum_j P[i][j] V[j][c]   (P is already the A-operand map)
-// Epilogue: phi_i = (acc[i][0:d] + 2a xc_i acc[i][d]) / N.
-template <int KP, int NCB>
-__global__ __launch_bounds__(256) void k_phi(const double *__restrict__ xc,
-                                            const double *__restrict__ cvec,
-                                            const double *__restrict__ V,
+// Epilogue: phi_i = (acc[i][0:d] + 2a xc_i acc[i][d]) / N (fp64).
+// T = double (default) or float (SVGD_F32: Gram, exp and contraction on
+// v_mfma_f32_16x16x4f32 / v_exp_f32 from fp32 copies xg, cvec, V).
+template <class T, int KP, int NCB>
+__global__ __launch_bounds__(256) void k_phi(const T *__restrict__ xg, const T *__restrict__ cvec,
+                                            const T *__restrict__ V,
                                             const double *__restrict__ a_ptr, int64_t row0,
                                             int64_t nrows, int64_t ntiles_j, int d,
                                             double inv_n, const double *__restrict__ wv,
+                                            const double *__restrict__ xc,
                                             double *__restrict__ phi)
 {
+    typedef typename Acc4<T>::type A4;
     constexpr int VW = 16 * NCB;
-    __shared__ double sX[KP * LDP];
-    __shared__ double sV[TB * VW];
-    __shared__ double sC[TB];
-    __shared__ double sAcc[4][16][VW + 1];
+    __shared__ T sX[KP * LDP];
+    __shared__ __attribute__((aligned(16))) T sV[TB * VW];
+    __shared__ T sC[TB];
+    __shared__ T sAcc[4][16][VW + 1];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int lo = lane & 15, hi = lane >> 4;
     const double a = *a_ptr;
-    const double alpha = 2.0 * a * LOG2E;
+    const T alpha = (T)(2.0 * a * LOG2E);
 
     const int64_t ibase = row0 + (int64_t)blockIdx.x * TB + w * 16;
-    // B operand of the Gram MFMA: X_I^T, lane holds xc[i = lo][k = 4kk + hi]
-    double bI[KP / 4];
+    // B operand of the Gram MFMA: X_I^T, lane holds xg[i = lo][k = 4kk + hi]
+    T bI[KP / 4];
 #pragma unroll
-    for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = xc[(ibase + lo) * KP + 4 * kk + hi];
-    const double ci = cvec[ibase + lo];
+    for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = xg[(ibase + lo) * KP + 4 * kk + hi];
+    const T ci = cvec[ibase + lo];
 
-    d4 acc[NCB];
+    A4 acc[NCB];
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) acc[cb] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int cb = 0; cb < NCB; ++cb) acc[cb] = A4{0, 0, 0, 0};
 
     for (int64_t jt = 0; jt < ntiles_j; ++jt) {
         const int64_t j0 = jt * TB;
@@ -195,45 +236,45 @@ __global__ __launch_bounds__(256) void k_phi(const double *__restrict__ xc,
         // stage X_J (k-major, padded rows) and V_J, c_J
         for (int e = tid; e < TB * KP; e += 256) {
             const int jl = e / KP, k = e - jl * KP;
-            sX[k * LDP + jl] = xc[(j0 + jl) * KP + k];
+            sX[k * LDP + jl] = xg[(j0 + jl) * KP + k];
         }
-        for (int e = tid; e < TB * VW / 2; e += 256)
-            reinterpret_cast<double2 *>(sV)[e] = reinterpret_cast<const double2 *>(V + j0 * VW)[e];
+        constexpr int NV = TB * VW * (int)sizeof(T) / 16; // 16-byte pieces
+        for (int e = tid; e < NV; e += 256)
+            reinterpret_cast<uint4 *>(sV)[e] = reinterpret_cast<const uint4 *>(V + j0 * VW)[e];
         if (tid < TB) sC[tid] = cvec[j0 + tid];
         __syncthreads();
 
 #pragma unroll
         for (int js = 0; js < 4; ++js) {
-            d4 dot = {0.0, 0.0, 0.0, 0.0};
+            A4 dot = {0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < KP / 4; ++kk)
-                dot = mfma64(sX[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
+                dot = mfma16(sX[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int jl = js * 16 + 4 * r + hi;
-                double t = fma(alpha, dot[r], ci + sC[jl]);
-                const double p = exp2_neg(fmin(t, 0.0));
+                const int jl = js * 16 + acc_row<T>(hi, r);
+                const T p = exp2_nonpos(fma(alpha, dot[r], ci + sC[jl]));
 #pragma unroll
                 for (int cb = 0; cb < NCB; ++cb)
-                    acc[cb] = mfma64(p, sV[jl * VW + cb * 16 + lo], acc[cb]);
+                    acc[cb] = mfma16(p, sV[jl * VW + cb * 16 + lo], acc[cb]);
             }
         }
     }
 
-    // epilogue: acc lane map row i = hi + 4q, col c = lo (+16cb)
+    // epilogue (fp64): acc lane map row i = acc_row(hi, q), col c = lo (+16cb)
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sAcc[w][hi + 4 * q][cb * 16 + lo] = acc[cb][q];
+        for (int q = 0; q < 4; ++q) sAcc[w][acc_row<T>(hi, q)][cb * 16 + lo] = acc[cb][q];
     __syncthreads();
     const double two_a = 2.0 * a;
     for (int e = lane; e < 16 * d; e += 64) {
         const int il = e / d, c = e - il * d;
         const int64_t i = ibase + il;
         if (i - row0 < nrows) {
-            const double s1 = sAcc[w][il][d];
+            const double s1 = (double)sAcc[w][il][d];
             const double wgt = wv ? wv[i * d + c] : two_a * xc[i * KP + c];
-            phi[(i - row0) * d + c] = inv_n * (sAcc[w][il][c] + wgt * s1);
+            phi[(i - row0) * d + c] = inv_n * ((double)sAcc[w][il][c] + wgt * s1);
         }
     }
 }
@@ -331,15 +372,16 @@ struct SinkDebug {
     int64_t n;
 };
 
-template <int KP, int MODE>
-__global__ __launch_bounds__(256) void k_pair_tiles(const double *__restrict__ xc,
-                                                   const double *__restrict__ nrm, int64_t n,
+template <class T, int KP, int MODE>
+__global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
+                                                   const T *__restrict__ nrm, int64_t n,
                                                    int64_t nb, int64_t t0, int64_t t1,
                                                    SinkCollect sc, SinkHist sh, SinkDebug sd)
 {
-    __shared__ double sXI[KP * LDP];
-    __shared__ double sXJ[KP * LDP];
-    __shared__ double sNI[TB], sNJ[TB];
+    typedef typename Acc4<T>::type A4;
+    __shared__ T sXI[KP * LDP];
+    __shared__ T sXJ[KP * LDP];
+    __shared__ T sNI[TB], sNJ[TB];
     __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
     __shared__ uint32_t sCnt;
     __shared__ unsigned long long sBelow[4];
@@ -391,25 +433,26 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const double *__restrict__ x
         __syncthreads();
         curI = I;
 
-        double bI[KP / 4];
+        T bI[KP / 4];
 #pragma unroll
         for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = sXI[(4 * kk + hi) * LDP + w * 16 + lo];
         const int il = w * 16 + lo;
         const int64_t i = I * TB + il;
-        const double ni = sNI[il];
+        const T ni = sNI[il];
 
 #pragma unroll
         for (int js = 0; js < 4; ++js) {
-            d4 dot = {0.0, 0.0, 0.0, 0.0};
+            A4 dot = {0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < KP / 4; ++kk)
-                dot = mfma64(sXJ[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
+                dot = mfma16(sXJ[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int jl = js * 16 + 4 * r + hi;
+                const int jl = js * 16 + acc_row<T>(hi, r);
                 const int64_t j = J * TB + jl;
                 const bool valid = (i < n) && (j < n) && (I != J || il < jl);
-                const double s = fmax(fma(-2.0, dot[r], ni + sNJ[jl]), 0.0);
+                // key of the distance in the kernel's precision (fp32 keys widen exactly)
+                const double s = (double)fmax(fma((T)-2, dot[r], ni + sNJ[jl]), (T)0);
                 const uint64_t key = key_of(s);
                 if (MODE == 0) {
                     const bool in = valid && key >= lo_key && key < hi_key;
@@ -1395,7 +1438,6 @@ __global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec
         int64_t I, J;
         const int64_t t = item / NSUB;
         tile_coords(nb, t, &I, &J);
-        const int q = (int)(item % NSUB);
         if (I != curI) {
             if (curI >= 0) flush_rows();
             else firstI = I;
@@ -1846,14 +1888,16 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
 
 #define SVGD_PHI_CASE(KPv, NCBv)                                                             \
     if (KP == KPv && NCB == NCBv) {                                                          \
-        hipLaunchKernelGGL((k_phi<KPv, NCBv>), dim3(grid), dim3(256), 0, stream, xc, cvec, V, \
-                           a_ptr, row0, nrows, ntiles_j, d, inv_n, wv, phi);                 \
+        hipLaunchKernelGGL((k_phi<T, KPv, NCBv>), dim3(grid), dim3(256), 0, stream, xg, cvec,  \
+                           V, a_ptr, row0, nrows, ntiles_j, d, inv_n, wv, xc, phi);          \
         return hipGetLastError();                                                            \
     }
 
-hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
-                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
-                      double inv_n, const double *wv, double *phi, hipStream_t stream)
+template <class T>
+static hipError_t launch_phi_t(int KP, int NCB, const T *xg, const T *cvec, const T *V,
+                               const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j,
+                               int d, double inv_n, const double *wv, const double *xc,
+                               double *phi, hipStream_t stream)
 {
     const int64_t grid = (nrows + TB - 1) / TB;
     if (grid == 0) return hipSuccess;
@@ -1868,32 +1912,50 @@ hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, con
     SVGD_PHI_CASE(64, 5)
     return hipErrorInvalidValue;
 }
+#undef SVGD_PHI_CASE
+
+hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
+                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
+                      double inv_n, const double *wv, double *phi, hipStream_t stream)
+{
+    return launch_phi_t<double>(KP, NCB, xc, cvec, V, a_ptr, row0, nrows, ntiles_j, d, inv_n, wv,
+                                xc, phi, stream);
+}
+
+hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, const float *V,
+                          const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j,
+                          int d, double inv_n, const double *wv, const double *xc, double *phi,
+                          hipStream_t stream)
+{
+    return launch_phi_t<float>(KP, NCB, xg, cvec, V, a_ptr, row0, nrows, ntiles_j, d, inv_n, wv,
+                               xc, phi, stream);
+}
 
 #define SVGD_TILE_CASE(KPv)                                                                  \
     if (KP == KPv) {                                                                         \
         if (mode == 0)                                                                       \
-            hipLaunchKernelGGL((k_pair_tiles<KPv, 0>), dim3(grid), dim3(256), 0, stream, xc, \
-                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+            hipLaunchKernelGGL((k_pair_tiles<T, KPv, 0>), dim3(grid), dim3(256), 0, stream,  \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
         else if (mode == 1)                                                                  \
-            hipLaunchKernelGGL((k_pair_tiles<KPv, 1>), dim3(grid), dim3(256), 0, stream, xc, \
-                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+            hipLaunchKernelGGL((k_pair_tiles<T, KPv, 1>), dim3(grid), dim3(256), 0, stream,  \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
         else                                                                                 \
-            hipLaunchKernelGGL((k_pair_tiles<KPv, 2>), dim3(grid), dim3(256), 0, stream, xc, \
-                               nrm, n, nb, t0, t1, sc, sh, sd);                              \
+            hipLaunchKernelGGL((k_pair_tiles<T, KPv, 2>), dim3(grid), dim3(256), 0, stream,  \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
         return hipGetLastError();                                                            \
     }
 
-hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
-                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
-                             int64_t cap, uint32_t *counts, unsigned long long *below,
-                             const SelState *st, uint32_t *ghist, double *dbg_out,
-                             hipStream_t stream)
+template <class T>
+static hipError_t launch_pair_tiles_t(int KP, int mode, int grid, const T *xc, const T *nrm,
+                                      int64_t n, int64_t nb, int64_t t0, int64_t t1,
+                                      uint64_t *regions, int64_t cap, uint32_t *counts,
+                                      unsigned long long *below, const SelState *st,
+                                      uint32_t *ghist, double *dbg_out, hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
     SinkCollect sc{st, regions, cap, counts, below};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n};
-    (void)sc;
     SVGD_TILE_CASE(4)
     SVGD_TILE_CASE(8)
     SVGD_TILE_CASE(12)
@@ -1901,6 +1963,36 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
     SVGD_TILE_CASE(32)
     SVGD_TILE_CASE(64)
     return hipErrorInvalidValue;
+}
+#undef SVGD_TILE_CASE
+
+hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
+                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                             int64_t cap, uint32_t *counts, unsigned long long *below,
+                             const SelState *st, uint32_t *ghist, double *dbg_out,
+                             hipStream_t stream)
+{
+    return launch_pair_tiles_t<double>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
+                                       counts, below, st, ghist, dbg_out, stream);
+}
+
+hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, const float *nrm,
+                                 int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                                 int64_t cap, uint32_t *counts, unsigned long long *below,
+                                 const SelState *st, uint32_t *ghist, double *dbg_out,
+                                 hipStream_t stream)
+{
+    return launch_pair_tiles_t<float>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
+                                      counts, below, st, ghist, dbg_out, stream);
+}
+
+hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream)
+{
+    if (cnt <= 0) return hipSuccess;
+    int64_t g = (cnt + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_cvt_f32, dim3(g), dim3(256), 0, stream, src, cnt, dst);
+    return hipGetLastError();
 }
 
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,

@@ -1,0 +1,112 @@
+"""fp32 compute path (SVGD_F32) against the fp64 oracle.  GPU only.
+
+The O(N^2) work (median distances, kernel values, phi contraction) runs on the
+fp32 MFMA tile kernels; centring, the phi epilogue and the optimizer stay fp64.
+
+Tolerances (written here):
+  * phi_hat vs the fp64 oracle from identical (X, G, a):  max-abs <= 1e-4 * max|phi_hat|
+  * median / scale a vs the fp64 oracle:                rel <= 1e-5
+  * median selection:  BIT-EXACT order statistics of the device's own fp32 keys
+    (svgd_debug_pair_keys), on the direct, bracket and fallback paths
+"""
+import numpy as np
+import pytest
+
+import svgdcpp_amd as S
+from svgdcpp_amd import _capi as C
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-4
+
+
+def _ctx(X):
+    n, d = X.shape
+    c = S.Context(d, n, dtype=C.SVGD_F32)
+    c.set_particles(X)
+    return c
+
+
+@pytest.mark.parametrize("n,d", [(300, 64), (1000, 64), (2000, 33), (777, 8), (500, 2), (129, 17)])
+def test_f32_phi_matches_oracle(oracle, n, d):
+    X = oracle.splitmix((n, d), 3.0, 500 + n + d)
+    G = oracle.splitmix((n, d), 1.0, 600 + n + d)
+    a = float(np.log(n) / (2.0 * d * 3.0))  # typical median-heuristic magnitude
+    ph = _ctx(X).phi(G, a)
+    ref = oracle.phi(X, G, a)
+    assert np.all(np.isfinite(ph))
+    assert np.max(np.abs(ph - ref)) <= REL * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("n,d", [(400, 64), (333, 5)])
+def test_f32_median_exact_on_own_keys(oracle, n, d):
+    X = oracle.splitmix((n, d), 2.0, 7 * n + d)
+    c = _ctx(X)
+    a, med = c.median_scale()
+    keys = np.empty(n * (n - 1) // 2)
+    c.check(c.lib.svgd_debug_pair_keys(c.h, C.dptr(keys), keys.size))
+    # every key is an fp32 value (widened exactly)
+    assert np.array_equal(keys.astype(np.float32).astype(np.float64), keys)
+    iu = np.triu_indices(n, 1)
+    ref_keys = ((X[iu[0]] - X[iu[1]]) ** 2).sum(-1)
+    np.testing.assert_allclose(keys, ref_keys, rtol=1e-4, atol=1e-4)
+    u = np.sort(keys)
+    tot = n * n
+
+    def at(k):
+        return 0.0 if k < n else np.sqrt(u[(k - n) // 2])
+    exp = (at(tot // 2 - 1) + at(tot // 2)) / 2 if tot % 2 == 0 else at(tot // 2)
+    assert med == exp
+    assert med == pytest.approx(oracle.median_scale(X)[1], rel=1e-5)
+    assert a == pytest.approx(np.log(n) / (exp * exp), rel=1e-15)
+
+
+def test_f32_median_bracket_and_fallback_agree(oracle):
+    n, d = 1500, 24
+    X = oracle.splitmix((n, d), 1.0, 99)
+    a0, m0 = _ctx(X).median_scale()  # direct
+    c = _ctx(X)
+    c.check(c.lib.svgd_set_median_tuning(c.h, 0, 1 << 14, -1))
+    a1, m1 = c.median_scale()
+    assert c.last_scale()[2] == C.SVGD_MEDIAN_BRACKET
+    c2 = _ctx(X)
+    c2.check(c2.lib.svgd_set_median_tuning(c2.h, 0, 1 << 12, 1))
+    a2, m2 = c2.median_scale()
+    assert c2.last_scale()[2] == C.SVGD_MEDIAN_FALLBACK
+    assert m1 == m0 and m2 == m0 and a1 == a0 and a2 == a0
+
+
+def test_f32_step_tracks_f64(oracle):
+    """Full device steps (median + phi + Adam) in fp32 vs fp64: the scale
+    agrees to fp32 rounding, and positions after 3 steps stay close (Adam
+    normalises the increment, so only tiny phi components can differ)."""
+    n, d = 2048, 64
+    X0 = oracle.splitmix((n, d), 3.0, 11)
+    mu = oracle.splitmix((1, d), 0.5, 12)
+    model = S.GaussianSum(mu, np.eye(d)[None])
+    out, scale = {}, {}
+    for dt in (C.SVGD_F64, C.SVGD_F32):
+        c = S.Context(d, n, dtype=dt)
+        c.set_particles(X0)
+        c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999)
+        for _ in range(3):
+            c.step_with_model(model)
+        out[dt] = c.get_particles()
+        scale[dt] = c.last_scale()[0]
+    assert scale[C.SVGD_F32] == pytest.approx(scale[C.SVGD_F64], rel=1e-5)
+    diff = np.abs(out[C.SVGD_F32] - out[C.SVGD_F64])
+    assert np.all(np.isfinite(out[C.SVGD_F32]))
+    assert np.mean(diff) < 1e-3 and np.max(diff) <= 0.6
+
+
+def test_f32_matrix_scale(oracle):
+    n, d = 600, 20
+    X = oracle.splitmix((n, d), 2.0, 31)
+    G = oracle.splitmix((n, d), 1.0, 32)
+    B = oracle.splitmix((d, d), 0.2, 33)
+    M = (B @ B.T + 0.5 * np.eye(d)) / d
+    c = _ctx(X)
+    c.set_scale_matrix(M)
+    ph = c.phi(G, 0.0)
+    ref = oracle.phi_matrix(X, G, M)
+    assert np.max(np.abs(ph - ref)) <= REL * np.max(np.abs(ref))
