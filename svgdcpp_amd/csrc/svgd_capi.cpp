@@ -372,13 +372,21 @@ int median_begin(svgd_ctx *c)
         CHK(upload_state(c, 1, z, 0, ~0ull));
     } else {
         c->med_path = SVGD_MEDIAN_BRACKET;
-        const int64_t S = std::min<int64_t>(c->sample_size, M);
+        int64_t S = std::min<int64_t>(c->sample_size, M);
+        // tile path: whole random 64 x 64 tiles (MFMA Gram, ~1/1000 of the
+        // collect pass) instead of scattered pairs (2 random 8d-byte rows each)
+        const bool tile_sample = !c->rowpath && n / TB >= 2 && S >= TB * TB;
+        if (tile_sample) S = S / (TB * TB) * (TB * TB);
         if (c->sample_alloc < S) {
             CHK(dalloc(c, &c->sample_keys, S));
             c->sample_alloc = S;
         }
-        HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, S, c->sample_keys,
-                                     c->stream));
+        if (tile_sample)
+            HIPCHK(c, launch_sample_tiles(c->KP, c->xc, c->nrm, c->xcf, c->nrmf, n, S / (TB * TB),
+                                          c->sample_keys, c->stream));
+        else
+            HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, S,
+                                         c->sample_keys, c->stream));
         // sample ranks bracketing the target quantiles (6 sigma)
         const double qlo = (double)c->sel_rank[0] / (double)M;
         const double qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;

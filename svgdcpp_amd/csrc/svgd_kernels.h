@@ -49,6 +49,11 @@ hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, co
                                  const SelState *st, uint32_t *ghist, double *dbg_out,
                                  hipStream_t stream);
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream);
+// Sampled median keys on the tile path: ntiles random (block, block) pairs of
+// distinct full 64-particle blocks, all 64 x 64 keys each (xcf/nrmf: fp32 path)
+hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, const float *xcf,
+                               const float *nrmf, int64_t n, int64_t ntiles, uint64_t *keys,
+                               hipStream_t stream);
 hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
                              int64_t cnt, int d, double lr, double b1, double b2, double eps,
                              double c1, double c2, const double *lower, const double *upper,

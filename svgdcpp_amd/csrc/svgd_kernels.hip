@@ -368,9 +368,18 @@ struct SinkHist {
 };
 
 struct SinkDebug {
-    double *out;
+    double *out;    // MODE 2: every upper-triangle distance at its list index
     int64_t n;
+    uint64_t *keys; // MODE 3: 64 x 64 keys of each sampled tile
 };
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
 
 template <class T, int KP, int MODE>
 __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
@@ -416,7 +425,15 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     int64_t curI = -1;
     for (int64_t t = tb; t < te; ++t) {
         int64_t I, J;
-        tile_coords(nb, t, &I, &J);
+        if (MODE == 3) {
+            // sample tile t: a random pair of distinct full 64-particle blocks
+            const uint64_t h = mix64((uint64_t)t * 2 + 1);
+            const int64_t nbf = sd.n / TB;
+            I = (int64_t)(h % (uint64_t)nbf);
+            J = (I + 1 + (int64_t)((h >> 32) % (uint64_t)(nbf - 1))) % nbf;
+        } else {
+            tile_coords(nb, t, &I, &J);
+        }
         __syncthreads();
         if (I != curI) {
             for (int e = tid; e < TB * KP; e += 256) {
@@ -476,6 +493,8 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
                                 atomicAdd(&sHist[s2 * RADIX + ((key >> shift) & (RADIX - 1))], 1u);
                         }
                     }
+                } else if (MODE == 3) {
+                    sd.keys[t * (TB * TB) + il * TB + jl] = key;
                 } else {
                     if (valid) {
                         const int64_t a = i < j ? i : j, b = i < j ? j : i;
@@ -506,13 +525,6 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
 
 // Sampled keys: pair (i, j != i) from a splitmix hash of the sample index;
 // region b holds keys [b*per, (b+1)*per).
-__device__ __forceinline__ uint64_t mix64(uint64_t z)
-{
-    z += 0x9E3779B97F4A7C15ULL;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-    return z ^ (z >> 31);
-}
 
 __global__ void k_sample_keys(const double *__restrict__ xc, const double *__restrict__ nrm,
                               int64_t n, int d, int KP, int64_t S, uint64_t *__restrict__ keys)
@@ -1939,8 +1951,11 @@ hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, c
         else if (mode == 1)                                                                  \
             hipLaunchKernelGGL((k_pair_tiles<T, KPv, 1>), dim3(grid), dim3(256), 0, stream,  \
                                xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
-        else                                                                                 \
+        else if (mode == 2)                                                                  \
             hipLaunchKernelGGL((k_pair_tiles<T, KPv, 2>), dim3(grid), dim3(256), 0, stream,  \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
+        else                                                                                 \
+            hipLaunchKernelGGL((k_pair_tiles<T, KPv, 3>), dim3(grid), dim3(256), 0, stream,  \
                                xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
         return hipGetLastError();                                                            \
     }
@@ -1950,12 +1965,13 @@ static hipError_t launch_pair_tiles_t(int KP, int mode, int grid, const T *xc, c
                                       int64_t n, int64_t nb, int64_t t0, int64_t t1,
                                       uint64_t *regions, int64_t cap, uint32_t *counts,
                                       unsigned long long *below, const SelState *st,
-                                      uint32_t *ghist, double *dbg_out, hipStream_t stream)
+                                      uint32_t *ghist, double *dbg_out, hipStream_t stream,
+                                      uint64_t *sample_out = nullptr)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
     SinkCollect sc{st, regions, cap, counts, below};
     SinkHist sh{st, ghist};
-    SinkDebug sd{dbg_out, n};
+    SinkDebug sd{dbg_out, n, sample_out};
     SVGD_TILE_CASE(4)
     SVGD_TILE_CASE(8)
     SVGD_TILE_CASE(12)
@@ -1984,6 +2000,20 @@ hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, co
 {
     return launch_pair_tiles_t<float>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
                                       counts, below, st, ghist, dbg_out, stream);
+}
+
+hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, const float *xcf,
+                               const float *nrmf, int64_t n, int64_t ntiles, uint64_t *keys,
+                               hipStream_t stream)
+{
+    if (n / TB < 2 || ntiles <= 0) return hipErrorInvalidValue;
+    const int grid = (int)(ntiles < 1024 ? ntiles : 1024);
+    if (xcf)
+        return launch_pair_tiles_t<float>(KP, 3, grid, xcf, nrmf, n, 0, 0, ntiles, nullptr, 0,
+                                          nullptr, nullptr, nullptr, nullptr, nullptr, stream,
+                                          keys);
+    return launch_pair_tiles_t<double>(KP, 3, grid, xc, nrm, n, 0, 0, ntiles, nullptr, 0, nullptr,
+                                       nullptr, nullptr, nullptr, nullptr, stream, keys);
 }
 
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream)

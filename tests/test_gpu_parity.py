@@ -104,9 +104,10 @@ def _median_with_tuning(X, direct_max, sample, cap):
     return c, a, med
 
 
-@pytest.mark.parametrize("n", [700, 1501])
-def test_median_bracket_path_exact(oracle, n):
-    X = oracle.splitmix((n, 5), 1.0, n)
+@pytest.mark.parametrize("n,d", [(700, 5), (1501, 5), (1300, 40)])
+def test_median_bracket_path_exact(oracle, n, d):
+    """d = 40 runs the MFMA tile path, whose bracket comes from sampled 64 x 64 tiles."""
+    X = oracle.splitmix((n, d), 1.0, n)
     ref_c = _ctx(X)
     a0, m0 = ref_c.median_scale()  # direct path
     c, a, med = _median_with_tuning(X, 0, 1 << 14, -1)
