@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--k", type=int, default=4)
-    ap.add_argument("--cpu-rows", type=int, default=8192)
+    ap.add_argument("--cpu-rows", type=int, default=32768)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dtype", choices=["f64", "f32"], default=None,
                     help="compute dtype of the O(N^2) work (default: the config's; cfg5 is f32)")
