@@ -101,7 +101,11 @@ __global__ void k_cvt_f32(const double *__restrict__ src, int64_t cnt, float *__
 
 // ------------------------------------------------------------ centering --
 
-// Per-block partial column sums of X (n x d) -> partial[b*d + k].
+// Per-block partial column sums of X (n x d) -> partial[b*d + k].  Block b
+// sums a contiguous run of whole rows; thread t reads elements t, t + ST, ...
+// (ST = the largest multiple of d <= 256, so a thread always sees the same
+// column k = t mod d: coalesced loads), then the threads of each column are
+// summed in fixed order (deterministic).
 __global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
                                double *__restrict__ partial, unsigned long long *nmax_bits)
 {
@@ -109,17 +113,33 @@ __global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
     if (nmax_bits && blockIdx.x == 0 && threadIdx.x == 0) *nmax_bits = 0; // k_center's atomicMax target
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t j0 = per * blockIdx.x, j1 = min(n, j0 + per);
-    for (int k = 0; k < d; ++k) {
-        double s = 0.0;
-        for (int64_t j = j0 + threadIdx.x; j < j1; j += blockDim.x) s += X[j * d + k];
-        red[threadIdx.x] = s;
-        __syncthreads();
-        for (int o = 128; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-            __syncthreads();
+    const int ST = d <= 256 ? 256 - 256 % d : 0;
+    const int t = threadIdx.x;
+    double s = 0.0;
+    if (ST > 0 && t < ST && j1 > j0)
+        for (int64_t e = j0 * d + t; e < j1 * d; e += ST) s += X[e];
+    red[t] = s;
+    __syncthreads();
+    if (ST > 0) {
+        if (t < d) {
+            double c = 0.0;
+            for (int u = t; u < ST; u += d) c += red[u];
+            partial[blockIdx.x * d + t] = c;
         }
-        if (threadIdx.x == 0) partial[blockIdx.x * d + k] = red[0];
-        __syncthreads();
+    } else {
+        // d > 256: one column at a time (rare; not a hot configuration)
+        for (int k = 0; k < d; ++k) {
+            __syncthreads();
+            double c = 0.0;
+            for (int64_t j = j0 + t; j < j1; j += blockDim.x) c += X[j * d + k];
+            red[t] = c;
+            __syncthreads();
+            if (t == 0) {
+                double q = 0.0;
+                for (int u = 0; u < 256; ++u) q += red[u];
+                partial[blockIdx.x * d + k] = q;
+            }
+        }
     }
 }
 
@@ -141,6 +161,7 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
         mu[k] = s / (double)n;
     }
     __syncthreads();
+    unsigned long long bmax = 0;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
          j += (int64_t)gridDim.x * blockDim.x) {
         double s = 0.0;
@@ -159,7 +180,18 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
                 const unsigned long long t = __shfl_xor(m, o);
                 m = t > m ? t : m;
             }
-            if ((threadIdx.x & 63) == 0) atomicMax(nmax_bits, m);
+            bmax = m > bmax ? m : bmax;
+        }
+    }
+    if (xf) {
+        // one atomic per block (per-wave atomics on one address serialise)
+        __shared__ unsigned long long wmax[4];
+        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bmax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long m = 0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = wmax[w] > m ? wmax[w] : m;
+            atomicMax(nmax_bits, m);
         }
     }
 }
@@ -819,17 +851,20 @@ __constant__ double EXP2_TAB256[256] = {
 // 2^(u/256) for u <= ~0: u = k + f, |f| <= 1/2, 2^(u/256) = 2^(k>>8) 2^((k&255)/256) 2^(f/256);
 // 2^(f/256) = e^r, r = f ln2/256, |r| <= 1.36e-3, by its degree-4 Taylor
 // polynomial (remainder r^5/5! < 0.35 ulp; <= ~2 ulp overall).  9 fp64 ops.
+__device__ __forceinline__ double exp2_256_poly(double f)
+{
+    double p = 0x1.3b2ab6fba4e77p-39;
+    p = fma(p, f, 0x1.c6b08d704a0c0p-29);
+    p = fma(p, f, 0x1.ebfbdff82c58fp-19);
+    p = fma(p, f, 0x1.62e42fefa39efp-9);
+    return fma(p, f, 1.0);
+}
 __device__ __forceinline__ double exp2_256(double u, const double *tab)
 {
     const double k = __builtin_rint(u);
     const double f = u - k;
     const int ki = (int)k;
-    double p = 0x1.3b2ab6fba4e77p-39;
-    p = fma(p, f, 0x1.c6b08d704a0c0p-29);
-    p = fma(p, f, 0x1.ebfbdff82c58fp-19);
-    p = fma(p, f, 0x1.62e42fefa39efp-9);
-    p = fma(p, f, 1.0);
-    return __builtin_ldexp(p * tab[ki & 255], ki >> 8);
+    return __builtin_ldexp(exp2_256_poly(f) * tab[ki & 255], ki >> 8);
 }
 
 constexpr int CH_PHI = 16; // columns per LDS chunk of the phi row stream
@@ -901,23 +936,82 @@ __device__ __forceinline__ void lds_load8_u64_sync(const uint64_t *p, uint64_t (
 }
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// rec_j = [xc_j | G_j - 2a xc_j | -256 a log2e |xc_j|^2 | 0..], one thread per
+// element (coalesced stores of the np x RS array).
 __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restrict__ G,
                            const double *__restrict__ nrm, const double *__restrict__ a_ptr,
                            int64_t n, int64_t np, int d, int KP, int RS, double *__restrict__ rec)
 {
     const double a = *a_ptr;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
-         j += (int64_t)gridDim.x * blockDim.x) {
-        const bool live = j < n;
-        double *r = rec + j * RS;
-        for (int k = 0; k < d; ++k) {
-            const double x = live ? xc[j * KP + k] : 0.0;
-            r[k] = x;
-            r[d + k] = live ? G[j * d + k] - 2.0 * a * x : 0.0;
+    const int64_t tot = np * RS;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = e / RS;
+        const int k = (int)(e - j * RS);
+        double v = 0.0;
+        if (j < n) {
+            if (k < d)
+                v = xc[j * KP + k];
+            else if (k < 2 * d)
+                v = G[j * d + (k - d)] - 2.0 * a * xc[j * KP + (k - d)];
+            else if (k == 2 * d)
+                v = -256.0 * a * LOG2E * nrm[j];
         }
-        r[2 * d] = live ? -256.0 * a * LOG2E * nrm[j] : 0.0;
-        for (int k = 2 * d + 1; k < RS; ++k) r[k] = 0.0;
+        rec[e] = v;
     }
+}
+
+// One column record of the phi row stream, held in registers.
+template <int D> struct ColRec {
+    double x[D], v[D], c;
+    __device__ __forceinline__ void load(const double *rj)
+    {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            x[k] = rj[k];
+            v[k] = rj[D + k];
+        }
+        c = rj[2 * D];
+    }
+};
+
+// acc_i += K_ij [V_j, 1] for the lane's R rows against one column j.
+template <int D, int R>
+__device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (&xs)[R][D],
+                                              const double (&ci)[R], double (&acc)[R][D],
+                                              double (&acc1)[R], const double *tab)
+{
+    // the R rows' chains interleaved (independent FMAs back to back)
+    double u[R], K[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) u[r] = ci[r] + q.c;
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], q.x[k], u[r]);
+    // exp2_256 in stages: the R table reads are issued together and their
+    // LDS latency hides behind the R polynomials
+    double f[R], T[R];
+    int ki[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double k = __builtin_rint(u[r]);
+        f[r] = u[r] - k;
+        ki[r] = (int)k;
+        T[r] = tab[ki[r] & 255];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) K[r] = exp2_256_poly(f[r]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) K[r] = __builtin_ldexp(K[r] * T[r], ki[r] >> 8);
+#pragma unroll
+    for (int k = 0; k < D; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][k] = fma(K[r], q.v[k], acc[r][k]);
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc1[r] += K[r];
 }
 
 template <int D, int R>
@@ -928,6 +1022,9 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
 {
     constexpr int RS = RecLayout<D>::RS;
     constexpr int CHB = CH_PHI * RS * 8; // bytes per column chunk (multiple of 1 KiB)
+    // register double buffer of the column record only where it fits without
+    // spilling (row state R(2D+2) + two records 2(2D+1) doubles)
+    constexpr bool PIPE = (R * (2 * D + 2) + 2 * (2 * D + 1)) * 2 <= 232;
     // per-wave double-buffered column chunks, then the 2^(i/256) table
     __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + 256 * 8];
     double *tab = reinterpret_cast<double *>(smem + 4 * 2 * CHB);
@@ -978,25 +1075,32 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
         }
         const double *cb = reinterpret_cast<const double *>(wbuf + (c & 1) * CHB);
         const int cnt = (int)min<int64_t>(CH_PHI, j1 - j0 - c * CH_PHI);
-        for (int jj = 0; jj < cnt; ++jj) {
-            const double *rj = cb + jj * RS;
-            double xj[D], vj[D];
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                xj[k] = rj[k];
-                vj[k] = rj[D + k];
+        // two register copies of the column record: the broadcast LDS reads of
+        // column jj+1 are in flight while column jj is computed (the read past
+        // the chunk's last column stays inside smem and is discarded)
+        if constexpr (!PIPE) {
+            for (int jj = 0; jj < cnt; ++jj) {
+                ColRec<D> q;
+                q.load(cb + jj * RS);
+                phi_rows_pair<D, R>(q, xs, ci, acc, acc1, tab);
             }
-            const double cj = rj[2 * D];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                double u = ci[r] + cj;
-#pragma unroll
-                for (int k = 0; k < D; ++k) u = fma(xs[r][k], xj[k], u);
-                const double K = exp2_256(u, tab);
-#pragma unroll
-                for (int k = 0; k < D; ++k) acc[r][k] = fma(K, vj[k], acc[r][k]);
-                acc1[r] += K;
-            }
+            continue;
+        }
+        ColRec<D> qa, qb;
+        qa.load(cb);
+        __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0): nothing pending at the loop head
+        // (sched_barrier keeps the scheduler from sinking the prefetch reads
+        // back down to their first use)
+        for (int jj = 0; jj < cnt; jj += 2) {
+            qb.load(cb + (jj + 1) * RS);
+            __builtin_amdgcn_sched_barrier(0);
+            phi_rows_pair<D, R>(qa, xs, ci, acc, acc1, tab);
+            __builtin_amdgcn_sched_barrier(0);
+            if (jj + 1 >= cnt) break;
+            qa.load(cb + (jj + 2) * RS);
+            __builtin_amdgcn_sched_barrier(0);
+            phi_rows_pair<D, R>(qb, xs, ci, acc, acc1, tab);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 
@@ -1014,23 +1118,35 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
 
 // phi_i = (sum_s acc_s + 2a xc_i sum_s acc1_s) / N, partials summed in s order.
 // wv (full-matrix scale): 2 M xc_i per particle, in place of 2 a xc_i.
-__global__ void k_phi_reduce(const double *__restrict__ part, const double *__restrict__ rec,
-                             const double *__restrict__ a_ptr, int64_t row0, int64_t nrows,
-                             int d, int RS, int S, int64_t ldp, double inv_n,
-                             const double *__restrict__ wv, double *__restrict__ phi)
+// A block owns PHI_RED_ROWS rows: their (d+1)-element partial rows are
+// contiguous in every split s, so the sums are read coalesced into LDS, then
+// phi is written coalesced from LDS.
+constexpr int PHI_RED_ROWS = 128;
+__global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ part,
+                                                    const double *__restrict__ rec,
+                                                    const double *__restrict__ a_ptr, int64_t row0,
+                                                    int64_t nrows, int d, int RS, int S, int64_t ldp,
+                                                    double inv_n, const double *__restrict__ wv,
+                                                    double *__restrict__ phi)
 {
+    __shared__ double sm[PHI_RED_ROWS * 17];
     const double two_a = 2.0 * (*a_ptr);
-    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nrows;
-         li += (int64_t)gridDim.x * blockDim.x) {
-        double s1 = 0.0;
-        for (int s = 0; s < S; ++s) s1 += part[((int64_t)s * ldp + li) * (d + 1) + d];
-        const double *ri = rec + (row0 + li) * RS;
-        for (int k = 0; k < d; ++k) {
-            double sk = 0.0;
-            for (int s = 0; s < S; ++s) sk += part[((int64_t)s * ldp + li) * (d + 1) + k];
-            const double w = wv ? wv[(row0 + li) * d + k] : two_a * ri[k];
-            phi[li * d + k] = inv_n * (sk + w * s1);
-        }
+    const int DP = d + 1;
+    const int64_t rb = (int64_t)blockIdx.x * PHI_RED_ROWS;
+    const int rows = (int)min<int64_t>(PHI_RED_ROWS, nrows - rb);
+    if (rows <= 0) return;
+    const int E = rows * DP;
+    for (int e = threadIdx.x; e < E; e += blockDim.x) {
+        double acc = 0.0;
+        for (int s = 0; s < S; ++s) acc += part[((int64_t)s * ldp + rb) * DP + e];
+        sm[e] = acc;
+    }
+    __syncthreads();
+    for (int o = threadIdx.x; o < rows * d; o += blockDim.x) {
+        const int r = o / d, k = o - r * d;
+        const int64_t li = rb + r;
+        const double w = wv ? wv[(row0 + li) * d + k] : two_a * rec[(row0 + li) * RS + k];
+        phi[li * d + k] = inv_n * (sm[r * DP + k] + w * sm[r * DP + d]);
     }
 }
 
@@ -1049,7 +1165,7 @@ struct TileIt {
 };
 
 template <int D, int MODE>
-__global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 : 1, 8))) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
                                                   const double *__restrict__ nrm, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
@@ -1206,12 +1322,13 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
             // off-diagonal tiles (all but 1 in H+1): every valid row counts
             auto columns = [&](auto diag_tag) {
                 constexpr bool DIAG = decltype(diag_tag)::value;
-                for (int jj = 0; jj < cnt; ++jj) {
-                    const int64_t j = jb + jj;
-                    double xj[D];
-#pragma unroll
-                    for (int k = 0; k < D; ++k) xj[k] = cb[jj * KP + k]; // LDS broadcast
-                    const double hj = cb[jj * KP + D];
+                // MODE 0 off-diagonal tiles (the bulk): the column record of jj+1
+                // is read from LDS while column jj is classified (the read past
+                // the chunk's last column stays inside smem and is discarded)
+                constexpr bool PIPE = MODE == 0 && !DIAG;
+                auto column = [&](const double(&cr)[D + 1], const int64_t j) {
+                    const double *xj = cr;
+                    const double hj = cr[D];
                     // all rows' chains first (independent, interleaved), then
                     // the classification: no branch between the FMA chains
                     double ev[PR];
@@ -1288,6 +1405,32 @@ __global__ __launch_bounds__(256) void k_pair_rows(const double *__restrict__ xc
                                 }
                             }
                         }
+                    }
+                };
+                auto load = [&](double(&cr)[D + 1], int jj) {
+#pragma unroll
+                    for (int k = 0; k <= D; ++k) cr[k] = cb[jj * KP + k]; // LDS broadcast
+                };
+                if constexpr (PIPE) {
+                    double qa[D + 1], qb[D + 1];
+                    load(qa, 0);
+                    __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0) before the loop head
+                    for (int jj = 0; jj < cnt; jj += 2) {
+                        load(qb, jj + 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                        column(qa, jb + jj);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (jj + 1 >= cnt) break;
+                        load(qa, jj + 2);
+                        __builtin_amdgcn_sched_barrier(0);
+                        column(qb, jb + jj + 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                } else {
+                    for (int jj = 0; jj < cnt; ++jj) {
+                        double cr[D + 1];
+                        load(cr, jj);
+                        column(cr, jb + jj);
                     }
                 }
             };
@@ -1857,8 +2000,8 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
                            double *rec, hipStream_t stream)
 {
-    int64_t g = (np + 255) / 256;
-    if (g > 4096) g = 4096;
+    int64_t g = (np * RS + 255) / 256;
+    if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_prep_rec, dim3(g), dim3(256), 0, stream, xc, G, nrm, a_ptr, n, np, d, KP,
                        RS, rec);
     return hipGetLastError();
@@ -1875,8 +2018,8 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                                       nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
                                       SinkDebug{}, stream);
     if (e != hipSuccess) return e;
-    int64_t g = (nrows + 255) / 256;
-    if (g > 4096) g = 4096;
+    if (d > 16) return hipErrorInvalidValue; // k_phi_reduce's LDS holds d + 1 <= 17
+    const int64_t g = (nrows + PHI_RED_ROWS - 1) / PHI_RED_ROWS;
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
                        d, phi_rec_stride(d), S, ldp, inv_n, wv, phi);
     return hipGetLastError();

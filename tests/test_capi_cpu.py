@@ -136,7 +136,7 @@ def test_exp2_table_and_coefficients_match_generator():
     body = body[body.index("{") + 1:body.index("}")]
     vals = [float.fromhex(v.strip()) for v in body.replace("\n", " ").split(",") if v.strip()]
     assert vals == mk.table()
-    fn = src[src.index("double exp2_256("):]
+    fn = src[src.index("double exp2_256_poly("):]
     fn = fn[:fn.index("return")]
     lits = [float.fromhex(t) for t in re.findall(r"0x1\.[0-9a-f]+p[-+]\d+", fn)]
     c = mk.coeffs()
