@@ -91,6 +91,9 @@ struct svgd_ctx {
     int64_t sample_alloc = 0;
     uint64_t *regions = nullptr;
     int64_t regions_alloc = 0;
+    uint64_t *cbuf = nullptr;          // compacted candidates (regions_alloc keys)
+    unsigned long long *ccount = nullptr;
+    uint32_t *gpart = nullptr;         // per-block histograms (HIST_PART_BLOCKS x 2 RADIX)
     uint32_t *counts = nullptr;
     unsigned long long *below = nullptr;
     int collect_grid = 0;
@@ -398,10 +401,9 @@ int median_begin(svgd_ctx *c)
         if (shi > S - 1) shi = (double)(S - 1);
         uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
         CHK(upload_state(c, 2, sr, 0, ~0ull));
-        const int parts = (int)std::max<int64_t>(1, std::min<int64_t>(1024, S / 4096));
         for (int p = 0; p < 2; ++p) {
-            HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, S, parts, c->st, c->ghist,
-                                          c->stream));
+            HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, S, 0, c->st, c->gpart,
+                                          c->ghist, c->stream));
             HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
         }
         // bracket [lo_key, hi_key) stays on the device (read by the collect pass)
@@ -417,6 +419,7 @@ int median_begin(svgd_ctx *c)
     const int64_t need = c->reg_cap * c->nregions;
     if (c->regions_alloc < need) {
         CHK(dalloc(c, &c->regions, need));
+        CHK(dalloc(c, &c->cbuf, need));
         c->regions_alloc = need;
     }
     HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
@@ -468,16 +471,36 @@ int median_finish(svgd_ctx *c)
     }
     CHK(upload_state(c, c->nsel, ranks, 0, ~0ull, known_from, lo_key));
     const int passes = (known_from + RADIX_BITS - 1) / RADIX_BITS;
-    for (int p = 0; p < passes; ++p) {
-        if (path == SVGD_MEDIAN_FALLBACK) {
+    if (path == SVGD_MEDIAN_FALLBACK) {
+        // streamed radix select over every pair (rare: the bracket missed)
+        for (int p = 0; p < passes; ++p) {
             const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 2048));
             HIPCHK(c, pair_pass(c, 1, grid, nullptr, 0, nullptr));
-        } else {
-            HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->nregions, c->reg_cap, 1,
-                                          c->st, c->ghist, c->stream));
+            CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
+            HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
         }
+    } else if (passes > 0) {
+        // first digit over every candidate, then only the keys in the chosen
+        // bucket(s) are kept (compacted) for the remaining digits
+        HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->nregions, c->reg_cap, 0, c->st,
+                                      c->gpart, c->ghist, c->stream));
         CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
         HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+        if (passes > 1) {
+            HIPCHK(c, launch_compact(c->regions, c->counts, c->nregions, c->reg_cap, c->st, c->cbuf,
+                                     c->ccount, c->stream));
+            if (c->world == 1) {
+                // remaining digits in one work-group, no launches in between
+                HIPCHK(c, launch_select_tail(c->st, c->cbuf, c->ccount, passes - 1, c->stream));
+            } else {
+                for (int p = 1; p < passes; ++p) {
+                    HIPCHK(c, launch_hist_count(c->cbuf, c->ccount, c->regions_alloc, c->st,
+                                                c->gpart, c->ghist, c->stream));
+                    CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
+                    HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+                }
+            }
+        }
     }
     HIPCHK(c, launch_finalize(c->st, c->navg, c->src_lo, c->src_hi, logn, c->scal, c->scal + 1,
                               c->stream));
@@ -783,6 +806,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->cnt3, 8));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
+    CHK(dalloc(c, &c->gpart, (int64_t)HIST_PART_BLOCKS * 2 * RADIX));
+    CHK(dalloc(c, &c->ccount, 1));
     const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
     HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocDefault));
@@ -865,7 +890,7 @@ int svgd_destroy(svgd_ctx *c)
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
-                     c->xf,          c->nmax,    c->sc_err, c->wgI};
+                     c->xf,          c->nmax,    c->sc_err, c->wgI,   c->cbuf, c->ccount, c->gpart};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal, c->h_err};

@@ -70,8 +70,18 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
 hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
                               int d, int KP, int64_t S, uint64_t *keys, hipStream_t stream);
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                               int64_t cap, int parts, const SelState *st, uint32_t *ghist,
-                               hipStream_t stream);
+                               int64_t cap, int max_blocks, const SelState *st, uint32_t *gpart,
+                               uint32_t *ghist, hipStream_t stream);
+// gpart: HIST_PART_BLOCKS x 2 RADIX u32 scratch for per-block histograms
+constexpr int HIST_PART_BLOCKS = 256;
+hipError_t launch_compact(const uint64_t *keys, const uint32_t *counts, int64_t nreg, int64_t cap,
+                          const SelState *st, uint64_t *cbuf, unsigned long long *ccount,
+                          hipStream_t stream);
+hipError_t launch_select_tail(SelState *st, const uint64_t *cbuf, const unsigned long long *ccount,
+                              int passes, hipStream_t stream);
+hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *ccount, int64_t cap,
+                             const SelState *st, uint32_t *gpart, uint32_t *ghist,
+                             hipStream_t stream);
 hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream);
 hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
                                 int64_t nblk, int64_t cap, const SelState *st,

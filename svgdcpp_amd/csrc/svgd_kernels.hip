@@ -116,8 +116,17 @@ __global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
     const int ST = d <= 256 ? 256 - 256 % d : 0;
     const int t = threadIdx.x;
     double s = 0.0;
-    if (ST > 0 && t < ST && j1 > j0)
-        for (int64_t e = j0 * d + t; e < j1 * d; e += ST) s += X[e];
+    if (ST > 0 && t < ST && j1 > j0) {
+        const int64_t e1 = j1 * d;
+        for (int64_t e0 = j0 * d + t; e0 < e1; e0 += 8 * ST) {
+            double v[8]; // 8 loads in flight, added in order
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = e0 + u * ST < e1 ? X[e0 + u * ST] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (e0 + u * ST < e1) s += v[u];
+        }
+    }
     red[t] = s;
     __syncthreads();
     if (ST > 0) {
@@ -156,8 +165,16 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
 {
     __shared__ double mu[256];
     for (int k = threadIdx.x; k < d; k += blockDim.x) {
+        // partials added in b order; 8 loads in flight
         double s = 0.0;
-        for (int b = 0; b < nparts; ++b) s += partial[b * d + k];
+        for (int b0 = 0; b0 < nparts; b0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = b0 + u < nparts ? partial[(b0 + u) * d + k] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + u < nparts) s += v[u];
+        }
         mu[k] = s / (double)n;
     }
     __syncthreads();
@@ -585,55 +602,250 @@ __global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict
                                                          int64_t S, uint64_t *__restrict__ keys)
 {
     constexpr int KF = med_f32_stride(D);
-    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S;
-         g += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t h = mix64((uint64_t)g * 2 + 1);
-        const int64_t i = mulhi_index((uint32_t)(h >> 32), n);
-        int64_t j = i + 1 + mulhi_index((uint32_t)h, n - 1);
-        if (j >= n) j -= n;
-        float a[KF], b[KF];
-        const float4 *ri = reinterpret_cast<const float4 *>(xf + i * KF);
-        const float4 *rj = reinterpret_cast<const float4 *>(xf + j * KF);
+    // SU samples per thread with their record loads in flight together
+    constexpr int SU = 1; // (4 in flight measured slower: occupancy, L2-rate bound)
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g0 < S; g0 += stride * SU) {
+        float4 ra[SU][KF / 4], rb[SU][KF / 4];
 #pragma unroll
-        for (int q = 0; q < KF / 4; ++q) {
-            const float4 u = ri[q], v = rj[q];
-            a[4 * q] = u.x, a[4 * q + 1] = u.y, a[4 * q + 2] = u.z, a[4 * q + 3] = u.w;
-            b[4 * q] = v.x, b[4 * q + 1] = v.y, b[4 * q + 2] = v.z, b[4 * q + 3] = v.w;
+        for (int u = 0; u < SU; ++u) {
+            const int64_t g = g0 + u * stride;
+            const uint64_t h = mix64((uint64_t)(g < S ? g : 0) * 2 + 1);
+            const int64_t i = mulhi_index((uint32_t)(h >> 32), n);
+            int64_t j = i + 1 + mulhi_index((uint32_t)h, n - 1);
+            if (j >= n) j -= n;
+            const float4 *ri = reinterpret_cast<const float4 *>(xf + i * KF);
+            const float4 *rj = reinterpret_cast<const float4 *>(xf + j * KF);
+#pragma unroll
+            for (int q = 0; q < KF / 4; ++q) {
+                ra[u][q] = ri[q];
+                rb[u][q] = rj[q];
+            }
         }
-        float e = a[D] + b[D]; // -(n_i + n_j) / 2
 #pragma unroll
-        for (int k = 0; k < D; ++k) e = fmaf(a[k], b[k], e);
-        keys[g] = key_of(fmax(-2.0 * (double)e, 0.0));
+        for (int u = 0; u < SU; ++u) {
+            const int64_t g = g0 + u * stride;
+            if (g >= S) break;
+            const float *a = reinterpret_cast<const float *>(ra[u]);
+            const float *b = reinterpret_cast<const float *>(rb[u]);
+            float e = a[D] + b[D]; // -(n_i + n_j) / 2
+#pragma unroll
+            for (int k = 0; k < D; ++k) e = fmaf(a[k], b[k], e);
+            keys[g] = key_of(fmax(-2.0 * (double)e, 0.0));
+        }
     }
 }
 
 // Histogram of keys in `nreg` regions (region r: keys[r*cap .. r*cap+cnt_r)),
-// cnt_r = counts ? min(counts[r], cap) : cap.  Grid = nreg * parts.
+// cnt_r = counts ? min(counts[r], cap) : cap, for the current digit of each
+// active selection (keys whose resolved high bits match its prefix).  Block b
+// of HIST_BLOCKS (or fewer) takes regions b, b + G, ... (nreg >= G) or one of
+// G / nreg slices of a region, and writes its whole LDS histogram to
+// gpart[b][2 RADIX] (no global atomics: one flush per block instead of one
+// per non-zero bin); k_hist_sum adds the partials in block order.
+constexpr int HIST_BLOCKS = 256;
 __global__ __launch_bounds__(256) void k_hist_regions(const uint64_t *__restrict__ keys,
                                                      const uint32_t *__restrict__ counts,
-                                                     int64_t nreg, int64_t cap, int parts,
+                                                     int64_t nreg, int64_t cap,
                                                      const SelState *__restrict__ st,
-                                                     uint32_t *__restrict__ ghist)
+                                                     uint32_t *__restrict__ gpart)
 {
     __shared__ uint32_t sHist[2 * RADIX];
     for (int e = threadIdx.x; e < 2 * RADIX; e += 256) sHist[e] = 0;
     __syncthreads();
     const int nsel = st->nsel, shift = st->shift, hsh = shift + st->width;
     const uint64_t p0 = st->prefix[0], p1 = st->prefix[1];
-    const int64_t r = blockIdx.x / parts, part = blockIdx.x - r * parts;
-    int64_t cnt = counts ? (int64_t)counts[r] : cap;
-    if (cnt > cap) cnt = cap;
-    const uint64_t *kr = keys + r * cap;
-    for (int64_t e = part * 256 + threadIdx.x; e < cnt; e += (int64_t)parts * 256) {
-        const uint64_t key = kr[e];
-        const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
-        if (hsh >= 64 || (key >> hsh) == (p0 >> hsh)) atomicAdd(&sHist[dg], 1u);
-        if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (p1 >> hsh)))
-            atomicAdd(&sHist[RADIX + dg], 1u);
+    const int64_t G = gridDim.x;
+    const int64_t parts = nreg >= G ? 1 : G / nreg;
+    const int64_t rstep = nreg >= G ? G : nreg;
+    const int64_t part = nreg >= G ? 0 : blockIdx.x % parts;
+    for (int64_t r = nreg >= G ? blockIdx.x : blockIdx.x / parts; r < nreg; r += rstep) {
+        if (nreg < G && (int64_t)blockIdx.x >= parts * nreg) break;
+        int64_t cnt = counts ? (int64_t)counts[r] : cap;
+        if (cnt > cap) cnt = cap;
+        const uint64_t *kr = keys + r * cap;
+        // HU independent loads in flight per thread (the loop is latency bound)
+        constexpr int HU = 8;
+        for (int64_t e0 = part * 256 * HU + threadIdx.x; e0 < cnt; e0 += parts * 256 * HU) {
+            uint64_t kk[HU];
+#pragma unroll
+            for (int u = 0; u < HU; ++u) {
+                const int64_t e = e0 + u * 256;
+                kk[u] = e < cnt ? kr[e] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < HU; ++u) {
+                if (e0 + u * 256 >= cnt) break;
+                const uint64_t key = kk[u];
+                const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
+                if (hsh >= 64 || (key >> hsh) == (p0 >> hsh)) atomicAdd(&sHist[dg], 1u);
+                if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (p1 >> hsh)))
+                    atomicAdd(&sHist[RADIX + dg], 1u);
+            }
+        }
+        if (nreg < G) break;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 2 * RADIX; e += 256)
-        if (sHist[e]) atomicAdd(&ghist[e], sHist[e]);
+    uint32_t *o = gpart + (int64_t)blockIdx.x * 2 * RADIX;
+    for (int e = threadIdx.x; e < 2 * RADIX; e += 256) o[e] = sHist[e];
+}
+
+// ghist[e] = sum_b gpart[b][e] (integer sums: order-free).  A block covers 64
+// bins; its 4 waves take every 4th partial, 8 loads in flight per lane.
+__global__ __launch_bounds__(256) void k_hist_sum(const uint32_t *__restrict__ gpart, int nparts,
+                                                 uint32_t *__restrict__ ghist)
+{
+    __shared__ uint32_t sAcc[4][64];
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
+    uint32_t acc = 0;
+    for (int b0 = g; b0 < nparts; b0 += 32) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int b = b0 + 4 * u;
+            v[u] = b < nparts ? gpart[(int64_t)b * 2 * RADIX + e] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    sAcc[g][lane] = acc;
+    __syncthreads();
+    if (g == 0) ghist[e] = sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
+}
+
+// Keys of the regions whose resolved high bits (>= shift + width after the
+// last k_select_scan) match either selection's prefix -> cbuf, count in
+// *ccount (order of the compacted keys is irrelevant to the selection).
+__global__ __launch_bounds__(256) void k_compact(const uint64_t *__restrict__ keys,
+                                                const uint32_t *__restrict__ counts, int64_t nreg,
+                                                int64_t cap, const SelState *__restrict__ st,
+                                                uint64_t *__restrict__ cbuf,
+                                                unsigned long long *__restrict__ ccount)
+{
+    __shared__ int sCnt[4];
+    __shared__ unsigned long long sBase;
+    const int nsel = st->nsel, hsh = st->shift + st->width;
+    const uint64_t p0 = st->prefix[0], p1 = st->prefix[1];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t r = blockIdx.x; r < nreg; r += gridDim.x) {
+        int64_t cnt = counts ? (int64_t)counts[r] : cap;
+        if (cnt > cap) cnt = cap;
+        const uint64_t *kr = keys + r * cap;
+        constexpr int CU = 8; // loads in flight per thread
+        for (int64_t b = 0; b < cnt; b += 256 * CU) {
+            uint64_t kk[CU];
+            unsigned long long bal[CU];
+            int wtot = 0;
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                const int64_t e = b + u * 256 + threadIdx.x;
+                kk[u] = e < cnt ? kr[e] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                const int64_t e = b + u * 256 + threadIdx.x;
+                const uint64_t key = kk[u];
+                const bool m = e < cnt && (hsh >= 64 || (key >> hsh) == (p0 >> hsh) ||
+                                           (nsel > 1 && (key >> hsh) == (p1 >> hsh)));
+                bal[u] = __ballot(m);
+                wtot += __popcll(bal[u]);
+            }
+            // one global atomic per block and chunk (a shared counter hit by
+            // every wave with a match serialises at the L2)
+            if (lane == 0) sCnt[w] = wtot;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int tot = sCnt[0] + sCnt[1] + sCnt[2] + sCnt[3];
+                sBase = tot ? atomicAdd(ccount, (unsigned long long)tot) : 0ull;
+            }
+            __syncthreads();
+            unsigned long long base = sBase;
+            for (int v = 0; v < w; ++v) base += sCnt[v];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                if ((bal[u] >> lane) & 1ull) cbuf[base + __popcll(bal[u] & ((1ull << lane) - 1ull))] = kk[u];
+                base += __popcll(bal[u]);
+            }
+            __syncthreads(); // sCnt / sBase reused by the next chunk
+        }
+    }
+}
+
+// The remaining digits of the selection over the compacted keys, in one
+// work-group (single rank only): per digit an LDS histogram of the matching
+// keys and the same scan as k_select_scan.  Leaves st as the passes would.
+__global__ __launch_bounds__(1024) void k_select_tail(SelState *st, const uint64_t *__restrict__ cbuf,
+                                                     const unsigned long long *__restrict__ ccount,
+                                                     int passes)
+{
+    __shared__ uint32_t sHist[2 * RADIX];
+    __shared__ unsigned long long sPart[1024];
+    __shared__ int sDigit;
+    __shared__ unsigned long long sBelowD;
+    const int tid = threadIdx.x;
+    const int64_t cnt = (int64_t)*ccount;
+    const int nsel = st->nsel;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = st->shift, hsh = shift + st->width;
+        const uint64_t p0 = st->prefix[0], p1 = st->prefix[1];
+        for (int e = tid; e < 2 * RADIX; e += 1024) sHist[e] = 0;
+        __syncthreads();
+        for (int64_t e = tid; e < cnt; e += 1024) {
+            const uint64_t key = cbuf[e];
+            const uint32_t dg = (uint32_t)((key >> shift) & (RADIX - 1));
+            if (hsh >= 64 || (key >> hsh) == (p0 >> hsh)) atomicAdd(&sHist[dg], 1u);
+            if (nsel > 1 && (hsh >= 64 || (key >> hsh) == (p1 >> hsh)))
+                atomicAdd(&sHist[RADIX + dg], 1u);
+        }
+        __syncthreads();
+        constexpr int PER = RADIX / 1024;
+        for (int s = 0; s < nsel; ++s) {
+            const uint32_t *h = sHist + s * RADIX;
+            unsigned long long loc = 0;
+            for (int q = 0; q < PER; ++q) loc += h[tid * PER + q];
+            sPart[tid] = loc;
+            if (tid == 0) sDigit = -1;
+            __syncthreads();
+            for (int o = 1; o < 1024; o <<= 1) {
+                const unsigned long long v = tid >= o ? sPart[tid - o] : 0ull;
+                __syncthreads();
+                sPart[tid] += v;
+                __syncthreads();
+            }
+            const unsigned long long rank = st->rank[s];
+            const unsigned long long excl = tid ? sPart[tid - 1] : 0ull;
+            if (rank >= excl && rank < sPart[tid]) {
+                unsigned long long c = excl;
+                for (int q = 0; q < PER; ++q) {
+                    const unsigned long long hv = h[tid * PER + q];
+                    if (rank < c + hv) {
+                        sDigit = tid * PER + q;
+                        sBelowD = c;
+                        break;
+                    }
+                    c += hv;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (sDigit < 0) {
+                    st->error = 1;
+                } else {
+                    st->prefix[s] |= (uint64_t)sDigit << shift;
+                    st->rank[s] = rank - sBelowD;
+                }
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            st->pass += 1;
+            const int nshift = shift - RADIX_BITS;
+            st->shift = nshift >= 0 ? nshift : 0;
+            st->width = nshift >= 0 ? RADIX_BITS : shift;
+        }
+        __syncthreads();
+    }
 }
 
 // One radix-select step: for each active selection find the digit holding
@@ -2232,13 +2444,49 @@ hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *
 }
 
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                               int64_t cap, int parts, const SelState *st, uint32_t *ghist,
-                               hipStream_t stream)
+                               int64_t cap, int max_blocks, const SelState *st, uint32_t *gpart,
+                               uint32_t *ghist, hipStream_t stream)
 {
     if (nreg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hist_regions, dim3(nreg * parts), dim3(256), 0, stream, keys, counts,
-                       nreg, cap, parts, st, ghist);
+    int64_t G = HIST_BLOCKS;
+    if (max_blocks > 0 && G > max_blocks) G = max_blocks;
+    if (nreg < G) G = (G / nreg) * nreg; // whole slices per region
+    if (G < 1) G = 1;
+    hipLaunchKernelGGL(k_hist_regions, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap, st,
+                       gpart);
+    hipLaunchKernelGGL(k_hist_sum, dim3(2 * RADIX / 64), dim3(256), 0, stream, gpart, (int)G,
+                       ghist);
     return hipGetLastError();
+}
+
+hipError_t launch_compact(const uint64_t *keys, const uint32_t *counts, int64_t nreg, int64_t cap,
+                          const SelState *st, uint64_t *cbuf, unsigned long long *ccount,
+                          hipStream_t stream)
+{
+    if (nreg <= 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(ccount, 0, sizeof(unsigned long long), stream);
+    if (e != hipSuccess) return e;
+    const int64_t G = nreg < 8192 ? nreg : 8192;
+    hipLaunchKernelGGL(k_compact, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap, st, cbuf,
+                       ccount);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_tail(SelState *st, const uint64_t *cbuf, const unsigned long long *ccount,
+                              int passes, hipStream_t stream)
+{
+    if (passes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_select_tail, dim3(1), dim3(1024), 0, stream, st, cbuf, ccount, passes);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *ccount, int64_t cap,
+                             const SelState *st, uint32_t *gpart, uint32_t *ghist,
+                             hipStream_t stream)
+{
+    // one region whose count lives on the device (compacted keys; < 2^32)
+    return launch_hist_regions(keys, reinterpret_cast<const uint32_t *>(ccount), 1, cap, 64, st,
+                               gpart, ghist, stream);
 }
 
 hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream)
