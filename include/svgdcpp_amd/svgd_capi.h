@@ -224,6 +224,13 @@ int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi);
 int64_t svgd_plan_pair_tiles(int64_t n, int block, int world, int rank);
 void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
                          int64_t *row_block, int64_t *col_block);
+/* Median bucket select: from the all-reduced histogram of candidate keys in
+ * `nb` ascending key-range buckets, the bucket holding each of the `nsel`
+ * (1 or 2) candidate ranks, the rank inside it, and the total count of the
+ * distinct selected buckets (the keys a rank compacts and all-gathers).
+ * Returns 0, or -1 if a rank lies past the counted candidates. */
+int svgd_plan_bucket_select(const unsigned long long *counts, int nb, int nsel,
+                            const int64_t *ranks, int *bsel, int64_t *rank_in, int64_t *total);
 
 #ifdef __cplusplus
 }

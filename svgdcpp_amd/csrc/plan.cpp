@@ -82,4 +82,34 @@ void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
     *col_block = slot == 0 ? I : (I + slot) % nb;
 }
 
+// Bucket of each selection from the all-reduced key-range bucket counts
+// (NBK buckets, ascending key order): ranks[s] is the rank among the
+// candidates; writes the bucket and the rank within it, and the total count
+// of the distinct selected buckets.  Returns -1 if a rank lies past the
+// counted candidates.
+int svgd_plan_bucket_select(const unsigned long long *counts, int nb, int nsel,
+                            const int64_t *ranks, int *bsel, int64_t *rank_in, int64_t *total)
+{
+    if (nsel < 1 || nsel > 2) return -1;
+    int64_t cum = 0;
+    bsel[0] = bsel[1] = -1;
+    for (int b = 0; b < nb; ++b) {
+        const int64_t c = (int64_t)counts[b];
+        for (int s = 0; s < nsel; ++s)
+            if (bsel[s] < 0 && ranks[s] >= cum && ranks[s] < cum + c) {
+                bsel[s] = b;
+                rank_in[s] = ranks[s] - cum;
+            }
+        cum += c;
+    }
+    for (int s = 0; s < nsel; ++s)
+        if (bsel[s] < 0) return -1;
+    if (nsel == 1) {
+        bsel[1] = bsel[0];
+        rank_in[1] = rank_in[0];
+    }
+    *total = (int64_t)counts[bsel[0]] + (bsel[1] != bsel[0] ? (int64_t)counts[bsel[1]] : 0);
+    return 0;
+}
+
 } // extern "C"

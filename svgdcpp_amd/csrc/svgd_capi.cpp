@@ -94,6 +94,9 @@ struct svgd_ctx {
     uint64_t *cbuf = nullptr;          // compacted candidates (regions_alloc keys)
     unsigned long long *ccount = nullptr;
     uint32_t *gpart = nullptr;         // per-block histograms (HIST_PART_BLOCKS x 2 RADIX)
+    uint32_t *bpart = nullptr;         // collect blocks' key-range bucket histograms (1024 x NBK)
+    uint64_t *gseg = nullptr;          // world x (CAPG + 1): compacted selected-bucket keys
+    int64_t bucket_cap = CAPG;         // bucket select path if the selected buckets hold <= this
     uint32_t *counts = nullptr;
     unsigned long long *below = nullptr;
     int collect_grid = 0;
@@ -258,11 +261,26 @@ int allreduce_cnt3(svgd_ctx *c)
     // below, candidate and overflowed-region totals are sums; [3..4] (the
     // bracket) is identical on every rank and stays local
     if (c->hcomm) {
-        if (hostcomm_allreduce_u64(c->hcomm, c->cnt3, 3, c->stream))
+        if (hostcomm_allreduce_u64(c->hcomm, c->cnt3, 3 + NBK, c->stream))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
         return SVGD_OK;
     }
-    NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 3, ncclUint64, ncclSum, c->comm, c->stream));
+    NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 3 + NBK, ncclUint64, ncclSum, c->comm, c->stream));
+    return SVGD_OK;
+}
+
+// In-place all-gather of `cnt` u64 per rank (rank r's part at buf + r * cnt).
+int allgather_u64(svgd_ctx *c, uint64_t *buf, size_t cnt)
+{
+    if (c->world == 1) return SVGD_OK;
+    if (c->hcomm) {
+        if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(uint64_t),
+                               c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-gather failed.");
+        return SVGD_OK;
+    }
+    NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclUint64, c->comm,
+                             c->stream));
     return SVGD_OK;
 }
 
@@ -309,6 +327,7 @@ int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, 
     s.width = known_from > RADIX_BITS ? RADIX_BITS : known_from;
     s.lo_key = lo_key;
     s.hi_key = hi_key;
+    s.binv = (double)NBK / (double)(hi_key - lo_key);
     *c->h_st = s;
     HIPCHK(c, hipMemcpyAsync(c->st, c->h_st, sizeof(SelState), hipMemcpyHostToDevice, c->stream));
     return SVGD_OK;
@@ -318,18 +337,20 @@ int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, 
 // histogram, 2 debug dump) on the row-stream (d <= 16) or MFMA tile kernel.
 hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t cap, double *dbg)
 {
+    // the collect pass (mode 0) also histograms its candidates in key-range buckets
+    uint32_t *bp = mode == 0 ? c->bpart : nullptr;
     if (c->rowpath)
         return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->xf, c->nmax, c->n,
                                 c->pnb, c->tile0,
                                 c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
-                                c->ghist, dbg, c->stream);
+                                c->ghist, bp, dbg, c->stream);
     if (c->dtype == SVGD_F32)
         return launch_pair_tiles_f32(c->KP, mode, grid, c->xcf, c->nrmf, c->n, c->pnb, c->tile0,
                                      c->tile0 + c->own_tiles, regions, cap, c->counts, c->below,
-                                     c->st, c->ghist, dbg, c->stream);
+                                     c->st, c->ghist, bp, dbg, c->stream);
     return launch_pair_tiles(c->KP, mode, grid, c->xc, c->nrm, c->n, c->pnb, c->tile0,
                              c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
-                             c->ghist, dbg, c->stream);
+                             c->ghist, bp, dbg, c->stream);
 }
 
 // Phase 1 of the median: candidate bracket + collect pass + counts.
@@ -423,10 +444,10 @@ int median_begin(svgd_ctx *c)
         c->regions_alloc = need;
     }
     HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
-    HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->cnt3,
-                                   c->stream));
+    HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
+                                   c->collect_grid, c->cnt3, c->stream));
     CHK(allreduce_cnt3(c));
-    HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, 5 * sizeof(unsigned long long),
+    HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, CNT_LEN * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_cnt, c->stream));
     return SVGD_OK;
@@ -448,7 +469,7 @@ int median_finish(svgd_ctx *c)
     }
     HIPCHK(c, hipEventSynchronize(c->ev_cnt));
     const unsigned long long below = c->h_cnt[0], cand = c->h_cnt[1], ovf = c->h_cnt[2];
-    const uint64_t lo_key = c->h_cnt[3], hi_key = c->h_cnt[4];
+    const uint64_t lo_key = c->h_cnt[CNT_LO], hi_key = c->h_cnt[CNT_HI];
     const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
     bool ok = !ovf && r0 >= below && r1 < below + cand;
     int path = c->med_path;
@@ -460,6 +481,33 @@ int median_finish(svgd_ctx *c)
         path = SVGD_MEDIAN_FALLBACK;
         ranks[0] = c->sel_rank[0];
         ranks[1] = c->sel_rank[c->nsel - 1];
+    }
+    // Bucket select: the collect pass histogrammed the candidates in NBK
+    // key-range buckets (all-reduced with the counts), so the bucket holding
+    // each order statistic is known here.  If those buckets are small, every
+    // rank compacts its keys in them, the compacted keys are all-gathered once
+    // and one work-group selects exactly -- no per-digit all-reduces.
+    if (ok && c->bucket_cap > 0) {
+        const int64_t rr[2] = {(int64_t)ranks[0], (int64_t)ranks[1]};
+        int bsel[2];
+        int64_t rin[2], tot = 0;
+        const int ns = (c->nsel > 1 && ranks[1] != ranks[0]) ? 2 : 1;
+        if (svgd_plan_bucket_select(c->h_cnt + 3, NBK, ns, rr, bsel, rin, &tot) == 0 &&
+            tot <= std::min<int64_t>(c->bucket_cap, CAPG)) {
+            HIPCHK(c, launch_set_sel(c->st, c->nsel, (uint64_t)rin[0],
+                                     (uint64_t)(c->nsel > 1 ? rin[ns - 1] : rin[0]), bsel[0],
+                                     bsel[ns - 1], c->stream));
+            uint64_t *seg = c->gseg + (size_t)c->rank * (CAPG + 1);
+            HIPCHK(c, hipMemsetAsync(seg, 0, sizeof(uint64_t), c->stream));
+            HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st,
+                                             seg, c->stream));
+            CHK(allgather_u64(c, c->gseg, CAPG + 1));
+            HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, c->stream));
+            HIPCHK(c, launch_finalize(c->st, c->navg, c->src_lo, c->src_hi, logn, c->scal,
+                                      c->scal + 1, c->stream));
+            c->last_path = path;
+            return SVGD_OK;
+        }
     }
     // every candidate key lies in [lo_key, hi_key): their common leading bits
     // are known, so the radix passes start below them (bracket path only)
@@ -803,7 +851,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->scal, 2));
     CHK(dalloc(c, &c->counts, 4096)); // <= 4 regions per collect block, <= 1024 blocks
     CHK(dalloc(c, &c->below, 4096));
-    CHK(dalloc(c, &c->cnt3, 8));
+    CHK(dalloc(c, &c->cnt3, CNT_LEN + 3));
+    CHK(dalloc(c, &c->bpart, (int64_t)1024 * NBK)); // collect grid <= 1024
+    CHK(dalloc(c, &c->gseg, (int64_t)c->world * (CAPG + 1)));
+    if (const char *e = std::getenv("SVGD_BUCKET_CAP")) c->bucket_cap = std::atoll(e);
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
     CHK(dalloc(c, &c->gpart, (int64_t)HIST_PART_BLOCKS * 2 * RADIX));
@@ -811,7 +862,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
     HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, 8 * sizeof(unsigned long long), hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, (CNT_LEN + 3) * sizeof(unsigned long long),
+                            hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_st, sizeof(SelState), hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_scal, 2 * sizeof(double), hipHostMallocDefault));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));
@@ -859,8 +911,10 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
     if (world > 1 && std::getenv("SVGD_HOSTCOMM")) {
         // rehearsal backend: ranks sharing one GPU, collectives through host shm
         const size_t slot = std::max<size_t>(
-            std::max<size_t>((size_t)c->chunk * c->dim, (size_t)c->dim * c->dim) * sizeof(double),
-            2 * RADIX * sizeof(uint32_t));
+            std::max<size_t>(
+                std::max<size_t>((size_t)c->chunk * c->dim, (size_t)c->dim * c->dim) * sizeof(double),
+                2 * RADIX * sizeof(uint32_t)),
+            std::max<size_t>((CAPG + 1) * sizeof(uint64_t), (3 + NBK) * sizeof(uint64_t)));
         if (hostcomm_create(&c->hcomm, std::getenv("SVGD_HOSTCOMM"), world, rank, slot))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host communicator setup failed.");
         return SVGD_OK;
@@ -890,7 +944,8 @@ int svgd_destroy(svgd_ctx *c)
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
-                     c->xf,          c->nmax,    c->sc_err, c->wgI,   c->cbuf, c->ccount, c->gpart};
+                     c->xf,          c->nmax,    c->sc_err, c->wgI,   c->cbuf, c->ccount, c->gpart,
+                     c->bpart,       c->gseg};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal, c->h_err};

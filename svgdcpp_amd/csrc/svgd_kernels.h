@@ -22,7 +22,17 @@ struct SelState {
     int32_t pass;         // digits resolved so far
     int32_t error;        // rank outside the histogram (should not happen)
     int32_t pad_;
+    double binv;          // key-range buckets of [lo_key, hi_key): NBK / (hi - lo)
+    int32_t bsel[2];      // bucket of each selection (bucket select path)
 };
+
+// Key-range buckets of the candidate bracket: bucket(key) = floor((key - lo)
+// * binv), clamped to [0, NBK) -- monotone in the key, so buckets are
+// contiguous key ranges.  The collect pass histograms them, so one all-reduce
+// (counts + buckets) tells every rank which bucket holds each order statistic.
+constexpr int NBK = 2048;
+// per-rank capacity of the compacted selected-bucket keys (gathered over ranks)
+constexpr int CAPG = 16384;
 
 // xc = X - mean (stride KP, zero padded), nrm = |xc|^2; nrm_in_slot also
 // stores |xc|^2 at xc[j*KP + d] (the row-stream median record).
@@ -46,8 +56,8 @@ hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, c
 hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, const float *nrm,
                                  int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                                  int64_t cap, uint32_t *counts, unsigned long long *below,
-                                 const SelState *st, uint32_t *ghist, double *dbg_out,
-                                 hipStream_t stream);
+                                 const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                                 double *dbg_out, hipStream_t stream);
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream);
 // Sampled median keys on the tile path: ntiles random (block, block) pairs of
 // distinct full 64-particle blocks, all 64 x 64 keys each (xcf/nrmf: fp32 path)
@@ -61,11 +71,12 @@ hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, do
 // mode 0: collect keys in [st->lo_key, st->hi_key) into per-block regions and count
 // keys below lo_key; mode 1: radix histogram pass over all pairs (fallback);
 // mode 2: debug dump of every key in (i<j) row-major order.
+// bpart (mode 0, optional): per-block key-range bucket histograms [grid][NBK]
 hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
                              int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                              int64_t cap, uint32_t *counts, unsigned long long *below,
-                             const SelState *st, uint32_t *ghist, double *dbg_out,
-                             hipStream_t stream);
+                             const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                             double *dbg_out, hipStream_t stream);
 // xf != nullptr (d <= 16): keys from the fp32 records (a bracket estimate only)
 hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
                               int d, int KP, int64_t S, uint64_t *keys, hipStream_t stream);
@@ -83,9 +94,24 @@ hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *cco
                              const SelState *st, uint32_t *gpart, uint32_t *ghist,
                              hipStream_t stream);
 hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream);
+// cnt = [below, candidates, overflowed regions, NBK bucket counts (zero without
+// bpart), lo_key, hi_key]: the first 3 + NBK entries are sums over ranks.
+constexpr int CNT_LO = 3 + NBK, CNT_HI = 4 + NBK, CNT_LEN = 5 + NBK;
 hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
                                 int64_t nblk, int64_t cap, const SelState *st,
+                                const uint32_t *bpart, int64_t nbpart,
                                 unsigned long long *cnt, hipStream_t stream);
+// bucket select path: the selections' ranks within their buckets (other fields kept)
+hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
+                          hipStream_t stream);
+// keys of the selected buckets st->bsel[] -> seg = [count, keys (<= CAPG)]
+// (seg[0] must be zero on entry)
+hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
+                                  int64_t cap, const SelState *st, uint64_t *seg,
+                                  hipStream_t stream);
+// exact selection of st->rank[s] within bucket st->bsel[s] over nseg gathered
+// segments [count, keys...] of stride CAPG + 1 -> st->prefix[s] = that key
+hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, hipStream_t stream);
 hipError_t launch_bracket(SelState *st, hipStream_t stream);
 
 // Row-stream path (d <= 16): particle records rec_j = [xc_j | G_j - 2a xc_j | c_j | 0..],
@@ -136,8 +162,8 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                             const float *xf, const unsigned long long *nmax_bits,
                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
-                            const SelState *st, uint32_t *ghist, double *dbg_out,
-                            hipStream_t stream);
+                            const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                            double *dbg_out, hipStream_t stream);
 int phi_rows_blocks_per_cu(int d, int R);
 // G = grad log p of the Gaussian-sum model for `rows` particle rows (d <= 64)
 hipError_t launch_gauss_grad(const double *X, int64_t rows, int d, int k, const double *mu,

@@ -378,6 +378,13 @@ __device__ __forceinline__ uint64_t key_of(double s)
     return (uint64_t)__double_as_longlong(s) & 0x7fffffffffffffffull; // s >= 0 (+0, never -0)
 }
 
+// Key-range bucket of a candidate key (SelState::binv): monotone in the key.
+__device__ __forceinline__ int kbucket(uint64_t key, uint64_t lo, double binv)
+{
+    const double t = (double)(key - lo) * binv;
+    return t < (double)(NBK - 1) ? (t > 0.0 ? (int)t : 0) : NBK - 1;
+}
+
 // Device copy of plan_pair_tile (plan.cpp): tile index -> (row block, col block).
 __device__ __forceinline__ void tile_coords(int64_t nb, int64_t t, int64_t *I, int64_t *J)
 {
@@ -409,6 +416,7 @@ struct SinkCollect {
     unsigned long long *below_out;
     const float *xf;                     // fp32 records (unused by the collect pass)
     const unsigned long long *nmax_bits; // max |xc|^2 (double bits): classification margin
+    uint32_t *bpart;                     // per-block key-range bucket histograms (optional)
 };
 
 struct SinkHist {
@@ -443,6 +451,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
     __shared__ uint32_t sCnt;
     __shared__ unsigned long long sBelow[4];
+    __shared__ uint32_t sBk[(MODE == 0) ? NBK : 1];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int lo = lane & 15, hi = lane >> 4;
@@ -464,10 +473,15 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
         for (int e = tid; e < 2 * RADIX; e += 256) sHist[e] = 0;
     }
     uint64_t lo_key = 0, hi_key = 0;
+    double binv = 0.0;
     if (MODE == 0) {
         lo_key = sc.st->lo_key;
         hi_key = sc.st->hi_key;
+        binv = sc.st->binv;
         if (tid == 0) sCnt = 0;
+        if (sc.bpart)
+            for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
+        __syncthreads();
     }
     uint32_t below = 0;
 
@@ -532,6 +546,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
                             const int64_t pos =
                                 base + __popcll(mask & ((1ull << lane) - 1ull));
                             if (pos < sc.cap) sc.region[blockIdx.x * sc.cap + pos] = key;
+                            if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
                         }
                     }
                 } else if (MODE == 1) {
@@ -565,6 +580,8 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
             sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
             sc.count_out[blockIdx.x] = sCnt;
         }
+        if (sc.bpart)
+            for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
     } else if (MODE == 1) {
         __syncthreads();
         for (int e = tid; e < 2 * RADIX; e += 256)
@@ -848,6 +865,216 @@ __global__ __launch_bounds__(1024) void k_select_tail(SelState *st, const uint64
     }
 }
 
+// ------------------------------------------------ bucket select path --
+// cnt[3 + e] = sum_b bpart[b][e] (integer sums: order-free); 64 buckets per
+// block, its 4 waves take every 4th partial with 8 loads in flight.
+__global__ __launch_bounds__(256) void k_bucket_sum(const uint32_t *__restrict__ bpart, int nparts,
+                                                   unsigned long long *__restrict__ out)
+{
+    __shared__ unsigned long long sAcc[4][64];
+    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
+    unsigned long long acc = 0;
+    for (int b0 = g; b0 < nparts; b0 += 32) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int b = b0 + 4 * u;
+            v[u] = b < nparts ? bpart[(int64_t)b * NBK + e] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    sAcc[g][lane] = acc;
+    __syncthreads();
+    if (g == 0) out[e] = sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
+}
+
+__global__ void k_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1)
+{
+    st->nsel = nsel;
+    st->rank[0] = r0;
+    st->rank[1] = r1;
+    st->bsel[0] = b0;
+    st->bsel[1] = b1;
+    st->prefix[0] = st->prefix[1] = 0;
+    st->error = 0;
+}
+
+// Keys of the regions in the selected bucket(s) -> seg = [count, keys]; one
+// global atomic per block and chunk (positions past CAPG are dropped: the host
+// only takes this path when the selected buckets hold <= CAPG keys in total).
+__global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restrict__ keys,
+                                                        const uint32_t *__restrict__ counts,
+                                                        int64_t nreg, int64_t cap,
+                                                        const SelState *__restrict__ st,
+                                                        uint64_t *__restrict__ seg)
+{
+    __shared__ int sCnt[4];
+    __shared__ unsigned long long sBase;
+    const int nsel = st->nsel, b0 = st->bsel[0], b1 = nsel > 1 ? st->bsel[1] : -1;
+    const uint64_t lo = st->lo_key;
+    const double binv = st->binv;
+    unsigned long long *ctr = reinterpret_cast<unsigned long long *>(seg);
+    uint64_t *outk = seg + 1;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t r = blockIdx.x; r < nreg; r += gridDim.x) {
+        int64_t cnt = counts ? (int64_t)counts[r] : cap;
+        if (cnt > cap) cnt = cap;
+        const uint64_t *kr = keys + r * cap;
+        constexpr int CU = 8;
+        for (int64_t b = 0; b < cnt; b += 256 * CU) {
+            uint64_t kk[CU];
+            unsigned long long bal[CU];
+            int wtot = 0;
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                const int64_t e = b + u * 256 + threadIdx.x;
+                kk[u] = e < cnt ? kr[e] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                const int64_t e = b + u * 256 + threadIdx.x;
+                const int kb = kbucket(kk[u], lo, binv);
+                bal[u] = __ballot(e < cnt && (kb == b0 || kb == b1));
+                wtot += __popcll(bal[u]);
+            }
+            if (lane == 0) sCnt[w] = wtot;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int tot = sCnt[0] + sCnt[1] + sCnt[2] + sCnt[3];
+                sBase = tot ? atomicAdd(ctr, (unsigned long long)tot) : 0ull;
+            }
+            __syncthreads();
+            unsigned long long base = sBase;
+            for (int v = 0; v < w; ++v) base += sCnt[v];
+#pragma unroll
+            for (int u = 0; u < CU; ++u) {
+                if ((bal[u] >> lane) & 1ull) {
+                    const unsigned long long pos = base + __popcll(bal[u] & ((1ull << lane) - 1ull));
+                    if (pos < (unsigned long long)CAPG) outk[pos] = kk[u];
+                }
+                base += __popcll(bal[u]);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Exact selection over the gathered segments (one per rank): for each
+// selection s, the rank[s]-th smallest key of bucket bsel[s].  Radix passes
+// (11-bit digits, LDS histogram, block scan) start below the common prefix of
+// the bucket's min and max key, so a narrow bucket needs 1-3 passes.
+__global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint64_t *__restrict__ segs,
+                                                      int nseg)
+{
+    __shared__ uint32_t sHist[RADIX];
+    __shared__ unsigned long long sPart[1024];
+    __shared__ unsigned long long sMn[16], sMx[16];
+    __shared__ int sDigit;
+    __shared__ unsigned long long sBelowD;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t lo = st->lo_key;
+    const double binv = st->binv;
+    const int nsel = st->nsel;
+    for (int s = 0; s < nsel; ++s) {
+        const int b = st->bsel[s];
+        unsigned long long rank = st->rank[s];
+        uint64_t mn = ~0ull, mx = 0;
+        for (int g = 0; g < nseg; ++g) {
+            const uint64_t *sg = segs + (int64_t)g * (CAPG + 1);
+            const int64_t cnt = min<int64_t>((int64_t)sg[0], CAPG);
+            for (int64_t e = tid; e < cnt; e += 1024) {
+                const uint64_t key = sg[1 + e];
+                if (kbucket(key, lo, binv) == b) {
+                    mn = key < mn ? key : mn;
+                    mx = key > mx ? key : mx;
+                }
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a = __shfl_xor(mn, o), c = __shfl_xor(mx, o);
+            mn = a < mn ? a : mn;
+            mx = c > mx ? c : mx;
+        }
+        if (lane == 0) {
+            sMn[wv] = mn;
+            sMx[wv] = mx;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t a = sMn[0], c = sMx[0];
+            for (int q = 1; q < 16; ++q) {
+                a = sMn[q] < a ? sMn[q] : a;
+                c = sMx[q] > c ? sMx[q] : c;
+            }
+            sMn[0] = a;
+            sMx[0] = c;
+        }
+        __syncthreads();
+        mn = sMn[0];
+        mx = sMx[0];
+        const uint64_t diff = mn ^ mx;
+        int known = diff ? 64 - __clzll((long long)diff) : 0;
+        uint64_t prefix = known >= 64 ? 0ull : (mn & ~((1ull << known) - 1ull));
+        while (known > 0) {
+            const int width = known >= RADIX_BITS ? RADIX_BITS : known;
+            const int shift = known - width;
+            for (int e = tid; e < RADIX; e += 1024) sHist[e] = 0;
+            __syncthreads();
+            for (int g = 0; g < nseg; ++g) {
+                const uint64_t *sg = segs + (int64_t)g * (CAPG + 1);
+                const int64_t cnt = min<int64_t>((int64_t)sg[0], CAPG);
+                for (int64_t e = tid; e < cnt; e += 1024) {
+                    const uint64_t key = sg[1 + e];
+                    if (kbucket(key, lo, binv) == b &&
+                        (known >= 64 || (key >> known) == (prefix >> known)))
+                        atomicAdd(&sHist[(key >> shift) & ((1u << width) - 1u)], 1u);
+                }
+            }
+            __syncthreads();
+            constexpr int PER = RADIX / 1024;
+            unsigned long long loc = 0;
+            for (int q = 0; q < PER; ++q) loc += sHist[tid * PER + q];
+            sPart[tid] = loc;
+            if (tid == 0) sDigit = -1;
+            __syncthreads();
+            for (int o = 1; o < 1024; o <<= 1) {
+                const unsigned long long v = tid >= o ? sPart[tid - o] : 0ull;
+                __syncthreads();
+                sPart[tid] += v;
+                __syncthreads();
+            }
+            const unsigned long long excl = tid ? sPart[tid - 1] : 0ull;
+            if (rank >= excl && rank < sPart[tid]) {
+                unsigned long long c = excl;
+                for (int q = 0; q < PER; ++q) {
+                    const unsigned long long hv = sHist[tid * PER + q];
+                    if (rank < c + hv) {
+                        sDigit = tid * PER + q;
+                        sBelowD = c;
+                        break;
+                    }
+                    c += hv;
+                }
+            }
+            __syncthreads();
+            const int dg = sDigit;
+            const unsigned long long bd = sBelowD;
+            __syncthreads();
+            if (dg < 0) { // rank outside the bucket (the host checked; should not happen)
+                if (tid == 0) st->error = 1;
+                break;
+            }
+            prefix |= (uint64_t)dg << shift;
+            rank -= bd;
+            known = shift;
+        }
+        if (tid == 0) st->prefix[s] = prefix;
+        __syncthreads();
+    }
+}
+
 // One radix-select step: for each active selection find the digit holding
 // its remaining rank, append it to the prefix, subtract the count below,
 // zero the histogram and advance to the next digit.
@@ -939,8 +1166,8 @@ __global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
         cnt[0] = s0[0];
         cnt[1] = s1[0];
         cnt[2] = s2[0];
-        cnt[3] = st->lo_key;
-        cnt[4] = st->hi_key;
+        cnt[CNT_LO] = st->lo_key;
+        cnt[CNT_HI] = st->hi_key;
     }
 }
 
@@ -952,6 +1179,7 @@ __global__ void k_bracket(SelState *st)
     st->lo_key = st->prefix[0];
     const uint64_t top = st->prefix[1] + (sh >= 64 ? 0ull : (1ull << sh));
     st->hi_key = (top < st->prefix[1]) ? ~0ull : top;
+    st->binv = (double)NBK / (double)(st->hi_key - st->lo_key);
 }
 
 // med = (sqrt(u_lo) + sqrt(u_hi)) / 2 (or the single middle value);
@@ -1121,6 +1349,11 @@ __device__ __forceinline__ void lds_store_u64(const uint64_t *p, uint64_t v)
 {
     const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint64_t *)p;
     asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lds_add_u32(const uint32_t *p, uint32_t v)
+{
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t *)p;
+    asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
 // Loads: the destination registers are only valid after lgkmcnt drains and the
 // compiler does not know that, so every load helper waits inside the same asm
@@ -1393,7 +1626,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
     // staging.  The staging lives inside smem on purpose: a separate
     // __shared__ array makes the compiler drain the in-flight column DMA
     // before every LDS read of the loop.
-    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + (MODE == 0 ? 4 * STG * 8 : 0)];
+    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + (MODE == 0 ? 4 * STG * 8 + NBK * 4 : 0)];
     __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     // wave index made provably uniform (wave-uniform tile walk)
@@ -1407,6 +1640,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
     // after each column-DMA wait, so the global stores drain during a whole
     // chunk instead of stalling the next vmcnt wait; no LDS atomics.
     uint64_t(*sStage)[STG] = reinterpret_cast<uint64_t(*)[STG]>(smem + 4 * 2 * CHB);
+    // (MODE 0) key-range bucket histogram of the staged keys, updated with asm
+    // LDS atomics in flush() for the same reason as the staging stores
+    uint32_t *sBk = reinterpret_cast<uint32_t *>(smem + 4 * 2 * CHB + (MODE == 0 ? 4 * STG * 8 : 0));
+    uint64_t blo = 0;
+    double binv = 0.0;
     const int64_t wreg = (int64_t)blockIdx.x * 4 + w;
     int64_t wcnt = 0; // keys written to the region
     int scnt = 0;     // keys staged in sStage[w]
@@ -1419,7 +1657,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
 #pragma unroll
         for (int t = 0; t < STG / 64; ++t) {
             const int64_t pos = wcnt + t * 64 + lane;
-            if (t * 64 + lane < scnt && pos < sc.cap) wregion[pos] = v[t];
+            if (t * 64 + lane < scnt) {
+                if (pos < sc.cap) wregion[pos] = v[t];
+                if (sc.bpart) lds_add_u32(&sBk[kbucket(v[t], blo, binv)], 1u);
+            }
         }
         wcnt += scnt;
         scnt = 0;
@@ -1432,6 +1673,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
         lo_key = sc.st->lo_key;
         hi_key = sc.st->hi_key;
         nmax = __longlong_as_double((long long)*sc.nmax_bits);
+        blo = lo_key;
+        binv = sc.st->binv;
+        if (sc.bpart)
+            for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
     } else if (MODE == 1) {
         nsel = sh.st->nsel;
         shift = sh.st->shift;
@@ -1660,6 +1905,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
         if (lane == 0) {
             sc.below_out[wreg] = below;
             sc.count_out[wreg] = (uint32_t)min<int64_t>(wcnt, 0xffffffffll);
+        }
+        if (sc.bpart) {
+            lgkm_wait(); // this wave's asm bucket atomics
+            __syncthreads();
+            for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
         }
     } else if (MODE == 1) {
         __syncthreads();
@@ -2241,12 +2491,12 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                             const float *xf, const unsigned long long *nmax_bits,
                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
-                            const SelState *st, uint32_t *ghist, double *dbg_out,
-                            hipStream_t stream)
+                            const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                            double *dbg_out, hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
     if (mode == 0 && !nmax_bits) return hipErrorInvalidValue;
-    SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits};
+    SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, mode == 0 ? bpart : nullptr};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n};
     return launch_rows_kernel(10 + mode, d, 1, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, xc,
@@ -2320,11 +2570,11 @@ static hipError_t launch_pair_tiles_t(int KP, int mode, int grid, const T *xc, c
                                       int64_t n, int64_t nb, int64_t t0, int64_t t1,
                                       uint64_t *regions, int64_t cap, uint32_t *counts,
                                       unsigned long long *below, const SelState *st,
-                                      uint32_t *ghist, double *dbg_out, hipStream_t stream,
-                                      uint64_t *sample_out = nullptr)
+                                      uint32_t *ghist, uint32_t *bpart, double *dbg_out,
+                                      hipStream_t stream, uint64_t *sample_out = nullptr)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
-    SinkCollect sc{st, regions, cap, counts, below};
+    SinkCollect sc{st, regions, cap, counts, below, nullptr, nullptr, mode == 0 ? bpart : nullptr};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n, sample_out};
     SVGD_TILE_CASE(4)
@@ -2340,21 +2590,21 @@ static hipError_t launch_pair_tiles_t(int KP, int mode, int grid, const T *xc, c
 hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
                              int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                              int64_t cap, uint32_t *counts, unsigned long long *below,
-                             const SelState *st, uint32_t *ghist, double *dbg_out,
-                             hipStream_t stream)
+                             const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                             double *dbg_out, hipStream_t stream)
 {
     return launch_pair_tiles_t<double>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
-                                       counts, below, st, ghist, dbg_out, stream);
+                                       counts, below, st, ghist, bpart, dbg_out, stream);
 }
 
 hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, const float *nrm,
                                  int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                                  int64_t cap, uint32_t *counts, unsigned long long *below,
-                                 const SelState *st, uint32_t *ghist, double *dbg_out,
-                                 hipStream_t stream)
+                                 const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                                 double *dbg_out, hipStream_t stream)
 {
     return launch_pair_tiles_t<float>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
-                                      counts, below, st, ghist, dbg_out, stream);
+                                      counts, below, st, ghist, bpart, dbg_out, stream);
 }
 
 hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, const float *xcf,
@@ -2365,10 +2615,10 @@ hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, cons
     const int grid = (int)(ntiles < 1024 ? ntiles : 1024);
     if (xcf)
         return launch_pair_tiles_t<float>(KP, 3, grid, xcf, nrmf, n, 0, 0, ntiles, nullptr, 0,
-                                          nullptr, nullptr, nullptr, nullptr, nullptr, stream,
-                                          keys);
+                                          nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                          stream, keys);
     return launch_pair_tiles_t<double>(KP, 3, grid, xc, nrm, n, 0, 0, ntiles, nullptr, 0, nullptr,
-                                       nullptr, nullptr, nullptr, nullptr, stream, keys);
+                                       nullptr, nullptr, nullptr, nullptr, nullptr, stream, keys);
 }
 
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream)
@@ -2497,10 +2747,42 @@ hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream)
 
 hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
                                 int64_t nblk, int64_t cap, const SelState *st,
+                                const uint32_t *bpart, int64_t nbpart,
                                 unsigned long long *cnt, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_counts_reduce, dim3(1), dim3(256), 0, stream, below, counts, nblk, cap,
                        st, cnt);
+    if (bpart && nbpart > 0) {
+        hipLaunchKernelGGL(k_bucket_sum, dim3(NBK / 64), dim3(256), 0, stream, bpart, (int)nbpart,
+                           cnt + 3);
+    } else {
+        hipError_t e = hipMemsetAsync(cnt + 3, 0, NBK * sizeof(unsigned long long), stream);
+        if (e != hipSuccess) return e;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
+                          hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_set_sel, dim3(1), dim3(1), 0, stream, st, nsel, r0, r1, b0, b1);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
+                                  int64_t cap, const SelState *st, uint64_t *seg,
+                                  hipStream_t stream)
+{
+    if (nreg <= 0) return hipSuccess;
+    const int64_t G = nreg < 8192 ? nreg : 8192;
+    hipLaunchKernelGGL(k_compact_buckets, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap,
+                       st, seg);
+    return hipGetLastError();
+}
+
+hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg);
     return hipGetLastError();
 }
 

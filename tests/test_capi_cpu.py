@@ -157,3 +157,41 @@ def test_host_model_hessian_sum_matches_oracle(oracle):
     m = S.GaussianSum(list(mus), covs)
     np.testing.assert_allclose(m.neg_hess_sum(X), oracle.neg_hess_sum_gmm(X, mus, np.stack(covs)),
                                rtol=1e-11, atol=1e-11)
+
+
+def test_plan_bucket_select():
+    """Bucket of each median rank from an ascending bucket histogram (the
+    all-reduced key-range counts of the collect pass)."""
+    lib = C.lib()
+    rng = np.random.default_rng(7)
+    for trial in range(50):
+        nb = int(rng.integers(1, 64))
+        counts = rng.integers(0, 5, nb).astype(np.uint64)
+        tot = int(counts.sum())
+        if tot == 0:
+            continue
+        cum = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        nsel = int(rng.integers(1, 3))
+        r = np.sort(rng.integers(0, tot, nsel)).astype(np.int64)
+        bsel = (ctypes.c_int * 2)()
+        rin = (ctypes.c_int64 * 2)()
+        tot_sel = ctypes.c_int64()
+        rc = lib.svgd_plan_bucket_select(counts.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), nb, nsel,
+                                         r.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), bsel, rin,
+                                         ctypes.byref(tot_sel))
+        assert rc == 0
+        exp_b = [int(np.searchsorted(cum, x, side="right") - 1) for x in r]
+        for s in range(nsel):
+            assert bsel[s] == exp_b[s]
+            assert rin[s] == r[s] - cum[exp_b[s]]
+        bs = sorted(set(exp_b))
+        assert tot_sel.value == sum(int(counts[b]) for b in bs)
+    # a rank past the candidates is refused
+    counts = np.array([1, 2, 0], dtype=np.uint64)
+    r = np.array([3], dtype=np.int64)
+    bsel = (ctypes.c_int * 2)()
+    rin = (ctypes.c_int64 * 2)()
+    t = ctypes.c_int64()
+    assert lib.svgd_plan_bucket_select(counts.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 3, 1,
+                                       r.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), bsel, rin,
+                                       ctypes.byref(t)) == -1

@@ -115,6 +115,36 @@ def test_median_bracket_path_exact(oracle, n, d):
     assert med == m0 and a == a0
 
 
+@pytest.mark.parametrize("n,d,sample", [(700, 5, 1 << 14), (1501, 5, 1 << 14), (1300, 40, 1 << 14),
+                                         (2100, 3, 1 << 18), (900, 4, 1 << 10)])
+def test_median_bucket_select_matches_digit_passes(oracle, monkeypatch, n, d, sample):
+    """The bucket select (selected key-range buckets compacted and selected in
+    one work-group) and the per-digit radix passes pick the same keys."""
+    X = oracle.splitmix((n, d), 1.0, 3 * n + d)
+    res = []
+    for cap in ("16384", "0"):  # default path, then the digit passes only
+        monkeypatch.setenv("SVGD_BUCKET_CAP", cap)
+        c, a, med = _median_with_tuning(X, 0, sample, -1)
+        assert c.last_scale()[2] == C.SVGD_MEDIAN_BRACKET
+        res.append((a, med))
+    assert res[0] == res[1]
+    ref_a, ref_med = oracle.median_scale(X)
+    assert res[0][1] == pytest.approx(ref_med, rel=1e-12)
+
+
+def test_median_bucket_select_ties(oracle, monkeypatch):
+    """Heavy ties inside the selected bucket (5 distinct points)."""
+    base = oracle.splitmix((5, 3), 1.0, 11)
+    X = np.repeat(base, 60, axis=0)
+    out = []
+    for cap in ("16384", "0"):
+        monkeypatch.setenv("SVGD_BUCKET_CAP", cap)
+        c, a, med = _median_with_tuning(X, 0, 1 << 12, -1)
+        out.append(med)
+    assert out[0] == out[1]
+    assert out[0] == pytest.approx(oracle.median_scale(X)[1], rel=1e-12)
+
+
 def test_median_fallback_path_exact(oracle):
     n = 900
     X = oracle.splitmix((n, 4), 1.0, 42)
