@@ -494,11 +494,10 @@ int median_finish(svgd_ctx *c)
         const int ns = (c->nsel > 1 && ranks[1] != ranks[0]) ? 2 : 1;
         if (svgd_plan_bucket_select(c->h_cnt + 3, NBK, ns, rr, bsel, rin, &tot) == 0 &&
             tot <= std::min<int64_t>(c->bucket_cap, CAPG)) {
+            uint64_t *seg = c->gseg + (size_t)c->rank * (CAPG + 1);
             HIPCHK(c, launch_set_sel(c->st, c->nsel, (uint64_t)rin[0],
                                      (uint64_t)(c->nsel > 1 ? rin[ns - 1] : rin[0]), bsel[0],
-                                     bsel[ns - 1], c->stream));
-            uint64_t *seg = c->gseg + (size_t)c->rank * (CAPG + 1);
-            HIPCHK(c, hipMemsetAsync(seg, 0, sizeof(uint64_t), c->stream));
+                                     bsel[ns - 1], seg, c->stream));
             HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st,
                                              seg, c->stream));
             CHK(allgather_u64(c, c->gseg, CAPG + 1));

@@ -101,9 +101,10 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
                                 int64_t nblk, int64_t cap, const SelState *st,
                                 const uint32_t *bpart, int64_t nbpart,
                                 unsigned long long *cnt, hipStream_t stream);
-// bucket select path: the selections' ranks within their buckets (other fields kept)
+// bucket select path: the selections' ranks within their buckets (other fields
+// kept) and a zeroed counter seg[0] for launch_compact_buckets
 hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
-                          hipStream_t stream);
+                          uint64_t *seg, hipStream_t stream);
 // keys of the selected buckets st->bsel[] -> seg = [count, keys (<= CAPG)]
 // (seg[0] must be zero on entry)
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,

@@ -866,32 +866,41 @@ __global__ __launch_bounds__(1024) void k_select_tail(SelState *st, const uint64
 }
 
 // ------------------------------------------------ bucket select path --
-// cnt[3 + e] = sum_b bpart[b][e] (integer sums: order-free); 64 buckets per
-// block, its 4 waves take every 4th partial with 8 loads in flight.
+// out[e] += sum over a slice of the partials bpart[b][e] (integer sums:
+// order-free).  Grid = (NBK / 64 bucket groups) x BSUM_SLICES partial slices;
+// out must be zero on entry (k_counts_reduce clears it).
+constexpr int BSUM_SLICES = 16;
 __global__ __launch_bounds__(256) void k_bucket_sum(const uint32_t *__restrict__ bpart, int nparts,
                                                    unsigned long long *__restrict__ out)
 {
     __shared__ unsigned long long sAcc[4][64];
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;
+    const int per = (nparts + BSUM_SLICES - 1) / BSUM_SLICES;
+    const int p0 = blockIdx.y * per, p1 = min(nparts, p0 + per);
     unsigned long long acc = 0;
-    for (int b0 = g; b0 < nparts; b0 += 32) {
+    for (int b0 = p0 + g; b0 < p1; b0 += 32) {
         uint32_t v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int b = b0 + 4 * u;
-            v[u] = b < nparts ? bpart[(int64_t)b * NBK + e] : 0u;
+            v[u] = b < p1 ? bpart[(int64_t)b * NBK + e] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) acc += v[u];
     }
     sAcc[g][lane] = acc;
     __syncthreads();
-    if (g == 0) out[e] = sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
+    if (g == 0) {
+        const unsigned long long t = sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
+        if (t) atomicAdd(&out[e], t);
+    }
 }
 
-__global__ void k_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1)
+__global__ void k_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
+                          uint64_t *seg)
 {
+    seg[0] = 0; // compaction counter of this rank's segment
     st->nsel = nsel;
     st->rank[0] = r0;
     st->rank[1] = r1;
@@ -901,32 +910,50 @@ __global__ void k_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int 
     st->error = 0;
 }
 
-// Keys of the regions in the selected bucket(s) -> seg = [count, keys]; one
-// global atomic per block and chunk (positions past CAPG are dropped: the host
-// only takes this path when the selected buckets hold <= CAPG keys in total).
+// Keys of the regions in the selected bucket(s) -> seg = [count, keys].  A
+// block gathers its regions' matches in LDS and reserves output space with
+// one global atomic per flush (a counter that every block hits per region
+// serialises at the L2).  Positions past CAPG are dropped: the host only takes
+// this path when the selected buckets hold <= CAPG keys in total.
+constexpr int CB_LDS = 4096; // keys buffered per block between flushes
 __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ counts,
                                                         int64_t nreg, int64_t cap,
                                                         const SelState *__restrict__ st,
                                                         uint64_t *__restrict__ seg)
 {
-    __shared__ int sCnt[4];
+    __shared__ uint64_t sK[CB_LDS];
+    __shared__ int sN;
     __shared__ unsigned long long sBase;
     const int nsel = st->nsel, b0 = st->bsel[0], b1 = nsel > 1 ? st->bsel[1] : -1;
     const uint64_t lo = st->lo_key;
     const double binv = st->binv;
     unsigned long long *ctr = reinterpret_cast<unsigned long long *>(seg);
     uint64_t *outk = seg + 1;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    constexpr int CU = 8; // loads in flight per thread; <= 256 * CU matches per chunk
+    if (threadIdx.x == 0) sN = 0;
+    __syncthreads();
+    auto flush = [&]() {
+        __syncthreads();
+        const int m = sN;
+        if (threadIdx.x == 0 && m) sBase = atomicAdd(ctr, (unsigned long long)m);
+        __syncthreads();
+        for (int e = threadIdx.x; e < m; e += 256) {
+            const unsigned long long pos = sBase + e;
+            if (pos < (unsigned long long)CAPG) outk[pos] = sK[e];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) sN = 0;
+        __syncthreads();
+    };
     for (int64_t r = blockIdx.x; r < nreg; r += gridDim.x) {
         int64_t cnt = counts ? (int64_t)counts[r] : cap;
         if (cnt > cap) cnt = cap;
         const uint64_t *kr = keys + r * cap;
-        constexpr int CU = 8;
         for (int64_t b = 0; b < cnt; b += 256 * CU) {
+            if (sN > CB_LDS - 256 * CU) flush(); // block-uniform (read after a barrier)
             uint64_t kk[CU];
-            unsigned long long bal[CU];
-            int wtot = 0;
 #pragma unroll
             for (int u = 0; u < CU; ++u) {
                 const int64_t e = b + u * 256 + threadIdx.x;
@@ -936,142 +963,179 @@ __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restr
             for (int u = 0; u < CU; ++u) {
                 const int64_t e = b + u * 256 + threadIdx.x;
                 const int kb = kbucket(kk[u], lo, binv);
-                bal[u] = __ballot(e < cnt && (kb == b0 || kb == b1));
-                wtot += __popcll(bal[u]);
-            }
-            if (lane == 0) sCnt[w] = wtot;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                const int tot = sCnt[0] + sCnt[1] + sCnt[2] + sCnt[3];
-                sBase = tot ? atomicAdd(ctr, (unsigned long long)tot) : 0ull;
-            }
-            __syncthreads();
-            unsigned long long base = sBase;
-            for (int v = 0; v < w; ++v) base += sCnt[v];
-#pragma unroll
-            for (int u = 0; u < CU; ++u) {
-                if ((bal[u] >> lane) & 1ull) {
-                    const unsigned long long pos = base + __popcll(bal[u] & ((1ull << lane) - 1ull));
-                    if (pos < (unsigned long long)CAPG) outk[pos] = kk[u];
+                const bool m = e < cnt && (kb == b0 || kb == b1);
+                const unsigned long long bal = __ballot(m);
+                if (bal) {
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(&sN, __popcll(bal));
+                    base = __shfl(base, 0);
+                    if (m) sK[base + __popcll(bal & ((1ull << lane) - 1ull))] = kk[u];
                 }
-                base += __popcll(bal[u]);
             }
             __syncthreads();
         }
     }
+    flush();
+}
+
+// Inclusive prefix sum of v over a 1024-thread block (wave shuffles + one
+// LDS step over the 16 wave totals).  sW: 16 entries of scratch.
+__device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long v,
+                                                              unsigned long long *sW)
+{
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) sW[wv] = v;
+    __syncthreads();
+    if (wv == 0) {
+        unsigned long long w = lane < 16 ? sW[lane] : 0ull;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const unsigned long long t = __shfl_up(w, o);
+            if (lane >= o) w += t;
+        }
+        if (lane < 16) sW[lane] = w;
+    }
+    __syncthreads();
+    if (wv > 0) v += sW[wv - 1];
+    __syncthreads(); // sW reusable
+    return v;
 }
 
 // Exact selection over the gathered segments (one per rank): for each
-// selection s, the rank[s]-th smallest key of bucket bsel[s].  Radix passes
-// (11-bit digits, LDS histogram, block scan) start below the common prefix of
-// the bucket's min and max key, so a narrow bucket needs 1-3 passes.
+// selection s, the rank[s]-th smallest key of bucket bsel[s].  Both
+// selections advance together: radix passes (11-bit digits, LDS histograms,
+// block scan) start below the common prefix of the selected buckets' keys
+// (bits above it are equal for every key of a bucket), so a narrow bucket
+// needs 2-3 passes.
 __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint64_t *__restrict__ segs,
                                                       int nseg)
 {
-    __shared__ uint32_t sHist[RADIX];
-    __shared__ unsigned long long sPart[1024];
-    __shared__ unsigned long long sMn[16], sMx[16];
-    __shared__ int sDigit;
-    __shared__ unsigned long long sBelowD;
+    __shared__ uint32_t sHist[2][RADIX];
+    __shared__ unsigned long long sW[16];
+    __shared__ unsigned long long sMn[2][16], sMx[2][16];
+    __shared__ int sDigit[2];
+    __shared__ unsigned long long sBelowD[2];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t lo = st->lo_key;
     const double binv = st->binv;
     const int nsel = st->nsel;
-    for (int s = 0; s < nsel; ++s) {
-        const int b = st->bsel[s];
-        unsigned long long rank = st->rank[s];
-        uint64_t mn = ~0ull, mx = 0;
+    const int bs[2] = {st->bsel[0], nsel > 1 ? st->bsel[1] : st->bsel[0]};
+    unsigned long long rank[2] = {st->rank[0], nsel > 1 ? st->rank[1] : st->rank[0]};
+    // min / max key of each selected bucket
+    uint64_t mn[2] = {~0ull, ~0ull}, mx[2] = {0, 0};
+    for (int g = 0; g < nseg; ++g) {
+        const uint64_t *sg = segs + (int64_t)g * (CAPG + 1);
+        const int64_t cnt = min<int64_t>((int64_t)sg[0], CAPG);
+        for (int64_t e = tid; e < cnt; e += 1024) {
+            const uint64_t key = sg[1 + e];
+            const int kb = kbucket(key, lo, binv);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (kb == bs[q]) {
+                    mn[q] = key < mn[q] ? key : mn[q];
+                    mx[q] = key > mx[q] ? key : mx[q];
+                }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t a = __shfl_xor(mn[q], o), c = __shfl_xor(mx[q], o);
+            mn[q] = a < mn[q] ? a : mn[q];
+            mx[q] = c > mx[q] ? c : mx[q];
+        }
+        if (lane == 0) {
+            sMn[q][wv] = mn[q];
+            sMx[q][wv] = mx[q];
+        }
+    }
+    __syncthreads();
+    if (tid < 2) {
+        uint64_t a = sMn[tid][0], c = sMx[tid][0];
+        for (int w = 1; w < 16; ++w) {
+            a = sMn[tid][w] < a ? sMn[tid][w] : a;
+            c = sMx[tid][w] > c ? sMx[tid][w] : c;
+        }
+        sMn[tid][0] = a;
+        sMx[tid][0] = c;
+    }
+    __syncthreads();
+    int known = 0;
+    uint64_t prefix[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t diff = sMn[q][0] ^ sMx[q][0];
+        const int kq = diff ? 64 - __clzll((long long)diff) : 0;
+        known = kq > known ? kq : known;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+        prefix[q] = known >= 64 ? 0ull : (sMn[q][0] & ~((1ull << known) - 1ull));
+    bool err = false;
+    while (known > 0) {
+        const int width = known >= RADIX_BITS ? RADIX_BITS : known;
+        const int shift = known - width;
+        for (int e = tid; e < 2 * RADIX; e += 1024) (&sHist[0][0])[e] = 0;
+        __syncthreads();
         for (int g = 0; g < nseg; ++g) {
             const uint64_t *sg = segs + (int64_t)g * (CAPG + 1);
             const int64_t cnt = min<int64_t>((int64_t)sg[0], CAPG);
             for (int64_t e = tid; e < cnt; e += 1024) {
                 const uint64_t key = sg[1 + e];
-                if (kbucket(key, lo, binv) == b) {
-                    mn = key < mn ? key : mn;
-                    mx = key > mx ? key : mx;
-                }
+                const int kb = kbucket(key, lo, binv);
+                const uint32_t dg = (uint32_t)((key >> shift) & ((1u << width) - 1u));
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (kb == bs[q] && (known >= 64 || (key >> known) == (prefix[q] >> known)))
+                        atomicAdd(&sHist[q][dg], 1u);
             }
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-            const uint64_t a = __shfl_xor(mn, o), c = __shfl_xor(mx, o);
-            mn = a < mn ? a : mn;
-            mx = c > mx ? c : mx;
-        }
-        if (lane == 0) {
-            sMn[wv] = mn;
-            sMx[wv] = mx;
         }
         __syncthreads();
-        if (tid == 0) {
-            uint64_t a = sMn[0], c = sMx[0];
-            for (int q = 1; q < 16; ++q) {
-                a = sMn[q] < a ? sMn[q] : a;
-                c = sMx[q] > c ? sMx[q] : c;
-            }
-            sMn[0] = a;
-            sMx[0] = c;
-        }
-        __syncthreads();
-        mn = sMn[0];
-        mx = sMx[0];
-        const uint64_t diff = mn ^ mx;
-        int known = diff ? 64 - __clzll((long long)diff) : 0;
-        uint64_t prefix = known >= 64 ? 0ull : (mn & ~((1ull << known) - 1ull));
-        while (known > 0) {
-            const int width = known >= RADIX_BITS ? RADIX_BITS : known;
-            const int shift = known - width;
-            for (int e = tid; e < RADIX; e += 1024) sHist[e] = 0;
-            __syncthreads();
-            for (int g = 0; g < nseg; ++g) {
-                const uint64_t *sg = segs + (int64_t)g * (CAPG + 1);
-                const int64_t cnt = min<int64_t>((int64_t)sg[0], CAPG);
-                for (int64_t e = tid; e < cnt; e += 1024) {
-                    const uint64_t key = sg[1 + e];
-                    if (kbucket(key, lo, binv) == b &&
-                        (known >= 64 || (key >> known) == (prefix >> known)))
-                        atomicAdd(&sHist[(key >> shift) & ((1u << width) - 1u)], 1u);
-                }
-            }
-            __syncthreads();
-            constexpr int PER = RADIX / 1024;
+        constexpr int PER = RADIX / 1024;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
             unsigned long long loc = 0;
-            for (int q = 0; q < PER; ++q) loc += sHist[tid * PER + q];
-            sPart[tid] = loc;
-            if (tid == 0) sDigit = -1;
+            for (int u = 0; u < PER; ++u) loc += sHist[q][tid * PER + u];
+            const unsigned long long incl = block_scan_1024(loc, sW);
+            const unsigned long long excl = incl - loc;
+            if (tid == 0) sDigit[q] = -1;
             __syncthreads();
-            for (int o = 1; o < 1024; o <<= 1) {
-                const unsigned long long v = tid >= o ? sPart[tid - o] : 0ull;
-                __syncthreads();
-                sPart[tid] += v;
-                __syncthreads();
-            }
-            const unsigned long long excl = tid ? sPart[tid - 1] : 0ull;
-            if (rank >= excl && rank < sPart[tid]) {
+            if (rank[q] >= excl && rank[q] < incl) {
                 unsigned long long c = excl;
-                for (int q = 0; q < PER; ++q) {
-                    const unsigned long long hv = sHist[tid * PER + q];
-                    if (rank < c + hv) {
-                        sDigit = tid * PER + q;
-                        sBelowD = c;
+                for (int u = 0; u < PER; ++u) {
+                    const unsigned long long hv = sHist[q][tid * PER + u];
+                    if (rank[q] < c + hv) {
+                        sDigit[q] = tid * PER + u;
+                        sBelowD[q] = c;
                         break;
                     }
                     c += hv;
                 }
             }
             __syncthreads();
-            const int dg = sDigit;
-            const unsigned long long bd = sBelowD;
-            __syncthreads();
-            if (dg < 0) { // rank outside the bucket (the host checked; should not happen)
-                if (tid == 0) st->error = 1;
-                break;
-            }
-            prefix |= (uint64_t)dg << shift;
-            rank -= bd;
-            known = shift;
         }
-        if (tid == 0) st->prefix[s] = prefix;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            if (sDigit[q] < 0) {
+                err = true;
+            } else {
+                prefix[q] |= (uint64_t)sDigit[q] << shift;
+                rank[q] -= sBelowD[q];
+            }
+        }
         __syncthreads();
+        if (err) break; // uniform: rank outside the bucket (the host checked; should not happen)
+        known = shift;
+    }
+    if (tid == 0) {
+        if (err) st->error = 1;
+        st->prefix[0] = prefix[0];
+        if (nsel > 1) st->prefix[1] = prefix[1];
     }
 }
 
@@ -1144,6 +1208,7 @@ __global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
                                 unsigned long long *__restrict__ cnt)
 {
     __shared__ unsigned long long s0[256], s1[256], s2[256];
+    for (int e = threadIdx.x; e < NBK; e += 256) cnt[3 + e] = 0; // k_bucket_sum adds into these
     unsigned long long b = 0, c = 0, o = 0;
     for (int64_t e = threadIdx.x; e < nblk; e += 256) {
         b += below[e];
@@ -2752,20 +2817,17 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
 {
     hipLaunchKernelGGL(k_counts_reduce, dim3(1), dim3(256), 0, stream, below, counts, nblk, cap,
                        st, cnt);
-    if (bpart && nbpart > 0) {
-        hipLaunchKernelGGL(k_bucket_sum, dim3(NBK / 64), dim3(256), 0, stream, bpart, (int)nbpart,
-                           cnt + 3);
-    } else {
-        hipError_t e = hipMemsetAsync(cnt + 3, 0, NBK * sizeof(unsigned long long), stream);
-        if (e != hipSuccess) return e;
-    }
+    // (k_counts_reduce cleared the bucket counts cnt[3 .. 3 + NBK))
+    if (bpart && nbpart > 0)
+        hipLaunchKernelGGL(k_bucket_sum, dim3(NBK / 64, BSUM_SLICES), dim3(256), 0, stream, bpart,
+                           (int)nbpart, cnt + 3);
     return hipGetLastError();
 }
 
 hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
-                          hipStream_t stream)
+                          uint64_t *seg, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_set_sel, dim3(1), dim3(1), 0, stream, st, nsel, r0, r1, b0, b1);
+    hipLaunchKernelGGL(k_set_sel, dim3(1), dim3(1), 0, stream, st, nsel, r0, r1, b0, b1, seg);
     return hipGetLastError();
 }
 
@@ -2774,7 +2836,7 @@ hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, 
                                   hipStream_t stream)
 {
     if (nreg <= 0) return hipSuccess;
-    const int64_t G = nreg < 8192 ? nreg : 8192;
+    const int64_t G = nreg < 512 ? nreg : 512;
     hipLaunchKernelGGL(k_compact_buckets, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap,
                        st, seg);
     return hipGetLastError();
