@@ -1847,7 +1847,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
                 // MODE 0 off-diagonal tiles (the bulk): the column record of jj+1
                 // is read from LDS while column jj is classified (the read past
                 // the chunk's last column stays inside smem and is discarded)
-                constexpr bool PIPE = MODE == 0 && !DIAG;
+                constexpr bool PIPE = false; // (MODE == 0 && !DIAG: no gain measured, and its 18 extra VGPRs spill at 3 waves/SIMD)
                 auto column = [&](const double(&cr)[D + 1], const int64_t j) {
                     const double *xj = cr;
                     const double hj = cr[D];
