@@ -854,6 +854,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->bpart, (int64_t)1024 * NBK)); // collect grid <= 1024
     CHK(dalloc(c, &c->gseg, (int64_t)c->world * (CAPG + 1)));
     if (const char *e = std::getenv("SVGD_BUCKET_CAP")) c->bucket_cap = std::atoll(e);
+    if (const char *e = std::getenv("SVGD_MEDIAN_SAMPLE")) c->sample_size = std::max<int64_t>(1, std::atoll(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
     CHK(dalloc(c, &c->gpart, (int64_t)HIST_PART_BLOCKS * 2 * RADIX));

@@ -1668,6 +1668,11 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
 constexpr int PR = 4;     // rows per lane of the median sweep
 constexpr int PBLK = 256; // = 64 * PR: tile block of the row-stream median plan
 constexpr int CH_MED = 32; // columns per LDS chunk of the median stream
+// collect: two columns per step (2 waves/SIMD) instead of one (3 waves/SIMD)
+#ifndef SVGD_COLLECT_PAIR2
+#define SVGD_COLLECT_PAIR2 0
+#endif
+constexpr bool PAIR2 = SVGD_COLLECT_PAIR2;
 
 struct TileIt {
     int64_t t, I, J, slot;
@@ -1675,7 +1680,7 @@ struct TileIt {
 };
 
 template <int D, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 : 1, 8))) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !PAIR2 ? 3 : 1, 8))) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
                                                   const double *__restrict__ nrm, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
@@ -1797,9 +1802,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
         dma_to_lds<CHB>(src(it), wbuf, lane);
         int64_t curI = -1;
         double xi[PR][D], ni[PR], TL[PR], TH[PR];
-        int64_t irow[PR];
-        bool ivalid[PR];
-        unsigned long long vmask[PR];
+        // row index / validity recomputed where needed (the diagonal tiles and
+        // the rare key path) instead of held in 12 VGPRs across the loop
+        auto irow = [&](int r) -> int64_t { return curI * PBLK + 64 * r + lane; };
+        auto ivalid = [&](int r) -> bool { return irow(r) < n; };
         for (int q = 0; it.t < te; ++q) {
             TileIt nx = it;
             advance(nx);
@@ -1818,10 +1824,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
             if (I != curI) {
 #pragma unroll
                 for (int r = 0; r < PR; ++r) {
-                    irow[r] = I * PBLK + 64 * r + lane;
-                    ivalid[r] = irow[r] < n;
-                    vmask[r] = __ballot(ivalid[r]);
-                    const int64_t ic = ivalid[r] ? irow[r] : n - 1;
+                    const int64_t ir = I * PBLK + 64 * r + lane;
+                    const bool iv = ir < n;
+                    const int64_t ic = iv ? ir : n - 1;
 #pragma unroll
                     for (int k = 0; k < D; ++k) xi[r][k] = xc[ic * KP + k];
                     ni[r] = -2.0 * xc[ic * KP + D];
@@ -1829,7 +1834,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
                         const double m = 0x1p-48 * (ni[r] + nmax);
                         TL[r] = lo_key == 0 ? __builtin_inf() : 0.5 * (ni[r] - lo_d + m);
                         TH[r] = 0.5 * (ni[r] - hi_d - m); // -inf when hi is +inf
-                        if (!ivalid[r]) TL[r] = TH[r] = __builtin_inf(); // never counted
+                        if (!iv) TL[r] = TH[r] = __builtin_inf(); // never counted
                     }
                 }
                 // row registers complete here (rare: once per row block), not
@@ -1842,12 +1847,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
             const int cnt = (int)min<int64_t>(CH_MED, n - jb);
             const double *cb = reinterpret_cast<const double *>(wbuf + (q & 1) * CHB);
             // off-diagonal tiles (all but 1 in H+1): every valid row counts
+            // the bracket band of one column: form the keys of the rows in mcs
+            auto band = [&](const double(&ev)[PR], const unsigned long long(&mcs)[PR]) {
+#pragma unroll
+                for (int r = 0; r < PR; ++r) {
+                    const unsigned long long mc = mcs[r];
+                    if (!mc) continue;
+                    const double sx = fmax(fma(-2.0, ev[r], ni[r]), 0.0);
+                    const unsigned long long mb = __ballot(sx < lo_d) & mc;
+                    below += __popcll(mb);
+                    const unsigned long long mask = __ballot(sx < hi_d) & mc & ~mb;
+                    if (mask) {
+                        if (scnt + 64 > STG) flush(); // rare: > STG-64 keys in a chunk
+                        if ((mask >> lane) & 1ull)
+                            lds_store_u64(&sStage[w][scnt + __popcll(mask & ((1ull << lane) - 1ull))],
+                                          key_of(sx));
+                        scnt += __popcll(mask);
+                    }
+                }
+            };
             auto columns = [&](auto diag_tag) {
                 constexpr bool DIAG = decltype(diag_tag)::value;
                 // MODE 0 off-diagonal tiles (the bulk): the column record of jj+1
                 // is read from LDS while column jj is classified (the read past
                 // the chunk's last column stays inside smem and is discarded)
-                constexpr bool PIPE = false; // (MODE == 0 && !DIAG: no gain measured, and its 18 extra VGPRs spill at 3 waves/SIMD)
+                constexpr bool PIPE = false; // (MODE == 0 && !DIAG: measured no faster)
                 auto column = [&](const double(&cr)[D + 1], const int64_t j) {
                     const double *xj = cr;
                     const double hj = cr[D];
@@ -1871,7 +1895,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
                             const unsigned long long ml = __ballot(ev[r] > TL[r]);
                             const unsigned long long mh = __ballot(ev[r] > TH[r]);
                             if constexpr (DIAG) {
-                                const unsigned long long vm = __ballot(ivalid[r] && irow[r] < j);
+                                const unsigned long long vm = __ballot(ivalid(r) && irow(r) < j);
                                 below += __popcll(ml & vm);
                                 mcs[r] = mh & ~ml & vm;
                             } else {
@@ -1880,31 +1904,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
                                 mcs[r] = mh & ~ml;
                             }
                         }
-                        if ((mcs[0] | mcs[1] | mcs[2] | mcs[3]) != 0) {
+                        unsigned long long anyc = 0;
 #pragma unroll
-                            for (int r = 0; r < PR; ++r) {
-                                const unsigned long long mc = mcs[r];
-                                if (!mc) continue;
-                                // the bracket band: form the key
-                                const double sx = fmax(fma(-2.0, ev[r], ni[r]), 0.0);
-                                const unsigned long long mb = __ballot(sx < lo_d) & mc;
-                                below += __popcll(mb);
-                                const unsigned long long mask = __ballot(sx < hi_d) & mc & ~mb;
-                                if (mask) {
-                                    if (scnt + 64 > STG) flush(); // rare: > STG-64 keys in a chunk
-                                    if ((mask >> lane) & 1ull)
-                                        lds_store_u64(&sStage[w][scnt + __popcll(mask & ((1ull << lane) -
-                                                                                         1ull))],
-                                                      key_of(sx));
-                                    scnt += __popcll(mask);
-                                }
-                            }
-                        }
+                        for (int r = 0; r < PR; ++r) anyc |= mcs[r];
+                        if (anyc) band(ev, mcs);
                     }
 #pragma unroll
                     for (int r = 0; r < PR; ++r) {
                         const double e = ev[r];
-                        const bool valid = ivalid[r] && (!DIAG || irow[r] < j);
+                        const bool valid = ivalid(r) && (!DIAG || irow(r) < j);
                         if constexpr (MODE == 0) {
                             (void)e;
                             (void)valid;
@@ -1921,7 +1929,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
                                 }
                             } else {
                                 if (valid) {
-                                    const int64_t i = irow[r];
+                                    const int64_t i = irow(r);
                                     const int64_t a = i < j ? i : j, b = i < j ? j : i;
                                     sd.out[a * (2 * sd.n - a - 1) / 2 + (b - a - 1)] = sk;
                                 }
@@ -1947,6 +1955,50 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 3 
                         __builtin_amdgcn_sched_barrier(0);
                         column(qb, jb + jj + 1);
                         __builtin_amdgcn_sched_barrier(0);
+                    }
+                } else if constexpr (MODE == 0 && !DIAG && PAIR2) {
+                    // two columns per step: twice the independent FMA chains
+                    // and one wave-uniform band test per two columns
+                    int jj = 0;
+                    for (; jj + 1 < cnt; jj += 2) {
+                        double c0[D + 1], c1[D + 1];
+                        load(c0, jj);
+                        load(c1, jj + 1);
+                        double e0[PR], e1[PR];
+#pragma unroll
+                        for (int r = 0; r < PR; ++r) {
+                            e0[r] = c0[D];
+                            e1[r] = c1[D];
+                        }
+#pragma unroll
+                        for (int k = 0; k < D; ++k)
+#pragma unroll
+                            for (int r = 0; r < PR; ++r) {
+                                e0[r] = fma(xi[r][k], c0[k], e0[r]);
+                                e1[r] = fma(xi[r][k], c1[k], e1[r]);
+                            }
+                        unsigned long long m0[PR], m1[PR];
+                        unsigned long long any = 0;
+#pragma unroll
+                        for (int r = 0; r < PR; ++r) {
+                            const unsigned long long l0 = __ballot(e0[r] > TL[r]);
+                            const unsigned long long h0 = __ballot(e0[r] > TH[r]);
+                            const unsigned long long l1 = __ballot(e1[r] > TL[r]);
+                            const unsigned long long h1 = __ballot(e1[r] > TH[r]);
+                            wbelow += (uint32_t)(__popcll(l0) + __popcll(l1));
+                            m0[r] = h0 & ~l0;
+                            m1[r] = h1 & ~l1;
+                            any |= m0[r] | m1[r];
+                        }
+                        if (any) {
+                            band(e0, m0);
+                            band(e1, m1);
+                        }
+                    }
+                    if (jj < cnt) {
+                        double cr[D + 1];
+                        load(cr, jj);
+                        column(cr, jb + jj);
                     }
                 } else {
                     for (int jj = 0; jj < cnt; ++jj) {
