@@ -9,7 +9,7 @@ SRC_DIR := svgdcpp_amd/csrc
 LIB := svgdcpp_amd/libsvgdcpp_amd.so
 OBJS := $(SRC_DIR)/svgd_kernels.o $(SRC_DIR)/svgd_capi.o $(SRC_DIR)/plan.o $(SRC_DIR)/host_models.o \
         $(SRC_DIR)/hostcomm.o
-HDRS := $(SRC_DIR)/svgd_kernels.h include/svgdcpp_amd/svgd_capi.h
+HDRS := $(SRC_DIR)/svgd_kernels.h $(SRC_DIR)/svgd_exp_table.h include/svgdcpp_amd/svgd_capi.h
 
 all: $(LIB)
 

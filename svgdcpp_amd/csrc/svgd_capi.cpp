@@ -1185,9 +1185,11 @@ int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
 int svgd_finish_step(svgd_ctx *c, const double *G_shard)
 {
     CHK(check_ready(c));
-    CHK(upload_g_begin(c, G_shard)); // overlaps the median's selection passes
-    CHK(scale_finish(c));
+    CHK(upload_g_begin(c, G_shard));
+    // the G all-gather is queued before the host waits for the median counts
+    // (scale_finish), so the device runs it during that round trip
     CHK(upload_g_finish(c));
+    CHK(scale_finish(c));
     CHK(run_phi(c));
     CHK(run_opt(c));
     return SVGD_OK;

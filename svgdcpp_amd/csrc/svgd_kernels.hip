@@ -22,6 +22,7 @@
 #include <stdint.h>
 
 #include "svgd_kernels.h"
+#include "svgd_exp_table.h"
 
 namespace svgd_amd {
 
@@ -1276,13 +1277,13 @@ __global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi,
 // whatever its type), so for small d the phi pass minimises instructions
 // per pair instead of using MFMA:
 //
-//   lane = R particle rows i (pre-scaled by 512 a log2e), column particle j
+//   lane = R particle rows i (pre-scaled by 8192 a log2e), column particle j
 //   wave-uniform: its record arrives in LDS by DMA (per-wave double-buffered
 //   chunks) and is read with broadcast ds_read_b128.
-//   per (i, j):  u    add + d FMA    (u = 256 log2 K_ij, Gram form on centred x)
-//                2^(u/256)           256-entry LDS table x degree-4 poly, ldexp
+//   per (i, j):  u    add + d FMA    (u = 4096 log2 K_ij, Gram form on centred x)
+//                2^(u/4096)          4096-entry LDS table x degree-2 form, ldexp
 //                acc  d FMA + 1      (sum_j K_ij V_j, sum_j K_ij)
-//   3d + 11 f64 ops per ordered pair (d = 8: 35 incl. the integer ops).
+//   3d + 9 f64 ops per ordered pair (d = 8: 33 incl. the integer ops).
 // Columns are split over S workgroups (partials reduced by k_phi_reduce in a
 // fixed order, so results are deterministic).
 
@@ -1372,9 +1373,20 @@ __device__ __forceinline__ double exp2_256(double u, const double *tab)
     return __builtin_ldexp(exp2_256_poly(f) * tab[ki & 255], ki >> 8);
 }
 
-constexpr int CH_PHI = 16; // columns per LDS chunk of the phi row stream
+// Row-stream form: 2^(u/4096) for u <= ~0, u = k + f, |f| <= 1/2:
+// 2^(k>>12) 2^((k&4095)/4096) 2^(f/4096), the last by the levelled degree-2
+// form 1 + c1 f + c2 f^2 (tools/make_exp_table.py coeffs4096: relative error
+// <= 2.6e-14, i.e. phi_hat within 2.6e-14 max|V| of the exact-exp sum, far
+// inside the 1e-10 bound).  Two FMA fewer per pair than exp2_256 (32 KiB table).
+__device__ __forceinline__ double exp2_4096_poly(double f)
+{
+    return fma(fma(0x1.ebfbdff82c58fp-27, f, 0x1.62e42ff4f7b0ap-13), f, 1.0);
+}
 
-// rec_j = [xc_j (D) | V_j = G_j - 2a xc_j (D) | c_j = -256 a log2e |xc_j|^2 | 0 ...],
+constexpr int CH_PHI = 16; // columns per LDS chunk of the phi row stream
+constexpr int EXP_TB = 4096; // row-stream exp table entries
+
+// rec_j = [xc_j (D) | V_j = G_j - 2a xc_j (D) | c_j = -4096 a log2e |xc_j|^2 | 0 ...],
 // stride phi_rec_stride(D) = roundup(2D+1, 8) doubles, so CH_PHI records are
 // a whole number of 1 KiB LDS-DMA pieces.
 template <int D> struct RecLayout {
@@ -1446,7 +1458,7 @@ __device__ __forceinline__ void lds_load8_u64_sync(const uint64_t *p, uint64_t (
 }
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// rec_j = [xc_j | G_j - 2a xc_j | -256 a log2e |xc_j|^2 | 0..], one thread per
+// rec_j = [xc_j | G_j - 2a xc_j | -4096 a log2e |xc_j|^2 | 0..], one thread per
 // element (coalesced stores of the np x RS array).
 __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restrict__ G,
                            const double *__restrict__ nrm, const double *__restrict__ a_ptr,
@@ -1465,7 +1477,7 @@ __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restri
             else if (k < 2 * d)
                 v = G[j * d + (k - d)] - 2.0 * a * xc[j * KP + (k - d)];
             else if (k == 2 * d)
-                v = -256.0 * a * LOG2E * nrm[j];
+                v = -4096.0 * a * LOG2E * nrm[j];
         }
         rec[e] = v;
     }
@@ -1508,14 +1520,14 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
         const double k = __builtin_rint(u[r]);
         f[r] = u[r] - k;
         ki[r] = (int)k;
-        T[r] = tab[ki[r] & 255];
+        T[r] = tab[ki[r] & (EXP_TB - 1)];
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < R; ++r) K[r] = exp2_256_poly(f[r]);
+    for (int r = 0; r < R; ++r) K[r] = exp2_4096_poly(f[r]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < R; ++r) K[r] = __builtin_ldexp(K[r] * T[r], ki[r] >> 8);
+    for (int r = 0; r < R; ++r) K[r] = __builtin_ldexp(K[r] * T[r], ki[r] >> 12);
 #pragma unroll
     for (int k = 0; k < D; ++k)
 #pragma unroll
@@ -1535,10 +1547,11 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     // register double buffer of the column record only where it fits without
     // spilling (row state R(2D+2) + two records 2(2D+1) doubles)
     constexpr bool PIPE = (R * (2 * D + 2) + 2 * (2 * D + 1)) * 2 <= 232;
-    // per-wave double-buffered column chunks, then the 2^(i/256) table
-    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + 256 * 8];
+    // per-wave double-buffered column chunks, then the 2^(i/4096) table
+    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + EXP_TB * 8];
     double *tab = reinterpret_cast<double *>(smem + 4 * 2 * CHB);
-    tab[threadIdx.x] = EXP2_TAB256[threadIdx.x];
+#pragma unroll
+    for (int e = 0; e < EXP_TB / 256; ++e) tab[e * 256 + threadIdx.x] = EXP2_TAB4096[e * 256 + threadIdx.x];
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -1547,9 +1560,9 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     const int64_t iblk = blockIdx.x / S;
     const int s = (int)(blockIdx.x - iblk * S);
     const int64_t rbase = iblk * (256 * R) + w * (64 * R); // local row of this wave's lane 0
-    // u_ij = c_i + c_j + 512 a log2e xc_i.xc_j = -256 a log2e |xc_i - xc_j|^2;
-    // the row coordinates are pre-scaled by 512 a log2e
-    const double alpha = 512.0 * LOG2E * (*a_ptr);
+    // u_ij = c_i + c_j + 8192 a log2e xc_i.xc_j = -4096 a log2e |xc_i - xc_j|^2;
+    // the row coordinates are pre-scaled by 8192 a log2e
+    const double alpha = 8192.0 * LOG2E * (*a_ptr);
 
     double xs[R][D], ci[R], acc[R][D], acc1[R];
 #pragma unroll
@@ -2408,7 +2421,7 @@ __global__ void k_scale_chol(const double *__restrict__ src, double factor, int 
 }
 
 // Row-stream records for the matrix scale: rec_j = [z_j | G_j - 2 M xc_j |
-// -256 log2e |z_j|^2 | 0..], wv_j = 2 M xc_j.
+// -4096 log2e |z_j|^2 | 0..], wv_j = 2 M xc_j.
 __global__ void k_prep_rec_mat(const double *__restrict__ xc, const double *__restrict__ G,
                                const double *__restrict__ M, const double *__restrict__ L,
                                int64_t n, int64_t np, int d, int KP, int RS,
@@ -2432,7 +2445,7 @@ __global__ void k_prep_rec_mat(const double *__restrict__ xc, const double *__re
             wv[j * d + k] = 2.0 * mx;
             zz = fma(z, z, zz);
         }
-        r[2 * d] = live ? -256.0 * LOG2E * zz : 0.0;
+        r[2 * d] = live ? -4096.0 * LOG2E * zz : 0.0;
         for (int k = 2 * d + 1; k < RS; ++k) r[k] = 0.0;
     }
 }

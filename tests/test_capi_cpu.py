@@ -143,6 +143,34 @@ def test_exp2_table_and_coefficients_match_generator():
     assert lits == [c[4], c[3], c[2], c[1]]
 
 
+def test_exp2_4096_table_and_coefficients_match_generator():
+    """The row-stream phi kernel's 2^(i/4096) table (svgd_exp_table.h) and its
+    levelled degree-2 coefficients are what tools/make_exp_table.py derives, and
+    the form's relative error stays <= 2.6e-14 on |f| <= 1/2 (checked at 60
+    digits)."""
+    import importlib.util
+    import os
+    from decimal import Decimal, getcontext
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("mk", os.path.join(root, "tools", "make_exp_table.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    hdr = open(os.path.join(root, "svgdcpp_amd", "csrc", "svgd_exp_table.h")).read()
+    assert hdr == mk.header_text()
+    src = open(os.path.join(root, "svgdcpp_amd", "csrc", "svgd_kernels.hip")).read()
+    fn = src[src.index("double exp2_4096_poly("):]
+    fn = fn[:fn.index("}")]
+    lits = [float.fromhex(t) for t in re.findall(r"0x1\.[0-9a-f]+p[-+]\d+", fn)]
+    c1, c2 = mk.coeffs4096()
+    assert lits == [c2, c1]
+    getcontext().prec = 60
+    k = Decimal(2).ln() / 4096
+    worst = max(abs((1 + Decimal(c1) * f + Decimal(c2) * f * f) / (k * f).exp() - 1)
+                for f in (Decimal(i) / 1000 for i in range(-500, 501)))
+    assert worst <= Decimal("2.6e-14")
+
+
 def test_host_model_hessian_sum_matches_oracle(oracle):
     import svgdcpp_amd as S
 
