@@ -75,6 +75,7 @@ extern "C" {
 #define SVGD_MEDIAN_DIRECT 0   /* all pair keys stored and selected exactly */
 #define SVGD_MEDIAN_BRACKET 1  /* sampled bracket + candidate selection (exact) */
 #define SVGD_MEDIAN_FALLBACK 2 /* bracket missed: streamed radix select (exact) */
+#define SVGD_MEDIAN_REBRACKET 3 /* bracket missed: wider bracket, collect again (exact) */
 
 typedef struct svgd_ctx svgd_ctx;
 

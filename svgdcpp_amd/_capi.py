@@ -33,6 +33,7 @@ SVGD_SCALE_HESSIAN = 1
 SVGD_MEDIAN_DIRECT = 0
 SVGD_MEDIAN_BRACKET = 1
 SVGD_MEDIAN_FALLBACK = 2
+SVGD_MEDIAN_REBRACKET = 3
 
 _D = ctypes.POINTER(ctypes.c_double)
 _I64 = ctypes.c_int64

@@ -86,6 +86,9 @@ struct svgd_ctx {
     // median
     int64_t direct_max_pairs = int64_t(1) << 24;
     int64_t sample_size = int64_t(1) << 22;
+    double bracket_sigma = 3.0; // sample-quantile standard deviations either side
+    int64_t samp_S = 0;         // this step's sample: size and target quantiles
+    double samp_qlo = 0.0, samp_qhi = 0.0;
     int64_t cand_capacity = 0; // 0 = automatic
     uint64_t *sample_keys = nullptr;
     int64_t sample_alloc = 0;
@@ -353,6 +356,10 @@ hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t
                              c->ghist, bp, dbg, c->stream);
 }
 
+constexpr double WIDE_SIGMA = 8.0; // re-bracket after a miss
+int sample_bracket(svgd_ctx *c, double sigma);
+int collect_counts(svgd_ctx *c);
+
 // Phase 1 of the median: candidate bracket + collect pass + counts.
 // Leaves the reduced counts in c->h_cnt (ready at c->ev_cnt).
 int median_begin(svgd_ctx *c)
@@ -411,28 +418,14 @@ int median_begin(svgd_ctx *c)
         else
             HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, S,
                                          c->sample_keys, c->stream));
-        // sample ranks bracketing the target quantiles (6 sigma)
-        const double qlo = (double)c->sel_rank[0] / (double)M;
-        const double qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;
-        const double sig_lo = std::sqrt((double)S * qlo * (1 - qlo)) + 1.0;
-        const double sig_hi = std::sqrt((double)S * qhi * (1 - qhi)) + 1.0;
-        double slo = std::floor(qlo * S - 6.0 * sig_lo) - 1;
-        double shi = std::ceil(qhi * S + 6.0 * sig_hi) + 1;
-        if (slo < 0) slo = 0;
-        if (shi > S - 1) shi = (double)(S - 1);
-        uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
-        CHK(upload_state(c, 2, sr, 0, ~0ull));
-        for (int p = 0; p < 2; ++p) {
-            HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, S, 0, c->st, c->gpart,
-                                          c->ghist, c->stream));
-            HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
-        }
-        // bracket [lo_key, hi_key) stays on the device (read by the collect pass)
-        HIPCHK(c, launch_bracket(c->st, c->stream));
+        c->samp_S = S;
+        c->samp_qlo = (double)c->sel_rank[0] / (double)M;
+        c->samp_qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;
+        CHK(sample_bracket(c, c->bracket_sigma));
         int64_t pairs_own = tiles * c->pblock * c->pblock;
         int64_t total = c->cand_capacity;
         if (total <= 0) {
-            const double frac = (qhi - qlo) + 16.0 / std::sqrt((double)S) + 0.004;
+            const double frac = (c->samp_qhi - c->samp_qlo) + 16.0 / std::sqrt((double)S) + 0.004;
             total = (int64_t)(2.0 * frac * (double)pairs_own) + 2048 * c->nregions;
         }
         c->reg_cap = std::max<int64_t>(1, total / c->nregions);
@@ -443,6 +436,37 @@ int median_begin(svgd_ctx *c)
         CHK(dalloc(c, &c->cbuf, need));
         c->regions_alloc = need;
     }
+    return collect_counts(c);
+}
+
+// Sample ranks bracketing the target quantiles (sigma sample-quantile standard
+// deviations either side) -> bracket [lo_key, hi_key), which stays on the
+// device (read by the collect pass).
+int sample_bracket(svgd_ctx *c, double sigma)
+{
+    const int64_t S = c->samp_S;
+    const double qlo = c->samp_qlo, qhi = c->samp_qhi;
+    const double sig_lo = std::sqrt((double)S * qlo * (1 - qlo)) + 1.0;
+    const double sig_hi = std::sqrt((double)S * qhi * (1 - qhi)) + 1.0;
+    double slo = std::floor(qlo * S - sigma * sig_lo) - 1;
+    double shi = std::ceil(qhi * S + sigma * sig_hi) + 1;
+    if (slo < 0) slo = 0;
+    if (shi > S - 1) shi = (double)(S - 1);
+    uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
+    CHK(upload_state(c, 2, sr, 0, ~0ull));
+    for (int p = 0; p < 2; ++p) {
+        HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, S, 0, c->st, c->gpart, c->ghist,
+                                      c->stream));
+        HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+    }
+    HIPCHK(c, launch_bracket(c->st, c->stream));
+    return SVGD_OK;
+}
+
+// Collect pass over this rank's pair tiles, then the all-reduced counts to the
+// host (ready at ev_cnt).
+int collect_counts(svgd_ctx *c)
+{
     HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
                                    c->collect_grid, c->cnt3, c->stream));
@@ -468,11 +492,24 @@ int median_finish(svgd_ctx *c)
         return SVGD_OK;
     }
     HIPCHK(c, hipEventSynchronize(c->ev_cnt));
+    const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
+    auto in_bracket = [&]() {
+        return !c->h_cnt[2] && r0 >= c->h_cnt[0] && r1 < c->h_cnt[0] + c->h_cnt[1];
+    };
+    int path = c->med_path;
+    if (!in_bracket() && path == SVGD_MEDIAN_BRACKET && !c->h_cnt[2]) {
+        // the order statistics fell outside the sampled bracket (probability
+        // ~2e-3 per step at the default 3 sigma): bracket again from the same
+        // sample at WIDE_SIGMA and repeat the collect pass (one more pass)
+        // instead of the streamed radix select (one pass per 11-bit digit)
+        CHK(sample_bracket(c, std::max(c->bracket_sigma, WIDE_SIGMA)));
+        CHK(collect_counts(c));
+        HIPCHK(c, hipEventSynchronize(c->ev_cnt));
+        path = SVGD_MEDIAN_REBRACKET;
+    }
     const unsigned long long below = c->h_cnt[0], cand = c->h_cnt[1], ovf = c->h_cnt[2];
     const uint64_t lo_key = c->h_cnt[CNT_LO], hi_key = c->h_cnt[CNT_HI];
-    const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
-    bool ok = !ovf && r0 >= below && r1 < below + cand;
-    int path = c->med_path;
+    bool ok = in_bracket();
     uint64_t ranks[2];
     if (ok) {
         ranks[0] = c->sel_rank[0] - below;
@@ -511,7 +548,7 @@ int median_finish(svgd_ctx *c)
     // every candidate key lies in [lo_key, hi_key): their common leading bits
     // are known, so the radix passes start below them (bracket path only)
     int known_from = 63;
-    if (path == SVGD_MEDIAN_BRACKET && hi_key > lo_key) {
+    if ((path == SVGD_MEDIAN_BRACKET || path == SVGD_MEDIAN_REBRACKET) && hi_key > lo_key) {
         const uint64_t diff = lo_key ^ (hi_key - 1);
         known_from = diff ? 64 - __builtin_clzll(diff) : 0;
         if (known_from > 63) known_from = 63;
@@ -855,6 +892,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->gseg, (int64_t)c->world * (CAPG + 1)));
     if (const char *e = std::getenv("SVGD_BUCKET_CAP")) c->bucket_cap = std::atoll(e);
     if (const char *e = std::getenv("SVGD_MEDIAN_SAMPLE")) c->sample_size = std::max<int64_t>(1, std::atoll(e));
+    if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
     CHK(dalloc(c, &c->gpart, (int64_t)HIST_PART_BLOCKS * 2 * RADIX));

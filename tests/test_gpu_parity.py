@@ -111,7 +111,7 @@ def test_median_bracket_path_exact(oracle, n, d):
     ref_c = _ctx(X)
     a0, m0 = ref_c.median_scale()  # direct path
     c, a, med = _median_with_tuning(X, 0, 1 << 14, -1)
-    assert c.last_scale()[2] == C.SVGD_MEDIAN_BRACKET
+    assert c.last_scale()[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
     assert med == m0 and a == a0
 
 
@@ -125,7 +125,7 @@ def test_median_bucket_select_matches_digit_passes(oracle, monkeypatch, n, d, sa
     for cap in ("16384", "0"):  # default path, then the digit passes only
         monkeypatch.setenv("SVGD_BUCKET_CAP", cap)
         c, a, med = _median_with_tuning(X, 0, sample, -1)
-        assert c.last_scale()[2] == C.SVGD_MEDIAN_BRACKET
+        assert c.last_scale()[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
         res.append((a, med))
     assert res[0] == res[1]
     ref_a, ref_med = oracle.median_scale(X)
@@ -143,6 +143,24 @@ def test_median_bucket_select_ties(oracle, monkeypatch):
         out.append(med)
     assert out[0] == out[1]
     assert out[0] == pytest.approx(oracle.median_scale(X)[1], rel=1e-12)
+
+
+@pytest.mark.parametrize("d", [5, 40])
+def test_median_rebracket_path_exact(oracle, monkeypatch, d):
+    """A bracket of ~0 sample-quantile sigmas (SVGD_MEDIAN_SIGMA=0) misses the
+    order statistics most of the time: the library brackets again from the same
+    sample at 8 sigma and repeats the collect pass.  Every outcome stays exact;
+    at least one of the seeds must take the re-bracket path."""
+    monkeypatch.setenv("SVGD_MEDIAN_SIGMA", "0")
+    paths = []
+    for seed in range(6):
+        n = 1200 + 37 * seed
+        X = oracle.splitmix((n, d), 1.0, 100 + seed)
+        a0, m0 = _ctx(X).median_scale()  # direct path
+        c, a, med = _median_with_tuning(X, 0, 1 << 14, -1)
+        paths.append(c.last_scale()[2])
+        assert med == m0 and a == a0, (seed, paths[-1])
+    assert C.SVGD_MEDIAN_REBRACKET in paths, paths
 
 
 def test_median_fallback_path_exact(oracle):
