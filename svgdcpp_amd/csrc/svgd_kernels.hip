@@ -1457,6 +1457,12 @@ __device__ __forceinline__ void lds_load8_u64_sync(const uint64_t *p, uint64_t (
                  : "memory");
 }
 __device__ __forceinline__ void lgkm_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ uint64_t lds_load_u64_sync(const uint64_t *p)
+{
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
 
 // rec_j = [xc_j | G_j - 2a xc_j | -4096 a log2e |xc_j|^2 | 0..], one thread per
 // element (coalesced stores of the np x RS array).
@@ -1732,25 +1738,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !
     int64_t wcnt = 0; // keys written to the region
     int scnt = 0;     // keys staged in sStage[w]
     uint64_t *wregion = MODE == 0 ? sc.region + wreg * sc.cap : nullptr;
+    int nsel = 0, shift = 0, hsh = 63;
+    uint64_t pfx0 = 0, pfx1 = 0, lo_key = 0, hi_key = 0;
+    unsigned long long below = 0; // wave-uniform (scalar) count
+    // staged keys: those below lo are counted, those in [lo, hi) appended to
+    // the region (and bucketed), the rest dropped; only the occupied 64-key
+    // groups are read
     auto flush = [&]() {
         if (scnt == 0) return;
-        uint64_t v[8];
-        static_assert(MODE != 0 || STG == 512, "flush reads 8 x 64 staged keys");
-        lds_load8_u64_sync(&sStage[w][lane], v);
-#pragma unroll
-        for (int t = 0; t < STG / 64; ++t) {
-            const int64_t pos = wcnt + t * 64 + lane;
-            if (t * 64 + lane < scnt) {
-                if (pos < sc.cap) wregion[pos] = v[t];
-                if (sc.bpart) lds_add_u32(&sBk[kbucket(v[t], blo, binv)], 1u);
+        const int ng = (scnt + 63) >> 6;
+        for (int t = 0; t < ng; ++t) {
+            const uint64_t key = lds_load_u64_sync(&sStage[w][t * 64 + lane]);
+            const bool valid = t * 64 + lane < scnt;
+            below += __popcll(__ballot(valid && key < lo_key));
+            const bool keep = valid && key >= lo_key && key < hi_key;
+            const unsigned long long mk = __ballot(keep);
+            if (keep) {
+                const int64_t pos = wcnt + __popcll(mk & ((1ull << lane) - 1ull));
+                if (pos < sc.cap) wregion[pos] = key;
+                if (sc.bpart) lds_add_u32(&sBk[kbucket(key, blo, binv)], 1u);
             }
+            wcnt += __popcll(mk);
         }
-        wcnt += scnt;
         scnt = 0;
     };
 
-    int nsel = 0, shift = 0, hsh = 63;
-    uint64_t pfx0 = 0, pfx1 = 0, lo_key = 0, hi_key = 0;
     double nmax = 0.0;
     if (MODE == 0) {
         lo_key = sc.st->lo_key;
@@ -1784,7 +1796,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !
     const int64_t W = (int64_t)gridDim.x * 4, gw = (int64_t)blockIdx.x * 4 + w;
     const int64_t T = t1 - t0;
     const int64_t tb = t0 + T * gw / W, te = t0 + T * (gw + 1) / W;
-    unsigned long long below = 0; // wave-uniform (scalar) count
     uint32_t wbelow = 0;          // 32-bit scalar count, flushed per chunk (MODE 0)
 
     if (tb < te) {
@@ -1864,19 +1875,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !
             auto band = [&](const double(&ev)[PR], const unsigned long long(&mcs)[PR]) {
 #pragma unroll
                 for (int r = 0; r < PR; ++r) {
+                    // every key of the threshold band is staged as is; flush()
+                    // classifies it exactly (below lo / in [lo, hi) / above)
+                    // once per 64 staged keys instead of once per band row
                     const unsigned long long mc = mcs[r];
                     if (!mc) continue;
-                    const double sx = fmax(fma(-2.0, ev[r], ni[r]), 0.0);
-                    const unsigned long long mb = __ballot(sx < lo_d) & mc;
-                    below += __popcll(mb);
-                    const unsigned long long mask = __ballot(sx < hi_d) & mc & ~mb;
-                    if (mask) {
-                        if (scnt + 64 > STG) flush(); // rare: > STG-64 keys in a chunk
-                        if ((mask >> lane) & 1ull)
-                            lds_store_u64(&sStage[w][scnt + __popcll(mask & ((1ull << lane) - 1ull))],
-                                          key_of(sx));
-                        scnt += __popcll(mask);
-                    }
+                    if (scnt + 64 > STG) flush(); // rare: > STG-64 keys in a chunk
+                    if ((mc >> lane) & 1ull)
+                        lds_store_u64(&sStage[w][scnt + __popcll(mc & ((1ull << lane) - 1ull))],
+                                      key_of(fmax(fma(-2.0, ev[r], ni[r]), 0.0)));
+                    scnt += __popcll(mc);
                 }
             };
             auto columns = [&](auto diag_tag) {
