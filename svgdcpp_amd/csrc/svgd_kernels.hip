@@ -1699,7 +1699,7 @@ struct TileIt {
 };
 
 template <int D, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !PAIR2 ? 3 : 1, 8))) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !PAIR2 ? 4 : 1, 8))) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
                                                   const double *__restrict__ nrm, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
@@ -1710,7 +1710,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !
     //   s_ij = max(fl(-2 h_i - 2 e_ij), 0) = |xc_i - xc_j|^2 up to rounding.
     constexpr int KP = med_rec_stride(D);
     constexpr int CHB = CH_MED * KP * 8; // bytes per column chunk (multiple of 1 KiB)
-    constexpr int STG = MODE == 0 ? 512 : 1; // staged keys per wave (MODE 0)
+    constexpr int STG = MODE == 0 ? 256 : 1; // staged keys per wave (MODE 0)
     // per-wave double-buffered column chunks, then (MODE 0) per-wave key
     // staging.  The staging lives inside smem on purpose: a separate
     // __shared__ array makes the compiler drain the in-flight column DMA
