@@ -87,6 +87,9 @@ struct svgd_ctx {
     int64_t direct_max_pairs = int64_t(1) << 24;
     int64_t sample_size = int64_t(1) << 22;
     double bracket_sigma = 3.0; // sample-quantile standard deviations either side
+    bool shard_sample = true;   // P > 1: ranks draw disjoint parts of the sample
+    bool samp_shard = false;    // this step's sample is sharded
+    int64_t samp_local = 0;     // sample keys held by this rank
     int64_t samp_S = 0;         // this step's sample: size and target quantiles
     double samp_qlo = 0.0, samp_qhi = 0.0;
     int64_t cand_capacity = 0; // 0 = automatic
@@ -415,8 +418,14 @@ int median_begin(svgd_ctx *c)
         if (tile_sample)
             HIPCHK(c, launch_sample_tiles(c->KP, c->xc, c->nrm, c->xcf, c->nrmf, n, S / (TB * TB),
                                           c->sample_keys, c->stream));
-        else
-            HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, S,
+        // sharded (P > 1, scattered pairs): rank r draws pairs [S r/P, S (r+1)/P)
+        // of the one counter-based sequence and the bracket's histograms are
+        // all-reduced -- the same sample, hence the same bracket, as on one rank
+        c->samp_shard = !tile_sample && c->world > 1 && c->shard_sample;
+        const int64_t g0 = c->samp_shard ? S * c->rank / c->world : 0;
+        c->samp_local = c->samp_shard ? S * (c->rank + 1) / c->world - g0 : S;
+        if (!tile_sample)
+            HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, g0, c->samp_local,
                                          c->sample_keys, c->stream));
         c->samp_S = S;
         c->samp_qlo = (double)c->sel_rank[0] / (double)M;
@@ -455,8 +464,9 @@ int sample_bracket(svgd_ctx *c, double sigma)
     uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
     CHK(upload_state(c, 2, sr, 0, ~0ull));
     for (int p = 0; p < 2; ++p) {
-        HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, S, 0, c->st, c->gpart, c->ghist,
-                                      c->stream));
+        HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, c->samp_local, 0, c->st, c->gpart,
+                                      c->ghist, c->stream));
+        if (c->samp_shard) CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
         HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
     }
     HIPCHK(c, launch_bracket(c->st, c->stream));
@@ -892,6 +902,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->gseg, (int64_t)c->world * (CAPG + 1)));
     if (const char *e = std::getenv("SVGD_BUCKET_CAP")) c->bucket_cap = std::atoll(e);
     if (const char *e = std::getenv("SVGD_MEDIAN_SAMPLE")) c->sample_size = std::max<int64_t>(1, std::atoll(e));
+    if (const char *e = std::getenv("SVGD_SAMPLE_SHARD")) c->shard_sample = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));

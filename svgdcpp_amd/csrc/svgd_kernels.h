@@ -77,9 +77,12 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
                              int64_t cap, uint32_t *counts, unsigned long long *below,
                              const SelState *st, uint32_t *ghist, uint32_t *bpart,
                              double *dbg_out, hipStream_t stream);
-// xf != nullptr (d <= 16): keys from the fp32 records (a bracket estimate only)
+// xf != nullptr (d <= 16): keys from the fp32 records (a bracket estimate only).
+// Sample pairs g0 .. g0+S-1 of the counter-based sequence -> keys[0 .. S-1]
+// (ranks draw disjoint index ranges of one sequence).
 hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
-                              int d, int KP, int64_t S, uint64_t *keys, hipStream_t stream);
+                              int d, int KP, int64_t g0, int64_t S, uint64_t *keys,
+                              hipStream_t stream);
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                int64_t cap, int max_blocks, const SelState *st, uint32_t *gpart,
                                uint32_t *ghist, hipStream_t stream);

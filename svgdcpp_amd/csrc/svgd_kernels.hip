@@ -594,11 +594,12 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
 // region b holds keys [b*per, (b+1)*per).
 
 __global__ void k_sample_keys(const double *__restrict__ xc, const double *__restrict__ nrm,
-                              int64_t n, int d, int KP, int64_t S, uint64_t *__restrict__ keys)
+                              int64_t n, int d, int KP, int64_t g0, int64_t S,
+                              uint64_t *__restrict__ keys)
 {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S;
          g += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t h = mix64((uint64_t)g * 2 + 1);
+        const uint64_t h = mix64((uint64_t)(g0 + g) * 2 + 1);
         const int64_t i = (int64_t)(h % (uint64_t)n);
         const int64_t j = (i + 1 + (int64_t)((h >> 32) % (uint64_t)(n - 1))) % n;
         double dot = 0.0;
@@ -617,7 +618,8 @@ __device__ __forceinline__ int64_t mulhi_index(uint32_t r, int64_t n)
 
 template <int D>
 __global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict__ xf, int64_t n,
-                                                         int64_t S, uint64_t *__restrict__ keys)
+                                                         int64_t g0, int64_t S,
+                                                         uint64_t *__restrict__ keys)
 {
     constexpr int KF = med_f32_stride(D);
     // SU samples per thread with their record loads in flight together
@@ -628,7 +630,7 @@ __global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const int64_t g = g0 + u * stride;
-            const uint64_t h = mix64((uint64_t)(g < S ? g : 0) * 2 + 1);
+            const uint64_t h = mix64((uint64_t)(g0 + (g < S ? g : 0)) * 2 + 1);
             const int64_t i = mulhi_index((uint32_t)(h >> 32), n);
             int64_t j = i + 1 + mulhi_index((uint32_t)h, n - 1);
             if (j >= n) j -= n;
@@ -2808,16 +2810,18 @@ hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, do
 
 #define SVGD_SAMPLE_CASE(Dv)                                                                 \
     case Dv:                                                                                 \
-        hipLaunchKernelGGL((k_sample_keys_f32<Dv>), dim3(g), dim3(256), 0, stream, xf, n, S, keys); \
+        hipLaunchKernelGGL((k_sample_keys_f32<Dv>), dim3(g), dim3(256), 0, stream, xf, n, g0, S, keys); \
         break;
 
 hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
-                              int d, int KP, int64_t S, uint64_t *keys, hipStream_t stream)
+                              int d, int KP, int64_t g0, int64_t S, uint64_t *keys,
+                              hipStream_t stream)
 {
     int64_t g = (S + 255) / 256;
     if (g > 4096) g = 4096;
     if (!xf) {
-        hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, d, KP, S, keys);
+        hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, d, KP, g0, S,
+                           keys);
         return hipGetLastError();
     }
     switch (d) {
