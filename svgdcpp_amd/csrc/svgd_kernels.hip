@@ -1506,7 +1506,9 @@ template <int D> struct ColRec {
 };
 
 // acc_i += K_ij [V_j, 1] for the lane's R rows against one column j.
-template <int D, int R>
+// FOLD: the row term c_i is left out of u (one add fewer per pair) and the
+// row's sums are scaled by 2^(c_i/4096) once at the end (k_phi_rows).
+template <int D, int R, bool FOLD>
 __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (&xs)[R][D],
                                               const double (&ci)[R], double (&acc)[R][D],
                                               double (&acc1)[R], const double *tab)
@@ -1514,7 +1516,7 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
     // the R rows' chains interleaved (independent FMAs back to back)
     double u[R], K[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) u[r] = ci[r] + q.c;
+    for (int r = 0; r < R; ++r) u[r] = FOLD ? q.c : ci[r] + q.c;
 #pragma unroll
     for (int k = 0; k < D; ++k)
 #pragma unroll
@@ -1596,7 +1598,18 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     const int64_t j0 = n * s / S, j1 = n * (s + 1) / S;
     const int64_t nch = (j1 - j0 + CH_PHI - 1) / CH_PHI;
     const char *gcol = reinterpret_cast<const char *>(rec + j0 * RS);
+    // Folding c_i out of the pair loop needs K_ij 2^(-c_i/4096) <= 2^(-c_i/4096)
+    // to stay far from overflow (with N |V| on top): whole waves whose rows
+    // all have -c_i/4096 = a log2e |xc_i|^2 <= FOLD_MAX take it (the usual
+    // case: particles within ~sqrt(400/a) of the mean), others the plain form.
+    constexpr double FOLD_MAX = 400.0;
+    bool fold_ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r) fold_ok = fold_ok && ci[r] >= -4096.0 * FOLD_MAX;
+    const bool fold = __all(fold_ok);
     if (nch > 0) dma_to_lds<CHB>(gcol, wbuf, lane);
+    auto stream_columns = [&](auto fold_tag) {
+    constexpr bool FOLD = decltype(fold_tag)::value;
     for (int64_t c = 0; c < nch; ++c) {
         if (c + 1 < nch) {
             dma_to_lds<CHB>(gcol + (c + 1) * CHB, wbuf + ((c + 1) & 1) * CHB, lane);
@@ -1613,7 +1626,7 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
             for (int jj = 0; jj < cnt; ++jj) {
                 ColRec<D> q;
                 q.load(cb + jj * RS);
-                phi_rows_pair<D, R>(q, xs, ci, acc, acc1, tab);
+                phi_rows_pair<D, R, FOLD>(q, xs, ci, acc, acc1, tab);
             }
             continue;
         }
@@ -1625,14 +1638,31 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
         for (int jj = 0; jj < cnt; jj += 2) {
             qb.load(cb + (jj + 1) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R>(qa, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
             if (jj + 1 >= cnt) break;
             qa.load(cb + (jj + 2) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R>(qb, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD>(qb, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
         }
+    }
+    };
+    if (fold) {
+        stream_columns(std::true_type{});
+        // K_ij = 2^(c_i/4096) 2^((c_j + ..)/4096): the row factor, once
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const double k = __builtin_rint(ci[r]);
+            const int ki = (int)k;
+            const double g = __builtin_ldexp(exp2_4096_poly(ci[r] - k) * tab[ki & (EXP_TB - 1)],
+                                             ki >> 12);
+#pragma unroll
+            for (int k2 = 0; k2 < D; ++k2) acc[r][k2] *= g;
+            acc1[r] *= g;
+        }
+    } else {
+        stream_columns(std::false_type{});
     }
 
 #pragma unroll

@@ -1,7 +1,7 @@
 """Sharded step rehearsal on one GPU: world = 2, 3 and 8 ranks on device 0 with
 the host shared-memory collective backend (SVGD_HOSTCOMM) vs the same
-problem on one rank.  The median is an exact order statistic, so the scale
-must agree bit for bit; phi sums columns in a different split, so positions
+problem on one rank.  The median is an exact order statistic, so the first
+step's scale must agree bit for bit (later steps: to rounding of X_t); phi sums columns in a different split, so positions
 agree to fp64 rounding, which Adam's normalised step can amplify where
 phi_hat ~ 0: 1e-10 after 4 steps (observed <= 1.3e-12).  The RCCL calls themselves are the same
 in-place all-gather / sum all-reduce at the same call sites."""
@@ -49,7 +49,10 @@ def test_sharded_step_matches_single_rank(world, n):
     for (a0, a1), (b0, b1) in zip(shards, shards[1:]):
         assert a1 == b0
     for rank, (X, scales, _) in multi.items():
-        # every rank holds the all-gathered particles and the same exact scale
-        assert [s[0] for s in scales] == [s[0] for s in s1], (rank, scales, s1)
+        # every rank holds the all-gathered particles; the first step's scale
+        # (same X_0) is bit-identical to one rank's, later ones follow X_t,
+        # which differs from one rank's in the last bits (phi splits)
+        assert scales[0][0] == s1[0][0], (rank, scales, s1)
+        np.testing.assert_allclose([s[0] for s in scales], [s[0] for s in s1], rtol=1e-13)
         assert [s[2] for s in scales] == [s[2] for s in s1]
         np.testing.assert_allclose(X, X1, rtol=0, atol=1e-10)

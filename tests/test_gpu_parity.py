@@ -72,6 +72,21 @@ def test_phi_far_from_origin(oracle):
     assert np.max(np.abs(ph - ref)) <= PHI_TOL
 
 
+@pytest.mark.parametrize("d", [2, 8])
+def test_phi_outliers_mixed_fold(oracle, d):
+    """A few particles far out (a log2e |x_i - mean|^2 >> 400): their waves keep
+    the row term inside the pair loop, every other wave folds it into one
+    factor per row (k_phi_rows FOLD); both agree with the oracle."""
+    n = 1500
+    X = oracle.splitmix((n, d), 1.0, 77 + d)
+    X[[5, 700, 1499]] += 40.0
+    G = oracle.splitmix((n, d), 1.0, 78 + d)
+    a = 2.0
+    ref = oracle.phi(X, G, a)
+    ph = _ctx(X).phi(G, a)
+    assert np.max(np.abs(ph - ref)) <= PHI_TOL
+
+
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 9, 64, 65, 127, 400, 777])
 def test_median_exact_selection_direct(oracle, n):
     d = 3
