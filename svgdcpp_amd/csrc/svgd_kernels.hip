@@ -1635,7 +1635,27 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
         __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0): nothing pending at the loop head
         // (sched_barrier keeps the scheduler from sinking the prefetch reads
         // back down to their first use)
-        for (int jj = 0; jj < cnt; jj += 2) {
+        // 4 columns per iteration without exit tests, then the 0..3 rest
+        int jj = 0;
+        for (; jj + 4 <= cnt; jj += 4) {
+            qb.load(cb + (jj + 1) * RS);
+            __builtin_amdgcn_sched_barrier(0);
+            phi_rows_pair<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
+            __builtin_amdgcn_sched_barrier(0);
+            qa.load(cb + (jj + 2) * RS);
+            __builtin_amdgcn_sched_barrier(0);
+            phi_rows_pair<D, R, FOLD>(qb, xs, ci, acc, acc1, tab);
+            __builtin_amdgcn_sched_barrier(0);
+            qb.load(cb + (jj + 3) * RS);
+            __builtin_amdgcn_sched_barrier(0);
+            phi_rows_pair<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
+            __builtin_amdgcn_sched_barrier(0);
+            qa.load(cb + (jj + 4) * RS);
+            __builtin_amdgcn_sched_barrier(0);
+            phi_rows_pair<D, R, FOLD>(qb, xs, ci, acc, acc1, tab);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        for (; jj < cnt; jj += 2) {
             qb.load(cb + (jj + 1) * RS);
             __builtin_amdgcn_sched_barrier(0);
             phi_rows_pair<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
