@@ -2074,7 +2074,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !
                         column(cr, jb + jj);
                     }
                 } else {
-                    for (int jj = 0; jj < cnt; ++jj) {
+                    // 2 columns per iteration (one loop test per two), then the rest
+                    int jj = 0;
+                    for (; jj + 2 <= cnt; jj += 2) {
+                        double cr[D + 1];
+                        load(cr, jj);
+                        column(cr, jb + jj);
+                        load(cr, jj + 1);
+                        column(cr, jb + jj + 1);
+                    }
+                    if (jj < cnt) {
                         double cr[D + 1];
                         load(cr, jj);
                         column(cr, jb + jj);
