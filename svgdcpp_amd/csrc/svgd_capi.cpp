@@ -88,6 +88,7 @@ struct svgd_ctx {
     int64_t sample_size = int64_t(1) << 22;
     double bracket_sigma = 3.0; // sample-quantile standard deviations either side
     bool shard_sample = true;   // P > 1: ranks draw disjoint parts of the sample
+    int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
     bool samp_shard = false;    // this step's sample is sharded
     int64_t samp_local = 0;     // sample keys held by this rank
     int64_t samp_S = 0;         // this step's sample: size and target quantiles
@@ -394,7 +395,7 @@ int median_begin(svgd_ctx *c)
 
     const int64_t M = upper_pairs(n);
     const int64_t tiles = c->own_tiles;
-    c->collect_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, 1024));
+    c->collect_grid = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, c->collect_blocks));
     c->nregions = c->rowpath ? 4 * (int64_t)c->collect_grid : c->collect_grid;
     const int64_t tiles_per_blk = (tiles + c->nregions - 1) / c->nregions;
 
@@ -856,6 +857,12 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim, c->R) * ncu;
         const int64_t iblocks = std::max<int64_t>(1, (c->nrows + 256 * c->R - 1) / (256 * c->R));
         int64_t S = std::max<int64_t>(1, (resident + iblocks - 1) / iblocks);
+        // 2 blocks per resident slot: one block wave per slot left a tail of
+        // idle CUs (measured at cfg3, phi launch: S x1 4.00 ms, x2 3.83-3.93,
+        // x4 3.81-3.90, x8 3.91-3.95 -- x2 and x4 tie, x2 has half the partials)
+        int split_mult = 2;
+        if (const char *e = std::getenv("SVGD_PHI_SPLIT_MULT")) split_mult = std::max(1, std::atoi(e));
+        S *= split_mult;
         S = std::min<int64_t>(S, std::max<int64_t>(1, n / 256));
         c->S = (int)S;
         c->RS = phi_rec_stride(dim);
@@ -902,6 +909,9 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->gseg, (int64_t)c->world * (CAPG + 1)));
     if (const char *e = std::getenv("SVGD_BUCKET_CAP")) c->bucket_cap = std::atoll(e);
     if (const char *e = std::getenv("SVGD_MEDIAN_SAMPLE")) c->sample_size = std::max<int64_t>(1, std::atoll(e));
+    // (buffers below are sized for <= 1024 collect blocks: smaller values only)
+    if (const char *e = std::getenv("SVGD_COLLECT_BLOCKS"))
+        c->collect_blocks = std::min(1024, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SVGD_SAMPLE_SHARD")) c->shard_sample = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
