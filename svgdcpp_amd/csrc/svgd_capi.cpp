@@ -34,6 +34,8 @@ struct EvPair {
 
 } // namespace
 
+constexpr int64_t MAX_COLLECT_BLOCKS = 2048; // collect-pass grid limit (buffer sizes)
+
 struct svgd_ctx {
     int dim = 0;
     int64_t n = 0;
@@ -101,7 +103,7 @@ struct svgd_ctx {
     uint64_t *cbuf = nullptr;          // compacted candidates (regions_alloc keys)
     unsigned long long *ccount = nullptr;
     uint32_t *gpart = nullptr;         // per-block histograms (HIST_PART_BLOCKS x 2 RADIX)
-    uint32_t *bpart = nullptr;         // collect blocks' key-range bucket histograms (1024 x NBK)
+    uint32_t *bpart = nullptr;         // collect blocks' key-range bucket histograms (max blocks x NBK)
     uint64_t *gseg = nullptr;          // world x (CAPG + 1): compacted selected-bucket keys
     int64_t bucket_cap = CAPG;         // bucket select path if the selected buckets hold <= this
     uint32_t *counts = nullptr;
@@ -361,6 +363,7 @@ hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t
 }
 
 constexpr double WIDE_SIGMA = 8.0; // re-bracket after a miss
+
 int sample_bracket(svgd_ctx *c, double sigma);
 int collect_counts(svgd_ctx *c);
 
@@ -902,16 +905,15 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->upper, dim));
     CHK(dalloc(c, &c->partial, (int64_t)c->nparts * dim));
     CHK(dalloc(c, &c->scal, 2));
-    CHK(dalloc(c, &c->counts, 4096)); // <= 4 regions per collect block, <= 1024 blocks
-    CHK(dalloc(c, &c->below, 4096));
+    CHK(dalloc(c, &c->counts, 4 * MAX_COLLECT_BLOCKS)); // <= 4 regions per collect block
+    CHK(dalloc(c, &c->below, 4 * MAX_COLLECT_BLOCKS));
     CHK(dalloc(c, &c->cnt3, CNT_LEN + 3));
-    CHK(dalloc(c, &c->bpart, (int64_t)1024 * NBK)); // collect grid <= 1024
+    CHK(dalloc(c, &c->bpart, (int64_t)MAX_COLLECT_BLOCKS * NBK));
     CHK(dalloc(c, &c->gseg, (int64_t)c->world * (CAPG + 1)));
     if (const char *e = std::getenv("SVGD_BUCKET_CAP")) c->bucket_cap = std::atoll(e);
     if (const char *e = std::getenv("SVGD_MEDIAN_SAMPLE")) c->sample_size = std::max<int64_t>(1, std::atoll(e));
-    // (buffers below are sized for <= 1024 collect blocks: smaller values only)
-    if (const char *e = std::getenv("SVGD_COLLECT_BLOCKS"))
-        c->collect_blocks = std::min(1024, std::max(1, std::atoi(e)));
+    if (const char *e = std::getenv("SVGD_COLLECT_BLOCKS")) // buffers hold <= MAX_COLLECT_BLOCKS
+        c->collect_blocks = std::min<int64_t>(MAX_COLLECT_BLOCKS, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SVGD_SAMPLE_SHARD")) c->shard_sample = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
