@@ -240,7 +240,7 @@ def main():
             },
             "phases_ms_per_step": {"phi": phi_ms.value / max(1, args.steps),
                                    "median": med_ms.value / max(1, args.steps)},
-            "median_path": ["direct", "bracket", "fallback"][path],
+            "median_path": ["direct", "bracket", "fallback", "rebracket"][path],
             "scale_a": a,
         }
         if args.config != "cfg3" or args.device_model or dtype != "f64":
