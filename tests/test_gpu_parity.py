@@ -178,6 +178,31 @@ def test_median_rebracket_path_exact(oracle, monkeypatch, d):
     assert C.SVGD_MEDIAN_REBRACKET in paths, paths
 
 
+def test_step_rebracket_matches_normal_bracket(oracle, monkeypatch):
+    """Full steps whose bracket misses (SVGD_MEDIAN_SIGMA=0: re-bracket + a
+    second collect pass, or the radix fallback) give bit-identical particles
+    to steps with the default bracket: the median is exact either way."""
+    n, d = 6000, 8  # N^2/2 > 2^24 pairs: the bracket path
+    mus, covs = _gmm(oracle, d, 4, 31)
+    X0 = oracle.splitmix((n, d), 3.0, 32)
+    out = []
+    for sigma in (None, "0"):
+        if sigma is None:
+            monkeypatch.delenv("SVGD_MEDIAN_SIGMA", raising=False)
+        else:
+            monkeypatch.setenv("SVGD_MEDIAN_SIGMA", sigma)
+        c = _ctx(X0)
+        c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+        paths = []
+        for _ in range(3):
+            c.step_with_model(S.GaussianSum(list(mus), list(covs)))
+            paths.append(c.last_scale()[2])
+        out.append((c.get_particles(), paths))
+    assert all(p == C.SVGD_MEDIAN_BRACKET for p in out[0][1]), out[0][1]
+    assert any(p in (C.SVGD_MEDIAN_REBRACKET, C.SVGD_MEDIAN_FALLBACK) for p in out[1][1]), out[1][1]
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+
+
 def test_median_fallback_path_exact(oracle):
     n = 900
     X = oracle.splitmix((n, 4), 1.0, 42)
