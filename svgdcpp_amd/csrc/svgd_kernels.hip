@@ -439,6 +439,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
     return z ^ (z >> 31);
 }
 
+// next representable value towards +inf of a finite non-negative float/double
+__device__ __forceinline__ float nextafter_up(float x)
+{
+    return __int_as_float(__float_as_int(x) + 1);
+}
+__device__ __forceinline__ double nextafter_up(double x)
+{
+    return __longlong_as_double(__double_as_longlong(x) + 1);
+}
+
 template <class T, int KP, int MODE>
 __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
                                                    const T *__restrict__ nrm, int64_t n,
@@ -475,10 +485,22 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     }
     uint64_t lo_key = 0, hi_key = 0;
     double binv = 0.0;
+    // MODE 0 classifies s in the kernel's precision: for non-negative s,
+    // key_of(s) < lo_key <=> s < loT with loT the smallest T >= the double of
+    // lo_key (keys of non-negative doubles order like the doubles; fp32 keys
+    // widen exactly), likewise hi; the key itself is formed in the band only
+    T loT = (T)0, hiT = (T)0;
     if (MODE == 0) {
         lo_key = sc.st->lo_key;
         hi_key = sc.st->hi_key;
         binv = sc.st->binv;
+        const double lo_d = __longlong_as_double((long long)lo_key);
+        const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
+                                                            : __longlong_as_double((long long)hi_key);
+        loT = (T)lo_d;
+        if ((double)loT < lo_d) loT = nextafter_up(loT);
+        hiT = (T)hi_d;
+        if ((double)hiT < hi_d) hiT = nextafter_up(hiT);
         if (tid == 0) sCnt = 0;
         if (sc.bpart)
             for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
@@ -514,6 +536,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
         __syncthreads();
         curI = I;
 
+        const bool full = I != J && (I + 1) * TB <= n && (J + 1) * TB <= n;
         T bI[KP / 4];
 #pragma unroll
         for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = sXI[(4 * kk + hi) * LDP + w * 16 + lo];
@@ -531,26 +554,35 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
             for (int r = 0; r < 4; ++r) {
                 const int jl = js * 16 + acc_row<T>(hi, r);
                 const int64_t j = J * TB + jl;
-                const bool valid = (i < n) && (j < n) && (I != J || il < jl);
-                // key of the distance in the kernel's precision (fp32 keys widen exactly)
-                const double s = (double)fmax(fma((T)-2, dot[r], ni + sNJ[jl]), (T)0);
-                const uint64_t key = key_of(s);
-                if (MODE == 0) {
-                    const bool in = valid && key >= lo_key && key < hi_key;
-                    below += (valid && key < lo_key) ? 1u : 0u;
+                if constexpr (MODE == 0) {
+                    // off-diagonal tiles of two full blocks (all but a few):
+                    // every pair is valid
+                    const bool valid = full || ((i < n) && (j < n) && (I != J || il < jl));
+                    const T sv = fmax(fma((T)-2, dot[r], ni + sNJ[jl]), (T)0);
+                    const bool isb = sv < loT;
+                    const bool in = valid && !isb && sv < hiT;
+                    below += (valid && isb) ? 1u : 0u;
                     const unsigned long long mask = __ballot(in);
                     if (mask) {
                         uint32_t base = 0;
                         if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mask));
                         base = __shfl(base, 0);
                         if (in) {
+                            // key of the distance in the kernel's precision
+                            const uint64_t key = key_of((double)sv);
                             const int64_t pos =
                                 base + __popcll(mask & ((1ull << lane) - 1ull));
                             if (pos < sc.cap) sc.region[blockIdx.x * sc.cap + pos] = key;
                             if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
                         }
                     }
-                } else if (MODE == 1) {
+                    continue;
+                }
+                const bool valid = (i < n) && (j < n) && (I != J || il < jl);
+                // key of the distance in the kernel's precision (fp32 keys widen exactly)
+                const double s = (double)fmax(fma((T)-2, dot[r], ni + sNJ[jl]), (T)0);
+                const uint64_t key = key_of(s);
+                if (MODE == 1) {
                     if (valid) {
                         for (int s2 = 0; s2 < nsel; ++s2) {
                             const bool match = hsh >= 64 || (key >> hsh) == (pfx[s2] >> hsh);
