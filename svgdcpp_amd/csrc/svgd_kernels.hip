@@ -508,18 +508,36 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     }
     uint32_t below = 0;
 
-    int64_t curI = -1;
-    for (int64_t t = tb; t < te; ++t) {
-        int64_t I, J;
+    auto coords = [&](int64_t t, int64_t *I, int64_t *J) {
         if (MODE == 3) {
             // sample tile t: a random pair of distinct full 64-particle blocks
             const uint64_t h = mix64((uint64_t)t * 2 + 1);
             const int64_t nbf = sd.n / TB;
-            I = (int64_t)(h % (uint64_t)nbf);
-            J = (I + 1 + (int64_t)((h >> 32) % (uint64_t)(nbf - 1))) % nbf;
+            *I = (int64_t)(h % (uint64_t)nbf);
+            *J = (*I + 1 + (int64_t)((h >> 32) % (uint64_t)(nbf - 1))) % nbf;
         } else {
-            tile_coords(nb, t, &I, &J);
+            tile_coords(nb, t, I, J);
         }
+    };
+    // the next tile's column block is loaded into registers while the current
+    // tile is computed, then stored to LDS between the two barriers
+    constexpr int PU = TB * KP / 256;
+    T preX[PU];
+    T preN = (T)0;
+    auto fetch = [&](int64_t Jn) {
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
+            preX[u] = xc[(Jn * TB + jl) * KP + k];
+        }
+        if (tid < TB) preN = nrm[Jn * TB + tid];
+    };
+    int64_t curI = -1, I = 0, J = 0;
+    if (tb < te) {
+        coords(tb, &I, &J);
+        fetch(J);
+    }
+    for (int64_t t = tb; t < te; ++t) {
         __syncthreads();
         if (I != curI) {
             for (int e = tid; e < TB * KP; e += 256) {
@@ -528,20 +546,26 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
             }
             if (tid < TB) sNI[tid] = nrm[I * TB + tid];
         }
-        for (int e = tid; e < TB * KP; e += 256) {
-            const int jl = e / KP, k = e - jl * KP;
-            sXJ[k * LDP + jl] = xc[(J * TB + jl) * KP + k];
+#pragma unroll
+        for (int u = 0; u < PU; ++u) {
+            const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
+            sXJ[k * LDP + jl] = preX[u];
         }
-        if (tid < TB) sNJ[tid] = nrm[J * TB + tid];
+        if (tid < TB) sNJ[tid] = preN;
         __syncthreads();
         curI = I;
+        const int64_t Ic = I, Jc = J;
+        if (t + 1 < te) {
+            coords(t + 1, &I, &J);
+            fetch(J);
+        }
 
-        const bool full = I != J && (I + 1) * TB <= n && (J + 1) * TB <= n;
+        const bool full = Ic != Jc && (Ic + 1) * TB <= n && (Jc + 1) * TB <= n;
         T bI[KP / 4];
 #pragma unroll
         for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = sXI[(4 * kk + hi) * LDP + w * 16 + lo];
         const int il = w * 16 + lo;
-        const int64_t i = I * TB + il;
+        const int64_t i = Ic * TB + il;
         const T ni = sNI[il];
 
 #pragma unroll
@@ -553,11 +577,11 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int jl = js * 16 + acc_row<T>(hi, r);
-                const int64_t j = J * TB + jl;
+                const int64_t j = Jc * TB + jl;
                 if constexpr (MODE == 0) {
                     // off-diagonal tiles of two full blocks (all but a few):
                     // every pair is valid
-                    const bool valid = full || ((i < n) && (j < n) && (I != J || il < jl));
+                    const bool valid = full || ((i < n) && (j < n) && (Ic != Jc || il < jl));
                     const T sv = fmax(fma((T)-2, dot[r], ni + sNJ[jl]), (T)0);
                     const bool isb = sv < loT;
                     const bool in = valid && !isb && sv < hiT;
@@ -578,7 +602,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
                     }
                     continue;
                 }
-                const bool valid = (i < n) && (j < n) && (I != J || il < jl);
+                const bool valid = (i < n) && (j < n) && (Ic != Jc || il < jl);
                 // key of the distance in the kernel's precision (fp32 keys widen exactly)
                 const double s = (double)fmax(fma((T)-2, dot[r], ni + sNJ[jl]), (T)0);
                 const uint64_t key = key_of(s);
