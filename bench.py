@@ -244,7 +244,10 @@ def main():
             "scale_a": a,
         }
         if args.config != "cfg3" or args.device_model or dtype != "f64":
-            out["metric"] = (f"particle-updates/s, {cfg['desc']}"
+            desc = cfg["desc"]
+            if dtype != cfg.get("dtype", "f64"):
+                desc = desc.replace("fp32 compute", "fp64 compute") + (", fp32 compute" if dtype == "f32" and "fp32" not in desc else "")
+            out["metric"] = (f"particle-updates/s, {desc}"
                              f"{', device grad log p' if args.device_model else ''} (not the headline config)")
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows)
