@@ -87,7 +87,7 @@ struct svgd_ctx {
 
     // median
     int64_t direct_max_pairs = int64_t(1) << 24;
-    int64_t sample_size = int64_t(1) << 22;
+    int64_t sample_size = 0; // 0: auto, clamp(M / 256, 2^18, 2^22) for M pairs
     double bracket_sigma = 3.0; // sample-quantile standard deviations either side
     bool shard_sample = true;   // P > 1: ranks draw disjoint parts of the sample
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
@@ -410,7 +410,14 @@ int median_begin(svgd_ctx *c)
         CHK(upload_state(c, 1, z, 0, ~0ull));
     } else {
         c->med_path = SVGD_MEDIAN_BRACKET;
-        int64_t S = std::min<int64_t>(c->sample_size, M);
+        // sample size: the band it leaves costs the collect pass, sampling and
+        // the two bracket passes cost ~S; measured optimum near M / 256 pairs
+        // (cfg2, M = 1.3e8: 2^19 -> median 0.222 vs 0.262 ms at 2^22), capped
+        // at 2^22 (cfg3, M = 2.1e9)
+        int64_t S = c->sample_size > 0
+                        ? std::min<int64_t>(c->sample_size, M)
+                        : std::min<int64_t>(std::max<int64_t>(M / 256, int64_t(1) << 18), int64_t(1) << 22);
+        S = std::min<int64_t>(S, M);
         // tile path: whole random 64 x 64 tiles (MFMA Gram, ~1/1000 of the
         // collect pass) instead of scattered pairs (2 random 8d-byte rows each)
         const bool tile_sample = !c->rowpath && n / TB >= 2 && S >= TB * TB;
