@@ -77,31 +77,82 @@ def config_workload(name, n, d, k):
     return workload(n, d, k)
 
 
-def cpu_baseline(X0, mus, covs, rows):
+def _host_cpu():
+    """CPU model (as lscpu prints it) and the cores this process may run on."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    return model, cores
+
+
+def _cpu_sample(o, X0, mus, covs, rows):
+    n, d = X0.shape
+    t0 = time.perf_counter()
+    o.median_rows_work(X0, 0, rows)
+    G = o.logp_grad_gmm(X0, mus, covs)  # all rows: phi needs every G_j
+    ph = o.phi(X0, G, 0.5, rows=(0, rows))  # the value of a is irrelevant to the cost
+    Xs = X0[:rows].copy()
+    o.apply_update(Xs, o.Adam((rows, d), 0.1, 0.9, 0.999).step(ph))
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(X0, mus, covs, rows, rows_1t):
     """Oracle (CPU port of the reference arithmetic) on a row sample of one step:
-    median work of `rows` rows, their log-gradients, phi_hat and Adam."""
+    median work of `rows` rows, their log-gradients, phi_hat and Adam -- with
+    the OpenMP threads of this box (OMP_NUM_THREADS) and with one thread."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as o
 
     n, d = X0.shape
-    rows = min(rows, n)
-    t0 = time.perf_counter()
-    o.median_rows_work(X0, 0, rows)
-    G = o.logp_grad_gmm(X0, mus, covs)  # all rows: phi needs every G_j
-    a = 0.5  # value irrelevant to the cost
-    ph = o.phi(X0, G, a, rows=(0, rows))
-    Xs = X0[:rows].copy()
-    o.apply_update(Xs, o.Adam((rows, d), 0.1, 0.9, 0.999).step(ph))
-    dt = time.perf_counter() - t0
+    rows, rows_1t = min(rows, n), min(rows_1t, n)
+    threads = int(o.num_threads())
+    dt = _cpu_sample(o, X0, mus, covs, rows)
+    o.set_threads(1)
+    dt1 = _cpu_sample(o, X0, mus, covs, rows_1t)
+    o.set_threads(threads)
+    model, host_cores = _host_cpu()
     return {
         "value": rows / dt,
         "unit": "particle-updates/s",
-        "cores": int(o.num_threads()),
+        "cores": threads,
         "kind": "port",
+        "host_cpu": model,
+        "host_cores": host_cores,
+        "value_1thread": rows_1t / dt1,
         "sample": f"one step of the N={n} d={d} Gaussian-sum(k={len(mus)}) workload restricted to {rows} particle rows "
                   f"(their median pair share, grad log p of all N, phi_hat of {rows} rows against all N, "
-                  f"Adam); {dt:.2f} s, OpenMP threads={o.num_threads()}",
+                  f"Adam); {dt:.2f} s on {threads} OpenMP threads; 1 thread: {rows_1t} rows in {dt1:.2f} s",
     }
+
+
+def spawn_ranks(nproc):
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per
+    GPU) before anything touches a GPU, wait, exit with the worst status."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
+                   LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def main():
@@ -114,6 +165,7 @@ def main():
     ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--cpu-rows", type=int, default=32768)
+    ap.add_argument("--cpu-rows-1t", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dtype", choices=["f64", "f32"], default=None,
                     help="compute dtype of the O(N^2) work (default: the config's; cfg5 is f32)")
@@ -121,6 +173,8 @@ def main():
                     help="grad log p on the device (SURVEY 8(f) rank 1) instead of the host; "
                          "not the north-star configuration")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import svgdcpp_amd as S
@@ -228,8 +282,12 @@ def main():
                 "n": n, "d": d, "k": k, "parallelism": f"rows{world}",
             },
             "roofline": {
-                "kernel": "k_phi (fused RBF + grad + phi contraction)",
-                "bound": "mfma",
+                # fp64 d <= 16: VALU row stream (f64 MFMA shares the VALU issue
+                # slots on gfx950); otherwise the MFMA tile kernel
+                "kernel": ("k_phi_rows (fused RBF + grad + phi contraction, fp64 VALU row stream)"
+                           if dtype == "f64" and d <= 16 else
+                           "k_phi (fused RBF + grad + phi contraction, MFMA tiles)"),
+                "bound": "valu" if dtype == "f64" and d <= 16 else "mfma",
                 "achieved": achieved,
                 "peak": peak,
                 "unit": "TFLOP/s",
@@ -250,7 +308,7 @@ def main():
             out["metric"] = (f"particle-updates/s, {desc}"
                              f"{', device grad log p' if args.device_model else ''} (not the headline config)")
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows)
+            out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows, args.cpu_rows_1t)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

@@ -19,6 +19,15 @@
  * on the host between the two device calls (GaussianRBFKernel.hpp:189-210).
  * LogIntermediateMatrices re-evaluates K and Kg on the host from the step's
  * scale (debug aid for small N, same text format as SVGD.hpp:345-365).
+ *
+ * Generic kernels: any other Kernel -- a UpdateKernel closed
+ * form, a composition, or a derived class overriding EvaluateKernel /
+ * EvaluateKernelGrad (Kernel.hpp:279-297) -- runs the reference's serial /
+ * parallel ComputePhi on the HOST (SVGD.hpp:373-454: per particle i,
+ * UpdateLocation(x_i), then k(x_j, x_i) and grad k(x_j, x_i) for every j),
+ * with the plugin optimizer's own Step and the clamp.  The choice is made
+ * once, by kernel type, at construction (UsesDevicePath()); a
+ * GaussianRBFKernel never takes the host path, and the host path needs no GPU.
  */
 #ifndef SVGDCPP_AMD_SVGD_HPP
 #define SVGDCPP_AMD_SVGD_HPP
@@ -47,6 +56,9 @@ struct SVGDOptions
     bool Parallel = false;
     bool LogIntermediateMatrices = false;
     int Device = 0;
+    /** Extension: significant digits of the logged matrices (0 = the stream
+     *  default, 6, as the reference writes them). */
+    int IntermediateMatricesPrecision = 0;
     SVGDOptions() {}
 };
 
@@ -58,6 +70,7 @@ public:
                o.LowerBound, o.UpperBound, o.Parallel, o.LogIntermediateMatrices, o.IntermediateMatricesOutputPath,
                o.Device)
     {
+        log_precision_ = o.IntermediateMatricesPrecision;
     }
 
     SVGD(const size_t &dim, const size_t &iter, const std::shared_ptr<Eigen::MatrixXd> &coord_mat_ptr,
@@ -119,8 +132,13 @@ public:
             throw std::invalid_argument(SVGDCPP_LOG_PREFIX + "[Argument Error] Invalid Optimizer object pointer.");
         rbf_ptr_ = std::dynamic_pointer_cast<GaussianRBFKernel>(kernel_ptr_);
         if (!rbf_ptr_)
-            throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
-                                        "[Argument Error] The device path requires a GaussianRBFKernel.");
+        {
+            // generic kernel: the reference's per-pair ComputePhi on the host
+            std::cout << SVGDCPP_LOG_PREFIX + "Kernel is not a GaussianRBFKernel: phi_hat runs on the host "
+                                              "(generic kernel path)."
+                      << std::endl;
+            return;
+        }
         if (optimizer_ptr_->Kind() < 0)
             throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
                                         "[Argument Error] The device path requires Adam, AdaGrad or RMSProp.");
@@ -140,7 +158,8 @@ public:
         model_ptr_->Initialize();
         kernel_ptr_->Initialize();
         optimizer_ptr_->Initialize();
-        ConfigureDevice();
+        if (UsesDevicePath())
+            ConfigureDevice();
         if (log_intermediate_matrices_)
         {
             intermediate_matrices_sstream_vector_.clear();
@@ -154,7 +173,8 @@ public:
     {
         kernel_ptr_->UpdateParameters(params);
         kernel_ptr_->Initialize();
-        ConfigureScale();
+        if (UsesDevicePath())
+            ConfigureScale();
     }
 
     /** SVGD.hpp:328-332 */
@@ -169,6 +189,14 @@ public:
     {
         if (!initialized_)
             throw UnsetException("SVGD::Initialize must be called before Run.");
+        if (!UsesDevicePath())
+        {
+            for (size_t iter = 0; iter < num_iterations_; ++iter)
+                HostStep(iter);
+            if (log_intermediate_matrices_)
+                WriteIntermediateMatricesToFile();
+            return;
+        }
         svgd_ctx *c = ctx_.get();
         Check(svgd_set_particles(c, coord_matrix_ptr_->data()));
         double *hx = nullptr, *hg = nullptr;
@@ -186,8 +214,13 @@ public:
             WriteIntermediateMatricesToFile();
     }
 
-    /** The context (for callers that need the C ABI directly). */
+    /** The context (for callers that need the C ABI directly); null on the
+     *  generic-kernel host path. */
     svgd_ctx *Context() const { return ctx_.get(); }
+
+    /** True for a GaussianRBFKernel (the HIP path), false for the generic
+     *  host path of any other kernel. */
+    bool UsesDevicePath() const { return rbf_ptr_ != nullptr; }
 
 protected:
     /** SVGD.hpp:373-400 on the device; the model gradient stays on the host. */
@@ -204,6 +237,87 @@ protected:
         }
         model_ptr_->LogModelGradBatch(hx, (int64_t)num_particles_, hg);
         Check(svgd_finish_step(c, hg));
+    }
+
+    /** The reference's SVGD::Step with ComputePhi (SVGD.hpp:373-454) for a
+     *  generic kernel, on the host: K(j, i) = k(x_j, x_i) and
+     *  Kg(j d .. j d + d - 1, i) = grad_{x_j} k(x_j, x_i) with the kernel's
+     *  location at x_i, phi_i = (1/N) sum_j (K(j, i) G_j + Kg_j), then
+     *  X += optimizer.Step(phi) and the clamp.  Parallel mode gives every
+     *  OpenMP thread its own kernel clone (the reference clones per particle,
+     *  SVGD.hpp:245-248). */
+    void HostStep(size_t iter)
+    {
+        Eigen::MatrixXd &X = *coord_matrix_ptr_;
+        const long n = (long)num_particles_, d = dimension_;
+        model_ptr_->Step();
+        kernel_ptr_->Step();
+        Eigen::MatrixXd G(d, n), phi(d, n);
+        model_ptr_->LogModelGradBatch(X.data(), n, G.data());
+        const bool log = log_intermediate_matrices_;
+        Eigen::MatrixXd K, Kg;
+        if (log)
+        {
+            K.resize(n, n);
+            Kg.resize(d * n, n);
+        }
+        const double inv_n = 1.0 / (double)n;
+        auto row = [&](Kernel &k, long i) {
+            k.UpdateLocation(X.col(i));
+            k.Initialize();
+            std::vector<double> acc((size_t)d, 0.0);
+            for (long j = 0; j < n; ++j)
+            {
+                const Eigen::VectorXd xj = X.col(j);
+                const double kv = k.EvaluateKernel(xj);
+                const Eigen::VectorXd kg = k.EvaluateKernelGrad(xj);
+                for (long q = 0; q < d; ++q)
+                    acc[(size_t)q] += G(q, j) * kv + kg(q);
+                if (log)
+                {
+                    K(j, i) = kv;
+                    for (long q = 0; q < d; ++q)
+                        Kg(j * d + q, i) = kg(q);
+                }
+            }
+            for (long q = 0; q < d; ++q)
+                phi(q, i) = inv_n * acc[(size_t)q];
+        };
+#ifdef _OPENMP
+        if (parallel_)
+        {
+#pragma omp parallel
+            {
+                std::unique_ptr<Kernel> k = kernel_ptr_->CloneUniquePointer();
+#pragma omp for schedule(static)
+                for (long i = 0; i < n; ++i)
+                    row(*k, i);
+            }
+        }
+        else
+#endif
+        {
+            for (long i = 0; i < n; ++i)
+                row(*kernel_ptr_, i);
+        }
+        X += optimizer_ptr_->Step(phi);
+        if (check_bounds_)
+            for (long i = 0; i < n; ++i)
+                for (long q = 0; q < d; ++q)
+                    X(q, i) = std::max(std::min(X(q, i), upper_[(size_t)q]), lower_[(size_t)q]);
+        if (log)
+            LogMatrices(iter, G, K, Kg, X);
+    }
+
+    void LogMatrices(size_t iter, const Eigen::MatrixXd &G, const Eigen::MatrixXd &K, const Eigen::MatrixXd &Kg,
+                     const Eigen::MatrixXd &X)
+    {
+        std::stringstream &ss = intermediate_matrices_sstream_vector_[iter];
+        if (log_precision_ > 0)
+            ss.precision(log_precision_);
+        ss << "========== Step " << iter + 1 << " =========="
+           << "\nLogModelGrad=\n" << G << "\n\nKernel=\n" << K << "\n\nKernelGrad=\n" << Kg << "\n\nCoordMat=\n" << X
+           << "\n\n";
     }
 
     void ConfigureDevice()
@@ -281,9 +395,7 @@ protected:
                     Kg(j * d + k, i) = -2.0 * Md[(size_t)k] * kv;
             }
         Check(svgd_get_particles(ctx_.get(), X.data()));
-        intermediate_matrices_sstream_vector_[iter] << "========== Step " << iter + 1 << " =========="
-                                                    << "\nLogModelGrad=\n" << G << "\n\nKernel=\n" << K
-                                                    << "\n\nKernelGrad=\n" << Kg << "\n\nCoordMat=\n" << X << "\n\n";
+        LogMatrices(iter, G, K, Kg, X);
     }
 
     /** SVGD.hpp:460-476 */
@@ -310,6 +422,7 @@ protected:
     bool check_bounds_ = false;
     bool log_intermediate_matrices_ = false;
     bool initialized_ = false;
+    int log_precision_ = 0;
     std::vector<double> lower_, upper_;
     std::shared_ptr<Kernel> kernel_ptr_;
     std::shared_ptr<GaussianRBFKernel> rbf_ptr_;

@@ -167,6 +167,12 @@ int svgd_sync(svgd_ctx *ctx);
 
 /* Scale a and median of the last step (host copies). */
 int svgd_last_scale(const svgd_ctx *ctx, double *a_out, double *med_out, int *median_path);
+/* The two upper-list order statistics (squared distances) the last median
+ * averaged, and their ranks among the n(n-1)/2 upper-triangle distances
+ * (svgd_plan_median_ranks; rank -1 = a diagonal zero, value 0).  For
+ * size-independent rank checks of the selection at full size. */
+int svgd_last_median_keys(svgd_ctx *ctx, double *sq_lo, double *sq_hi, int64_t *rank_lo,
+                          int64_t *rank_hi);
 /* Enable HIP-event timing of the phi kernel and the median phase on the
  * context stream; get returns accumulated milliseconds and launch count. */
 int svgd_set_timing(svgd_ctx *ctx, int enable);

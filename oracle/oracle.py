@@ -57,6 +57,9 @@ def lib():
         l.or_median_rows_work.argtypes = [_D, ctypes.c_int, _L, _L, _L]
         l.or_median_rows_work.restype = ctypes.c_double
         l.or_num_threads.restype = ctypes.c_int
+        l.or_set_threads.argtypes = [ctypes.c_int]
+        l.or_upper_sqdist_counts.argtypes = [_D, ctypes.c_int, _L, _D, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_longlong)]
         l.or_neg_hess_sum_gmm.argtypes = [_D, ctypes.c_int, _L, ctypes.c_int, _D, _D, _D]
         l.or_phi_matrix_rows.argtypes = [_D, _D, ctypes.c_int, _L, _D, _L, _L, _D]
         _lib = l
@@ -102,6 +105,15 @@ def median_scale(X: np.ndarray):
 def upper_sqdist_kth(X: np.ndarray, k: int) -> float:
     n, d = X.shape
     return lib().or_upper_sqdist_kth(_p(np.ascontiguousarray(X)), d, n, k)
+
+
+def upper_sqdist_counts(X: np.ndarray, thresholds):
+    """For each threshold t: #pairs i<j with direct-form D^2 < t (one streamed pass)."""
+    n, d = X.shape
+    t = np.ascontiguousarray(thresholds, dtype=np.float64)
+    out = (ctypes.c_longlong * len(t))()
+    lib().or_upper_sqdist_counts(_p(np.ascontiguousarray(X)), d, n, _p(t), len(t), out)
+    return [int(v) for v in out]
 
 
 def phi(X, G, a, rows=None, materialise=False):
@@ -223,6 +235,10 @@ def phi_matrix(X, G, M, rows=None):
 
 def num_threads() -> int:
     return lib().or_num_threads()
+
+
+def set_threads(n: int) -> None:
+    lib().or_set_threads(int(n))
 
 
 def run_svgd(X0, grad_fn, steps, optimizer, scale="median", lower=None, upper=None):

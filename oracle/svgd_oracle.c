@@ -174,6 +174,54 @@ double or_upper_sqdist_kth(const double *X, int d, long n, long k)
     return r;
 }
 
+/* Rank check of a selected order statistic at sizes where the n(n-1)/2
+ * distances cannot be stored: for each of nt (<= 8) thresholds t[q], the
+ * number of upper-triangle (i<j) pairs whose DIRECT-form squared distance is
+ * < t[q] (one streamed pass, OpenMP over rows, 64-bit counts).  s is the k-th
+ * smallest iff count(< s) <= k < count(<= s); tests pass s*(1 -+ eps) to
+ * absorb the last bits in which the device's centred Gram form differs. */
+__attribute__((optimize("O3"))) void or_upper_sqdist_counts(const double *X, int d, long n, const double *t, int nt,
+                            long long *out)
+{
+    long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (nt > 8) nt = 8;
+    /* dimension-major copy: the j loop below is a plain vectorisable stream */
+    double *Xt = (double *)malloc(sizeof(double) * (size_t)n * (size_t)d);
+    for (long i = 0; i < n; ++i)
+        for (int c = 0; c < d; ++c) Xt[(size_t)c * n + i] = X[(size_t)i * d + c];
+    enum { JB = 512 };
+#pragma omp parallel
+    {
+        long long loc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        double sb[JB];
+#pragma omp for schedule(dynamic, 16)
+        for (long i = 0; i < n; ++i) {
+            for (long j0 = i + 1; j0 < n; j0 += JB) {
+                const long m = (n - j0) < JB ? (n - j0) : JB;
+                for (long q = 0; q < m; ++q) sb[q] = 0.0;
+                for (int c = 0; c < d; ++c) {
+                    const double xi = Xt[(size_t)c * n + i];
+                    const double *xc = Xt + (size_t)c * n + j0;
+                    for (long q = 0; q < m; ++q) {
+                        const double u = xi - xc[q];
+                        sb[q] += u * u;
+                    }
+                }
+                for (int k = 0; k < nt; ++k) {
+                    long long cnt = 0;
+                    const double tk = t[k];
+                    for (long q = 0; q < m; ++q) cnt += sb[q] < tk;
+                    loc[k] += cnt;
+                }
+            }
+        }
+#pragma omp critical
+        for (int k = 0; k < nt; ++k) acc[k] += loc[k];
+    }
+    free(Xt);
+    for (int k = 0; k < nt; ++k) out[k] = acc[k];
+}
+
 /* The median work of rows [i0, i1) alone, for timing a bounded sample of a
  * large step (bench.py cpu_baseline): each row's share of the n(n-1)/2
  * distinct pairs (partners i+1 .. i+floor(n/2), cyclic), Gram-form distances
@@ -454,5 +502,15 @@ int or_num_threads(void)
     return omp_get_max_threads();
 #else
     return 1;
+#endif
+}
+
+/* thread count of the OpenMP loops (the cpu_baseline's 1-thread run) */
+void or_set_threads(int n)
+{
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
 #endif
 }

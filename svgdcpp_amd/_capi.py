@@ -64,6 +64,7 @@ SIGNATURES = {
     "svgd_host_buffers": (ctypes.c_int, [_P, ctypes.POINTER(_D), ctypes.POINTER(_D)]),
     "svgd_sync": (ctypes.c_int, [_P]),
     "svgd_last_scale": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(ctypes.c_int)]),
+    "svgd_last_median_keys": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "svgd_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "svgd_get_timing": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(_I64)]),
     "svgd_set_median_tuning": (ctypes.c_int, [_P, _I64, _I64, _I64]),

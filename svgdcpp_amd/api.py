@@ -225,17 +225,83 @@ def _gaussian_components(m):
 # ----------------------------------------------------------------- kernels --
 
 class Kernel:
-    """Kernel base (Kernel.hpp:19-420).  Only the Gaussian RBF kernel has a
-    device implementation; a plain Kernel cannot drive SVGD here."""
+    """Kernel base (Kernel.hpp:19-420).
+
+    The Gaussian RBF kernel runs fused on the device.  Any other kernel -- a
+    closed form set with UpdateKernel(f, grad_f), a composition k1 + k2,
+    k1 - k2, k1 * k2, k1 / k2 (Kernel.hpp:55-223, parameters concatenated), or
+    a subclass overriding EvaluateKernel / EvaluateKernelGrad (:279-297) --
+    drives SVGD's generic host path (SVGD.Run).  f and grad_f take
+    (x, params, location) like the reference's KernelFun (:391-399); there is
+    no tape engine, so the gradient is given in closed form."""
 
     def __init__(self, dim: int = -1):
         self.dimension_ = int(dim)
+        self.location_ = np.zeros(max(0, self.dimension_))
+        self.kernel_parameters_ = []
+        self._fun = None
+        self._grad = None
 
     def Initialize(self):
         pass
 
     def Step(self):
         pass
+
+    def UpdateKernel(self, kernel_fun, kernel_grad_fun):
+        self._fun, self._grad = kernel_fun, kernel_grad_fun
+
+    def UpdateParameters(self, params):
+        self.kernel_parameters_ = [np.asarray(p, dtype=np.float64) for p in params]
+
+    def GetParameters(self):
+        return list(self.kernel_parameters_)
+
+    def UpdateLocation(self, x):
+        x = np.asarray(x, dtype=np.float64).reshape(-1)
+        if x.shape[0] != self.dimension_:
+            raise DimensionMismatchException(
+                f"Dimension mismatch between provided location and kernel dimension "
+                f"({x.shape[0]} vs. {self.dimension_}).")
+        self.location_ = x
+
+    def EvaluateKernel(self, x):
+        if self._fun is None:
+            raise UnsetException("Kernel function is unset.")
+        return float(self._fun(np.asarray(x, dtype=np.float64), self.kernel_parameters_, self.location_))
+
+    def EvaluateKernelGrad(self, x):
+        if self._grad is None:
+            raise UnsetException("Kernel function is unset.")
+        return np.asarray(self._grad(np.asarray(x, dtype=np.float64), self.kernel_parameters_, self.location_),
+                          dtype=np.float64)
+
+    def _compose(self, other, f, g):
+        if self.dimension_ != other.dimension_:
+            raise DimensionMismatchException("Only kernels with the same variable dimensions can be added.")
+        if None in (self._fun, self._grad, other._fun, other._grad):
+            raise UnsetException("One of the kernel functions is unset; functional composition requires both "
+                                 "kernel functions to be set.")
+        n1 = len(self.kernel_parameters_)
+        f1, g1, f2, g2 = self._fun, self._grad, other._fun, other._grad
+        out = Kernel(self.dimension_)
+        out.kernel_parameters_ = list(self.kernel_parameters_) + list(other.kernel_parameters_)
+        out._fun = lambda x, p, loc: f(f1(x, p[:n1], loc), f2(x, p[n1:], loc))
+        out._grad = lambda x, p, loc: g(f1(x, p[:n1], loc), np.asarray(g1(x, p[:n1], loc)),
+                                        f2(x, p[n1:], loc), np.asarray(g2(x, p[n1:], loc)))
+        return out
+
+    def __add__(self, other):  # Kernel.hpp:55-88
+        return self._compose(other, lambda a, b: a + b, lambda a, ga, b, gb: ga + gb)
+
+    def __sub__(self, other):  # Kernel.hpp:96-129
+        return self._compose(other, lambda a, b: a - b, lambda a, ga, b, gb: ga - gb)
+
+    def __mul__(self, other):  # Kernel.hpp:137-170 (product rule)
+        return self._compose(other, lambda a, b: a * b, lambda a, ga, b, gb: b * ga + a * gb)
+
+    def __truediv__(self, other):  # Kernel.hpp:178-223 (quotient rule)
+        return self._compose(other, lambda a, b: a / b, lambda a, ga, b, gb: (b * ga - a * gb) / (b * b))
 
 
 class GaussianRBFKernel(Kernel):
@@ -266,6 +332,21 @@ class GaussianRBFKernel(Kernel):
         self.scale_ = float(scale)
         self.scale_matrix_ = None  # full M for ScaleMethod.Constant
 
+    def scale_matrix(self):
+        """M of k(x, x') = exp(-(x-x')^T M (x-x'))."""
+        if self.scale_matrix_ is not None:
+            return self.scale_matrix_
+        return self.scale_ * np.eye(self.dimension_)
+
+    def EvaluateKernel(self, x):  # GaussianRBFKernel.hpp:75-81
+        diff = np.asarray(x, dtype=np.float64) - self.location_
+        return float(np.exp(-diff @ self.scale_matrix() @ diff))
+
+    def EvaluateKernelGrad(self, x):
+        diff = np.asarray(x, dtype=np.float64) - self.location_
+        M = self.scale_matrix()
+        return -2.0 * (M @ diff) * np.exp(-diff @ M @ diff)
+
     def UpdateParameters(self, params):
         M = np.asarray(params[0], dtype=np.float64)
         if M.ndim == 0:
@@ -290,9 +371,18 @@ class Optimizer:
     def __init__(self, lr, epsilon=1.0e-8):
         self.learning_rate_ = float(lr)
         self.stabilizer_ = float(epsilon)
+        self.counter_ = 0
+        self.m_ = self.v_ = None
 
     def Initialize(self):
-        pass
+        """Optimizer.hpp:35: zero the state (the device path keeps its own copy)."""
+        self.counter_ = 0
+        self.m_ = self.v_ = None
+
+    def Step(self, grad):
+        """Optimizer.hpp:42: the increment for grad (d, n) -- used on the
+        generic-kernel host path; the device path runs the same update fused."""
+        raise NotImplementedError
 
 
 class Adam(Optimizer):
@@ -310,6 +400,17 @@ class Adam(Optimizer):
     def params(self):
         return (self.learning_rate_, self.decay_rate_1_, self.decay_rate_2_, self.stabilizer_)
 
+    def Step(self, g):  # Adam.hpp:75-96
+        g = np.asarray(g, dtype=np.float64)
+        if self.m_ is None:
+            self.m_, self.v_ = np.zeros_like(g), np.zeros_like(g)
+        b1, b2 = self.decay_rate_1_, self.decay_rate_2_
+        self.m_ = b1 * self.m_ + (1 - b1) * g
+        self.v_ = b2 * self.v_ + (1 - b2) * (g * g)
+        self.counter_ += 1
+        c1, c2 = 1.0 - b1 ** self.counter_, 1.0 - b2 ** self.counter_
+        return (self.learning_rate_ * (1.0 / (self.stabilizer_ + np.sqrt(self.v_ / c2)))) * (self.m_ / c1)
+
 
 class AdaGrad(Optimizer):
     """AdaGrad.hpp:22-76."""
@@ -322,6 +423,13 @@ class AdaGrad(Optimizer):
 
     def params(self):
         return (self.learning_rate_, 0.0, 0.0, self.stabilizer_)
+
+    def Step(self, g):  # AdaGrad.hpp:60-65
+        g = np.asarray(g, dtype=np.float64)
+        if self.v_ is None:
+            self.v_ = np.zeros_like(g)
+        self.v_ = self.v_ + g * g
+        return self.learning_rate_ * g / (self.stabilizer_ + np.sqrt(self.v_))
 
 
 class RMSProp(Optimizer):
@@ -339,6 +447,14 @@ class RMSProp(Optimizer):
     def params(self):
         return (self.learning_rate_, self.decay_rate_, 0.0, self.stabilizer_)
 
+    def Step(self, g):  # RMSProp.hpp:69-74
+        g = np.asarray(g, dtype=np.float64)
+        if self.v_ is None:
+            self.v_ = np.zeros_like(g)
+        b = self.decay_rate_
+        self.v_ = b * self.v_ + (1 - b) * (g * g)
+        return self.learning_rate_ * g / (self.stabilizer_ + np.sqrt(self.v_))
+
 
 # --------------------------------------------------------------- the driver --
 
@@ -355,6 +471,7 @@ class SVGDOptions:
         self.LowerBound = np.array([-np.inf])
         self.UpperBound = np.array([np.inf])
         self.IntermediateMatricesOutputPath = "log.txt"
+        self.IntermediateMatricesPrecision = 0  # extension: digits of the log (0 = 6, the reference's)
         self.Parallel = False
         self.LogIntermediateMatrices = False
         self.Device = 0
@@ -367,7 +484,7 @@ class Context:
         self.lib = C.lib()
         h = ctypes.c_void_p()
         dt = C.SVGD_F64 if dtype is None else int(dtype)
-        if world == 1:
+        if world == 1 and unique_id is None:
             rc = self.lib.svgd_create(ctypes.byref(h), int(dim), int(n), dt, int(device))
         else:
             rc = self.lib.svgd_create_dist(ctypes.byref(h), int(dim), int(n), dt,
@@ -452,6 +569,19 @@ class Context:
         self.check(self.lib.svgd_last_scale(self.h, ctypes.byref(a), ctypes.byref(m), ctypes.byref(p)))
         return a.value, m.value, p.value
 
+    def last_median_keys(self):
+        """(sq_lo, sq_hi, rank_lo, rank_hi): the upper-list order statistics
+        (squared distances) the last median averaged, and their ranks."""
+        a, b = ctypes.c_double(), ctypes.c_double()
+        r0, r1 = ctypes.c_int64(), ctypes.c_int64()
+        self.check(self.lib.svgd_last_median_keys(self.h, ctypes.byref(a), ctypes.byref(b),
+                                                  ctypes.byref(r0), ctypes.byref(r1)))
+        return a.value, b.value, r0.value, r1.value
+
+    def set_median_tuning(self, direct_max_pairs=-1, sample_size=-1, candidate_capacity=-1):
+        self.check(self.lib.svgd_set_median_tuning(self.h, int(direct_max_pairs), int(sample_size),
+                                                   int(candidate_capacity)))
+
     def step_with_model(self, model, hessian=False):
         """One SVGD::Step with host gradients from `model` (overlapped with the
         device median via begin/finish).  hessian=True: the Hessian kernel
@@ -504,9 +634,14 @@ class Context:
 class SVGD:
     """SVGD.hpp:84-511 on the MI355X path.
 
-    Parallel=True is accepted for API compatibility; the device path is
-    always parallel.  LogIntermediateMatrices is not supported on the device
-    path (it needs the N x N matrices the fused kernel never materialises)."""
+    A GaussianRBFKernel runs every step on the device (UsesDevicePath()).  Any
+    other kernel runs the reference's ComputePhi on the host (the generic
+    kernel path, SURVEY 8(f) 4: SVGD.hpp:407-454 with the kernel's location
+    at each x_i, then the optimizer's own Step and the clamp); the choice is
+    made by kernel type at construction.  Parallel=True is accepted for API
+    compatibility.  LogIntermediateMatrices writes the reference's text
+    format (SVGD.hpp:345-365, 460-476); on the device path K and Kg are
+    re-evaluated on the host from the step's scale (small N only)."""
 
     def __init__(self, *args, **kw):
         if len(args) == 1 and isinstance(args[0], SVGDOptions):
@@ -515,6 +650,7 @@ class SVGD:
                     o.OptimizerPtr, o.LowerBound, o.UpperBound, o.Parallel,
                     o.LogIntermediateMatrices, o.IntermediateMatricesOutputPath)
             kw.setdefault("device", o.Device)
+            kw.setdefault("log_precision", o.IntermediateMatricesPrecision)
         dim, iters, coord, kernel, model, opt = args[:6]
         rest = list(args[6:])
         if rest and isinstance(rest[0], (bool, np.bool_)) and len(rest) == 1:
@@ -548,21 +684,31 @@ class SVGD:
             raise ValueError(PREFIX + "[Argument Error] Invalid Model object pointer.")
         if opt is None:
             raise ValueError(PREFIX + "[Argument Error] Invalid Optimizer object pointer.")
-        if not isinstance(kernel, GaussianRBFKernel):
-            raise ValueError(PREFIX + "[Argument Error] The device path needs a GaussianRBFKernel.")
-        if log:
-            raise ValueError(PREFIX + "[Argument Error] LogIntermediateMatrices is not supported "
-                             "on the device path.")
         self.kernel_, self.model_, self.optimizer_ = kernel, model, opt
         self.parallel_ = bool(parallel)
-        self.ctx = Context(self.dimension_, coord.shape[1], device=kw.get("device", 0))
+        self.log_ = bool(log)
+        self.log_path_ = (args[10] if len(args) > 10 else kw.get("log_path", "log.txt"))
+        self.log_precision_ = int(kw.get("log_precision", 0))
+        self.logs_ = []
+        self.ctx = None
+        if isinstance(kernel, GaussianRBFKernel):
+            self.ctx = Context(self.dimension_, coord.shape[1], device=kw.get("device", 0))
+        elif not hasattr(opt, "Step"):
+            raise ValueError(PREFIX + "[Argument Error] Invalid Optimizer object pointer.")
+
+    def UsesDevicePath(self):
+        return self.ctx is not None
 
     def Initialize(self):
         """SVGD.hpp:268-296: model, kernel and optimizer initialisation."""
         self.model_.Initialize()
         self.kernel_.Initialize()
         self.optimizer_.Initialize()
+        self.logs_ = []
+        self._initialized = True
         c = self.ctx
+        if c is None:
+            return
         c.set_optimizer(self.optimizer_.kind, *self.optimizer_.params())
         c.set_bounds(*(self.bounds_ if self.bounds_ is not None else (None, None)))
         k = self.kernel_
@@ -582,6 +728,11 @@ class SVGD:
         caller's (d, n) matrix."""
         if not getattr(self, "_initialized", False):
             raise UnsetException("SVGD::Initialize must be called before Run.")
+        if self.ctx is None:
+            for it in range(self.num_iterations_):
+                self._host_step(it)
+            self._write_logs()
+            return
         c = self.ctx
         c.set_particles(np.ascontiguousarray(self.coord_matrix_.T))
         hess = self.kernel_.scale_method_ == GaussianRBFKernel.ScaleMethod.Hessian
@@ -600,12 +751,77 @@ class SVGD:
                 c.check(c.lib.svgd_finish_step(c.h, c.g_host_ptr))
             else:
                 c.step_with_model(self.model_, hessian=hess)
+            if self.log_:
+                self._log_device_step(len(self.logs_))
         X = c.get_particles()
         self.coord_matrix_[...] = X.T
+        self._write_logs()
+
+    # -- generic kernel: the reference's ComputePhi on the host (SVGD.hpp:373-454)
+    def _host_step(self, it):
+        X = self.coord_matrix_  # (d, n), updated in place like *coord_matrix_ptr_
+        d, n = X.shape
+        self.model_.Step()
+        self.kernel_.Step()
+        P = np.ascontiguousarray(X.T)
+        G = self.model_.log_model_grad(P)  # (n, d)
+        K = np.empty((n, n))
+        Kg = np.empty((d * n, n))
+        k = self.kernel_
+        for i in range(n):
+            k.UpdateLocation(P[i])
+            k.Initialize()
+            for j in range(n):
+                K[j, i] = k.EvaluateKernel(P[j])  # k(x_j, x_i)
+                Kg[j * d:(j + 1) * d, i] = k.EvaluateKernelGrad(P[j])
+        phi = (1.0 / n) * (G.T @ K + Kg.reshape(n, d, n).sum(axis=0))
+        X += self.optimizer_.Step(phi)
+        if self.bounds_ is not None:
+            lo, hi = self.bounds_
+            X[...] = np.maximum(np.minimum(X, hi[:, None]), lo[:, None])
+        if self.log_:
+            self._log(it, G.T, K, Kg, X)
+
+    def _log_device_step(self, it):
+        c = self.ctx
+        n = self.coord_matrix_.shape[1]
+        nr = c.row1 - c.row0
+        P, G = c.x_host[:nr].copy(), c.g_host[:nr].copy()  # X_t and grad log p(X_t) of the step
+        d = P.shape[1]
+        M = c.get_scale_matrix()
+        K = np.empty((n, n))
+        Kg = np.empty((d * n, n))
+        for i in range(n):
+            diff = P - P[i]  # x_j - x_i
+            Md = diff @ M.T
+            kv = np.exp(-np.einsum("jk,jk->j", diff, Md))
+            K[:, i] = kv
+            Kg[:, i] = (-2.0 * Md * kv[:, None]).reshape(-1)
+        self._log(it, G.T, K, Kg, c.get_particles().T)
+
+    def _log(self, it, G, K, Kg, X):
+        def fmt(A):
+            prec = self.log_precision_ or 6
+            cells = [[f"{v:.{prec}g}" for v in row] for row in np.atleast_2d(A)]
+            w = max(len(c) for row in cells for c in row)
+            return "\n".join(" ".join(c.rjust(w) for c in row) for row in cells)
+        self.logs_.append(f"========== Step {it + 1} ==========\nLogModelGrad=\n{fmt(G)}\n\nKernel=\n{fmt(K)}"
+                          f"\n\nKernelGrad=\n{fmt(Kg)}\n\nCoordMat=\n{fmt(X)}\n\n")
+
+    def _write_logs(self):
+        if not self.log_:
+            return
+        try:
+            with open(self.log_path_, "w") as f:
+                f.write("".join(self.logs_))
+        except OSError:
+            raise RuntimeError(PREFIX + f"[Runtime Error] Cannot open {self.log_path_} for writing.")
 
     def UpdateKernelParameters(self, params):  # SVGD.hpp:304-320
         self.kernel_.UpdateParameters(params)
-        self.Initialize()
+        self.kernel_.Initialize()
+        if self.ctx is not None:
+            self.Initialize()
 
     def UpdateModelParameters(self, params):  # SVGD.hpp:328-332
         self.model_.UpdateParameters(params)

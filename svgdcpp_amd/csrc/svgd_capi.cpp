@@ -74,12 +74,6 @@ struct svgd_ctx {
     double *rec = nullptr;  // np x RS particle records
     double *part = nullptr; // S x ldp x (d+1) phi partials
     float *xf = nullptr;    // np x med_f32_stride(d) fp32 median records
-    // symmetric phi pass (k_phi_sym): pair tiles of sym_block(d) particles
-    bool sym = false;
-    int64_t snb = 0, st0 = 0, st1 = 0; // blocks, this rank's tile range
-    int sgrid = 0, srslots = 0;
-    double *srec = nullptr, *colpart = nullptr, *rowpart = nullptr, *Ssum = nullptr;
-    int64_t *wgI = nullptr;
     unsigned long long *nmax = nullptr; // max |xc|^2 (double bits)
     int S = 1;
     int R = 2; // rows per lane of k_phi_rows
@@ -112,7 +106,7 @@ struct svgd_ctx {
     int64_t nregions = 0; // candidate regions: one per wave (row-stream) or per block (tiles)
     unsigned long long *cnt3 = nullptr;
     SelState *st = nullptr;
-    uint32_t *ghist = nullptr;
+    unsigned long long *ghist = nullptr; // [2][RADIX] radix histograms (64-bit counts)
     int64_t own_tiles = 0, tile0 = 0; // this rank's range of the median tile plan
     int pblock = 64;                  // median tile block (SVGD_PAIR_BLOCK)
     int64_t pnb = 0;                  // median row blocks
@@ -128,7 +122,6 @@ struct svgd_ctx {
     // pinned host
     double *h_x = nullptr, *h_g = nullptr;
     unsigned long long *h_cnt = nullptr;
-    SelState *h_st = nullptr;
     double *h_scal = nullptr;
     hipEvent_t ev_x = nullptr, ev_cnt = nullptr, ev_scal = nullptr;
     // host<->device copies of the X / G shards run on their own stream so
@@ -239,7 +232,7 @@ int64_t upper_pairs(int64_t n) { return n * (n - 1) / 2; }
 
 int allgather_rows(svgd_ctx *c, double *buf)
 {
-    if (c->world == 1) return SVGD_OK;
+    if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
     const size_t cnt = (size_t)c->chunk * c->dim;
     if (c->hcomm) {
         if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(double),
@@ -252,36 +245,29 @@ int allgather_rows(svgd_ctx *c, double *buf)
     return SVGD_OK;
 }
 
-int allreduce_u32(svgd_ctx *c, uint32_t *buf, size_t cnt)
+int allreduce_u64(svgd_ctx *c, unsigned long long *buf, size_t cnt)
 {
-    if (c->world == 1) return SVGD_OK;
+    if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
     if (c->hcomm) {
-        if (hostcomm_allreduce_u32(c->hcomm, buf, cnt, c->stream))
+        if (hostcomm_allreduce_u64(c->hcomm, buf, cnt, c->stream))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
         return SVGD_OK;
     }
-    NCCLCHK(c, ncclAllReduce(buf, buf, cnt, ncclUint32, ncclSum, c->comm, c->stream));
+    NCCLCHK(c, ncclAllReduce(buf, buf, cnt, ncclUint64, ncclSum, c->comm, c->stream));
     return SVGD_OK;
 }
 
 int allreduce_cnt3(svgd_ctx *c)
 {
-    if (c->world == 1) return SVGD_OK;
-    // below, candidate and overflowed-region totals are sums; [3..4] (the
-    // bracket) is identical on every rank and stays local
-    if (c->hcomm) {
-        if (hostcomm_allreduce_u64(c->hcomm, c->cnt3, 3 + NBK, c->stream))
-            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
-        return SVGD_OK;
-    }
-    NCCLCHK(c, ncclAllReduce(c->cnt3, c->cnt3, 3 + NBK, ncclUint64, ncclSum, c->comm, c->stream));
-    return SVGD_OK;
+    // below, candidate and overflowed-region totals and the bucket counts are
+    // sums; the bracket (CNT_LO, CNT_HI) is identical on every rank and stays local
+    return allreduce_u64(c, c->cnt3, 3 + NBK);
 }
 
 // In-place all-gather of `cnt` u64 per rank (rank r's part at buf + r * cnt).
 int allgather_u64(svgd_ctx *c, uint64_t *buf, size_t cnt)
 {
-    if (c->world == 1) return SVGD_OK;
+    if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
     if (c->hcomm) {
         if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(uint64_t),
                                c->stream))
@@ -297,7 +283,7 @@ bool matrix_scale(const svgd_ctx *c);
 
 int allreduce_f64(svgd_ctx *c, double *buf, size_t cnt)
 {
-    if (c->world == 1) return SVGD_OK;
+    if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
     if (c->hcomm) {
         if (hostcomm_allreduce_f64(c->hcomm, buf, cnt, c->stream))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
@@ -337,8 +323,7 @@ int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, 
     s.lo_key = lo_key;
     s.hi_key = hi_key;
     s.binv = (double)NBK / (double)(hi_key - lo_key);
-    *c->h_st = s;
-    HIPCHK(c, hipMemcpyAsync(c->st, c->h_st, sizeof(SelState), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_set_state(s, c->st, c->stream));
     return SVGD_OK;
 }
 
@@ -414,13 +399,17 @@ int median_begin(svgd_ctx *c)
         // the two bracket passes cost ~S; measured optimum near M / 256 pairs
         // (cfg2, M = 1.3e8: 2^19 -> median 0.222 vs 0.262 ms at 2^22), capped
         // at 2^22 (cfg3, M = 2.1e9)
-        int64_t S = c->sample_size > 0
-                        ? std::min<int64_t>(c->sample_size, M)
-                        : std::min<int64_t>(std::max<int64_t>(M / 256, int64_t(1) << 18), int64_t(1) << 22);
-        S = std::min<int64_t>(S, M);
         // tile path: whole random 64 x 64 tiles (MFMA Gram, ~1/1000 of the
-        // collect pass) instead of scattered pairs (2 random 8d-byte rows each)
-        const bool tile_sample = !c->rowpath && n / TB >= 2 && S >= TB * TB;
+        // collect pass) instead of scattered pairs (2 random 8d-byte rows each).
+        // Its keys come in correlated 4096-key tiles, so it keeps 2^22 (1024
+        // tiles) whatever M: the bracket's sigma assumes many independent draws.
+        const bool tile_path = !c->rowpath && n / TB >= 2;
+        int64_t S = c->sample_size > 0 ? c->sample_size
+                    : tile_path       ? int64_t(1) << 22
+                                      : std::min<int64_t>(std::max<int64_t>(M / 256, int64_t(1) << 18),
+                                                          int64_t(1) << 22);
+        S = std::min<int64_t>(S, M);
+        const bool tile_sample = tile_path && S >= TB * TB;
         if (tile_sample) S = S / (TB * TB) * (TB * TB);
         if (c->sample_alloc < S) {
             CHK(dalloc(c, &c->sample_keys, S));
@@ -432,7 +421,7 @@ int median_begin(svgd_ctx *c)
         // sharded (P > 1, scattered pairs): rank r draws pairs [S r/P, S (r+1)/P)
         // of the one counter-based sequence and the bracket's histograms are
         // all-reduced -- the same sample, hence the same bracket, as on one rank
-        c->samp_shard = !tile_sample && c->world > 1 && c->shard_sample;
+        c->samp_shard = !tile_sample && (c->comm || c->hcomm) && c->shard_sample;
         const int64_t g0 = c->samp_shard ? S * c->rank / c->world : 0;
         c->samp_local = c->samp_shard ? S * (c->rank + 1) / c->world - g0 : S;
         if (!tile_sample)
@@ -477,7 +466,7 @@ int sample_bracket(svgd_ctx *c, double sigma)
     for (int p = 0; p < 2; ++p) {
         HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, c->samp_local, 0, c->st, c->gpart,
                                       c->ghist, c->stream));
-        if (c->samp_shard) CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
+        if (c->samp_shard) CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
         HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
     }
     HIPCHK(c, launch_bracket(c->st, c->stream));
@@ -581,7 +570,7 @@ int median_finish(svgd_ctx *c)
         for (int p = 0; p < passes; ++p) {
             const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 2048));
             HIPCHK(c, pair_pass(c, 1, grid, nullptr, 0, nullptr));
-            CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
+            CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
             HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
         }
     } else if (passes > 0) {
@@ -589,19 +578,19 @@ int median_finish(svgd_ctx *c)
         // bucket(s) are kept (compacted) for the remaining digits
         HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->nregions, c->reg_cap, 0, c->st,
                                       c->gpart, c->ghist, c->stream));
-        CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
+        CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
         HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
         if (passes > 1) {
             HIPCHK(c, launch_compact(c->regions, c->counts, c->nregions, c->reg_cap, c->st, c->cbuf,
                                      c->ccount, c->stream));
-            if (c->world == 1) {
+            if (!c->comm && !c->hcomm) {
                 // remaining digits in one work-group, no launches in between
                 HIPCHK(c, launch_select_tail(c->st, c->cbuf, c->ccount, passes - 1, c->stream));
             } else {
                 for (int p = 1; p < passes; ++p) {
                     HIPCHK(c, launch_hist_count(c->cbuf, c->ccount, c->regions_alloc, c->st,
                                                 c->gpart, c->ghist, c->stream));
-                    CHK(allreduce_u32(c, c->ghist, 2 * RADIX));
+                    CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
                     HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
                 }
             }
@@ -652,49 +641,6 @@ int upload_g(svgd_ctx *c, const double *G_shard)
     return upload_g_finish(c);
 }
 
-int run_phi_sym(svgd_ctx *c, bool mat)
-{
-    const int d = c->dim;
-    if (mat) {
-        const double factor = c->scale_method == SVGD_SCALE_HESSIAN
-                                  ? 1.0 / (2.0 * (double)d * (double)c->n)
-                                  : 1.0;
-        HIPCHK(c, launch_scale_chol(c->sc_src, factor, d, c->sc_M, c->sc_L, c->scal, c->sc_err,
-                                    c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->h_err, c->sc_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
-    }
-    HIPCHK(c, launch_prep_srec(c->xc, c->G, c->nrm, c->scal, mat ? c->sc_M : nullptr,
-                               mat ? c->sc_L : nullptr, c->n, c->snb * sym_block(d), d, c->KP, c->srec,
-                               c->wv, c->stream));
-    EvPair ev{};
-    if (c->timing) {
-        ev = take_pair(c);
-        HIPCHK(c, hipEventRecord(ev.a, c->stream));
-    }
-    HIPCHK(c, launch_phi_sym(d, c->sgrid, c->srec, c->scal, c->snb, c->st0, c->st1, c->srslots,
-                             c->colpart, c->rowpart, c->wgI, c->stream));
-    if (c->timing) {
-        HIPCHK(c, hipEventRecord(ev.b, c->stream));
-        c->ev_phi.push_back(ev);
-    }
-    HIPCHK(c, launch_sym_reduce(c->colpart, c->rowpart, c->wgI, c->n, d, c->snb, c->st0, c->st1,
-                                c->sgrid, c->srslots, c->Ssum, c->stream));
-    if (c->world > 1) {
-        // every rank's tiles touch every particle: sum S over ranks onto the row owners
-        const size_t cnt = (size_t)c->chunk * (d + 1);
-        if (c->hcomm) {
-            if (hostcomm_allreduce_f64(c->hcomm, c->Ssum, cnt * c->world, c->stream))
-                return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
-        } else {
-            NCCLCHK(c, ncclReduceScatter(c->Ssum, c->Ssum + (size_t)c->rank * cnt, cnt, ncclDouble,
-                                         ncclSum, c->comm, c->stream));
-        }
-    }
-    HIPCHK(c, launch_sym_finish(c->Ssum, c->srec, c->scal, mat ? c->wv : nullptr, c->row0, c->nrows,
-                                d, 1.0 / (double)c->n, c->phi, c->stream));
-    return SVGD_OK;
-}
-
 bool matrix_scale(const svgd_ctx *c)
 {
     return c->scale_method == SVGD_SCALE_MATRIX || c->scale_method == SVGD_SCALE_HESSIAN;
@@ -703,7 +649,6 @@ bool matrix_scale(const svgd_ctx *c)
 int run_phi(svgd_ctx *c)
 {
     const bool mat = matrix_scale(c);
-    if (c->sym) return run_phi_sym(c, mat);
     if (mat) {
         // M = factor * src, L = chol(M), a_eff = 1 (GaussianRBFKernel.hpp:189-210)
         const double factor = c->scale_method == SVGD_SCALE_HESSIAN
@@ -797,10 +742,10 @@ int scale_finish(svgd_ctx *c)
         return SVGD_OK;
     }
     if (c->scale_method == SVGD_SCALE_FIXED) {
+        HIPCHK(c, launch_set_scal(c->fixed_a, NAN, c->scal, c->stream));
+        HIPCHK(c, hipEventSynchronize(c->ev_scal)); // no D2H into h_scal pending
         c->h_scal[0] = c->fixed_a;
         c->h_scal[1] = NAN;
-        HIPCHK(c, hipMemcpyAsync(c->scal, c->h_scal, sizeof(double), hipMemcpyHostToDevice,
-                                 c->stream));
         return SVGD_OK;
     }
     CHK(median_finish(c));
@@ -881,26 +826,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
         CHK(dalloc(c, &c->nmax, 1));
         CHK(dalloc(c, &c->part, (int64_t)c->S * c->ldp * (dim + 1)));
-        // symmetric phi (each unordered pair's kernel value used for both rows)
-        c->sym = false; // opt-in until measured faster (SVGD_PHI_SYM=1)
-        if (const char *e = std::getenv("SVGD_PHI_SYM")) c->sym = std::atoi(e) != 0;
-        if (c->sym) {
-            c->snb = (n + sym_block(dim) - 1) / sym_block(dim);
-            const int64_t T = c->snb * (c->snb + 1) / 2;
-            c->st0 = T * c->rank / c->world;
-            c->st1 = T * (c->rank + 1) / c->world;
-            const int64_t items = (c->st1 - c->st0) * sym_subtiles(dim);
-            c->sgrid = (int)std::max<int64_t>(1, std::min<int64_t>(items, ncu));
-            // distinct row blocks a work group can meet: its items / (items per row block) + 2
-            const int64_t per_wg = (items + c->sgrid - 1) / c->sgrid;
-            const int64_t per_block = ((c->snb - 1) / 2 + 1) * sym_subtiles(dim);
-            c->srslots = (int)(per_wg / per_block + 2);
-            CHK(dalloc(c, &c->srec, c->snb * sym_block(dim) * SYM_REC));
-            CHK(dalloc(c, &c->colpart, std::max<int64_t>(1, items) * 64 * (dim + 1)));
-            CHK(dalloc(c, &c->rowpart, (int64_t)c->sgrid * c->srslots * sym_block(dim) * (dim + 1)));
-            CHK(dalloc(c, &c->wgI, c->sgrid));
-            CHK(dalloc(c, &c->Ssum, (int64_t)c->world * c->chunk * (dim + 1)));
-        }
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
@@ -932,7 +857,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, (CNT_LEN + 3) * sizeof(unsigned long long),
                             hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_st, sizeof(SelState), hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_scal, 2 * sizeof(double), hipHostMallocDefault));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_xready, hipEventDisableTiming));
@@ -981,13 +905,15 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
         const size_t slot = std::max<size_t>(
             std::max<size_t>(
                 std::max<size_t>((size_t)c->chunk * c->dim, (size_t)c->dim * c->dim) * sizeof(double),
-                2 * RADIX * sizeof(uint32_t)),
+                2 * RADIX * sizeof(unsigned long long)),
             std::max<size_t>((CAPG + 1) * sizeof(uint64_t), (3 + NBK) * sizeof(uint64_t)));
         if (hostcomm_create(&c->hcomm, std::getenv("SVGD_HOSTCOMM"), world, rank, slot))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host communicator setup failed.");
         return SVGD_OK;
     }
-    if (world > 1) {
+    // world == 1 with a unique id: a one-rank RCCL communicator, so every
+    // collective of the sharded step runs through RCCL on a single GPU
+    if (unique_id128) {
         ncclUniqueId id;
         std::memcpy(&id, unique_id128, sizeof(id));
         NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
@@ -1004,19 +930,18 @@ int svgd_destroy(svgd_ctx *c)
     if (c->hcomm) hostcomm_destroy(c->hcomm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
-                       c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
-                       c->srec,  c->colpart, c->rowpart, c->Ssum};
+                       c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc};
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
-                     c->xf,          c->nmax,    c->sc_err, c->wgI,   c->cbuf, c->ccount, c->gpart,
+                     c->xf,          c->nmax,    c->sc_err, c->cbuf, c->ccount, c->gpart,
                      c->bpart,       c->gseg};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
-    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_st, c->h_scal, c->h_err};
+    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
     for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})
@@ -1217,8 +1142,7 @@ int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
 {
     CHK(check_ready(c));
     CHK(center(c));
-    c->h_scal[0] = a;
-    HIPCHK(c, hipMemcpyAsync(c->scal, c->h_scal, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_set_scal(a, NAN, c->scal, c->stream));
     CHK(upload_g(c, G_shard));
     CHK(run_phi(c));
     if (phi_out && c->nrows > 0) {
@@ -1343,6 +1267,28 @@ int svgd_last_scale(const svgd_ctx *c, double *a_out, double *med_out, int *path
     if (a_out) *a_out = c->h_scal[0];
     if (med_out) *med_out = c->h_scal[1];
     if (path) *path = c->last_path;
+    return SVGD_OK;
+}
+
+int svgd_last_median_keys(svgd_ctx *c, double *sq_lo, double *sq_hi, int64_t *rank_lo,
+                          int64_t *rank_hi)
+{
+    if (!c) return SVGD_ERR_ARG;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    SelState s;
+    HIPCHK(c, hipMemcpy(&s, c->st, sizeof(SelState), hipMemcpyDeviceToHost));
+    int64_t rlo, rhi;
+    svgd_plan_median_ranks(c->n, &rlo, &rhi);
+    auto val = [&](int src) {
+        if (src < 0) return 0.0;
+        double v;
+        std::memcpy(&v, &s.prefix[src], sizeof(v));
+        return v;
+    };
+    if (sq_lo) *sq_lo = val(c->src_lo);
+    if (sq_hi) *sq_hi = val(c->src_hi);
+    if (rank_lo) *rank_lo = rlo;
+    if (rank_hi) *rank_hi = rhi;
     return SVGD_OK;
 }
 

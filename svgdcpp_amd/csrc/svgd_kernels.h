@@ -56,7 +56,7 @@ hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, c
 hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, const float *nrm,
                                  int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                                  int64_t cap, uint32_t *counts, unsigned long long *below,
-                                 const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                                 const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                                  double *dbg_out, hipStream_t stream);
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream);
 // Sampled median keys on the tile path: ntiles random (block, block) pairs of
@@ -75,7 +75,7 @@ hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, do
 hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
                              int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                              int64_t cap, uint32_t *counts, unsigned long long *below,
-                             const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                             const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                              double *dbg_out, hipStream_t stream);
 // xf != nullptr (d <= 16): keys from the fp32 records (a bracket estimate only).
 // Sample pairs g0 .. g0+S-1 of the counter-based sequence -> keys[0 .. S-1]
@@ -85,7 +85,7 @@ hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *
                               hipStream_t stream);
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                int64_t cap, int max_blocks, const SelState *st, uint32_t *gpart,
-                               uint32_t *ghist, hipStream_t stream);
+                               unsigned long long *ghist, hipStream_t stream);
 // gpart: HIST_PART_BLOCKS x 2 RADIX u32 scratch for per-block histograms
 constexpr int HIST_PART_BLOCKS = 256;
 hipError_t launch_compact(const uint64_t *keys, const uint32_t *counts, int64_t nreg, int64_t cap,
@@ -94,9 +94,9 @@ hipError_t launch_compact(const uint64_t *keys, const uint32_t *counts, int64_t 
 hipError_t launch_select_tail(SelState *st, const uint64_t *cbuf, const unsigned long long *ccount,
                               int passes, hipStream_t stream);
 hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *ccount, int64_t cap,
-                             const SelState *st, uint32_t *gpart, uint32_t *ghist,
+                             const SelState *st, uint32_t *gpart, unsigned long long *ghist,
                              hipStream_t stream);
-hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream);
+hipError_t launch_select_scan(SelState *st, unsigned long long *ghist, hipStream_t stream);
 // cnt = [below, candidates, overflowed regions, NBK bucket counts (zero without
 // bpart), lo_key, hi_key]: the first 3 + NBK entries are sums over ranks.
 constexpr int CNT_LO = 3 + NBK, CNT_HI = 4 + NBK, CNT_LEN = 5 + NBK;
@@ -104,6 +104,9 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
                                 int64_t nblk, int64_t cap, const SelState *st,
                                 const uint32_t *bpart, int64_t nbpart,
                                 unsigned long long *cnt, hipStream_t stream);
+// device state from kernel arguments (no host staging buffer)
+hipError_t launch_set_state(const SelState &s, SelState *st, hipStream_t stream);
+hipError_t launch_set_scal(double a, double med, double *scal, hipStream_t stream);
 // bucket select path: the selections' ranks within their buckets (other fields
 // kept) and a zeroed counter seg[0] for launch_compact_buckets
 hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
@@ -133,25 +136,6 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, double *phi,
                            hipStream_t stream);
-// symmetric phi pass (k_phi_sym): blocks of sym_block(d) particles on the pair-tile plan
-// rows per lane (register budget: 2 waves/SIMD for every d)
-constexpr int sym_rows(int d) { return d <= 4 ? 4 : (d <= 8 ? 2 : 1); }
-// particles per block (4 waves x 64 lanes x rows); 64-column sub-tiles per block
-constexpr int sym_block(int d) { return 256 * sym_rows(d); }
-constexpr int sym_subtiles(int d) { return sym_block(d) / 64; }
-constexpr int SYM_REC = 34; // record stride (doubles)
-hipError_t launch_prep_srec(const double *xc, const double *G, const double *nrm, const double *a_ptr,
-                            const double *M, const double *L, int64_t n, int64_t nsr, int d, int KP,
-                            double *srec, double *wv, hipStream_t stream);
-hipError_t launch_phi_sym(int d, int grid, const double *srec, const double *a_ptr, int64_t nb,
-                          int64_t t0, int64_t t1, int rslots, double *colpart, double *rowpart,
-                          int64_t *wg_first_I, hipStream_t stream);
-hipError_t launch_sym_reduce(const double *colpart, const double *rowpart, const int64_t *wg_first_I,
-                             int64_t n, int d, int64_t nb, int64_t t0, int64_t t1, int G, int rslots,
-                             double *S, hipStream_t stream);
-hipError_t launch_sym_finish(const double *S, const double *srec, const double *a_ptr,
-                             const double *wv, int64_t row0, int64_t nrows, int d, double inv_n,
-                             double *phi, hipStream_t stream);
 // full-matrix kernel scale (wv = 2 M xc replaces 2 a xc in the phi epilogue)
 hipError_t launch_scale_chol(const double *src, double factor, int d, double *M, double *L,
                              double *scal, int *err, hipStream_t stream);
@@ -166,7 +150,7 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                             const float *xf, const unsigned long long *nmax_bits,
                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
-                            const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                            const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                             double *dbg_out, hipStream_t stream);
 int phi_rows_blocks_per_cu(int d, int R);
 // G = grad log p of the Gaussian-sum model for `rows` particle rows (d <= 64)

@@ -461,7 +461,7 @@ struct SinkCollect {
 
 struct SinkHist {
     const SelState *st;
-    uint32_t *ghist; // [2][RADIX]
+    unsigned long long *ghist; // [2][RADIX] (64-bit: a streamed pass counts up to n(n-1)/2 keys)
 };
 
 struct SinkDebug {
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     } else if (MODE == 1) {
         __syncthreads();
         for (int e = tid; e < 2 * RADIX; e += 256)
-            if (sHist[e]) atomicAdd(&sh.ghist[e], sHist[e]);
+            if (sHist[e]) atomicAdd(&sh.ghist[e], (unsigned long long)sHist[e]);
     }
 }
 
@@ -720,11 +720,12 @@ __global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict
     // SU samples per thread with their record loads in flight together
     constexpr int SU = 1; // (4 in flight measured slower: occupancy, L2-rate bound)
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g0 < S; g0 += stride * SU) {
+    // (g: this rank's sample slot; g0 + g: the index in the one global sequence)
+    for (int64_t gb = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; gb < S; gb += stride * SU) {
         float4 ra[SU][KF / 4], rb[SU][KF / 4];
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
-            const int64_t g = g0 + u * stride;
+            const int64_t g = gb + u * stride;
             const uint64_t h = mix64((uint64_t)(g0 + (g < S ? g : 0)) * 2 + 1);
             const int64_t i = mulhi_index((uint32_t)(h >> 32), n);
             int64_t j = i + 1 + mulhi_index((uint32_t)h, n - 1);
@@ -739,7 +740,7 @@ __global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict
         }
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
-            const int64_t g = g0 + u * stride;
+            const int64_t g = gb + u * stride;
             if (g >= S) break;
             const float *a = reinterpret_cast<const float *>(ra[u]);
             const float *b = reinterpret_cast<const float *>(rb[u]);
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(256) void k_hist_regions(const uint64_t *__restrict
 // ghist[e] = sum_b gpart[b][e] (integer sums: order-free).  A block covers 64
 // bins; its 4 waves take every 4th partial, 8 loads in flight per lane.
 __global__ __launch_bounds__(256) void k_hist_sum(const uint32_t *__restrict__ gpart, int nparts,
-                                                 uint32_t *__restrict__ ghist)
+                                                 unsigned long long *__restrict__ ghist)
 {
     __shared__ uint32_t sAcc[4][64];
     const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
@@ -826,7 +827,8 @@ __global__ __launch_bounds__(256) void k_hist_sum(const uint32_t *__restrict__ g
     }
     sAcc[g][lane] = acc;
     __syncthreads();
-    if (g == 0) ghist[e] = sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
+    if (g == 0)
+        ghist[e] = (unsigned long long)sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
 }
 
 // Keys of the regions whose resolved high bits (>= shift + width after the
@@ -993,6 +995,15 @@ __global__ __launch_bounds__(256) void k_bucket_sum(const uint32_t *__restrict__
         const unsigned long long t = sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
         if (t) atomicAdd(&out[e], t);
     }
+}
+
+// Whole select state / scale from kernel arguments (captured at launch, so the
+// host never rewrites a staging buffer that an earlier queued copy still reads)
+__global__ void k_set_state(SelState s, SelState *st) { *st = s; }
+__global__ void k_set_scal(double a, double med, double *scal)
+{
+    scal[0] = a;
+    scal[1] = med;
 }
 
 __global__ void k_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
@@ -1240,7 +1251,7 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
 // One radix-select step: for each active selection find the digit holding
 // its remaining rank, append it to the prefix, subtract the count below,
 // zero the histogram and advance to the next digit.
-__global__ __launch_bounds__(256) void k_select_scan(SelState *st, uint32_t *ghist)
+__global__ __launch_bounds__(256) void k_select_scan(SelState *st, unsigned long long *ghist)
 {
     __shared__ unsigned long long sPart[256];
     __shared__ int sDigit;
@@ -1249,7 +1260,7 @@ __global__ __launch_bounds__(256) void k_select_scan(SelState *st, uint32_t *ghi
     const int nsel = st->nsel, shift = st->shift, width = st->width;
     constexpr int PER = RADIX / 256;
     for (int s = 0; s < nsel; ++s) {
-        const uint32_t *h = ghist + s * RADIX;
+        const unsigned long long *h = ghist + s * RADIX;
         unsigned long long loc = 0;
         for (int q = 0; q < PER; ++q) loc += h[tid * PER + q];
         sPart[tid] = loc;
@@ -1834,11 +1845,6 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
 constexpr int PR = 4;     // rows per lane of the median sweep
 constexpr int PBLK = 256; // = 64 * PR: tile block of the row-stream median plan
 constexpr int CH_MED = 32; // columns per LDS chunk of the median stream
-// collect: two columns per step (2 waves/SIMD) instead of one (3 waves/SIMD)
-#ifndef SVGD_COLLECT_PAIR2
-#define SVGD_COLLECT_PAIR2 0
-#endif
-constexpr bool PAIR2 = SVGD_COLLECT_PAIR2;
 
 struct TileIt {
     int64_t t, I, J, slot;
@@ -1846,7 +1852,7 @@ struct TileIt {
 };
 
 template <int D, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !PAIR2 ? 4 : 1, 8))) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 : 1, 8))) void k_pair_rows(const double *__restrict__ xc, int kp_arg,
                                                   const double *__restrict__ nrm, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
@@ -2124,50 +2130,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !
                         column(qb, jb + jj + 1);
                         __builtin_amdgcn_sched_barrier(0);
                     }
-                } else if constexpr (MODE == 0 && !DIAG && PAIR2) {
-                    // two columns per step: twice the independent FMA chains
-                    // and one wave-uniform band test per two columns
-                    int jj = 0;
-                    for (; jj + 1 < cnt; jj += 2) {
-                        double c0[D + 1], c1[D + 1];
-                        load(c0, jj);
-                        load(c1, jj + 1);
-                        double e0[PR], e1[PR];
-#pragma unroll
-                        for (int r = 0; r < PR; ++r) {
-                            e0[r] = c0[D];
-                            e1[r] = c1[D];
-                        }
-#pragma unroll
-                        for (int k = 0; k < D; ++k)
-#pragma unroll
-                            for (int r = 0; r < PR; ++r) {
-                                e0[r] = fma(xi[r][k], c0[k], e0[r]);
-                                e1[r] = fma(xi[r][k], c1[k], e1[r]);
-                            }
-                        unsigned long long m0[PR], m1[PR];
-                        unsigned long long any = 0;
-#pragma unroll
-                        for (int r = 0; r < PR; ++r) {
-                            const unsigned long long l0 = __ballot(e0[r] > TL[r]);
-                            const unsigned long long h0 = __ballot(e0[r] > TH[r]);
-                            const unsigned long long l1 = __ballot(e1[r] > TL[r]);
-                            const unsigned long long h1 = __ballot(e1[r] > TH[r]);
-                            wbelow += (uint32_t)(__popcll(l0) + __popcll(l1));
-                            m0[r] = h0 & ~l0;
-                            m1[r] = h1 & ~l1;
-                            any |= m0[r] | m1[r];
-                        }
-                        if (any) {
-                            band(e0, m0);
-                            band(e1, m1);
-                        }
-                    }
-                    if (jj < cnt) {
-                        double cr[D + 1];
-                        load(cr, jj);
-                        column(cr, jb + jj);
-                    }
                 } else {
                     // 2 columns per iteration (one loop test per two), then the rest
                     int jj = 0;
@@ -2208,341 +2170,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 && !
     } else if (MODE == 1) {
         __syncthreads();
         for (int e = tid; e < 2 * RADIX; e += 256)
-            if (sHist[e]) atomicAdd(&sh.ghist[e], sHist[e]);
-    }
-}
-
-// ================================================= symmetric phi pass ==
-//
-// K_ij = K_ji, so each unordered pair's kernel value can feed both rows:
-//   row i:    sum_j K_ij [V_j, 1]        column j:  sum_i K_ij [V_i, 1]
-// Work is the pair-tile plan (plan.cpp) with square blocks of B = 256 R
-// particles (R = sym_rows(d) rows per lane: 4, 2 or 1 by register budget):
-// tile (I, J != I) covers all B x B unordered pairs of two blocks once, the
-// diagonal tile (I, I) is done in ordered form (row sums only).  A workgroup
-// (4 waves) holds the B rows of I in registers (R per lane) and streams J in
-// 64-column LDS sub-tiles.  Within a sub-tile each
-// 16-lane row group walks a 16-column set in 16 steps on a skewed schedule:
-// at step s lane t pairs its rows with column (t + s) mod 16 (per-lane LDS
-// read; the record stride makes these conflict-free) and the column
-// accumulators rotate one lane per step (DPP row_ror:15), so both sums stay
-// in registers -- no cross-lane reductions.  After 16 steps each lane adds
-// its column's accumulator to the wave's LDS column slot; the 4 waves' slots
-// are summed in fixed order per sub-tile into colpart.  Rows are flushed to
-// rowpart whenever the workgroup's row block changes.  k_sym_reduce then adds
-// every partial of a particle in a fixed order (deterministic), for all N
-// particles (rank-summed by a reduce-scatter when sharded).
-//
-// Per unordered pair and row: 9 (u) + 13 (exp) + 9 (row acc) + 9 (col acc);
-// per step and lane: a few LDS reads + 2(d+1) DPP moves, amortised over R rows.
-constexpr int SYM_SUB = 64;           // columns per LDS sub-tile
-constexpr int SYM_RS = 34;            // record stride (doubles): 2*34 = 4 (mod 64) dwords
-constexpr int SYM_SUB_BYTES = SYM_SUB * SYM_RS * 8; // 17 KiB
-static_assert(SYM_SUB_BYTES % 1024 == 0, "whole LDS-DMA pieces");
-
-__device__ __forceinline__ int64_t sym_cnt(int64_t nb, int64_t I)
-{
-    const int64_t H = (nb - 1) / 2;
-    return ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
-}
-
-__device__ __forceinline__ int64_t sym_base(int64_t nb, int64_t I)
-{
-    const int64_t H = (nb - 1) / 2;
-    if ((nb & 1) == 0) {
-        const int64_t half = nb / 2;
-        return I < half ? I * (H + 2) : half * (H + 2) + (I - half) * (H + 1);
-    }
-    return I * (H + 1);
-}
-
-__device__ __forceinline__ double dpp_ror15(double v)
-{
-    // old = src: every lane has a source in a full-row rotation, and tying the
-    // two lets the move happen in place (no zeroed `old` register per move)
-    const int l = __double2loint(v), h = __double2hiint(v);
-    const int lo = __builtin_amdgcn_update_dpp(l, l, 0x12F, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(h, h, 0x12F, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
-}
-
-// Work-group item range (items = (tile, sub-tile) pairs of this rank).
-__device__ __forceinline__ int64_t sym_item_begin(int64_t i0, int64_t nitems, int64_t g, int64_t G)
-{
-    return i0 + nitems * g / G;
-}
-
-// Work-group barrier that only drains LDS operations: __syncthreads() would
-// also wait for the next sub-tile's in-flight DMA (vmcnt(0)); the DMA pieces
-// this barrier publishes were already waited for with a counted vmcnt.
-__device__ __forceinline__ void lds_barrier()
-{
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void k_phi_sym(const double *__restrict__ srec,
-                                                const double *__restrict__ a_ptr, int64_t nb,
-                                                int64_t t0, int64_t t1, int rslots,
-                                                double *__restrict__ colpart,
-                                                double *__restrict__ rowpart,
-                                                int64_t *__restrict__ wg_first_I)
-{
-    constexpr int R = sym_rows(D), B = sym_block(D), NSUB = sym_subtiles(D), RSS = SYM_RS,
-                  DP = D + 1;
-    constexpr int SCOL = 4 * SYM_SUB * DP; // doubles: per-wave column slots
-    __shared__ __attribute__((aligned(16))) char smem[2 * SYM_SUB_BYTES + SCOL * 8 + 256 * 8];
-    double *sCol = reinterpret_cast<double *>(smem + 2 * SYM_SUB_BYTES);
-    double *tab = sCol + SCOL;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int g = lane >> 4, tl = lane & 15;
-    tab[tid] = EXP2_TAB256[tid];
-    for (int e = tid; e < SCOL; e += 256) sCol[e] = 0.0;
-
-    const double alpha = 512.0 * LOG2E * (*a_ptr);
-    const int64_t i0 = t0 * NSUB, nitems = (t1 - t0) * NSUB;
-    const int64_t ib = sym_item_begin(i0, nitems, blockIdx.x, gridDim.x);
-    const int64_t ie = sym_item_begin(i0, nitems, blockIdx.x + 1, gridDim.x);
-
-    double xs[R][D], ci[R], vi[R][D], acc[R][D], acc1[R];
-    int64_t curI = -1, firstI = -1;
-    auto flush_rows = [&]() {
-        double *o = rowpart + ((int64_t)blockIdx.x * rslots + (curI - firstI)) * B * DP;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int lr = w * 64 * R + r * 64 + lane;
-#pragma unroll
-            for (int k = 0; k < D; ++k) o[lr * DP + k] = acc[r][k];
-            o[lr * DP + D] = acc1[r];
-        }
-    };
-    // DMA one 64-column sub-tile of block J into LDS buffer `buf` (17 pieces
-    // of 1 KiB over the 4 waves: wave 0 issues 5, the others 4)
-    auto issue = [&](int64_t item, int buf) {
-        int64_t I, J;
-        tile_coords(nb, item / NSUB, &I, &J);
-        const int q = (int)(item % NSUB);
-        const char *src = reinterpret_cast<const char *>(srec + (J * B + q * SYM_SUB) * RSS);
-        char *dst = smem + buf * SYM_SUB_BYTES;
-        for (int p = w; p < SYM_SUB_BYTES / 1024; p += 4)
-            __builtin_amdgcn_global_load_lds((gbl_void *)(src + p * 1024 + lane * 16),
-                                             (lds_void *)(dst + p * 1024), 16, 0, 0);
-    };
-    auto wait_issue = [&]() {
-        if (w == 0)
-            wait_vmcnt<(SYM_SUB_BYTES / 1024 + 3) / 4>();
-        else
-            wait_vmcnt<(SYM_SUB_BYTES / 1024) / 4>();
-    };
-
-    if (ib < ie) issue(ib, 0);
-    for (int64_t item = ib; item < ie; ++item) {
-        const int buf = (int)((item - ib) & 1);
-        if (item + 1 < ie) {
-            issue(item + 1, buf ^ 1);
-            wait_issue();
-        } else {
-            wait_vmcnt<0>();
-        }
-        lds_barrier(); // the sub-tile is in LDS for every wave
-        int64_t I, J;
-        const int64_t t = item / NSUB;
-        tile_coords(nb, t, &I, &J);
-        if (I != curI) {
-            if (curI >= 0) flush_rows();
-            else firstI = I;
-            curI = I;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const double *ri = srec + (I * B + w * 64 * R + r * 64 + lane) * RSS;
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    xs[r][k] = alpha * ri[k];
-                    vi[r][k] = ri[D + k];
-                    acc[r][k] = 0.0;
-                }
-                ci[r] = ri[2 * D];
-                acc1[r] = 0.0;
-            }
-            wait_vmcnt<0>();
-        }
-        const double *cb = reinterpret_cast<const double *>(smem + buf * SYM_SUB_BYTES);
-        if (I == J) {
-            // diagonal block: ordered pairs, row sums only (uniform column)
-            for (int c = 0; c < SYM_SUB; ++c) {
-                const double *rj = cb + c * RSS;
-                double xj[D], vj[D];
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    xj[k] = rj[k];
-                    vj[k] = rj[D + k];
-                }
-                const double cj = rj[2 * D];
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    double u = ci[r] + cj;
-#pragma unroll
-                    for (int k = 0; k < D; ++k) u = fma(xs[r][k], xj[k], u);
-                    const double K = exp2_256(u, tab);
-#pragma unroll
-                    for (int k = 0; k < D; ++k) acc[r][k] = fma(K, vj[k], acc[r][k]);
-                    acc1[r] += K;
-                }
-            }
-        } else {
-            double *myCol = sCol + w * SYM_SUB * DP;
-            for (int ph = 0; ph < 4; ++ph) {
-                const int set = (g + ph) & 3;
-                double cacc[DP];
-#pragma unroll
-                for (int k = 0; k < DP; ++k) cacc[k] = 0.0;
-                for (int s = 0; s < 16; ++s) {
-                    const double *rj = cb + (set * 16 + ((tl + s) & 15)) * RSS; // per lane
-                    double xj[D], vj[D];
-#pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        xj[k] = rj[k];
-                        vj[k] = rj[D + k];
-                    }
-                    const double cj = rj[2 * D];
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        double u = ci[r] + cj;
-#pragma unroll
-                        for (int k = 0; k < D; ++k) u = fma(xs[r][k], xj[k], u);
-                        const double K = exp2_256(u, tab);
-#pragma unroll
-                        for (int k = 0; k < D; ++k) {
-                            acc[r][k] = fma(K, vj[k], acc[r][k]);
-                            cacc[k] = fma(K, vi[r][k], cacc[k]);
-                        }
-                        acc1[r] += K;
-                        cacc[D] += K;
-                    }
-#pragma unroll
-                    for (int k = 0; k < DP; ++k) cacc[k] = dpp_ror15(cacc[k]);
-                }
-                // after 16 rotations lane tl holds column set*16 + tl (each
-                // phase a different group of the wave meets that column).
-                // Compiler-visible LDS: any wait it adds for the next sub-tile's
-                // DMA comes a whole phase after that DMA was issued.
-                double *sc = myCol + (set * 16 + tl) * DP;
-#pragma unroll
-                for (int k = 0; k < DP; ++k) sc[k] += cacc[k];
-            }
-            lds_barrier(); // every wave's column slots for this sub-tile are final
-            double *o = colpart + (item - i0) * SYM_SUB * DP;
-            for (int e = tid; e < SYM_SUB * DP; e += 256) {
-                double v = sCol[e];
-                for (int ww = 1; ww < 4; ++ww) v += sCol[ww * SYM_SUB * DP + e];
-                o[e] = v;
-                for (int ww = 0; ww < 4; ++ww) sCol[ww * SYM_SUB * DP + e] = 0.0;
-            }
-        }
-        lds_barrier(); // buffer `buf` and the column slots are free again
-    }
-    if (curI >= 0) flush_rows();
-    if (tid == 0) wg_first_I[blockIdx.x] = firstI;
-}
-
-// Sum every partial of particle p (rows block P), in a fixed order, into
-// S[p][0..D] (= sum_j K_pj [V_j, 1] over this rank's tiles).
-__global__ void k_sym_reduce(const double *__restrict__ colpart, const double *__restrict__ rowpart,
-                             const int64_t *__restrict__ wg_first_I, int64_t n, int D, int64_t nb,
-                             int64_t t0, int64_t t1, int G, int rslots, double *__restrict__ S)
-{
-    const int DP = D + 1;
-    const int B = sym_block(D), NSUB = sym_subtiles(D);
-    const int64_t i0 = t0 * NSUB, nitems = (t1 - t0) * NSUB;
-    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n;
-         p += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t P = p / B, pl = p - P * B;
-        const int q = (int)(pl / SYM_SUB), cl = (int)(pl % SYM_SUB);
-        double s[17];
-        for (int k = 0; k < DP; ++k) s[k] = 0.0;
-        // row role: work groups whose item range meets row block P
-        const int64_t tb = max(t0, sym_base(nb, P)), te = min(t1, sym_base(nb, P) + sym_cnt(nb, P));
-        if (tb < te) {
-            const int64_t first = tb * NSUB, last = te * NSUB - 1;
-            int64_t ga = (first - i0) * G / nitems;
-            while (ga > 0 && sym_item_begin(i0, nitems, ga, G) > first) --ga;
-            while (ga + 1 < G && sym_item_begin(i0, nitems, ga + 1, G) <= first) ++ga;
-            for (int64_t gg = ga; gg < G && sym_item_begin(i0, nitems, gg, G) <= last; ++gg) {
-                if (sym_item_begin(i0, nitems, gg + 1, G) <= first) continue;
-                const double *o = rowpart + ((gg * rslots + (P - wg_first_I[gg])) * B + pl) * DP;
-                for (int k = 0; k < DP; ++k) s[k] += o[k];
-            }
-        }
-        // column role: tiles (I, P) with slot >= 1
-        for (int64_t sl = 1; sl <= (nb - 1) / 2 + 1; ++sl) {
-            const int64_t I = ((P - sl) % nb + nb) % nb;
-            if (I == P || sl >= sym_cnt(nb, I)) continue;
-            const int64_t t = sym_base(nb, I) + sl;
-            if (t < t0 || t >= t1) continue;
-            const double *o = colpart + ((t * NSUB + q - i0) * SYM_SUB + cl) * DP;
-            for (int k = 0; k < DP; ++k) s[k] += o[k];
-        }
-        for (int k = 0; k < DP; ++k) S[p * DP + k] = s[k];
-    }
-}
-
-// phi_i = (S_i[0..d) + w_i S_i[d]) / N for this rank's rows; w_i = 2a xc_i
-// (srec holds xc) or the full-matrix 2 M xc_i (wv).
-__global__ void k_sym_finish(const double *__restrict__ S, const double *__restrict__ srec,
-                             const double *__restrict__ a_ptr, const double *__restrict__ wv,
-                             int64_t row0, int64_t nrows, int d, double inv_n,
-                             double *__restrict__ phi)
-{
-    const double two_a = 2.0 * (*a_ptr);
-    const int DP = d + 1;
-    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nrows;
-         li += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = row0 + li;
-        for (int k = 0; k < d; ++k) {
-            const double wgt = wv ? wv[i * d + k] : two_a * srec[i * SYM_RS + k];
-            phi[li * d + k] = inv_n * (S[i * DP + k] + wgt * S[i * DP + d]);
-        }
-    }
-}
-
-// Symmetric-path records (stride SYM_RS): [xc | G - 2a xc | -256 a log2e |xc|^2 | 0..];
-// rows >= n get c = -2^29 so every pair with them has K = 0 (u >= -2^31 keeps
-// exp2_256's integer conversion in range).  For the full-
-// matrix scale, xc is replaced by z = L^T xc and a by 1 (wv = 2 M xc).
-__global__ void k_prep_srec(const double *__restrict__ xc, const double *__restrict__ G,
-                            const double *__restrict__ nrm, const double *__restrict__ a_ptr,
-                            const double *__restrict__ M, const double *__restrict__ L,
-                            int64_t n, int64_t nsr, int d, int KP, double *__restrict__ srec,
-                            double *__restrict__ wv)
-{
-    const double a = M ? 1.0 : *a_ptr;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nsr;
-         j += (int64_t)gridDim.x * blockDim.x) {
-        const bool live = j < n;
-        double *r = srec + j * SYM_RS;
-        double zz = 0.0;
-        for (int k = 0; k < d; ++k) {
-            double z = 0.0, mx = 0.0;
-            if (live) {
-                if (M) {
-                    for (int l = 0; l < d; ++l) {
-                        const double x = xc[j * KP + l];
-                        z = fma(L[l * d + k], x, z);
-                        mx = fma(M[k * d + l], x, mx);
-                    }
-                    wv[j * d + k] = 2.0 * mx;
-                } else {
-                    z = xc[j * KP + k];
-                    mx = a * z;
-                }
-            }
-            r[k] = z;
-            r[d + k] = live ? G[j * d + k] - 2.0 * mx : 0.0;
-            zz = fma(z, z, zz);
-        }
-        r[2 * d] = live ? -256.0 * a * LOG2E * (M ? zz : nrm[j]) : -536870912.0;
-        for (int k = 2 * d + 1; k < SYM_RS; ++k) r[k] = 0.0;
+            if (sHist[e]) atomicAdd(&sh.ghist[e], (unsigned long long)sHist[e]);
     }
 }
 
@@ -2785,7 +2413,7 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                             const float *xf, const unsigned long long *nmax_bits,
                             int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
-                            const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                            const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                             double *dbg_out, hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
@@ -2864,7 +2492,7 @@ static hipError_t launch_pair_tiles_t(int KP, int mode, int grid, const T *xc, c
                                       int64_t n, int64_t nb, int64_t t0, int64_t t1,
                                       uint64_t *regions, int64_t cap, uint32_t *counts,
                                       unsigned long long *below, const SelState *st,
-                                      uint32_t *ghist, uint32_t *bpart, double *dbg_out,
+                                      unsigned long long *ghist, uint32_t *bpart, double *dbg_out,
                                       hipStream_t stream, uint64_t *sample_out = nullptr)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
@@ -2884,7 +2512,7 @@ static hipError_t launch_pair_tiles_t(int KP, int mode, int grid, const T *xc, c
 hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const double *nrm,
                              int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                              int64_t cap, uint32_t *counts, unsigned long long *below,
-                             const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                             const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                              double *dbg_out, hipStream_t stream)
 {
     return launch_pair_tiles_t<double>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
@@ -2894,7 +2522,7 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
 hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, const float *nrm,
                                  int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                                  int64_t cap, uint32_t *counts, unsigned long long *below,
-                                 const SelState *st, uint32_t *ghist, uint32_t *bpart,
+                                 const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                                  double *dbg_out, hipStream_t stream)
 {
     return launch_pair_tiles_t<float>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
@@ -2991,7 +2619,7 @@ hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *
 
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                int64_t cap, int max_blocks, const SelState *st, uint32_t *gpart,
-                               uint32_t *ghist, hipStream_t stream)
+                               unsigned long long *ghist, hipStream_t stream)
 {
     if (nreg <= 0) return hipSuccess;
     int64_t G = HIST_BLOCKS;
@@ -3027,7 +2655,7 @@ hipError_t launch_select_tail(SelState *st, const uint64_t *cbuf, const unsigned
 }
 
 hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *ccount, int64_t cap,
-                             const SelState *st, uint32_t *gpart, uint32_t *ghist,
+                             const SelState *st, uint32_t *gpart, unsigned long long *ghist,
                              hipStream_t stream)
 {
     // one region whose count lives on the device (compacted keys; < 2^32)
@@ -3035,7 +2663,7 @@ hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *cco
                                gpart, ghist, stream);
 }
 
-hipError_t launch_select_scan(SelState *st, uint32_t *ghist, hipStream_t stream)
+hipError_t launch_select_scan(SelState *st, unsigned long long *ghist, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_select_scan, dim3(1), dim3(256), 0, stream, st, ghist);
     return hipGetLastError();
@@ -3052,6 +2680,18 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
     if (bpart && nbpart > 0)
         hipLaunchKernelGGL(k_bucket_sum, dim3(NBK / 64, BSUM_SLICES), dim3(256), 0, stream, bpart,
                            (int)nbpart, cnt + 3);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_state(const SelState &s, SelState *st, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_set_state, dim3(1), dim3(1), 0, stream, s, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_scal(double a, double med, double *scal, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_set_scal, dim3(1), dim3(1), 0, stream, a, med, scal);
     return hipGetLastError();
 }
 
@@ -3082,63 +2722,6 @@ hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, hip
 hipError_t launch_bracket(SelState *st, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_bracket, dim3(1), dim3(1), 0, stream, st);
-    return hipGetLastError();
-}
-
-#define SVGD_SYM_CASE(Dv)                                                                    \
-    case Dv:                                                                                 \
-        hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(grid), dim3(256), 0, stream, srec, a_ptr, nb, t0, t1, \
-                           rslots, colpart, rowpart, wg_first_I);                            \
-        break;
-
-hipError_t launch_phi_sym(int d, int grid, const double *srec, const double *a_ptr, int64_t nb,
-                          int64_t t0, int64_t t1, int rslots, double *colpart, double *rowpart,
-                          int64_t *wg_first_I, hipStream_t stream)
-{
-    if (t1 <= t0 || grid <= 0) return hipSuccess;
-    switch (d) {
-        SVGD_SYM_CASE(1) SVGD_SYM_CASE(2) SVGD_SYM_CASE(3) SVGD_SYM_CASE(4)
-        SVGD_SYM_CASE(5) SVGD_SYM_CASE(6) SVGD_SYM_CASE(7) SVGD_SYM_CASE(8)
-        SVGD_SYM_CASE(9) SVGD_SYM_CASE(10) SVGD_SYM_CASE(11) SVGD_SYM_CASE(12)
-        SVGD_SYM_CASE(13) SVGD_SYM_CASE(14) SVGD_SYM_CASE(15) SVGD_SYM_CASE(16)
-    default:
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-#undef SVGD_SYM_CASE
-
-hipError_t launch_sym_reduce(const double *colpart, const double *rowpart, const int64_t *wg_first_I,
-                             int64_t n, int d, int64_t nb, int64_t t0, int64_t t1, int G, int rslots,
-                             double *S, hipStream_t stream)
-{
-    int64_t g = (n + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_sym_reduce, dim3(g), dim3(256), 0, stream, colpart, rowpart, wg_first_I, n, d,
-                       nb, t0, t1, G, rslots, S);
-    return hipGetLastError();
-}
-
-hipError_t launch_sym_finish(const double *S, const double *srec, const double *a_ptr,
-                             const double *wv, int64_t row0, int64_t nrows, int d, double inv_n,
-                             double *phi, hipStream_t stream)
-{
-    if (nrows <= 0) return hipSuccess;
-    int64_t g = (nrows + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_sym_finish, dim3(g), dim3(256), 0, stream, S, srec, a_ptr, wv, row0, nrows, d,
-                       inv_n, phi);
-    return hipGetLastError();
-}
-
-hipError_t launch_prep_srec(const double *xc, const double *G, const double *nrm, const double *a_ptr,
-                            const double *M, const double *L, int64_t n, int64_t nsr, int d, int KP,
-                            double *srec, double *wv, hipStream_t stream)
-{
-    int64_t g = (nsr + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_prep_srec, dim3(g), dim3(256), 0, stream, xc, G, nrm, a_ptr, M, L, n, nsr, d,
-                       KP, srec, wv);
     return hipGetLastError();
 }
 

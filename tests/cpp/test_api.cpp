@@ -75,7 +75,7 @@ private:
 
 // One host step: phi_i = 1/N sum_j [k(x_j, x_i) grad log p(x_j) + grad_{x_j} k(x_j, x_i)],
 // x += opt.Step(phi), clamp (test_svgd.cpp:21-60).
-static Eigen::MatrixXd ManualStep(const Eigen::MatrixXd &x, Model &model, GaussianRBFKernel &kernel,
+static Eigen::MatrixXd ManualStep(const Eigen::MatrixXd &x, Model &model, Kernel &kernel,
                                   Optimizer &opt, const Eigen::VectorXd *lo, const Eigen::VectorXd *hi)
 {
     const long d = x.rows(), n = x.cols();
@@ -133,9 +133,15 @@ static void TestArgumentChecks()
         [&] { SVGD s(d, 1, x, kernel, model, opt, Eigen::VectorXd::Constant(3, -1.0), Eigen::VectorXd::Constant(2, 1.0)); }));
     CHECK(Throws<DimensionMismatchException>(
         [&] { SVGD s(d, 1, x, kernel, model, opt, Eigen::VectorXd::Constant(2, -1.0), Eigen::VectorXd::Constant(5, 1.0)); }));
-    // a non-RBF kernel has no device path
+    // a kernel with neither a function nor overrides is unset (Kernel.hpp:393-396)
     std::shared_ptr<Kernel> plain = std::make_shared<Kernel>(d);
-    CHECK(Throws<std::invalid_argument>([&] { SVGD s(d, 1, x, plain, model, opt); }));
+    CHECK(Throws<UnsetException>([&] { plain->EvaluateKernel(Eigen::Vector2d(0.0, 0.0)); }));
+    {
+        SVGD s(d, 1, x, plain, model, opt);
+        CHECK(!s.UsesDevicePath());
+        s.Initialize();
+        CHECK(Throws<UnsetException>([&] { s.Run(); }));
+    }
     // optimizer parameter checks (Adam.hpp:52-55, RMSProp.hpp:47-50)
     CHECK(Throws<std::invalid_argument>([&] { Adam a(d, n, 0.1, 1.0, 0.999); }));
     CHECK(Throws<std::invalid_argument>([&] { RMSProp r(d, n, 0.1, 1.5); }));
@@ -307,10 +313,197 @@ static void TestSVGDMatrixScales(bool hessian)
     CHECK(MaxAbsDiff(kernel->GetScaleMatrix(), host_kernel.GetScaleMatrix()) < 1e-12);
 }
 
+// exp(-|x - x'|^2) as a closed-form generic kernel (test_svgd.cpp:92-103 +
+// its gradient :155-162), and an inverse multiquadric (c^2 + |x - x'|^2)^beta
+// derived class overriding EvaluateKernel/EvaluateKernelGrad (Kernel.hpp:279-297).
+static std::shared_ptr<Kernel> UnitRBF(size_t d)
+{
+    auto k = std::make_shared<Kernel>(d);
+    k->UpdateKernel(
+        [](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &, const Eigen::VectorXd &loc) {
+            const Eigen::VectorXd diff = x - loc;
+            return std::exp(-diff.squaredNorm());
+        },
+        [](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &, const Eigen::VectorXd &loc) {
+            const Eigen::VectorXd diff = x - loc;
+            return Eigen::VectorXd(diff * (-2.0 * std::exp(-diff.squaredNorm())));
+        });
+    return k;
+}
+
+class IMQKernel : public Kernel
+{
+public:
+    IMQKernel(size_t d, double c, double beta) : Kernel(d), c_(c), beta_(beta) {}
+    std::unique_ptr<Kernel> CloneUniquePointer() const override { return std::make_unique<IMQKernel>(*this); }
+    double EvaluateKernel(const Eigen::VectorXd &x) override
+    {
+        return std::pow(c_ * c_ + (x - location_).squaredNorm(), beta_);
+    }
+    Eigen::VectorXd EvaluateKernelGrad(const Eigen::VectorXd &x) override
+    {
+        const Eigen::VectorXd diff = x - location_;
+        const double s = c_ * c_ + diff.squaredNorm();
+        return Eigen::VectorXd(diff * (2.0 * beta_ * std::pow(s, beta_ - 1.0)));
+    }
+
+private:
+    double c_, beta_;
+};
+
+// Generic kernels on the host path: the SVGD class vs the
+// manual loop of test_svgd.cpp:21-60 (15 Adam steps, bounds [-1, 1], the
+// reference's own fixed-kernel scenario :66-203), with a closed-form kernel,
+// a derived override and a composed kernel; no GPU involved.
+static void TestGenericKernelHostPath()
+{
+    const size_t d = 2, n = 10, iters = 15;
+    const Eigen::Vector2d lo(-1.0, -1.0), hi(1.0, 1.0);
+    for (int variant = 0; variant < 3; ++variant)
+    {
+        std::srand(1);
+        auto x = std::make_shared<Eigen::MatrixXd>(Eigen::MatrixXd::Random(d, n));
+        const Eigen::MatrixXd x0 = *x;
+        std::shared_ptr<Kernel> kernel, host;
+        if (variant == 0)
+        {
+            kernel = UnitRBF(d);
+            host = UnitRBF(d);
+        }
+        else if (variant == 1)
+        {
+            kernel = std::make_shared<IMQKernel>(d, 1.0, -0.5);
+            host = std::make_shared<IMQKernel>(d, 1.0, -0.5);
+        }
+        else
+        {
+            kernel = std::make_shared<Kernel>(*UnitRBF(d) * *UnitRBF(d) + *UnitRBF(d));
+            host = std::make_shared<Kernel>(*UnitRBF(d) * *UnitRBF(d) + *UnitRBF(d));
+        }
+        auto model = std::make_shared<CosineModel>();
+        auto opt = std::make_shared<Adam>(d, n, 1.0e-1, 0.9, 0.999);
+        SVGDOptions o;
+        o.Dimension = d;
+        o.NumIterations = iters;
+        o.CoordinateMatrixPtr = x;
+        o.KernelPtr = kernel;
+        o.ModelPtr = model;
+        o.OptimizerPtr = opt;
+        o.LowerBound = lo;
+        o.UpperBound = hi;
+        SVGD svgd(o);
+        CHECK(!svgd.UsesDevicePath() && svgd.Context() == nullptr);
+        svgd.Initialize();
+        svgd.Run();
+        CosineModel host_model;
+        Adam host_opt(d, n, 1.0e-1, 0.9, 0.999);
+        host_opt.Initialize();
+        Eigen::MatrixXd xm = x0;
+        for (size_t t = 0; t < iters; ++t)
+            xm = ManualStep(xm, host_model, *host, host_opt, &lo, &hi);
+        const double err = MaxAbsDiff(*x, xm);
+        std::printf("generic kernel %d (host path) vs manual loop: max |dx| = %.3e\n", variant, err);
+        CHECK(err < 1e-12);
+        CHECK(MaxAbsDiff(*x, x0) > 1e-3);
+    }
+    // composition rules vs the operands (Kernel.hpp:55-223) and a central
+    // finite difference of the composed gradient
+    Kernel a = *UnitRBF(2), b = *UnitRBF(2);
+    b.UpdateKernel(
+        [](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &p, const Eigen::VectorXd &loc) {
+            return 1.0 + p.at(0)(0, 0) * (x - loc).squaredNorm();
+        },
+        [](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &p, const Eigen::VectorXd &loc) {
+            return Eigen::VectorXd((x - loc) * (2.0 * p.at(0)(0, 0)));
+        });
+    b.UpdateParameters({Eigen::MatrixXd::Constant(1, 1, 0.7)});
+    const Eigen::Vector2d loc(0.2, -0.4), x1(0.5, 0.3);
+    Kernel ops[4] = {a + b, a - b, a * b, a / b};
+    a.UpdateLocation(loc);
+    b.UpdateLocation(loc);
+    const double ka = a.EvaluateKernel(x1), kb = b.EvaluateKernel(x1);
+    const double expect[4] = {ka + kb, ka - kb, ka * kb, ka / kb};
+    for (int q = 0; q < 4; ++q)
+    {
+        Kernel &k = ops[q];
+        CHECK(k.GetParameters().size() == 1);
+        k.UpdateLocation(loc);
+        CHECK(std::fabs(k.EvaluateKernel(x1) - expect[q]) < 1e-15);
+        const Eigen::VectorXd g = k.EvaluateKernelGrad(x1);
+        for (long c = 0; c < 2; ++c)
+        {
+            Eigen::VectorXd xp = x1, xm = x1;
+            xp(c) += 1e-6;
+            xm(c) -= 1e-6;
+            CHECK(std::fabs(g(c) - (k.EvaluateKernel(xp) - k.EvaluateKernel(xm)) / 2e-6) < 1e-8);
+        }
+    }
+    Kernel k3(3);
+    CHECK(Throws<DimensionMismatchException>([&] { Kernel s = a + k3; }));
+    Kernel unset(2);
+    CHECK(Throws<UnsetException>([&] { Kernel s = a + unset; }));
+}
+
+// Logged-matrix runs for tests/test_cpp_api.py (value parity of the
+// intermediate-matrix log, SVGD.hpp:345-365, against the oracle):
+//   host   generic closed-form unit RBF (host path), test_svgd.cpp scenario
+//   const  GaussianRBFKernel, Constant M = I (device path), same scenario
+//   median GaussianRBFKernel, Median scale (device path), MVN model
+// Each writes its log at 17 significant digits and prints the initial and
+// final coordinates.
+static int LogRun(const std::string &which, const std::string &path)
+{
+    const size_t d = 2, n = 10, iters = which == "median" ? 5 : 15;
+    std::srand(1);
+    auto x = std::make_shared<Eigen::MatrixXd>(Eigen::MatrixXd::Random(d, n));
+    const Eigen::MatrixXd x0 = *x;
+    std::shared_ptr<Model> model = std::make_shared<CosineModel>();
+    std::shared_ptr<Kernel> kernel;
+    if (which == "host")
+        kernel = UnitRBF(d);
+    else if (which == "const")
+    {
+        auto k = std::make_shared<GaussianRBFKernel>(x, GaussianRBFKernel::ScaleMethod::Constant);
+        k->UpdateParameters({Eigen::MatrixXd::Identity(2, 2)});
+        kernel = k;
+    }
+    else
+    {
+        Eigen::Matrix2d cov;
+        cov << 0.2260, 0.1652, 0.1652, 0.6779;
+        model = std::make_shared<MultivariateNormal>(Eigen::Vector2d(-0.6871, 0.8010), 5.0 * cov);
+        kernel = std::make_shared<GaussianRBFKernel>(x, GaussianRBFKernel::ScaleMethod::Median, model);
+    }
+    SVGDOptions o;
+    o.Dimension = d;
+    o.NumIterations = iters;
+    o.CoordinateMatrixPtr = x;
+    o.KernelPtr = kernel;
+    o.ModelPtr = model;
+    o.OptimizerPtr = std::make_shared<Adam>(d, n, 1.0e-1, 0.9, 0.999);
+    if (which != "median")
+    {
+        o.LowerBound = Eigen::Vector2d(-1.0, -1.0);
+        o.UpperBound = Eigen::Vector2d(1.0, 1.0);
+    }
+    o.LogIntermediateMatrices = true;
+    o.IntermediateMatricesOutputPath = path;
+    o.IntermediateMatricesPrecision = 17;
+    SVGD svgd(o);
+    svgd.Initialize();
+    svgd.Run();
+    std::cout.precision(17);
+    std::cout << "INITIAL\n" << x0 << "\nFINAL\n" << *x << "\n";
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc > 3 && std::strcmp(argv[1], "log") == 0)
+        return LogRun(argv[2], argv[3]);
     const bool cpu_only = argc > 1 && std::strcmp(argv[1], "cpu") == 0;
     TestArgumentChecks();
+    TestGenericKernelHostPath();
     if (!cpu_only)
     {
         TestSVGDClassConstantScale();

@@ -77,26 +77,31 @@ def test_f32_median_bracket_and_fallback_agree(oracle):
 
 
 def test_f32_step_tracks_f64(oracle):
-    """Full device steps (median + phi + Adam) in fp32 vs fp64: the scale
-    agrees to fp32 rounding, and positions after 3 steps stay close (Adam
-    normalises the increment, so only tiny phi components can differ)."""
+    """Per-step fp32 vs fp64 along one fp64 trajectory: at every step both
+    contexts see the same X_t and G_t; the fp32 scale agrees to rel 1e-5 and
+    the fp32 phi_hat (with the fp64 scale) is within REL * max|phi_hat| of the
+    fp64 one.  (Positions after whole Adam steps are not compared: Adam's first
+    increments are +-lr * sign(phi), so a phi component near 0 may flip sign.)"""
     n, d = 2048, 64
-    X0 = oracle.splitmix((n, d), 3.0, 11)
+    X = oracle.splitmix((n, d), 3.0, 11)
     mu = oracle.splitmix((1, d), 0.5, 12)
     model = S.GaussianSum(mu, np.eye(d)[None])
-    out, scale = {}, {}
-    for dt in (C.SVGD_F64, C.SVGD_F32):
-        c = S.Context(d, n, dtype=dt)
-        c.set_particles(X0)
-        c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999)
-        for _ in range(3):
-            c.step_with_model(model)
-        out[dt] = c.get_particles()
-        scale[dt] = c.last_scale()[0]
-    assert scale[C.SVGD_F32] == pytest.approx(scale[C.SVGD_F64], rel=1e-5)
-    diff = np.abs(out[C.SVGD_F32] - out[C.SVGD_F64])
-    assert np.all(np.isfinite(out[C.SVGD_F32]))
-    assert np.mean(diff) < 1e-3 and np.max(diff) <= 0.6
+    c64 = S.Context(d, n, dtype=C.SVGD_F64)
+    c32 = S.Context(d, n, dtype=C.SVGD_F32)
+    adam = oracle.Adam((n, d), 0.1, 0.9, 0.999)
+    for _ in range(3):
+        c64.set_particles(X)
+        c32.set_particles(X)
+        a64, _ = c64.median_scale()
+        a32, _ = c32.median_scale()
+        assert a32 == pytest.approx(a64, rel=1e-5)
+        G = model.log_model_grad(X)
+        ph64 = c64.phi(G, a64)
+        ph32 = c32.phi(G, a64)
+        assert np.all(np.isfinite(ph32))
+        assert np.max(np.abs(ph32 - ph64)) <= REL * np.max(np.abs(ph64))
+        X = X.copy()
+        oracle.apply_update(X, adam.step(ph64))
 
 
 def test_f32_matrix_scale(oracle):

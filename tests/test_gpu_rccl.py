@@ -1,0 +1,54 @@
+"""The RCCL collectives of the sharded step, executed on one GPU.
+
+A context created with world = 1 and an RCCL unique id owns a one-rank RCCL
+communicator, so every collective call site of the multi-GPU step runs through
+RCCL (ncclCommInitRank, in-place ncclAllGather of X and G, ncclAllReduce of the
+bracket-sample histograms, of the median counts + bucket histogram and, on the
+fallback path, of each radix digit; ncclAllGather of the selected-bucket keys).
+RCCL refuses two ranks on one device, so this is the most of the RCCL path a
+one-GPU box can run; the multi-rank protocol itself is covered by
+tests/test_gpu_multirank.py (host shared-memory collectives, same call sites)
+and tests/test_multirank_cpu.py (gloo).
+
+Bar: bit-identical to the same steps without a communicator (a one-rank sum
+or gather is the identity), on the bracket, bucket-select and forced radix
+fallback paths.  GPU only."""
+import numpy as np
+import pytest
+
+import svgdcpp_amd as S
+from svgdcpp_amd import _capi as C
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(oracle, n, d, steps, rccl, monkeypatch, bucket_cap=None, sample=None):
+    if bucket_cap is not None:
+        monkeypatch.setenv("SVGD_BUCKET_CAP", str(bucket_cap))
+    uid = S.Context.unique_id() if rccl else None
+    c = S.Context(d, n, world=1, rank=0, unique_id=uid)
+    X0 = oracle.splitmix((n, d), 3.0, 71)
+    mus = oracle.splitmix((4, d), 3.0, 72)
+    model = S.GaussianSum(list(mus), [np.eye(d) * (1.0 + 0.25 * k) for k in range(4)])
+    c.set_particles(X0)
+    c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+    if sample:
+        c.check(c.lib.svgd_set_median_tuning(c.h, -1, sample, -1))
+    scales = []
+    for _ in range(steps):
+        c.step_with_model(model)
+        scales.append(c.last_scale())
+    X = c.get_particles()
+    c.close()
+    return X, scales
+
+
+@pytest.mark.parametrize("n,d,bucket_cap", [(6000, 8, None), (6000, 8, 0), (3000, 2, None), (700, 24, None)])
+def test_rccl_one_rank_step_bit_identical(oracle, monkeypatch, n, d, bucket_cap):
+    Xa, sa = _run(oracle, n, d, 3, True, monkeypatch, bucket_cap)
+    Xb, sb = _run(oracle, n, d, 3, False, monkeypatch, bucket_cap)
+    assert sa == sb
+    assert np.array_equal(Xa, Xb)
+    if n * (n - 1) // 2 > (1 << 24):
+        assert all(s[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET, C.SVGD_MEDIAN_FALLBACK)
+                   for s in sa)

@@ -1,10 +1,13 @@
 """World-size-2 (and 3) gloo rehearsal of the sharded SVGD step on CPU.
 
 The library's multi-GPU step shards rows with svgd_plan_rows,
-splits median pair tiles with svgd_plan_pair_tiles, all-reduces radix
-histograms and all-gathers X|G.  tests/_multirank_worker.py runs that
-protocol with gloo in place of RCCL and the oracle as the arithmetic; the
-result must equal the single-process oracle step.
+splits median pair tiles with svgd_plan_pair_tiles, brackets the median from
+a sharded sample (two histogram all-reduces), all-reduces the counts + bucket
+histogram once, all-gathers the selected buckets' keys once (or, after a
+bracket miss, runs the per-digit radix fallback) and all-gathers X and G.
+tests/_multirank_worker.py runs that protocol with gloo in place of RCCL and
+numpy/the oracle as the arithmetic; the result must equal the single-process
+oracle step.
 """
 import multiprocessing as mp
 import socket
@@ -21,12 +24,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,n,d,block", [(2, 301, 3, 64), (2, 64, 2, 64), (3, 700, 5, 256)])
-def test_sharded_step_matches_single_process(oracle, world, n, d, block):
+@pytest.mark.parametrize("world,n,d,block,sample,sigma,shift,path", [
+    (2, 301, 3, 64, 4096, 3.0, 0.0, "bracket"),
+    (2, 64, 2, 64, 512, 3.0, 0.0, "bracket"),
+    (3, 700, 5, 256, 4096, 3.0, 0.0, "bracket"),
+    (4, 900, 8, 256, 8192, 3.0, 0.0, "bracket"),
+    (3, 700, 5, 256, 4096, 3.0, 20.0, "fallback"),
+])
+def test_sharded_step_matches_single_process(oracle, world, n, d, block, sample, sigma, shift, path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=W.run, args=(r, world, port, n, d, block, q)) for r in range(world)]
+    procs = [ctx.Process(target=W.run, args=(r, world, port, n, d, block, q, sample, sigma, shift))
+             for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -45,6 +55,10 @@ def test_sharded_step_matches_single_process(oracle, world, n, d, block):
     assert res["total"] == n * (n - 1) // 2
     # G all-gather reassembles the full matrix bit-for-bit
     np.testing.assert_array_equal(res["G_all"], oracle.logp_grad_gmm(X, mus, covs))
+    assert res["path"] == path
+    # bracket path: 2 sample-histogram all-reduces + 1 counts all-reduce + 1 key all-gather
+    if path == "bracket":
+        assert res["collectives"] == 4
     # distributed exact median == single-process median (difference form vs Gram form)
     a_ref, med_ref = oracle.median_scale(X)
     assert res["med"] == pytest.approx(med_ref, rel=1e-13)
