@@ -7,14 +7,20 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 SRC_DIR := svgdcpp_amd/csrc
 LIB := svgdcpp_amd/libsvgdcpp_amd.so
-OBJS := $(SRC_DIR)/svgd_kernels.o $(SRC_DIR)/svgd_capi.o $(SRC_DIR)/plan.o $(SRC_DIR)/host_models.o \
+OBJS := $(SRC_DIR)/svgd_kernels.o $(SRC_DIR)/svgd_collect.o $(SRC_DIR)/svgd_capi.o $(SRC_DIR)/plan.o $(SRC_DIR)/host_models.o \
         $(SRC_DIR)/hostcomm.o
-HDRS := $(SRC_DIR)/svgd_kernels.h $(SRC_DIR)/svgd_exp_table.h include/svgdcpp_amd/svgd_capi.h
+HDRS := $(SRC_DIR)/svgd_kernels.h $(SRC_DIR)/svgd_device.h $(SRC_DIR)/svgd_exp_table.h \
+        include/svgdcpp_amd/svgd_capi.h
 
 all: $(LIB)
 
 $(SRC_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+# the matrix-core collect pass keeps its MFMA accumulators in VGPRs (gfx950's
+# unified register file): no AGPR copies in its classification loop
+$(SRC_DIR)/svgd_collect.o: $(SRC_DIR)/svgd_collect.hip $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -mllvm -amdgpu-mfma-vgpr-form -c $< -o $@
 
 $(SRC_DIR)/svgd_capi.o: $(SRC_DIR)/svgd_capi.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@

@@ -85,6 +85,7 @@ struct svgd_ctx {
     double bracket_sigma = 3.0; // sample-quantile standard deviations either side
     bool shard_sample = true;   // P > 1: ranks draw disjoint parts of the sample
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
+    bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol)
     bool samp_shard = false;    // this step's sample is sharded
     int64_t samp_local = 0;     // sample keys held by this rank
     int64_t samp_S = 0;         // this step's sample: size and target quantiles
@@ -477,7 +478,13 @@ int sample_bracket(svgd_ctx *c, double sigma)
 // host (ready at ev_cnt).
 int collect_counts(svgd_ctx *c)
 {
-    HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
+    if (c->rowpath && c->mcol && c->med_path != SVGD_MEDIAN_DIRECT)
+        // bracket collect: fp32 MFMA classification, exact keys for the band
+        HIPCHK(c, launch_pair_mcol(c->dim, c->collect_grid, c->xc, c->xf, c->nmax, c->n, c->pnb,
+                                   c->tile0, c->tile0 + c->own_tiles, c->regions, c->reg_cap,
+                                   c->counts, c->below, c->st, c->bpart, c->stream));
+    else
+        HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
                                    c->collect_grid, c->cnt3, c->stream));
     CHK(allreduce_cnt3(c));
@@ -847,6 +854,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     if (const char *e = std::getenv("SVGD_COLLECT_BLOCKS")) // buffers hold <= MAX_COLLECT_BLOCKS
         c->collect_blocks = std::min<int64_t>(MAX_COLLECT_BLOCKS, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SVGD_SAMPLE_SHARD")) c->shard_sample = std::atoi(e) != 0;
+    // A/B and test knob: the all-fp64 collect pass (k_pair_rows MODE 0) instead
+    if (const char *e = std::getenv("SVGD_COLLECT_FP64")) c->mcol = std::atoi(e) == 0;
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));

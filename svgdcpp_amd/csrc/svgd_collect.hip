@@ -1,0 +1,402 @@
+// svgd_collect.hip -- the median bracket collect pass on the matrix cores
+// (gfx950).  Built with VGPR-form MFMA operands (Makefile), which the other
+// kernels are not.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "svgd_device.h"
+
+namespace svgd_amd {
+
+typedef f4_t f4;
+
+// ====================================== median collect on the matrix cores ==
+//
+// The bracket collect pass (MODE 0 of k_pair_rows) for d <= 16, fp64 keys:
+// every pair is CLASSIFIED from an fp32 Gram product on v_mfma_f32_16x16x4f32
+// and only the pairs whose class the fp32 value cannot decide -- the band
+// around the bracket, ~0.2 % of pairs -- form their exact fp64 key, with the
+// same arithmetic as k_pair_rows / k_sample_keys (so every pass still agrees
+// bit for bit).  GaussianRBFKernel.hpp:179-187 (the pairwise distances whose
+// median is taken).
+//
+// MFMA roles: A = 16 columns j (lane l: x_j[j0 + l%16][4kk + l/16]), B = 16
+// rows i (same pattern), C = h_j = -|x_j|^2/2 of the lane's output rows, so
+// lane l holds ef = h_j + x_i.x_j for i = i0 + l%16, j = j0 + 4(l/16) + r.
+//
+// Error bound (u = 2^-24, MFMA f32 == an fmaf chain, MI355X_MICROARCH.md):
+// inputs rounded to fp32 (u each), products exact in the fma, D roundings of
+// the partial sums, so |ef - e| <= 1.01 (D + 3) u S with S = |h_j| +
+// sum_k |x_ik x_jk| <= 1.5 nmax.  MCOL_DELTA(D) = 4 (D + 4) u nmax (> 2.6x
+// that) plus 2^-100 for flushed denormals.  With the fp64 thresholds TL_i,
+// TH_i of k_pair_rows (e > TL => key < lo, e <= TH => key >= hi):
+//   ef >  TLf_i = up(TL_i + delta)    => below (counted)
+//   ef <= THf_i = down(TH_i - delta)  => above (dropped)
+// otherwise the pair is staged as (row, column) in LDS and finished exactly
+// in a batch (mcol_flush).  Data outside |x|^2 <= 2^40 sets delta = inf:
+// every pair is then finished exactly (correct, slow).
+constexpr int MC_STG = 512; // staged band pairs per wave
+constexpr int MC_NG = 4;    // 16-row blocks per classification group
+
+__device__ __forceinline__ float f32_up(double x)
+{
+    float f = (float)x;
+    if ((double)f < x) f = f == 0.0f ? 0x1p-149f : __int_as_float(__float_as_int(f) + (f > 0.0f ? 1 : -1));
+    return f;
+}
+__device__ __forceinline__ float f32_down(double x)
+{
+    float f = (float)x;
+    if ((double)f > x) f = f == 0.0f ? -0x1p-149f : __int_as_float(__float_as_int(f) + (f > 0.0f ? -1 : 1));
+    return f;
+}
+
+// The 4 values of one 16 x 16 block for one lane, in issue order (the
+// compiler otherwise hoists every compare of a group and spills their lane
+// masks): 8 compares straight into lane masks, then on the scalar unit
+//   nbelow += popc(v_r > tl)          (below lo, counted)
+//   h_r     = (v_r > th) & ~(v_r > tl)  (the band lanes of value r)
+// so the first scalar read of a mask comes 8 vector instructions after its
+// compare.  Returns h_0 | h_1 | h_2 | h_3; h_r stay in SGPRs for the staging.
+// Exec is all ones here (uniform control flow); a VALU-written SGPR read by
+// the SALU needs no wait states.
+__device__ __forceinline__ unsigned long long mcol_classify4(const f4_t &v, float tl, float th,
+                                                             uint32_t &nbelow,
+                                                             unsigned long long (&h)[4])
+{
+    unsigned long long l0, l1, l2, l3, any;
+    uint32_t t0, t1;
+    asm volatile("v_cmp_gt_f32_e64 %[l0], %[v0], %[tl]\n\t"
+                 "v_cmp_gt_f32_e64 %[h0], %[v0], %[th]\n\t"
+                 "v_cmp_gt_f32_e64 %[l1], %[v1], %[tl]\n\t"
+                 "v_cmp_gt_f32_e64 %[h1], %[v1], %[th]\n\t"
+                 "v_cmp_gt_f32_e64 %[l2], %[v2], %[tl]\n\t"
+                 "v_cmp_gt_f32_e64 %[h2], %[v2], %[th]\n\t"
+                 "v_cmp_gt_f32_e64 %[l3], %[v3], %[tl]\n\t"
+                 "v_cmp_gt_f32_e64 %[h3], %[v3], %[th]\n\t"
+                 "s_bcnt1_i32_b64 %[t0], %[l0]\n\t"
+                 "s_bcnt1_i32_b64 %[t1], %[l1]\n\t"
+                 "s_andn2_b64 %[h0], %[h0], %[l0]\n\t"
+                 "s_andn2_b64 %[h1], %[h1], %[l1]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t0]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t1]\n\t"
+                 "s_bcnt1_i32_b64 %[t0], %[l2]\n\t"
+                 "s_bcnt1_i32_b64 %[t1], %[l3]\n\t"
+                 "s_andn2_b64 %[h2], %[h2], %[l2]\n\t"
+                 "s_andn2_b64 %[h3], %[h3], %[l3]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t0]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t1]\n\t"
+                 "s_or_b64 %[any], %[h0], %[h1]\n\t"
+                 "s_or_b64 %[any], %[any], %[h2]\n\t"
+                 "s_or_b64 %[any], %[any], %[h3]"
+                 : [nb] "+s"(nbelow), [any] "=&s"(any), [l0] "=&s"(l0), [l1] "=&s"(l1),
+                   [l2] "=&s"(l2), [l3] "=&s"(l3), [h0] "=&s"(h[0]), [h1] "=&s"(h[1]),
+                   [h2] "=&s"(h[2]), [h3] "=&s"(h[3]), [t0] "=&s"(t0), [t1] "=&s"(t1)
+                 : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [tl] "v"(tl),
+                   [th] "v"(th)
+                 : "scc");
+    return any;
+}
+// Diagonal tiles (1 in nb/2 of them): lanes with xl > c (j > i) only.
+// Returns the band lanes of the value.
+__device__ __forceinline__ unsigned long long mcol_classify_diag(float v, float tl, float th, int xl,
+                                                                 int c, uint32_t &nbelow)
+{
+    unsigned long long ml, mh, ok;
+    uint32_t t;
+    asm volatile("v_cmp_gt_i32_e64 %[ok], %[xl], %[c]\n\t"
+                 "v_cmp_gt_f32_e64 %[ml], %[v], %[tl]\n\t"
+                 "v_cmp_gt_f32_e64 %[mh], %[v], %[th]\n\t"
+                 "s_and_b64 %[ml], %[ml], %[ok]\n\t"
+                 "s_and_b64 %[mh], %[mh], %[ok]\n\t"
+                 "s_bcnt1_i32_b64 %[t], %[ml]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t]\n\t"
+                 "s_andn2_b64 %[mh], %[mh], %[ml]"
+                 : [nb] "+s"(nbelow), [ml] "=&s"(ml), [mh] "=&s"(mh), [ok] "=&s"(ok), [t] "=&s"(t)
+                 : [v] "v"(v), [tl] "v"(tl), [th] "v"(th), [xl] "v"(xl), [c] "s"(c)
+                 : "scc");
+    return mh;
+}
+
+// Row operands of one 16-row block for one lane: B (KK fp32) | TLf | THf | pad.
+template <int D> struct McolRow {
+    static constexpr int KK = (D + 3) / 4;
+    static constexpr int RW = ((KK + 2 + 3) / 4) * 4; // floats per lane slot (16-byte units)
+};
+
+// A block's 4 waves share one tile at a time: the tile's 256 rows live in LDS
+// (B operands and thresholds, written when the row block changes), and wave w
+// takes the 16-column blocks w, w + 4, ...  Each wave stages its own band
+// pairs and owns region blockIdx * 4 + w, as k_pair_rows.
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_mcol(const double *__restrict__ xc,
+                                                  const float *__restrict__ xf, int64_t n,
+                                                  int64_t nb, int64_t t0, int64_t t1,
+                                                  SinkCollect sc)
+{
+    constexpr int KP = med_rec_stride(D);  // fp64 records [xc | h | 0..]
+    constexpr int KF = med_f32_stride(D);  // fp32 records [xc | h | 0..]
+    constexpr int KK = McolRow<D>::KK;     // MFMA k-steps
+    constexpr int RW = McolRow<D>::RW;
+    constexpr int NI = PBLK / 16;          // 16-row blocks of a tile
+    __shared__ __attribute__((aligned(16))) float sRow[NI * 64 * RW];
+    __shared__ uint32_t sStage[4][MC_STG];
+    __shared__ uint32_t sBk[NBK];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kq = lane >> 4, ql = lane & 15;
+    uint32_t *stage = sStage[w];
+
+    const uint64_t lo_key = sc.st->lo_key, hi_key = sc.st->hi_key;
+    const double binv = sc.st->binv;
+    const double nmax = __longlong_as_double((long long)*sc.nmax_bits);
+    const double lo_d = __longlong_as_double((long long)lo_key);
+    const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
+                                                        : __longlong_as_double((long long)hi_key);
+    const double delta = nmax <= 0x1p40 ? 4.0 * (D + 4) * 0x1p-24 * nmax + 0x1p-100 : __builtin_inf();
+    if (sc.bpart)
+        for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
+
+    const int64_t wreg = (int64_t)blockIdx.x * 4 + w;
+    uint64_t *wregion = sc.region + wreg * sc.cap;
+    int64_t wcnt = 0;             // keys written to the region
+    unsigned long long below = 0; // below count (scalar: classified + exact)
+    int scnt = 0;                 // staged band pairs
+    bool ovf = false;             // a group outgrew the staging area
+
+    // Staged pairs (row offset | column offset << 16 of the tile at rows ib,
+    // columns jbase) -> the exact fp64 key with k_pair_rows' arithmetic (e =
+    // h_j + fma chain over k ascending, s = max(fl(-2 h_i - 2 e), 0)), then
+    // below lo (counted) / in [lo, hi) (appended to the region, bucketed) /
+    // dropped.
+    auto flush = [&](int64_t ib, int64_t jbase) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // other lanes' staging stores
+        for (int q0 = 0; q0 < scnt; q0 += 64) {
+            const bool valid = q0 + lane < scnt;
+            const uint32_t e = valid ? stage[q0 + lane] : 0u;
+            const double *ri = xc + (valid ? ib + (e & 0xffffu) : 0) * KP;
+            const double *rj = xc + (valid ? jbase + (e >> 16) : 0) * KP;
+            double ev = rj[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) ev = fma(ri[k], rj[k], ev);
+            const double ni = -2.0 * ri[D];
+            const uint64_t key = key_of(fmax(fma(-2.0, ev, ni), 0.0));
+            below += __popcll(__ballot(valid && key < lo_key));
+            const bool keep = valid && key >= lo_key && key < hi_key;
+            const unsigned long long mk = __ballot(keep);
+            if (keep) {
+                const int64_t pos = wcnt + __popcll(mk & ((1ull << lane) - 1ull));
+                if (pos < sc.cap) wregion[pos] = key;
+                if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
+            }
+            wcnt += __popcll(mk);
+        }
+        scnt = 0;
+    };
+
+    const int64_t T = t1 - t0;
+    const int64_t tb = t0 + T * blockIdx.x / gridDim.x, te = t0 + T * (blockIdx.x + 1) / gridDim.x;
+    // lane-constant part of "j > i" inside a 16 x 16 block (diagonal tiles):
+    // j - i = (4 kq - ql) + r + (jl0 - il0)
+    const int xl = 4 * kq - ql;
+    if (tb < te) {
+        const int64_t H = (nb - 1) / 2;
+        int64_t I, J;
+        tile_coords(nb, tb, &I, &J);
+        int64_t slot = (J - I + nb) % nb;
+        int64_t curI = -1;
+        for (int64_t t = tb; t < te; ++t) {
+            const int64_t ib = I * PBLK, jbase = J * PBLK;
+            if (I != curI) {
+                // the tile's rows: lane slot (b, l) of row ib + 16 b + (l & 15)
+                __syncthreads(); // every wave is done with the previous rows
+                for (int e = tid; e < NI * 64; e += 256) {
+                    const int b = e >> 6, l = e & 63;
+                    const int64_t i = ib + 16 * b + (l & 15);
+                    const bool iv = i < n;
+                    const int64_t ic = iv ? i : n - 1;
+                    float *o = sRow + e * RW;
+#pragma unroll
+                    for (int kk = 0; kk < KK; ++kk) {
+                        const int k = 4 * kk + (l >> 4);
+                        o[kk] = k < D ? xf[ic * KF + k] : 0.0f; // slot D holds h
+                    }
+                    const double ni = -2.0 * xc[ic * KP + D];
+                    const double m = 0x1p-48 * (ni + nmax);
+                    const double TL = lo_key == 0 ? __builtin_inf() : 0.5 * (ni - lo_d + m);
+                    const double TH = 0.5 * (ni - hi_d - m);
+                    o[KK] = iv ? f32_up(TL + delta) : __builtin_inff();
+                    o[KK + 1] = iv ? f32_down(TH - delta) : __builtin_inff();
+                }
+                __syncthreads();
+                curI = I;
+            }
+            const bool diag = I == J;
+            const int njb = (int)min<int64_t>(PBLK / 16, (n - jbase + 15) / 16);
+            // this wave's 16-column blocks; the next one's operands load during
+            // the current one's MFMAs (xf rows [n, np) hold h = -inf: padding
+            // columns are never below or in the band; blocks end before np)
+            auto load_cols = [&](int jb, float (&A)[KK], f4 &hq) {
+                const float *xcol = xf + (jbase + 16 * jb) * KF;
+#pragma unroll
+                for (int kk = 0; kk < KK; ++kk) {
+                    const float x = xcol[ql * KF + 4 * kk + kq];
+                    A[kk] = (4 * kk + kq == D) ? 0.0f : x; // slot D holds h
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
+            };
+            // one group of MC_NG row blocks: its row operands from LDS, its MFMAs
+            auto group_mfma = [&](int g0, const f4 &hq, const float (&A)[KK],
+                                  float (&Bg)[MC_NG][RW], f4 (&acc)[MC_NG]) {
+#pragma unroll
+                for (int g = 0; g < MC_NG; ++g)
+#pragma unroll
+                    for (int q = 0; q < RW; q += 4)
+                        *reinterpret_cast<f4 *>(&Bg[g][q]) =
+                            *reinterpret_cast<const f4 *>(sRow + ((g0 + g) * 64 + lane) * RW + q);
+#pragma unroll
+                for (int g = 0; g < MC_NG; ++g) {
+                    acc[g] = hq;
+#pragma unroll
+                    for (int kk = 0; kk < KK; ++kk)
+                        acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[kk], Bg[g][kk], acc[g], 0, 0, 0);
+                }
+            };
+            // Per 16-column block: the groups' MFMAs run one group ahead of the
+            // classification (phase 2: two compares per value straight into
+            // lane masks -- below (v > TLf) counted on the scalar unit, band (v
+            // > THf but not below) OR-ed; phase 3, rare: stage the band pairs).
+            auto jloop = [&](auto diag_tag) {
+                constexpr bool DIAG = decltype(diag_tag)::value;
+                float A[KK], An[KK];
+                f4 hq, hqn;
+                if (w < njb) load_cols(w, A, hq);
+                for (int jb = w; jb < njb; jb += 4) {
+                    // (a block of 16 x 256 pairs stages ~10 band pairs; one that
+                    // outgrows the area marks the region overflowed)
+                    if (scnt > MC_STG / 2) flush(ib, jbase);
+                    if (jb + 4 < njb) load_cols(jb + 4, An, hqn);
+                    const int jl0 = 16 * jb;
+                    float Bg[MC_NG][RW], Bn[MC_NG][RW];
+                    f4 acc[MC_NG], accn[MC_NG];
+                    group_mfma(0, hq, A, Bg, acc);
+                    for (int g0 = 0; g0 < NI; g0 += MC_NG) {
+                        if (g0 + MC_NG < NI) group_mfma(g0 + MC_NG, hq, A, Bn, accn);
+                        uint32_t nbelow = 0;
+#pragma unroll
+                        for (int g = 0; g < MC_NG; ++g) {
+                            unsigned long long h[4], any = 0;
+                            if constexpr (DIAG) {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    h[r] = mcol_classify_diag(acc[g][r], Bg[g][KK], Bg[g][KK + 1], xl,
+                                                              16 * (g0 + g) - jl0 - r, nbelow);
+                                    any |= h[r];
+                                }
+                            } else {
+                                any = mcol_classify4(acc[g], Bg[g][KK], Bg[g][KK + 1], nbelow, h);
+                            }
+                            // rare (~0.4 of the blocks, ~1 band pair each): stage the band pairs
+                            if (__builtin_expect(any != 0, 0)) {
+                                const uint32_t il = 16 * (g0 + g) + ql;
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    const unsigned long long m = h[r];
+                                    if (!m) continue;
+                                    const int c = __popcll(m);
+                                    if (scnt + c > MC_STG) { // pathological band: give up
+                                        ovf = true;      // (region overflow -> exact fallback)
+                                        continue;
+                                    }
+                                    if ((m >> lane) & 1ull)
+                                        stage[scnt + __popcll(m & ((1ull << lane) - 1ull))] =
+                                            il | ((uint32_t)(jl0 + 4 * kq + r) << 16);
+                                    scnt += c;
+                                }
+                            }
+                        }
+                        below += nbelow;
+#pragma unroll
+                        for (int g = 0; g < MC_NG; ++g) {
+                            acc[g] = accn[g];
+#pragma unroll
+                            for (int q = 0; q < RW; ++q) Bg[g][q] = Bn[g][q];
+                        }
+                    }
+#pragma unroll
+                    for (int kk = 0; kk < KK; ++kk) A[kk] = An[kk];
+                    hq = hqn;
+                }
+            };
+            if (diag)
+                jloop(std::true_type{});
+            else
+                jloop(std::false_type{});
+            if (scnt) flush(ib, jbase);
+            // next tile (plan.cpp order, as k_pair_rows)
+            ++slot;
+            const int64_t cntI = ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
+            if (slot == cntI) {
+                ++I;
+                slot = 0;
+            }
+            J = slot == 0 ? I : (I + slot) % nb;
+        }
+    }
+
+    if (lane == 0) {
+        sc.below_out[wreg] = below;
+        // an overflowed staging area reports an overflowed region: the host
+        // then takes the exact streamed fallback
+        sc.count_out[wreg] = ovf ? 0xffffffffu : (uint32_t)min<int64_t>(wcnt, 0xffffffffll);
+    }
+    if (sc.bpart) {
+        __syncthreads();
+        for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
+    }
+}
+
+
+// ============================================================ launcher ==
+
+#define SVGD_MCOL_CASE(Dv)                                                                   \
+    case Dv:                                                                                 \
+        hipLaunchKernelGGL((k_pair_mcol<Dv>), dim3(grid), dim3(256), 0, stream, xc, xf, n, nb, t0, \
+                           t1, sc);                                                          \
+        break;
+
+hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
+                            const unsigned long long *nmax_bits, int64_t n, int64_t nb, int64_t t0,
+                            int64_t t1, uint64_t *regions, int64_t cap, uint32_t *counts,
+                            unsigned long long *below, const SelState *st, uint32_t *bpart,
+                            hipStream_t stream)
+{
+    if (grid <= 0 || t1 <= t0) return hipSuccess;
+    if (!nmax_bits || !xf) return hipErrorInvalidValue;
+    SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, bpart};
+    switch (d) {
+        SVGD_MCOL_CASE(1)
+        SVGD_MCOL_CASE(2)
+        SVGD_MCOL_CASE(3)
+        SVGD_MCOL_CASE(4)
+        SVGD_MCOL_CASE(5)
+        SVGD_MCOL_CASE(6)
+        SVGD_MCOL_CASE(7)
+        SVGD_MCOL_CASE(8)
+        SVGD_MCOL_CASE(9)
+        SVGD_MCOL_CASE(10)
+        SVGD_MCOL_CASE(11)
+        SVGD_MCOL_CASE(12)
+        SVGD_MCOL_CASE(13)
+        SVGD_MCOL_CASE(14)
+        SVGD_MCOL_CASE(15)
+        SVGD_MCOL_CASE(16)
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+} // namespace svgd_amd

@@ -1,0 +1,79 @@
+// svgd_device.h -- device helpers shared by the gfx950 kernel translation
+// units (svgd_kernels.hip, svgd_collect.hip).  Internal.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "svgd_kernels.h"
+
+namespace svgd_amd {
+
+typedef float f4_t __attribute__((ext_vector_type(4)));
+
+constexpr int PBLK = 256; // row/column block of the row-stream median tile plan (plan.cpp)
+
+// --------------------------------------------------------------- median --
+//
+// Keys: squared distances s = max((|xc_i|^2 + |xc_j|^2) - 2 xc_i.xc_j, 0)
+// (the reference's Gram form, GaussianRBFKernel.hpp:179-183, on centred
+// coordinates) as the IEEE bit pattern, which orders like uint64 for s >= 0.
+// Every unordered pair i<j is visited once by the tile sweep of plan.h.
+
+__device__ __forceinline__ uint64_t key_of(double s)
+{
+    return (uint64_t)__double_as_longlong(s) & 0x7fffffffffffffffull; // s >= 0 (+0, never -0)
+}
+
+// Key-range bucket of a candidate key (SelState::binv): monotone in the key.
+__device__ __forceinline__ int kbucket(uint64_t key, uint64_t lo, double binv)
+{
+    const double t = (double)(key - lo) * binv;
+    return t < (double)(NBK - 1) ? (t > 0.0 ? (int)t : 0) : NBK - 1;
+}
+
+// Device copy of plan_pair_tile (plan.cpp): tile index -> (row block, col block).
+__device__ __forceinline__ void tile_coords(int64_t nb, int64_t t, int64_t *I, int64_t *J)
+{
+    const int64_t H = (nb - 1) / 2;
+    int64_t slot;
+    if ((nb & 1) == 0) {
+        const int64_t c1 = H + 2, c2 = H + 1, half = nb / 2;
+        if (t < half * c1) {
+            *I = t / c1;
+            slot = t - *I * c1;
+        } else {
+            const int64_t u = t - half * c1;
+            *I = half + u / c2;
+            slot = u - (*I - half) * c2;
+        }
+    } else {
+        const int64_t c = H + 1;
+        *I = t / c;
+        slot = t - *I * c;
+    }
+    *J = slot == 0 ? *I : (*I + slot) % nb;
+}
+
+struct SinkCollect {
+    const SelState *st; // bracket [st->lo_key, st->hi_key)
+    uint64_t *region; // this block's region (capacity cap)
+    int64_t cap;
+    uint32_t *count_out;
+    unsigned long long *below_out;
+    const float *xf;                     // fp32 records (unused by the collect pass)
+    const unsigned long long *nmax_bits; // max |xc|^2 (double bits): classification margin
+    uint32_t *bpart;                     // per-block key-range bucket histograms (optional)
+};
+
+struct SinkHist {
+    const SelState *st;
+    unsigned long long *ghist; // [2][RADIX] (64-bit: a streamed pass counts up to n(n-1)/2 keys)
+};
+
+struct SinkDebug {
+    double *out;    // MODE 2: every upper-triangle distance at its list index
+    int64_t n;
+    uint64_t *keys; // MODE 3: 64 x 64 keys of each sampled tile
+};
+
+} // namespace svgd_amd

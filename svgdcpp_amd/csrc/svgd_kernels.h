@@ -152,6 +152,13 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                             int64_t cap, uint32_t *counts, unsigned long long *below,
                             const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                             double *dbg_out, hipStream_t stream);
+// Bracket collect (mode 0 of launch_pair_rows) with fp32 MFMA classification and
+// exact fp64 keys for the undecided band (d <= 16); same plan, outputs and keys.
+hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
+                            const unsigned long long *nmax_bits, int64_t n, int64_t nb, int64_t t0,
+                            int64_t t1, uint64_t *regions, int64_t cap, uint32_t *counts,
+                            unsigned long long *below, const SelState *st, uint32_t *bpart,
+                            hipStream_t stream);
 int phi_rows_blocks_per_cu(int d, int R);
 // G = grad log p of the Gaussian-sum model for `rows` particle rows (d <= 64)
 hipError_t launch_gauss_grad(const double *X, int64_t rows, int d, int k, const double *mu,

@@ -23,6 +23,7 @@
 
 #include "svgd_kernels.h"
 #include "svgd_exp_table.h"
+#include "svgd_device.h"
 
 namespace svgd_amd {
 
@@ -191,8 +192,10 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
         nrm[j] = s;
         if (KP > d && nrm_in_slot) xc[j * KP + d] = -0.5 * s; // median record [xc | -|xc|^2/2 | 0..]
         if (xf) {
+            // padding rows j >= n: h = -inf (k_pair_mcol reads whole 16-column blocks)
             for (int k = 0; k < KF; ++k)
-                xf[j * KF + k] = k < d ? (float)xc[j * KP + k] : (k == d ? (float)(-0.5 * s) : 0.0f);
+                xf[j * KF + k] = k < d ? (float)xc[j * KP + k]
+                                       : (k == d ? (j < n ? (float)(-0.5 * s) : -__builtin_inff()) : 0.0f);
             unsigned long long m = (unsigned long long)__double_as_longlong(s);
             for (int o = 32; o > 0; o >>= 1) {
                 const unsigned long long t = __shfl_xor(m, o);
@@ -407,68 +410,7 @@ __global__ void k_opt_update(int kind, const double *__restrict__ g, double *__r
 }
 
 // --------------------------------------------------------------- median --
-//
-// Keys: squared distances s = max((|xc_i|^2 + |xc_j|^2) - 2 xc_i.xc_j, 0)
-// (the reference's Gram form, GaussianRBFKernel.hpp:179-183, on centred
-// coordinates) as the IEEE bit pattern, which orders like uint64 for s >= 0.
-// Every unordered pair i<j is visited once by the tile sweep of plan.h.
-
-__device__ __forceinline__ uint64_t key_of(double s)
-{
-    return (uint64_t)__double_as_longlong(s) & 0x7fffffffffffffffull; // s >= 0 (+0, never -0)
-}
-
-// Key-range bucket of a candidate key (SelState::binv): monotone in the key.
-__device__ __forceinline__ int kbucket(uint64_t key, uint64_t lo, double binv)
-{
-    const double t = (double)(key - lo) * binv;
-    return t < (double)(NBK - 1) ? (t > 0.0 ? (int)t : 0) : NBK - 1;
-}
-
-// Device copy of plan_pair_tile (plan.cpp): tile index -> (row block, col block).
-__device__ __forceinline__ void tile_coords(int64_t nb, int64_t t, int64_t *I, int64_t *J)
-{
-    const int64_t H = (nb - 1) / 2;
-    int64_t slot;
-    if ((nb & 1) == 0) {
-        const int64_t c1 = H + 2, c2 = H + 1, half = nb / 2;
-        if (t < half * c1) {
-            *I = t / c1;
-            slot = t - *I * c1;
-        } else {
-            const int64_t u = t - half * c1;
-            *I = half + u / c2;
-            slot = u - (*I - half) * c2;
-        }
-    } else {
-        const int64_t c = H + 1;
-        *I = t / c;
-        slot = t - *I * c;
-    }
-    *J = slot == 0 ? *I : (*I + slot) % nb;
-}
-
-struct SinkCollect {
-    const SelState *st; // bracket [st->lo_key, st->hi_key)
-    uint64_t *region; // this block's region (capacity cap)
-    int64_t cap;
-    uint32_t *count_out;
-    unsigned long long *below_out;
-    const float *xf;                     // fp32 records (unused by the collect pass)
-    const unsigned long long *nmax_bits; // max |xc|^2 (double bits): classification margin
-    uint32_t *bpart;                     // per-block key-range bucket histograms (optional)
-};
-
-struct SinkHist {
-    const SelState *st;
-    unsigned long long *ghist; // [2][RADIX] (64-bit: a streamed pass counts up to n(n-1)/2 keys)
-};
-
-struct SinkDebug {
-    double *out;    // MODE 2: every upper-triangle distance at its list index
-    int64_t n;
-    uint64_t *keys; // MODE 3: 64 x 64 keys of each sampled tile
-};
+// (keys, key-range buckets, the tile plan and the pass sinks: svgd_device.h)
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z)
 {
@@ -1843,7 +1785,6 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
 // 2 xc_i.xc_j, 0) with the dot as an FMA chain in k order (bit-identical to
 // k_sample_keys).  MODE 0 collect, 1 histogram (fallback), 2 debug dump.
 constexpr int PR = 4;     // rows per lane of the median sweep
-constexpr int PBLK = 256; // = 64 * PR: tile block of the row-stream median plan
 constexpr int CH_MED = 32; // columns per LDS chunk of the median stream
 
 struct TileIt {
