@@ -86,6 +86,7 @@ struct svgd_ctx {
     bool shard_sample = true;   // P > 1: ranks draw disjoint parts of the sample
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
     bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol)
+    double band_est = 1.0;         // this step's bracket: expected share of the pairs
     bool samp_shard = false;    // this step's sample is sharded
     int64_t samp_local = 0;     // sample keys held by this rank
     int64_t samp_S = 0;         // this step's sample: size and target quantiles
@@ -349,6 +350,9 @@ hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t
 }
 
 constexpr double WIDE_SIGMA = 8.0; // re-bracket after a miss
+// k_pair_mcol stages ~4096 x band pairs per 16-column block and wave (512
+// slots): wider brackets (tiny samples, tests) take k_pair_rows' collect
+constexpr double MCOL_MAX_BAND = 0.02;
 
 int sample_bracket(svgd_ctx *c, double sigma);
 int collect_counts(svgd_ctx *c);
@@ -463,6 +467,7 @@ int sample_bracket(svgd_ctx *c, double sigma)
     if (slo < 0) slo = 0;
     if (shi > S - 1) shi = (double)(S - 1);
     uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
+    c->band_est = (shi - slo + 1.0) / (double)S; // expected share of pairs in the bracket
     CHK(upload_state(c, 2, sr, 0, ~0ull));
     for (int p = 0; p < 2; ++p) {
         HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, c->samp_local, 0, c->st, c->gpart,
@@ -478,8 +483,9 @@ int sample_bracket(svgd_ctx *c, double sigma)
 // host (ready at ev_cnt).
 int collect_counts(svgd_ctx *c)
 {
-    if (c->rowpath && c->mcol && c->med_path != SVGD_MEDIAN_DIRECT)
+    if (c->rowpath && c->mcol && c->med_path != SVGD_MEDIAN_DIRECT && c->band_est <= MCOL_MAX_BAND)
         // bracket collect: fp32 MFMA classification, exact keys for the band
+        // (a thin band only: each band pair is staged and finished one by one)
         HIPCHK(c, launch_pair_mcol(c->dim, c->collect_grid, c->xc, c->xf, c->nmax, c->n, c->pnb,
                                    c->tile0, c->tile0 + c->own_tiles, c->regions, c->reg_cap,
                                    c->counts, c->below, c->st, c->bpart, c->stream));
