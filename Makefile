@@ -57,8 +57,22 @@ build/test_api: tests/cpp/test_api.cpp $(CPP_HDRS) $(LIB)
 	@mkdir -p build
 	$(CXX) $(CPP_FLAGS) $< -o $@ $(CPP_LINK)
 
+# Host-code sanitizers (ASan + UBSan): planner, host models and the CPU oracle
+# linked into a self-checking driver (the HIP host code needs a GPU: see
+# tests/cpp/sanitize_host.cpp).  Run by tests/test_sanitize.py.
+SAN := -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=all
+build/sanitize_host: tests/cpp/sanitize_host.cpp $(SRC_DIR)/plan.cpp $(SRC_DIR)/host_models.cpp oracle/svgd_oracle.c
+	@mkdir -p build/san
+	gcc -O1 -g -std=c11 -fopenmp -ffp-contract=off $(SAN) -c oracle/svgd_oracle.c -o build/san/oracle.o
+	$(CXX) -O1 -g -std=c++17 -fopenmp $(SAN) -c $(SRC_DIR)/plan.cpp -o build/san/plan.o
+	$(CXX) -O1 -g -std=c++17 -fopenmp $(SAN) -c $(SRC_DIR)/host_models.cpp -o build/san/host_models.o
+	$(CXX) -O1 -g -std=c++17 -fopenmp $(SAN) tests/cpp/sanitize_host.cpp build/san/*.o -o $@ -lm
+
+sanitize: build/sanitize_host
+	ASAN_OPTIONS=detect_leaks=1 OMP_NUM_THREADS=2 ./build/sanitize_host
+
 clean:
-	rm -f $(OBJS) $(LIB) $(CPP_BINS)
+	rm -f $(OBJS) $(LIB) $(CPP_BINS) build/sanitize_host
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle cpp clean
+.PHONY: all oracle cpp clean sanitize

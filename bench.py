@@ -262,6 +262,13 @@ def main():
                 pmc = json.load(f)
             if pmc.get("n") == n and pmc.get("d") == d and pmc.get("world") == world:
                 traffic = pmc.get("bytes_per_launch")
+        issue = None  # SQ counters of the same kernel (committed profile, not this run)
+        issue_path = os.path.join(ROOT, "profiles", "phi_pmc_issue.json")
+        if os.path.exists(issue_path):
+            with open(issue_path) as f:
+                iss = json.load(f)
+            if iss.get("n") == n and iss.get("d") == d and iss.get("world") == world and dtype == "f64":
+                issue = iss
         out = {
             "metric": METRIC,
             "value": n * args.steps / elapsed,
@@ -301,6 +308,18 @@ def main():
             "median_path": ["direct", "bracket", "fallback", "rebracket"][path],
             "scale_a": a,
         }
+        if issue is not None:
+            # issue-slot view beside the flop fraction: the fp64 VALU pipe's
+            # share of issue slots used, and the clock the chip holds under this
+            # load (DVFS) -- the flop fraction at that clock is the ceiling this
+            # instruction mix can reach
+            clk = issue["clock_ghz_under_load"]
+            out["roofline"].update({
+                "valu_issue_util": issue["valu_issue_util"],
+                "clock_ghz_under_load": clk,
+                "frac_at_load_clock": (achieved / (peak * clk / 2.4)) if achieved else None,
+                "issue_source": issue["source"],
+            })
         if args.config != "cfg3" or args.device_model or dtype != "f64":
             desc = cfg["desc"]
             if dtype != cfg.get("dtype", "f64"):

@@ -142,6 +142,7 @@ struct svgd_ctx {
     // full-matrix scale (SVGD_SCALE_MATRIX / SVGD_SCALE_HESSIAN): device M, its
     // Cholesky factor L, the (rank-summed) Hessian sum, wv = 2 M xc, zc = L^T xc
     double *sc_src = nullptr, *sc_M = nullptr, *sc_L = nullptr, *wv = nullptr, *zc = nullptr;
+    double *sc_sgn = nullptr, *sc_work = nullptr; // M = L diag(sgn) L^T; Jacobi scratch
     int *sc_err = nullptr, *h_err = nullptr;
     bool hess_ready = false; // Hessian sum supplied for the current step
     std::vector<double> h_mat;
@@ -554,14 +555,18 @@ int median_finish(svgd_ctx *c)
         const int ns = (c->nsel > 1 && ranks[1] != ranks[0]) ? 2 : 1;
         if (svgd_plan_bucket_select(c->h_cnt + 3, NBK, ns, rr, bsel, rin, &tot) == 0 &&
             tot <= std::min<int64_t>(c->bucket_cap, CAPG)) {
-            uint64_t *seg = c->gseg + (size_t)c->rank * (CAPG + 1);
+            // one segment per rank, sized for the selected buckets' total (a
+            // rank holds at most that many): the all-gather moves tot keys per
+            // rank, not the CAPG capacity
+            const int64_t scap = std::max<int64_t>(1, tot);
+            uint64_t *seg = c->gseg + (size_t)c->rank * (scap + 1);
             HIPCHK(c, launch_set_sel(c->st, c->nsel, (uint64_t)rin[0],
                                      (uint64_t)(c->nsel > 1 ? rin[ns - 1] : rin[0]), bsel[0],
                                      bsel[ns - 1], seg, c->stream));
             HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st,
-                                             seg, c->stream));
-            CHK(allgather_u64(c, c->gseg, CAPG + 1));
-            HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, c->stream));
+                                             seg, scap, c->stream));
+            CHK(allgather_u64(c, c->gseg, (size_t)scap + 1));
+            HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, scap, c->stream));
             HIPCHK(c, launch_finalize(c->st, c->navg, c->src_lo, c->src_hi, logn, c->scal,
                                       c->scal + 1, c->stream));
             c->last_path = path;
@@ -667,12 +672,22 @@ int run_phi(svgd_ctx *c)
         const double factor = c->scale_method == SVGD_SCALE_HESSIAN
                                   ? 1.0 / (2.0 * (double)c->dim * (double)c->n)
                                   : 1.0;
-        HIPCHK(c, launch_scale_chol(c->sc_src, factor, c->dim, c->sc_M, c->sc_L, c->scal, c->sc_err,
-                                    c->stream));
+        HIPCHK(c, launch_scale_factor(c->sc_src, factor, c->dim, c->sc_M, c->sc_L, c->sc_sgn,
+                                      c->sc_work, c->scal, c->sc_err, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->h_err, c->sc_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+        if (!c->rowpath) {
+            // the MFMA tile kernels need M positive definite: check before phi
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            if (*c->h_err == 2)
+                return fail(c, SVGD_ERR_RUNTIME,
+                            "[Runtime Error] The kernel scale matrix is indefinite; the device "
+                            "path supports indefinite matrices for fp64 particles with d <= 16 only.");
+        }
+        if (*c->h_err == 1 && !c->rowpath)
+            return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] The kernel scale matrix is not finite.");
         if (c->rowpath)
-            HIPCHK(c, launch_prep_rec_mat(c->xc, c->G, c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
-                                          c->RS, c->rec, c->wv, c->stream));
+            HIPCHK(c, launch_prep_rec_mat(c->xc, c->G, c->sc_M, c->sc_L, c->sc_sgn, c->n, c->np,
+                                          c->dim, c->KP, c->RS, c->rec, c->wv, c->stream));
         else
             HIPCHK(c, launch_prep_v_mat(c->xc, c->G, c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
                                         c->VW, c->zc, c->V, c->cvec, c->wv, c->stream));
@@ -694,8 +709,8 @@ int run_phi(svgd_ctx *c)
     }
     if (c->rowpath)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
-                                  c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr, c->phi,
-                                  c->stream));
+                                  c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
+                                  mat ? c->sc_sgn : nullptr, c->phi, c->stream));
     else if (c->dtype == SVGD_F32)
         HIPCHK(c, launch_phi_f32(c->KP, c->NCB, mat ? c->zcf : c->xcf, c->cvf, c->Vf, c->scal,
                                  c->row0, c->nrows, (c->n + TB - 1) / TB, c->dim,
@@ -945,7 +960,8 @@ int svgd_destroy(svgd_ctx *c)
     if (c->hcomm) hostcomm_destroy(c->hcomm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
-                       c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc};
+                       c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
+                       c->sc_sgn,  c->sc_work};
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
@@ -1035,6 +1051,8 @@ int alloc_matrix_scale(svgd_ctx *c)
     CHK(dalloc(c, &c->sc_src, dd));
     CHK(dalloc(c, &c->sc_M, dd));
     CHK(dalloc(c, &c->sc_L, dd));
+    CHK(dalloc(c, &c->sc_sgn, c->dim));
+    CHK(dalloc(c, &c->sc_work, 2 * dd));
     CHK(dalloc(c, &c->wv, c->np * c->dim));
     if (!c->rowpath) CHK(dalloc(c, &c->zc, c->np * c->KP));
     if (c->dtype == SVGD_F32) CHK(dalloc(c, &c->zcf, c->np * c->KP));
@@ -1093,9 +1111,12 @@ int svgd_get_scale_matrix(svgd_ctx *c, double *M_out)
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int d = c->dim;
     if (matrix_scale(c)) {
-        if (*c->h_err)
+        if (*c->h_err == 1)
+            return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] The kernel scale matrix is not finite.");
+        if (*c->h_err == 2 && !c->rowpath)
             return fail(c, SVGD_ERR_RUNTIME,
-                        "[Runtime Error] The kernel scale matrix is not positive definite.");
+                        "[Runtime Error] The kernel scale matrix is indefinite; the device path "
+                        "supports indefinite matrices for fp64 particles with d <= 16 only.");
         HIPCHK(c, hipMemcpy(M_out, c->sc_M, sizeof(double) * (size_t)d * d, hipMemcpyDeviceToHost));
         return SVGD_OK;
     }

@@ -111,14 +111,15 @@ hipError_t launch_set_scal(double a, double med, double *scal, hipStream_t strea
 // kept) and a zeroed counter seg[0] for launch_compact_buckets
 hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
                           uint64_t *seg, hipStream_t stream);
-// keys of the selected buckets st->bsel[] -> seg = [count, keys (<= CAPG)]
+// keys of the selected buckets st->bsel[] -> seg = [count, keys (<= seg_cap)]
 // (seg[0] must be zero on entry)
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                                  int64_t cap, const SelState *st, uint64_t *seg,
+                                  int64_t cap, const SelState *st, uint64_t *seg, int64_t seg_cap,
                                   hipStream_t stream);
 // exact selection of st->rank[s] within bucket st->bsel[s] over nseg gathered
-// segments [count, keys...] of stride CAPG + 1 -> st->prefix[s] = that key
-hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, hipStream_t stream);
+// segments [count, keys...] of stride seg_cap + 1 -> st->prefix[s] = that key
+hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
+                               hipStream_t stream);
 hipError_t launch_bracket(SelState *st, hipStream_t stream);
 
 // Row-stream path (d <= 16): particle records rec_j = [xc_j | G_j - 2a xc_j | c_j | 0..],
@@ -134,14 +135,17 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            double *rec, hipStream_t stream);
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
-                           int64_t ldp, double inv_n, const double *wv, double *phi,
-                           hipStream_t stream);
-// full-matrix kernel scale (wv = 2 M xc replaces 2 a xc in the phi epilogue)
-hipError_t launch_scale_chol(const double *src, double factor, int d, double *M, double *L,
-                             double *scal, int *err, hipStream_t stream);
+                           int64_t ldp, double inv_n, const double *wv, const double *sgn,
+                           double *phi, hipStream_t stream);
+// full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,
+// or an eigendecomposition when M is indefinite and d <= ROWS_MAX_D);
+// err = 0 positive definite, 2 indefinite, 1 non-finite / no convergence.
+// wv = 2 M xc replaces 2 a xc in the phi epilogue.  work: 2 d^2 doubles.
+hipError_t launch_scale_factor(const double *src, double factor, int d, double *M, double *L,
+                               double *sgn, double *work, double *scal, int *err, hipStream_t stream);
 hipError_t launch_prep_rec_mat(const double *xc, const double *G, const double *M, const double *L,
-                               int64_t n, int64_t np, int d, int KP, int RS, double *rec,
-                               double *wv, hipStream_t stream);
+                               const double *sgn, int64_t n, int64_t np, int d, int KP, int RS,
+                               double *rec, double *wv, hipStream_t stream);
 hipError_t launch_prep_v_mat(const double *xc, const double *G, const double *M, const double *L,
                              int64_t n, int64_t np, int d, int KP, int VW, double *zc, double *V,
                              double *cvec, double *wv, hipStream_t stream);

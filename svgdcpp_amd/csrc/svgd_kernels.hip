@@ -964,14 +964,14 @@ __global__ void k_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int 
 // Keys of the regions in the selected bucket(s) -> seg = [count, keys].  A
 // block gathers its regions' matches in LDS and reserves output space with
 // one global atomic per flush (a counter that every block hits per region
-// serialises at the L2).  Positions past CAPG are dropped: the host only takes
-// this path when the selected buckets hold <= CAPG keys in total.
+// serialises at the L2).  Positions past seg_cap are dropped: the host only
+// takes this path when the selected buckets hold <= seg_cap keys in total.
 constexpr int CB_LDS = 4096; // keys buffered per block between flushes
 __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ counts,
                                                         int64_t nreg, int64_t cap,
                                                         const SelState *__restrict__ st,
-                                                        uint64_t *__restrict__ seg)
+                                                        uint64_t *__restrict__ seg, int64_t seg_cap)
 {
     __shared__ uint64_t sK[CB_LDS];
     __shared__ int sN;
@@ -992,7 +992,7 @@ __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restr
         __syncthreads();
         for (int e = threadIdx.x; e < m; e += 256) {
             const unsigned long long pos = sBase + e;
-            if (pos < (unsigned long long)CAPG) outk[pos] = sK[e];
+            if (pos < (unsigned long long)seg_cap) outk[pos] = sK[e];
         }
         __syncthreads();
         if (threadIdx.x == 0) sN = 0;
@@ -1064,7 +1064,7 @@ __device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long
 // (bits above it are equal for every key of a bucket), so a narrow bucket
 // needs 2-3 passes.
 __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint64_t *__restrict__ segs,
-                                                      int nseg)
+                                                      int nseg, int64_t seg_cap)
 {
     __shared__ uint32_t sHist[2][RADIX];
     __shared__ unsigned long long sW[16];
@@ -1080,8 +1080,8 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
     // min / max key of each selected bucket
     uint64_t mn[2] = {~0ull, ~0ull}, mx[2] = {0, 0};
     for (int g = 0; g < nseg; ++g) {
-        const uint64_t *sg = segs + (int64_t)g * (CAPG + 1);
-        const int64_t cnt = min<int64_t>((int64_t)sg[0], CAPG);
+        const uint64_t *sg = segs + (int64_t)g * (seg_cap + 1);
+        const int64_t cnt = min<int64_t>((int64_t)sg[0], seg_cap);
         for (int64_t e = tid; e < cnt; e += 1024) {
             const uint64_t key = sg[1 + e];
             const int kb = kbucket(key, lo, binv);
@@ -1134,8 +1134,8 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
         for (int e = tid; e < 2 * RADIX; e += 1024) (&sHist[0][0])[e] = 0;
         __syncthreads();
         for (int g = 0; g < nseg; ++g) {
-            const uint64_t *sg = segs + (int64_t)g * (CAPG + 1);
-            const int64_t cnt = min<int64_t>((int64_t)sg[0], CAPG);
+            const uint64_t *sg = segs + (int64_t)g * (seg_cap + 1);
+            const int64_t cnt = min<int64_t>((int64_t)sg[0], seg_cap);
             for (int64_t e = tid; e < cnt; e += 1024) {
                 const uint64_t key = sg[1 + e];
                 const int kb = kbucket(key, lo, binv);
@@ -1594,11 +1594,14 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
     for (int r = 0; r < R; ++r) acc1[r] += K[r];
 }
 
+// sgn (matrix scale, M = L S L^T): the row coordinates are scaled by S so
+// the pair term is z_i^T S z_j; nullptr = the isotropic scale (S = I).
 template <int D, int R>
 __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec,
                                                  const double *__restrict__ a_ptr, int64_t row0,
                                                  int64_t nrows, int64_t n, int S,
-                                                 double *__restrict__ part, int64_t ldp)
+                                                 double *__restrict__ part, int64_t ldp,
+                                                 const double *__restrict__ sgn)
 {
     constexpr int RS = RecLayout<D>::RS;
     constexpr int CHB = CH_PHI * RS * 8; // bytes per column chunk (multiple of 1 KiB)
@@ -1630,7 +1633,7 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
         const double *ri = rec + (row0 + li) * RS;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            xs[r][k] = alpha * ri[k];
+            xs[r][k] = (sgn ? alpha * sgn[k] : alpha) * ri[k];
             acc[r][k] = 0.0;
         }
         ci[r] = ri[2 * D];
@@ -1651,7 +1654,7 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     // all have -c_i/4096 = a log2e |xc_i|^2 <= FOLD_MAX take it (the usual
     // case: particles within ~sqrt(400/a) of the mean), others the plain form.
     constexpr double FOLD_MAX = 400.0;
-    bool fold_ok = true;
+    bool fold_ok = sgn == nullptr; // an indefinite S can make K_ij > 1: no fold
 #pragma unroll
     for (int r = 0; r < R; ++r) fold_ok = fold_ok && ci[r] >= -4096.0 * FOLD_MAX;
     const bool fold = __all(fold_ok);
@@ -2121,23 +2124,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
 // kernels run unchanged on z = L^T xc with a = 1 (|z_i - z_j|^2 is the
 // M-distance); V_j = G_j - 2 M xc_j and the reduce adds 2 M xc_i sum_j K_ij.
 //
-// One thread: M = factor * src (symmetrised), its Cholesky factor L (lower),
-// a_eff = 1 for the phi kernels.  err = 1 if M is not positive definite.
-__global__ void k_scale_chol(const double *__restrict__ src, double factor, int d,
-                             double *__restrict__ M, double *__restrict__ L,
-                             double *__restrict__ scal, int *__restrict__ err)
+// One thread: M = factor * src (symmetrised) and a factor M = L S L^T with
+// S = diag(sgn): the Cholesky factor (sgn = +1) when M is positive definite,
+// else (d <= ROWS_MAX_D) L = Q |Lambda|^(1/2), sgn = sign(Lambda) from a cyclic
+// Jacobi eigendecomposition -- the reference evaluates (x-x')^T M (x-x')
+// for any symmetric M (GaussianRBFKernel.hpp:75-81, 189-210), and the
+// sum of -Hessians of a Gaussian mixture can be indefinite between modes.
+// err = 0 (positive definite), 2 (indefinite: factored for d <= 16, else not),
+// 1 (non-finite M or no convergence).  a_eff = 1 for the phi kernels.
+// work: 2 d^2 doubles (Jacobi A and V).
+__global__ void k_scale_factor(const double *__restrict__ src, double factor, int d,
+                               double *__restrict__ M, double *__restrict__ L,
+                               double *__restrict__ sgn, double *__restrict__ work,
+                               double *__restrict__ scal, int *__restrict__ err)
 {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    scal[0] = 1.0;
+    scal[1] = __builtin_nan("");
+    double nrm = 0.0;
     for (int r = 0; r < d; ++r)
-        for (int c = 0; c < d; ++c)
-            M[r * d + c] = factor * 0.5 * (src[r * d + c] + src[c * d + r]);
-    int bad = 0;
-    for (int j = 0; j < d; ++j) {
+        for (int c = 0; c < d; ++c) {
+            const double m = factor * 0.5 * (src[r * d + c] + src[c * d + r]);
+            M[r * d + c] = m;
+            nrm += m * m;
+        }
+    if (!(nrm < __builtin_inf())) {
+        *err = 1;
+        return;
+    }
+    bool pd = true;
+    for (int j = 0; j < d && pd; ++j) {
         double s = M[j * d + j];
         for (int k = 0; k < j; ++k) s -= L[j * d + k] * L[j * d + k];
         if (!(s > 0.0)) {
-            bad = 1;
-            s = 1.0;
+            pd = false;
+            break;
         }
         const double ljj = sqrt(s);
         L[j * d + j] = ljj;
@@ -2147,18 +2168,74 @@ __global__ void k_scale_chol(const double *__restrict__ src, double factor, int 
             L[i * d + j] = t / ljj;
         }
         for (int c = j + 1; c < d; ++c) L[j * d + c] = 0.0;
+        sgn[j] = 1.0;
     }
-    scal[0] = 1.0;
-    scal[1] = __builtin_nan("");
-    *err = bad;
+    if (pd) {
+        *err = 0;
+        return;
+    }
+    if (d > ROWS_MAX_D) { // the MFMA tile kernels take positive definite M only
+        *err = 2;
+        return;
+    }
+    double *A = work, *V = work + d * d;
+    for (int r = 0; r < d; ++r)
+        for (int c = 0; c < d; ++c) {
+            A[r * d + c] = M[r * d + c];
+            V[r * d + c] = r == c ? 1.0 : 0.0;
+        }
+    bool conv = false;
+    for (int sweep = 0; sweep < 60 && !conv; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < d; ++p)
+            for (int q = p + 1; q < d; ++q) off += A[p * d + q] * A[p * d + q];
+        if (off <= 1e-34 * nrm) {
+            conv = true;
+            break;
+        }
+        for (int p = 0; p < d; ++p)
+            for (int q = p + 1; q < d; ++q) {
+                const double apq = A[p * d + q];
+                if (apq == 0.0) continue;
+                const double theta = (A[q * d + q] - A[p * d + p]) / (2.0 * apq);
+                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), sn = t * c;
+                for (int k = 0; k < d; ++k) { // A <- A J (columns p, q)
+                    const double akp = A[k * d + p], akq = A[k * d + q];
+                    A[k * d + p] = c * akp - sn * akq;
+                    A[k * d + q] = sn * akp + c * akq;
+                }
+                for (int k = 0; k < d; ++k) { // A <- J^T A (rows p, q)
+                    const double apk = A[p * d + k], aqk = A[q * d + k];
+                    A[p * d + k] = c * apk - sn * aqk;
+                    A[q * d + k] = sn * apk + c * aqk;
+                }
+                for (int k = 0; k < d; ++k) { // V <- V J
+                    const double vkp = V[k * d + p], vkq = V[k * d + q];
+                    V[k * d + p] = c * vkp - sn * vkq;
+                    V[k * d + q] = sn * vkp + c * vkq;
+                }
+            }
+    }
+    if (!conv) {
+        *err = 1;
+        return;
+    }
+    for (int k = 0; k < d; ++k) {
+        const double lam = A[k * d + k];
+        const double sq = sqrt(fabs(lam));
+        sgn[k] = lam > 0.0 ? 1.0 : (lam < 0.0 ? -1.0 : 0.0);
+        for (int l = 0; l < d; ++l) L[l * d + k] = V[l * d + k] * sq; // z_k = sum_l L[l][k] x_l
+    }
+    *err = 2;
 }
 
 // Row-stream records for the matrix scale: rec_j = [z_j | G_j - 2 M xc_j |
-// -4096 log2e |z_j|^2 | 0..], wv_j = 2 M xc_j.
+// -4096 log2e z_j^T S z_j | 0..], wv_j = 2 M xc_j (z = L^T xc, M = L S L^T).
 __global__ void k_prep_rec_mat(const double *__restrict__ xc, const double *__restrict__ G,
                                const double *__restrict__ M, const double *__restrict__ L,
-                               int64_t n, int64_t np, int d, int KP, int RS,
-                               double *__restrict__ rec, double *__restrict__ wv)
+                               const double *__restrict__ sgn, int64_t n, int64_t np, int d, int KP,
+                               int RS, double *__restrict__ rec, double *__restrict__ wv)
 {
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
          j += (int64_t)gridDim.x * blockDim.x) {
@@ -2176,7 +2253,7 @@ __global__ void k_prep_rec_mat(const double *__restrict__ xc, const double *__re
             r[k] = z;
             r[d + k] = live ? G[j * d + k] - 2.0 * mx : 0.0;
             wv[j * d + k] = 2.0 * mx;
-            zz = fma(z, z, zz);
+            zz = fma(sgn[k] * z, z, zz);
         }
         r[2 * d] = live ? -4096.0 * LOG2E * zz : 0.0;
         for (int k = 2 * d + 1; k < RS; ++k) r[k] = 0.0;
@@ -2274,13 +2351,13 @@ __global__ __launch_bounds__(256) void k_gauss_grad(const double *__restrict__ X
     case Dv:                                                                                 \
         if (kind == 0 && R == 1)                                                             \
             hipLaunchKernelGGL((k_phi_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp);                    \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn);               \
         else if (kind == 0 && R == 2)                                                        \
             hipLaunchKernelGGL((k_phi_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp);                    \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn);               \
         else if (kind == 0)                                                                  \
             hipLaunchKernelGGL((k_phi_rows<Dv, 4>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp);                    \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn);               \
         else if (kind == 10)                                                                 \
             hipLaunchKernelGGL((k_pair_rows<Dv, 0>), dim3(grid), dim3(256), 0, stream, xc, KP, \
                                nrm, n, nb, t0, t1, sc, sh, sd);                              \
@@ -2294,7 +2371,8 @@ __global__ __launch_bounds__(256) void k_gauss_grad(const double *__restrict__ X
 
 static hipError_t launch_rows_kernel(int kind, int D, int R, int grid, const double *rec,
                                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t n,
-                                     int S, double *part, int64_t ldp, const double *xc, int KP,
+                                     int S, double *part, int64_t ldp, const double *sgn,
+                                     const double *xc, int KP,
                                      const double *nrm, int64_t nb, int64_t t0, int64_t t1,
                                      SinkCollect sc, SinkHist sh, SinkDebug sd, hipStream_t stream)
 {
@@ -2334,12 +2412,12 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
 
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
-                           int64_t ldp, double inv_n, const double *wv, double *phi,
-                           hipStream_t stream)
+                           int64_t ldp, double inv_n, const double *wv, const double *sgn,
+                           double *phi, hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
     const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
-    hipError_t e = launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp,
+    hipError_t e = launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                       nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
                                       SinkDebug{}, stream);
     if (e != hipSuccess) return e;
@@ -2362,7 +2440,7 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
     SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, mode == 0 ? bpart : nullptr};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n};
-    return launch_rows_kernel(10 + mode, d, 1, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, xc,
+    return launch_rows_kernel(10 + mode, d, 1, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, nullptr, xc,
                               KP, nrm, nb, t0, t1, sc, sh, sd, stream);
 }
 
@@ -2644,19 +2722,20 @@ hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int 
 }
 
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                                  int64_t cap, const SelState *st, uint64_t *seg,
+                                  int64_t cap, const SelState *st, uint64_t *seg, int64_t seg_cap,
                                   hipStream_t stream)
 {
     if (nreg <= 0) return hipSuccess;
     const int64_t G = nreg < 512 ? nreg : 512;
     hipLaunchKernelGGL(k_compact_buckets, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap,
-                       st, seg);
+                       st, seg, seg_cap);
     return hipGetLastError();
 }
 
-hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, hipStream_t stream)
+hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
+                               hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg);
+    hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg, seg_cap);
     return hipGetLastError();
 }
 
@@ -2666,21 +2745,22 @@ hipError_t launch_bracket(SelState *st, hipStream_t stream)
     return hipGetLastError();
 }
 
-hipError_t launch_scale_chol(const double *src, double factor, int d, double *M, double *L,
-                             double *scal, int *err, hipStream_t stream)
+hipError_t launch_scale_factor(const double *src, double factor, int d, double *M, double *L,
+                               double *sgn, double *work, double *scal, int *err, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_scale_chol, dim3(1), dim3(64), 0, stream, src, factor, d, M, L, scal, err);
+    hipLaunchKernelGGL(k_scale_factor, dim3(1), dim3(64), 0, stream, src, factor, d, M, L, sgn, work,
+                       scal, err);
     return hipGetLastError();
 }
 
 hipError_t launch_prep_rec_mat(const double *xc, const double *G, const double *M, const double *L,
-                               int64_t n, int64_t np, int d, int KP, int RS, double *rec,
-                               double *wv, hipStream_t stream)
+                               const double *sgn, int64_t n, int64_t np, int d, int KP, int RS,
+                               double *rec, double *wv, hipStream_t stream)
 {
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_prep_rec_mat, dim3(g), dim3(256), 0, stream, xc, G, M, L, n, np, d, KP, RS,
-                       rec, wv);
+    hipLaunchKernelGGL(k_prep_rec_mat, dim3(g), dim3(256), 0, stream, xc, G, M, L, sgn, n, np, d, KP,
+                       RS, rec, wv);
     return hipGetLastError();
 }
 

@@ -70,12 +70,44 @@ def test_hessian_scale_errors(oracle):
         c.step_with_model(model)  # no Hessian sum supplied
     with pytest.raises(ValueError):
         c.set_scale_matrix(np.array([[1.0, 0.5], [0.4, 1.0]]))  # not symmetric
-    c2 = S.Context(d, n)
-    c2.set_particles(oracle.splitmix((n, d), 1.0, 3))
-    c2.set_scale_matrix(np.array([[1.0, 2.0], [2.0, 1.0]]))  # indefinite
-    c2.phi(np.zeros((n, d)), 0.0)
+    # an indefinite M on the MFMA tile path (d > 16) fails loudly before phi
+    d3 = 24
+    c3 = S.Context(d3, n)
+    c3.set_particles(oracle.splitmix((n, d3), 1.0, 3))
+    M3 = np.eye(d3)
+    M3[0, 0] = -0.5
+    c3.set_scale_matrix(M3)
     with pytest.raises(S.DeviceError):
-        c2.get_scale_matrix()
+        c3.phi(np.zeros((n, d3)), 0.0)
+
+
+def _indefinite(d, seed):
+    rng = np.random.default_rng(seed)
+    Q, _ = np.linalg.qr(rng.standard_normal((d, d)))
+    lam = rng.uniform(0.2, 1.0, d) * np.where(np.arange(d) % 3 == 1, -0.3, 1.0)
+    if d == 2:
+        lam = np.array([0.8, -0.25])
+    M = (Q * lam) @ Q.T
+    return 0.5 * (M + M.T)  # exactly symmetric
+
+
+@pytest.mark.parametrize("n,d", [(500, 2), (900, 5), (1500, 8), (700, 16)])
+def test_phi_indefinite_matrix_scale(oracle, n, d):
+    """GaussianRBFKernel.hpp:75-81 evaluates exp(-(x-x')^T M (x-x')) for any
+    symmetric M; an indefinite M (e.g. a Hessian sum between mixture modes)
+    is factored M = L S L^T by the Jacobi eigendecomposition on the row path."""
+    X = oracle.splitmix((n, d), 1.0, 21 + d)
+    G = oracle.splitmix((n, d), 1.0, 22 + d)
+    M = _indefinite(d, d) * (0.5 / d)
+    assert np.min(np.linalg.eigvalsh(M)) < 0
+    c = S.Context(d, n)
+    c.set_particles(X)
+    c.set_scale_matrix(M)
+    ph = c.phi(G, 0.0)
+    ref = oracle.phi_matrix(X, G, M)
+    assert np.max(np.abs(ph - ref)) <= 1e-10 * max(1.0, np.max(np.abs(ref)))
+    np.testing.assert_allclose(c.get_scale_matrix(), M, rtol=1e-15, atol=0)
+    c.close()
 
 
 def test_svgd_class_hessian_scale(oracle):
