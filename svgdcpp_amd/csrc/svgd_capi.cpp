@@ -98,7 +98,6 @@ struct svgd_ctx {
     int64_t regions_alloc = 0;
     uint64_t *cbuf = nullptr;          // compacted candidates (regions_alloc keys)
     unsigned long long *ccount = nullptr;
-    uint32_t *gpart = nullptr;         // per-block histograms (HIST_PART_BLOCKS x 2 RADIX)
     uint32_t *bpart = nullptr;         // collect blocks' key-range bucket histograms (max blocks x NBK)
     uint64_t *gseg = nullptr;          // world x (CAPG + 1): compacted selected-bucket keys
     int64_t bucket_cap = CAPG;         // bucket select path if the selected buckets hold <= this
@@ -125,7 +124,7 @@ struct svgd_ctx {
     double *h_x = nullptr, *h_g = nullptr;
     unsigned long long *h_cnt = nullptr;
     double *h_scal = nullptr;
-    hipEvent_t ev_x = nullptr, ev_cnt = nullptr, ev_scal = nullptr;
+    hipEvent_t ev_x = nullptr, ev_cnt = nullptr, ev_scal = nullptr, ev_fin = nullptr;
     // host<->device copies of the X / G shards run on their own stream so
     // they overlap the median kernels; RCCL calls stay on `stream` (one
     // communicator, one issue order on every rank)
@@ -157,6 +156,21 @@ struct svgd_ctx {
 
     int last_path = SVGD_MEDIAN_DIRECT;
     std::string err;
+
+    // Speculative step (device-side bucket plan, no mid-step host round trip):
+    // taken when the last synchronous median found the bucket path with the
+    // selected buckets under CAPR.  The plan's status is copied back and
+    // checked before the next call that depends on the step; a failed plan
+    // (bracket miss, overflow, big buckets) restores X, m, v, t from the
+    // backups and redoes the step on the synchronous path.
+    bool spec_allowed = true;  // SVGD_SPECULATE=0 disables
+    bool spec_step = false;    // this step's median is speculative
+    bool last_fast = false;    // the last resolved median could have been speculative
+    bool pending = false;      // a speculative step awaits its status
+    bool scal_fresh = true;    // h_scal holds the last scale (fetch_scale)
+    int *d_status = nullptr, *h_status = nullptr;
+    hipEvent_t ev_plan = nullptr, ev_status = nullptr;
+    double *bak = nullptr; // [X_t | m_t | v_t] of this rank's rows for the pending step
 };
 
 namespace {
@@ -301,7 +315,7 @@ int allreduce_f64(svgd_ctx *c, double *buf, size_t cnt)
 int center(svgd_ctx *c)
 {
     HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
-                                 c->nrm, c->rowpath ? 1 : 0, c->xf, c->nmax, c->stream));
+                                 c->nrm, c->rowpath ? 1 : 0, c->xf, c->nmax, c->cnt3 + 3, c->stream));
     if (c->dtype == SVGD_F32) {
         HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
         HIPCHK(c, launch_cvt_f32(c->nrm, c->np, c->nrmf, c->stream));
@@ -312,8 +326,8 @@ int center(svgd_ctx *c)
 // Upload a fresh select state from the host.  Bits >= known_from of every
 // selected key are already known to equal those of `prefix` (64: nothing
 // known; keys are < 2^63); the first digit is the RADIX_BITS below them.
-int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key,
-                 int known_from = 63, uint64_t prefix = 0)
+SelState make_state(int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key,
+                    int known_from = 63, uint64_t prefix = 0)
 {
     SelState s{};
     s.nsel = nsel;
@@ -326,7 +340,20 @@ int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, 
     s.lo_key = lo_key;
     s.hi_key = hi_key;
     s.binv = (double)NBK / (double)(hi_key - lo_key);
+    return s;
+}
+
+int upload_state_s(svgd_ctx *c, const SelState &s)
+{
     HIPCHK(c, launch_set_state(s, c->st, c->stream));
+    return SVGD_OK;
+}
+
+int upload_state(svgd_ctx *c, int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key,
+                 int known_from = 63, uint64_t prefix = 0)
+{
+    HIPCHK(c, launch_set_state(make_state(nsel, ranks, lo_key, hi_key, known_from, prefix), c->st,
+                               c->stream));
     return SVGD_OK;
 }
 
@@ -355,7 +382,8 @@ constexpr double WIDE_SIGMA = 8.0; // re-bracket after a miss
 // slots): wider brackets (tiny samples, tests) take k_pair_rows' collect
 constexpr double MCOL_MAX_BAND = 0.02;
 
-int sample_bracket(svgd_ctx *c, double sigma);
+SelState sample_state(svgd_ctx *c, double sigma);
+int sample_bracket(svgd_ctx *c, bool preset);
 int collect_counts(svgd_ctx *c);
 
 // Phase 1 of the median: candidate bracket + collect pass + counts.
@@ -430,13 +458,16 @@ int median_begin(svgd_ctx *c)
         c->samp_shard = !tile_sample && (c->comm || c->hcomm) && c->shard_sample;
         const int64_t g0 = c->samp_shard ? S * c->rank / c->world : 0;
         c->samp_local = c->samp_shard ? S * (c->rank + 1) / c->world - g0 : S;
-        if (!tile_sample)
-            HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, g0, c->samp_local,
-                                         c->sample_keys, c->stream));
         c->samp_S = S;
         c->samp_qlo = (double)c->sel_rank[0] / (double)M;
         c->samp_qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;
-        CHK(sample_bracket(c, c->bracket_sigma));
+        const SelState init = sample_state(c, c->bracket_sigma);
+        if (!tile_sample)
+            HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, g0, c->samp_local,
+                                         c->sample_keys, init, c->st, c->stream));
+        else
+            HIPCHK(c, launch_set_state(init, c->st, c->stream));
+        CHK(sample_bracket(c, true));
         int64_t pairs_own = tiles * c->pblock * c->pblock;
         int64_t total = c->cand_capacity;
         if (total <= 0) {
@@ -455,9 +486,8 @@ int median_begin(svgd_ctx *c)
 }
 
 // Sample ranks bracketing the target quantiles (sigma sample-quantile standard
-// deviations either side) -> bracket [lo_key, hi_key), which stays on the
-// device (read by the collect pass).
-int sample_bracket(svgd_ctx *c, double sigma)
+// deviations either side): the select state of the bracket passes.
+SelState sample_state(svgd_ctx *c, double sigma)
 {
     const int64_t S = c->samp_S;
     const double qlo = c->samp_qlo, qhi = c->samp_qhi;
@@ -467,16 +497,25 @@ int sample_bracket(svgd_ctx *c, double sigma)
     double shi = std::ceil(qhi * S + sigma * sig_hi) + 1;
     if (slo < 0) slo = 0;
     if (shi > S - 1) shi = (double)(S - 1);
-    uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
+    const uint64_t sr[2] = {(uint64_t)slo, (uint64_t)shi};
     c->band_est = (shi - slo + 1.0) / (double)S; // expected share of pairs in the bracket
-    CHK(upload_state(c, 2, sr, 0, ~0ull));
+    return make_state(2, sr, 0, ~0ull);
+}
+
+// The two radix passes over the sample from that state (already on the device
+// if preset: the sampler wrote it) -> bracket [lo_key, hi_key), which stays on
+// the device (read by the collect pass).  Per pass: one histogram launch
+// (atomics into ghist), the all-reduce if the sample is sharded, one scan
+// launch; the last scan also sets the bracket.
+int sample_bracket(svgd_ctx *c, bool preset)
+{
+    (void)preset;
     for (int p = 0; p < 2; ++p) {
-        HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, c->samp_local, 0, c->st, c->gpart,
-                                      c->ghist, c->stream));
+        HIPCHK(c, launch_hist_regions(c->sample_keys, nullptr, 1, c->samp_local, 0, c->st, c->ghist,
+                                      c->stream));
         if (c->samp_shard) CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
-        HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+        HIPCHK(c, launch_select_scan(c->st, c->ghist, p == 1, c->cnt3 + 3, c->stream));
     }
-    HIPCHK(c, launch_bracket(c->st, c->stream));
     return SVGD_OK;
 }
 
@@ -495,9 +534,33 @@ int collect_counts(svgd_ctx *c)
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
                                    c->collect_grid, c->cnt3, c->stream));
     CHK(allreduce_cnt3(c));
+    if (c->spec_step) return SVGD_OK; // the device plan reads the counts
     HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, CNT_LEN * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_cnt, c->stream));
+    return SVGD_OK;
+}
+
+// Speculative phase 2: plan, compact, gather and select on the device; the
+// plan's status goes to the host on the copy stream (resolve_pending).
+int median_finish_spec(svgd_ctx *c, double logn)
+{
+    uint64_t *seg = c->gseg + (size_t)c->rank * (CAPR + 1);
+    HIPCHK(c, launch_plan_select(c->cnt3, c->st, c->nsel, (uint64_t)c->sel_rank[0],
+                                 (uint64_t)c->sel_rank[c->nsel - 1],
+                                 std::min<int64_t>(c->bucket_cap, CAPR), seg, c->d_status, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_plan, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_plan, 0));
+    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, sizeof(int), hipMemcpyDeviceToHost,
+                             c->cstream));
+    HIPCHK(c, hipEventRecord(c->ev_status, c->cstream));
+    HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
+                                     c->d_status, c->stream));
+    CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
+    HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, CAPR, c->navg, c->src_lo, c->src_hi, logn,
+                                  c->scal, c->d_status, c->stream));
+    c->pending = true;
+    c->last_path = c->med_path;
     return SVGD_OK;
 }
 
@@ -515,6 +578,8 @@ int median_finish(svgd_ctx *c)
         c->last_path = SVGD_MEDIAN_DIRECT;
         return SVGD_OK;
     }
+    if (c->spec_step) return median_finish_spec(c, logn);
+    c->last_fast = false;
     HIPCHK(c, hipEventSynchronize(c->ev_cnt));
     const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
     auto in_bracket = [&]() {
@@ -526,12 +591,13 @@ int median_finish(svgd_ctx *c)
         // ~2e-3 per step at the default 3 sigma): bracket again from the same
         // sample at WIDE_SIGMA and repeat the collect pass (one more pass)
         // instead of the streamed radix select (one pass per 11-bit digit)
-        CHK(sample_bracket(c, std::max(c->bracket_sigma, WIDE_SIGMA)));
+        CHK(upload_state_s(c, sample_state(c, std::max(c->bracket_sigma, WIDE_SIGMA))));
+        CHK(sample_bracket(c, false));
         CHK(collect_counts(c));
         HIPCHK(c, hipEventSynchronize(c->ev_cnt));
         path = SVGD_MEDIAN_REBRACKET;
     }
-    const unsigned long long below = c->h_cnt[0], cand = c->h_cnt[1], ovf = c->h_cnt[2];
+    const unsigned long long below = c->h_cnt[0];
     const uint64_t lo_key = c->h_cnt[CNT_LO], hi_key = c->h_cnt[CNT_HI];
     bool ok = in_bracket();
     uint64_t ranks[2];
@@ -564,12 +630,14 @@ int median_finish(svgd_ctx *c)
                                      (uint64_t)(c->nsel > 1 ? rin[ns - 1] : rin[0]), bsel[0],
                                      bsel[ns - 1], seg, c->stream));
             HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st,
-                                             seg, scap, c->stream));
+                                             seg, scap, nullptr, c->stream));
             CHK(allgather_u64(c, c->gseg, (size_t)scap + 1));
-            HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, scap, c->stream));
-            HIPCHK(c, launch_finalize(c->st, c->navg, c->src_lo, c->src_hi, logn, c->scal,
-                                      c->scal + 1, c->stream));
+            HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, scap, c->navg, c->src_lo,
+                                          c->src_hi, logn, c->scal, nullptr, c->stream));
             c->last_path = path;
+            // the next step may take the device plan if this one would have
+            c->last_fast = (path == SVGD_MEDIAN_BRACKET || path == SVGD_MEDIAN_DIRECT) &&
+                           tot <= std::min<int64_t>(c->bucket_cap, CAPR);
             return SVGD_OK;
         }
     }
@@ -589,15 +657,15 @@ int median_finish(svgd_ctx *c)
             const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->own_tiles, 2048));
             HIPCHK(c, pair_pass(c, 1, grid, nullptr, 0, nullptr));
             CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
-            HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+            HIPCHK(c, launch_select_scan(c->st, c->ghist, 0, nullptr, c->stream));
         }
     } else if (passes > 0) {
         // first digit over every candidate, then only the keys in the chosen
         // bucket(s) are kept (compacted) for the remaining digits
         HIPCHK(c, launch_hist_regions(c->regions, c->counts, c->nregions, c->reg_cap, 0, c->st,
-                                      c->gpart, c->ghist, c->stream));
+                                      c->ghist, c->stream));
         CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
-        HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+        HIPCHK(c, launch_select_scan(c->st, c->ghist, 0, nullptr, c->stream));
         if (passes > 1) {
             HIPCHK(c, launch_compact(c->regions, c->counts, c->nregions, c->reg_cap, c->st, c->cbuf,
                                      c->ccount, c->stream));
@@ -607,9 +675,9 @@ int median_finish(svgd_ctx *c)
             } else {
                 for (int p = 1; p < passes; ++p) {
                     HIPCHK(c, launch_hist_count(c->cbuf, c->ccount, c->regions_alloc, c->st,
-                                                c->gpart, c->ghist, c->stream));
+                                                c->ghist, c->stream));
                     CHK(allreduce_u64(c, c->ghist, 2 * RADIX));
-                    HIPCHK(c, launch_select_scan(c->st, c->ghist, c->stream));
+                    HIPCHK(c, launch_select_scan(c->st, c->ghist, 0, nullptr, c->stream));
                 }
             }
         }
@@ -741,7 +809,8 @@ int run_opt(svgd_ctx *c)
     HIPCHK(c, launch_opt_update(c->opt_kind, c->phi, c->m, c->v, c->X + off, c->nrows * c->dim,
                                 c->dim, c->lr, c->b1, c->b2, c->eps, c1, c2,
                                 c->bounded ? c->lower : nullptr, c->bounded ? c->upper : nullptr,
-                                c->stream));
+                                // X_t, m_t, v_t of this rank's rows for a redo if the device plan failed
+                                c->spec_step ? c->bak : nullptr, c->stream));
     CHK(allgather_rows(c, c->X));
     HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
     return SVGD_OK;
@@ -749,6 +818,7 @@ int run_opt(svgd_ctx *c)
 
 int scale_begin(svgd_ctx *c)
 {
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0)); // the last [a, med] copy has read scal
     CHK(center(c));
     if (c->scale_method == SVGD_SCALE_FIXED || matrix_scale(c)) return SVGD_OK;
     EvPair ev{};
@@ -774,13 +844,69 @@ int scale_finish(svgd_ctx *c)
         HIPCHK(c, hipEventSynchronize(c->ev_scal)); // no D2H into h_scal pending
         c->h_scal[0] = c->fixed_a;
         c->h_scal[1] = NAN;
+        c->scal_fresh = true;
         return SVGD_OK;
     }
     CHK(median_finish(c));
     if (c->timing && !c->ev_med.empty()) HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+    // [a, med] reach the host only when asked (fetch_scale): no copy on the
+    // step's path; the event marks where this step's scale is final
+    HIPCHK(c, hipEventRecord(c->ev_fin, c->stream));
+    c->scal_fresh = false;
+    return SVGD_OK;
+}
+
+// [a, med] of the last scale to h_scal (waits for the step's scale only).
+int fetch_scale(svgd_ctx *c)
+{
+    if (c->scal_fresh) return SVGD_OK;
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_fin, 0));
     HIPCHK(c, hipMemcpyAsync(c->h_scal, c->scal, 2 * sizeof(double), hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipEventRecord(c->ev_scal, c->stream));
+                             c->cstream));
+    HIPCHK(c, hipEventRecord(c->ev_scal, c->cstream));
+    HIPCHK(c, hipEventSynchronize(c->ev_scal));
+    c->scal_fresh = true;
+    return SVGD_OK;
+}
+
+// Check the pending speculative step; on a failed device plan restore X_t,
+// m_t, v_t, t and redo the step on the synchronous path (G_t is still on the
+// device).  Every rank sees the same status (it derives from all-reduced
+// counts), so the redo's collectives match across ranks.
+int resolve_pending(svgd_ctx *c)
+{
+    if (!c->pending) return SVGD_OK;
+    c->pending = false;
+    HIPCHK(c, hipEventSynchronize(c->ev_status));
+    if (*c->h_status == 0) return SVGD_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->cstream));
+    // this rank's rows of X_t, m_t, v_t back, then X_t all-gathered again
+    const size_t sb = sizeof(double) * (size_t)c->nrows * c->dim;
+    const size_t cnt = (size_t)c->nrows * c->dim;
+    if (c->nrows > 0) {
+        HIPCHK(c, hipMemcpyAsync(c->X + (size_t)c->row0 * c->dim, c->bak, sb, hipMemcpyDeviceToDevice,
+                                 c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->m, c->bak + cnt, sb, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->v, c->bak + 2 * cnt, sb, hipMemcpyDeviceToDevice, c->stream));
+    }
+    CHK(allgather_rows(c, c->X));
+    c->t -= 1;
+    c->spec_step = false;
+    c->last_fast = false;
+    CHK(scale_begin(c));
+    CHK(scale_finish(c));
+    CHK(run_phi(c));
+    CHK(run_opt(c));
+    return SVGD_OK;
+}
+
+// Speculate this step's median when the last one would have allowed it.
+int plan_step(svgd_ctx *c)
+{
+    c->spec_step = c->spec_allowed && c->last_fast && c->scale_method == SVGD_SCALE_MEDIAN &&
+                   c->bucket_cap >= CAPR;
+    if (c->spec_step && !c->bak) CHK(dalloc(c, &c->bak, 3 * std::max<int64_t>(1, c->nrows) * c->dim));
     return SVGD_OK;
 }
 
@@ -880,7 +1006,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
-    CHK(dalloc(c, &c->gpart, (int64_t)HIST_PART_BLOCKS * 2 * RADIX));
     CHK(dalloc(c, &c->ccount, 1));
     const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
     HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
@@ -893,6 +1018,13 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_g, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_plan, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_status, hipEventDisableTiming));
+    CHK(dalloc(c, &c->d_status, 1));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_status, sizeof(int), hipHostMallocDefault));
+    *c->h_status = 0;
+    if (const char *e = std::getenv("SVGD_SPECULATE")) c->spec_allowed = std::atoi(e) != 0;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SVGD_OK;
 }
@@ -961,18 +1093,18 @@ int svgd_destroy(svgd_ctx *c)
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
-                       c->sc_sgn,  c->sc_work};
+                       c->sc_sgn,  c->sc_work, c->bak};
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
-                     c->xf,          c->nmax,    c->sc_err, c->cbuf, c->ccount, c->gpart,
+                     c->xf,          c->nmax,    c->sc_err, c->cbuf, c->ccount, c->d_status,
                      c->bpart,       c->gseg};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
-    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err};
+    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err, c->h_status};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
     for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})
@@ -985,6 +1117,9 @@ int svgd_destroy(svgd_ctx *c)
     if (c->ev_g) (void)hipEventDestroy(c->ev_g);
     if (c->ev_cnt) (void)hipEventDestroy(c->ev_cnt);
     if (c->ev_scal) (void)hipEventDestroy(c->ev_scal);
+    if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);
+    if (c->ev_plan) (void)hipEventDestroy(c->ev_plan);
+    if (c->ev_status) (void)hipEventDestroy(c->ev_status);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     delete c;
@@ -1004,6 +1139,7 @@ int svgd_shard(const svgd_ctx *c, int64_t *row0, int64_t *row1)
 int svgd_set_optimizer(svgd_ctx *c, int kind, double lr, double beta1, double beta2, double eps)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     if (kind == SVGD_OPT_ADAM && (beta1 >= 1.0 || beta1 < 0.0 || beta2 >= 1.0 || beta2 < 0.0))
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid value for decay parameter beta.");
     if (kind == SVGD_OPT_RMSPROP && (beta1 > 1.0 || beta1 < 0.0))
@@ -1021,6 +1157,7 @@ int svgd_set_optimizer(svgd_ctx *c, int kind, double lr, double beta1, double be
 int svgd_reset_optimizer(svgd_ctx *c)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     HIPCHK(c, hipSetDevice(c->device));
     const size_t bytes = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * c->dim;
     HIPCHK(c, hipMemsetAsync(c->m, 0, bytes, c->stream));
@@ -1032,6 +1169,7 @@ int svgd_reset_optimizer(svgd_ctx *c)
 int svgd_set_bounds(svgd_ctx *c, const double *lower, const double *upper)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     if (!lower && !upper) {
         c->bounded = false;
         return SVGD_OK;
@@ -1065,6 +1203,7 @@ int alloc_matrix_scale(svgd_ctx *c)
 int svgd_set_scale(svgd_ctx *c, int method, double fixed_a)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     if (method != SVGD_SCALE_MEDIAN && method != SVGD_SCALE_FIXED && method != SVGD_SCALE_HESSIAN)
         return fail(c, SVGD_ERR_ARG, "[Argument error] Invalid scale method Enum provided.");
     if (method == SVGD_SCALE_HESSIAN) CHK(alloc_matrix_scale(c));
@@ -1082,6 +1221,7 @@ int svgd_set_scale_matrix(svgd_ctx *c, const double *M)
         for (int q = 0; q < r; ++q)
             if (M[r * d + q] != M[q * d + r])
                 return fail(c, SVGD_ERR_ARG, "[Argument Error] The kernel scale matrix must be symmetric.");
+    CHK(resolve_pending(c));
     CHK(alloc_matrix_scale(c));
     HIPCHK(c, hipMemcpyAsync(c->sc_src, M, sizeof(double) * (size_t)d * d, hipMemcpyHostToDevice,
                              c->stream));
@@ -1093,6 +1233,7 @@ int svgd_set_scale_matrix(svgd_ctx *c, const double *M)
 int svgd_set_step_hessian_sum(svgd_ctx *c, const double *H_shard_sum)
 {
     if (!c || !H_shard_sum) return c ? fail(c, SVGD_ERR_ARG, "[Argument Error] Null Hessian sum.") : SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     if (c->scale_method != SVGD_SCALE_HESSIAN)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] The kernel scale method is not Hessian.");
     const size_t dd = (size_t)c->dim * c->dim;
@@ -1108,6 +1249,7 @@ int svgd_set_step_hessian_sum(svgd_ctx *c, const double *H_shard_sum)
 int svgd_get_scale_matrix(svgd_ctx *c, double *M_out)
 {
     if (!c || !M_out) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const int d = c->dim;
     if (matrix_scale(c)) {
@@ -1120,6 +1262,7 @@ int svgd_get_scale_matrix(svgd_ctx *c, double *M_out)
         HIPCHK(c, hipMemcpy(M_out, c->sc_M, sizeof(double) * (size_t)d * d, hipMemcpyDeviceToHost));
         return SVGD_OK;
     }
+    CHK(fetch_scale(c));
     const double a = c->scale_method == SVGD_SCALE_FIXED ? c->fixed_a : c->h_scal[0];
     for (int r = 0; r < d; ++r)
         for (int q = 0; q < d; ++q) M_out[r * d + q] = r == q ? a : 0.0;
@@ -1129,6 +1272,7 @@ int svgd_get_scale_matrix(svgd_ctx *c, double *M_out)
 int svgd_set_particles(svgd_ctx *c, const double *X)
 {
     if (!c || !X) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(c->X, X, sizeof(double) * (size_t)c->n * c->dim,
                              hipMemcpyHostToDevice, c->stream));
@@ -1141,6 +1285,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
 int svgd_get_particles(svgd_ctx *c, double *X)
 {
     CHK(check_ready(c));
+    CHK(resolve_pending(c));
     if (!X) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null output buffer.");
     HIPCHK(c, hipMemcpyAsync(X, c->X, sizeof(double) * (size_t)c->n * c->dim,
                              hipMemcpyDeviceToHost, c->stream));
@@ -1151,6 +1296,7 @@ int svgd_get_particles(svgd_ctx *c, double *X)
 int svgd_get_shard(svgd_ctx *c, double *X_shard)
 {
     CHK(check_ready(c));
+    CHK(resolve_pending(c));
     if (c->nrows == 0) return SVGD_OK;
     HIPCHK(c, hipMemcpyAsync(X_shard, c->X + (size_t)c->row0 * c->dim,
                              sizeof(double) * (size_t)c->nrows * c->dim, hipMemcpyDeviceToHost,
@@ -1162,6 +1308,8 @@ int svgd_get_shard(svgd_ctx *c, double *X_shard)
 int svgd_median_scale(svgd_ctx *c, double *a_out, double *med_out)
 {
     CHK(check_ready(c));
+    CHK(resolve_pending(c));
+    c->spec_step = false;
     const int keep = c->scale_method;
     c->scale_method = SVGD_SCALE_MEDIAN;
     int rc = scale_begin(c);
@@ -1169,6 +1317,7 @@ int svgd_median_scale(svgd_ctx *c, double *a_out, double *med_out)
     c->scale_method = keep;
     CHK(rc);
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    CHK(fetch_scale(c));
     if (a_out) *a_out = c->h_scal[0];
     if (med_out) *med_out = c->h_scal[1];
     return SVGD_OK;
@@ -1177,6 +1326,9 @@ int svgd_median_scale(svgd_ctx *c, double *a_out, double *med_out)
 int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
 {
     CHK(check_ready(c));
+    CHK(resolve_pending(c));
+    c->spec_step = false;
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0)); // the last [a, med] copy has read scal
     CHK(center(c));
     HIPCHK(c, launch_set_scal(a, NAN, c->scal, c->stream));
     CHK(upload_g(c, G_shard));
@@ -1192,6 +1344,7 @@ int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
 int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
 {
     CHK(check_ready(c));
+    CHK(resolve_pending(c));
     if (c->opt_kind < 0)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
     const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
@@ -1202,6 +1355,7 @@ int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
                                  hipMemcpyDeviceToHost, c->cstream));
         HIPCHK(c, hipEventRecord(c->ev_x, c->cstream));
     }
+    CHK(plan_step(c));
     CHK(scale_begin(c));
     if (X_shard_out && c->nrows > 0) {
         HIPCHK(c, hipEventSynchronize(c->ev_x));
@@ -1247,6 +1401,7 @@ int svgd_step(svgd_ctx *c, const double *G_shard)
 int svgd_set_device_model(svgd_ctx *c, const void *model)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     if (!model) {
         c->dm_k = 0;
         return SVGD_OK;
@@ -1270,6 +1425,7 @@ int svgd_set_device_model(svgd_ctx *c, const void *model)
 int svgd_device_logp_grad(svgd_ctx *c, double *G_shard_out)
 {
     CHK(check_ready(c));
+    CHK(resolve_pending(c));
     if (c->dm_k == 0) return fail(c, SVGD_ERR_UNSET, "[Unset Error] No device model set.");
     if (!G_shard_out) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null output buffer.");
     HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
@@ -1291,6 +1447,7 @@ int svgd_host_buffers(svgd_ctx *c, double **x_shard, double **g_shard)
 int svgd_sync(svgd_ctx *c)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SVGD_OK;
 }
@@ -1299,7 +1456,8 @@ int svgd_last_scale(const svgd_ctx *c, double *a_out, double *med_out, int *path
 {
     if (!c) return SVGD_ERR_ARG;
     svgd_ctx *m = const_cast<svgd_ctx *>(c);
-    if (m->ev_scal) (void)hipEventSynchronize(m->ev_scal);
+    CHK(resolve_pending(m));
+    CHK(fetch_scale(m));
     if (a_out) *a_out = c->h_scal[0];
     if (med_out) *med_out = c->h_scal[1];
     if (path) *path = c->last_path;
@@ -1310,6 +1468,7 @@ int svgd_last_median_keys(svgd_ctx *c, double *sq_lo, double *sq_hi, int64_t *ra
                           int64_t *rank_hi)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     SelState s;
     HIPCHK(c, hipMemcpy(&s, c->st, sizeof(SelState), hipMemcpyDeviceToHost));
@@ -1338,6 +1497,7 @@ int svgd_set_timing(svgd_ctx *c, int enable)
 int svgd_get_timing(svgd_ctx *c, double *phi_ms, double *median_ms, int64_t *count)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (auto &e : c->ev_phi) {
         float ms = 0;
@@ -1366,6 +1526,7 @@ int svgd_set_median_tuning(svgd_ctx *c, int64_t direct_max_pairs, int64_t sample
                            int64_t candidate_capacity)
 {
     if (!c) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
     if (direct_max_pairs >= 0) c->direct_max_pairs = direct_max_pairs;
     if (sample_size > 0) c->sample_size = sample_size;
     if (candidate_capacity >= 0) c->cand_capacity = candidate_capacity;
@@ -1375,6 +1536,7 @@ int svgd_set_median_tuning(svgd_ctx *c, int64_t direct_max_pairs, int64_t sample
 int svgd_debug_pair_keys(svgd_ctx *c, double *out, int64_t capacity)
 {
     CHK(check_ready(c));
+    CHK(resolve_pending(c));
     const int64_t M = upper_pairs(c->n);
     if (capacity < M) return fail(c, SVGD_ERR_ARG, "[Argument Error] Output buffer too small.");
     if (c->world != 1)

@@ -38,10 +38,11 @@ constexpr int CAPG = 16384;
 // stores |xc|^2 at xc[j*KP + d] (the row-stream median record).
 // xf (optional, d <= 16): fp32 median records [xc | -|xc|^2/2 | 0..] of stride
 // med_f32_stride(d); nmax_bits: max |xc|^2 as double bits (atomicMax).
+// bzero (optional): NBK counters zeroed (the step's collect-pass bucket counts)
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
-                              hipStream_t stream);
+                              unsigned long long *bzero, hipStream_t stream);
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);
@@ -64,10 +65,11 @@ hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_
 hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, const float *xcf,
                                const float *nrmf, int64_t n, int64_t ntiles, uint64_t *keys,
                                hipStream_t stream);
+// bak (optional, 3 cnt doubles): X_t, m_t, v_t of the cnt elements, saved in the pass
 hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
                              int64_t cnt, int d, double lr, double b1, double b2, double eps,
                              double c1, double c2, const double *lower, const double *upper,
-                             hipStream_t stream);
+                             double *bak, hipStream_t stream);
 // mode 0: collect keys in [st->lo_key, st->hi_key) into per-block regions and count
 // keys below lo_key; mode 1: radix histogram pass over all pairs (fallback);
 // mode 2: debug dump of every key in (i<j) row-major order.
@@ -80,23 +82,25 @@ hipError_t launch_pair_tiles(int KP, int mode, int grid, const double *xc, const
 // xf != nullptr (d <= 16): keys from the fp32 records (a bracket estimate only).
 // Sample pairs g0 .. g0+S-1 of the counter-based sequence -> keys[0 .. S-1]
 // (ranks draw disjoint index ranges of one sequence).
+// st_out (optional) <- init: the bracket passes' select state, set by the sampler.
 hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
                               int d, int KP, int64_t g0, int64_t S, uint64_t *keys,
-                              hipStream_t stream);
+                              const SelState &init, SelState *st_out, hipStream_t stream);
+// ghist (2 RADIX u64) += this pass's digit histogram; zero on entry
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                               int64_t cap, int max_blocks, const SelState *st, uint32_t *gpart,
+                               int64_t cap, int max_blocks, const SelState *st,
                                unsigned long long *ghist, hipStream_t stream);
-// gpart: HIST_PART_BLOCKS x 2 RADIX u32 scratch for per-block histograms
-constexpr int HIST_PART_BLOCKS = 256;
 hipError_t launch_compact(const uint64_t *keys, const uint32_t *counts, int64_t nreg, int64_t cap,
                           const SelState *st, uint64_t *cbuf, unsigned long long *ccount,
                           hipStream_t stream);
 hipError_t launch_select_tail(SelState *st, const uint64_t *cbuf, const unsigned long long *ccount,
                               int passes, hipStream_t stream);
 hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *ccount, int64_t cap,
-                             const SelState *st, uint32_t *gpart, unsigned long long *ghist,
-                             hipStream_t stream);
-hipError_t launch_select_scan(SelState *st, unsigned long long *ghist, hipStream_t stream);
+                             const SelState *st, unsigned long long *ghist, hipStream_t stream);
+// make_bracket: the sample's last pass also sets the candidate bracket (and
+// zeroes bzero[0 .. NBK), the coming collect pass's bucket counts)
+hipError_t launch_select_scan(SelState *st, unsigned long long *ghist, int make_bracket,
+                              unsigned long long *bzero, hipStream_t stream);
 // cnt = [below, candidates, overflowed regions, NBK bucket counts (zero without
 // bpart), lo_key, hi_key]: the first 3 + NBK entries are sums over ranks.
 constexpr int CNT_LO = 3 + NBK, CNT_HI = 4 + NBK, CNT_LEN = 5 + NBK;
@@ -115,12 +119,22 @@ hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int 
 // (seg[0] must be zero on entry)
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                   int64_t cap, const SelState *st, uint64_t *seg, int64_t seg_cap,
-                                  hipStream_t stream);
+                                  const int *status, hipStream_t stream);
 // exact selection of st->rank[s] within bucket st->bsel[s] over nseg gathered
-// segments [count, keys...] of stride seg_cap + 1 -> st->prefix[s] = that key
+// segments [count, keys...] of stride seg_cap + 1 -> st->prefix[s] = that key,
+// then the scale as launch_finalize
 hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
-                               hipStream_t stream);
-hipError_t launch_bracket(SelState *st, hipStream_t stream);
+                               int navg, int src_lo, int src_hi, double logn, double *scal,
+                               const int *status, hipStream_t stream);
+// Device-side bucket plan from the all-reduced counts (speculative step): the
+// select state, seg[0] = 0 and *status = 0, or *status = 1 (bracket miss),
+// 2 (overflowed region), 3 (selected buckets hold > capr keys).  The two
+// launchers above do nothing unless *status == 0 (status nullptr: always run).
+hipError_t launch_plan_select(const unsigned long long *cnt, SelState *st, int nsel, uint64_t r0,
+                              uint64_t r1, int64_t capr, uint64_t *seg, int *status,
+                              hipStream_t stream);
+// per-rank segment capacity of the speculative bucket select
+constexpr int CAPR = 4096;
 
 // Row-stream path (d <= 16): particle records rec_j = [xc_j | G_j - 2a xc_j | c_j | 0..],
 // stride phi_rec_stride(d).  phi partials over S column splits -> part[S][ldp][d+1].

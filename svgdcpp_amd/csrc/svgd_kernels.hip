@@ -163,8 +163,11 @@ __global__ void k_mean_partial(const double *__restrict__ X, int64_t n, int d,
 __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
                          const double *__restrict__ partial, int nparts, int64_t np,
                          double *__restrict__ xc, double *__restrict__ nrm, int nrm_in_slot,
-                         float *__restrict__ xf, int KF, unsigned long long *nmax_bits)
+                         float *__restrict__ xf, int KF, unsigned long long *nmax_bits,
+                         unsigned long long *bzero)
 {
+    if (bzero && blockIdx.x == 0) // this step's collect-pass bucket counts
+        for (int e = threadIdx.x; e < NBK; e += blockDim.x) bzero[e] = 0;
     __shared__ double mu[256];
     for (int k = threadIdx.x; k < d; k += blockDim.x) {
         // partials added in b order; 8 loads in flight
@@ -374,15 +377,23 @@ __global__ __launch_bounds__(256) void k_phi(const T *__restrict__ xg, const T *
 // ----------------------------------------------------------- optimizers --
 // Elementwise, bit-exact with the reference expressions (no FMA contraction).
 
+// bak (optional, the speculative step): bak[0..cnt) = X_t, bak[cnt..2cnt) =
+// m_t, bak[2cnt..3cnt) = v_t of these elements, written in the same pass.
 __global__ void k_opt_update(int kind, const double *__restrict__ g, double *__restrict__ m,
                              double *__restrict__ v, double *__restrict__ X, int64_t cnt, int d,
                              double lr, double b1, double b2, double eps, double c1, double c2,
-                             const double *__restrict__ lower, const double *__restrict__ upper)
+                             const double *__restrict__ lower, const double *__restrict__ upper,
+                             double *__restrict__ bak)
 {
 #pragma clang fp contract(off)
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cnt;
          e += (int64_t)gridDim.x * blockDim.x) {
         const double ge = g[e];
+        if (bak) {
+            bak[e] = X[e];
+            bak[cnt + e] = m[e];
+            bak[2 * cnt + e] = v[e];
+        }
         double delta;
         if (kind == 0) { // Adam.hpp:75-83
             const double me = b1 * m[e] + (1 - b1) * ge;
@@ -630,10 +641,13 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
 // Sampled keys: pair (i, j != i) from a splitmix hash of the sample index;
 // region b holds keys [b*per, (b+1)*per).
 
+// st_out (optional): the bracket passes' initial select state, written here
+// so it needs no launch of its own (kernel arguments are captured at launch).
 __global__ void k_sample_keys(const double *__restrict__ xc, const double *__restrict__ nrm,
                               int64_t n, int d, int KP, int64_t g0, int64_t S,
-                              uint64_t *__restrict__ keys)
+                              uint64_t *__restrict__ keys, SelState init, SelState *st_out)
 {
+    if (st_out && blockIdx.x == 0 && threadIdx.x == 0) *st_out = init;
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < S;
          g += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t h = mix64((uint64_t)(g0 + g) * 2 + 1);
@@ -656,8 +670,10 @@ __device__ __forceinline__ int64_t mulhi_index(uint32_t r, int64_t n)
 template <int D>
 __global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict__ xf, int64_t n,
                                                          int64_t g0, int64_t S,
-                                                         uint64_t *__restrict__ keys)
+                                                         uint64_t *__restrict__ keys, SelState init,
+                                                         SelState *st_out)
 {
+    if (st_out && blockIdx.x == 0 && threadIdx.x == 0) *st_out = init;
     constexpr int KF = med_f32_stride(D);
     // SU samples per thread with their record loads in flight together
     constexpr int SU = 1; // (4 in flight measured slower: occupancy, L2-rate bound)
@@ -698,15 +714,16 @@ __global__ __launch_bounds__(256) void k_sample_keys_f32(const float *__restrict
 // cnt_r = counts ? min(counts[r], cap) : cap, for the current digit of each
 // active selection (keys whose resolved high bits match its prefix).  Block b
 // of HIST_BLOCKS (or fewer) takes regions b, b + G, ... (nreg >= G) or one of
-// G / nreg slices of a region, and writes its whole LDS histogram to
-// gpart[b][2 RADIX] (no global atomics: one flush per block instead of one
-// per non-zero bin); k_hist_sum adds the partials in block order.
+// G / nreg slices of a region and adds its LDS histogram's non-zero bins into
+// ghist (64-bit integer atomics, order-free; the keys of one digit crowd into
+// few bins, so a block flushes few) -- one launch per pass, no partials sum.
+// ghist is zero on entry (k_select_scan clears it after each pass).
 constexpr int HIST_BLOCKS = 256;
 __global__ __launch_bounds__(256) void k_hist_regions(const uint64_t *__restrict__ keys,
                                                      const uint32_t *__restrict__ counts,
                                                      int64_t nreg, int64_t cap,
                                                      const SelState *__restrict__ st,
-                                                     uint32_t *__restrict__ gpart)
+                                                     unsigned long long *__restrict__ ghist)
 {
     __shared__ uint32_t sHist[2 * RADIX];
     for (int e = threadIdx.x; e < 2 * RADIX; e += 256) sHist[e] = 0;
@@ -744,33 +761,8 @@ __global__ __launch_bounds__(256) void k_hist_regions(const uint64_t *__restrict
         if (nreg < G) break;
     }
     __syncthreads();
-    uint32_t *o = gpart + (int64_t)blockIdx.x * 2 * RADIX;
-    for (int e = threadIdx.x; e < 2 * RADIX; e += 256) o[e] = sHist[e];
-}
-
-// ghist[e] = sum_b gpart[b][e] (integer sums: order-free).  A block covers 64
-// bins; its 4 waves take every 4th partial, 8 loads in flight per lane.
-__global__ __launch_bounds__(256) void k_hist_sum(const uint32_t *__restrict__ gpart, int nparts,
-                                                 unsigned long long *__restrict__ ghist)
-{
-    __shared__ uint32_t sAcc[4][64];
-    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + lane;
-    uint32_t acc = 0;
-    for (int b0 = g; b0 < nparts; b0 += 32) {
-        uint32_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int b = b0 + 4 * u;
-            v[u] = b < nparts ? gpart[(int64_t)b * 2 * RADIX + e] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc += v[u];
-    }
-    sAcc[g][lane] = acc;
-    __syncthreads();
-    if (g == 0)
-        ghist[e] = (unsigned long long)sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
+    for (int e = threadIdx.x; e < 2 * RADIX; e += 256)
+        if (sHist[e]) atomicAdd(&ghist[e], (unsigned long long)sHist[e]);
 }
 
 // Keys of the regions whose resolved high bits (>= shift + width after the
@@ -908,35 +900,79 @@ __global__ __launch_bounds__(1024) void k_select_tail(SelState *st, const uint64
 }
 
 // ------------------------------------------------ bucket select path --
-// out[e] += sum over a slice of the partials bpart[b][e] (integer sums:
-// order-free).  Grid = (NBK / 64 bucket groups) x BSUM_SLICES partial slices;
-// out must be zero on entry (k_counts_reduce clears it).
-constexpr int BSUM_SLICES = 16;
-__global__ __launch_bounds__(256) void k_bucket_sum(const uint32_t *__restrict__ bpart, int nparts,
-                                                   unsigned long long *__restrict__ out)
+// Device-side bucket plan (the speculative step: no host round trip between
+// the collect pass and the selection).  From the all-reduced counts: the
+// order statistics are in the bracket (no overflowed region, r0 >= below,
+// r1 < below + candidates), their buckets (svgd_plan_bucket_select's scan,
+// here 256 threads x 8 buckets + a block scan) and the selected buckets'
+// total <= capr.  Then the select state for k_compact_buckets /
+// k_select_small, this rank's segment counter zeroed, *status = 0; otherwise
+// *status = 1 (bracket miss), 2 (overflowed region) or 3 (selected buckets
+// above capr) and the selection kernels do nothing -- the host redoes the step
+// on its synchronous path.
+__global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *__restrict__ cnt,
+                                                    SelState *st, int nsel, uint64_t r0,
+                                                    uint64_t r1, int64_t capr, uint64_t *seg,
+                                                    int *status)
 {
-    __shared__ unsigned long long sAcc[4][64];
-    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
-    const int e = blockIdx.x * 64 + lane;
-    const int per = (nparts + BSUM_SLICES - 1) / BSUM_SLICES;
-    const int p0 = blockIdx.y * per, p1 = min(nparts, p0 + per);
-    unsigned long long acc = 0;
-    for (int b0 = p0 + g; b0 < p1; b0 += 32) {
-        uint32_t v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int b = b0 + 4 * u;
-            v[u] = b < p1 ? bpart[(int64_t)b * NBK + e] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc += v[u];
+    __shared__ unsigned long long sPart[256];
+    __shared__ int sB[2];
+    __shared__ unsigned long long sIn[2];
+    const int tid = threadIdx.x;
+    const unsigned long long below = cnt[0], cand = cnt[1], ovf = cnt[2];
+    if (ovf || r0 < below || r1 >= below + cand) {
+        if (tid == 0) *status = ovf ? 2 : 1;
+        return;
     }
-    sAcc[g][lane] = acc;
+    const unsigned long long q[2] = {r0 - below, r1 - below};
+    const int ns = (nsel > 1 && q[1] != q[0]) ? 2 : 1;
+    constexpr int PER = NBK / 256;
+    unsigned long long loc = 0;
+    for (int u = 0; u < PER; ++u) loc += cnt[3 + tid * PER + u];
+    sPart[tid] = loc;
+    if (tid < 2) sB[tid] = -1;
     __syncthreads();
-    if (g == 0) {
-        const unsigned long long t = sAcc[0][lane] + sAcc[1][lane] + sAcc[2][lane] + sAcc[3][lane];
-        if (t) atomicAdd(&out[e], t);
+    for (int o = 1; o < 256; o <<= 1) {
+        const unsigned long long v = tid >= o ? sPart[tid - o] : 0ull;
+        __syncthreads();
+        sPart[tid] += v;
+        __syncthreads();
     }
+    const unsigned long long excl = tid ? sPart[tid - 1] : 0ull;
+    for (int s = 0; s < ns; ++s)
+        if (q[s] >= excl && q[s] < sPart[tid]) {
+            unsigned long long c = excl;
+            for (int u = 0; u < PER; ++u) {
+                const unsigned long long h = cnt[3 + tid * PER + u];
+                if (q[s] < c + h) {
+                    sB[s] = tid * PER + u;
+                    sIn[s] = q[s] - c;
+                    break;
+                }
+                c += h;
+            }
+        }
+    __syncthreads();
+    if (tid != 0) return;
+    if (sB[0] < 0 || (ns > 1 && sB[1] < 0)) {
+        *status = 1;
+        return;
+    }
+    const int b0 = sB[0], b1 = ns > 1 ? sB[1] : sB[0];
+    const unsigned long long tot = cnt[3 + b0] + (b1 != b0 ? cnt[3 + b1] : 0ull);
+    if (tot > (unsigned long long)capr) {
+        *status = 3;
+        return;
+    }
+    st->nsel = nsel;
+    st->rank[0] = sIn[0];
+    st->rank[1] = nsel > 1 ? sIn[ns - 1] : sIn[0];
+    st->bsel[0] = b0;
+    st->bsel[1] = b1;
+    st->prefix[0] = st->prefix[1] = 0;
+    st->error = 0;
+    seg[0] = 0; // compaction counter of this rank's segment
+    *status = 0;
 }
 
 // Whole select state / scale from kernel arguments (captured at launch, so the
@@ -971,8 +1007,10 @@ __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restr
                                                         const uint32_t *__restrict__ counts,
                                                         int64_t nreg, int64_t cap,
                                                         const SelState *__restrict__ st,
-                                                        uint64_t *__restrict__ seg, int64_t seg_cap)
+                                                        uint64_t *__restrict__ seg, int64_t seg_cap,
+                                                        const int *__restrict__ status)
 {
+    if (status && *status != 0) return; // the device plan found no bucket path
     __shared__ uint64_t sK[CB_LDS];
     __shared__ int sN;
     __shared__ unsigned long long sBase;
@@ -1063,9 +1101,17 @@ __device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long
 // block scan) start below the common prefix of the selected buckets' keys
 // (bits above it are equal for every key of a bucket), so a narrow bucket
 // needs 2-3 passes.
+// The last thread also maps the selected keys to the scale (k_finalize's
+// arithmetic): scal = [a, med].
+__device__ __forceinline__ void finalize_scale(const SelState *st, int navg, int src_lo, int src_hi,
+                                               double logn, double *a_out, double *med_out);
 __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint64_t *__restrict__ segs,
-                                                      int nseg, int64_t seg_cap)
+                                                      int nseg, int64_t seg_cap, int navg,
+                                                      int src_lo, int src_hi, double logn,
+                                                      double *__restrict__ scal,
+                                                      const int *__restrict__ status)
 {
+    if (status && *status != 0) return; // the device plan found no bucket path
     __shared__ uint32_t sHist[2][RADIX];
     __shared__ unsigned long long sW[16];
     __shared__ unsigned long long sMn[2][16], sMx[2][16];
@@ -1187,14 +1233,20 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
         if (err) st->error = 1;
         st->prefix[0] = prefix[0];
         if (nsel > 1) st->prefix[1] = prefix[1];
+        finalize_scale(st, navg, src_lo, src_hi, logn, scal, scal + 1);
     }
 }
 
 // One radix-select step: for each active selection find the digit holding
 // its remaining rank, append it to the prefix, subtract the count below,
 // zero the histogram and advance to the next digit.
-__global__ __launch_bounds__(256) void k_select_scan(SelState *st, unsigned long long *ghist)
+// make_bracket (the sample's last pass): also the candidate bracket [lo_key,
+// hi_key) from the buckets of selection 0 (lower edge) and 1 (upper edge).
+__global__ __launch_bounds__(256) void k_select_scan(SelState *st, unsigned long long *ghist,
+                                                    int make_bracket, unsigned long long *bzero)
 {
+    if (make_bracket && bzero) // the coming collect pass's bucket counts
+        for (int e = threadIdx.x; e < NBK; e += 256) bzero[e] = 0;
     __shared__ unsigned long long sPart[256];
     __shared__ int sDigit;
     __shared__ unsigned long long sBelowD;
@@ -1247,19 +1299,60 @@ __global__ __launch_bounds__(256) void k_select_scan(SelState *st, unsigned long
         st->shift = nshift >= 0 ? nshift : 0;
         st->width = nshift >= 0 ? RADIX_BITS : shift;
         (void)width;
+        if (make_bracket) {
+            const int sh = st->shift + st->width; // bits below the resolved digits
+            st->lo_key = st->prefix[0];
+            const uint64_t top = st->prefix[1] + (sh >= 64 ? 0ull : (1ull << sh));
+            st->hi_key = (top < st->prefix[1]) ? ~0ull : top;
+            st->binv = (double)NBK / (double)(st->hi_key - st->lo_key);
+        }
     }
 }
 
-// Sum per-region collect outputs: cnt[0] = below, cnt[1] = candidates (true
-// count), cnt[2] = number of overflowed regions (all sums, so one all-reduce
-// serves every rank); cnt[3..4] = the bracket [lo_key, hi_key) for the host.
-__global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
-                                const uint32_t *__restrict__ counts, int64_t nblk, int64_t cap,
-                                const SelState *__restrict__ st,
-                                unsigned long long *__restrict__ cnt)
+// Collect outputs -> cnt, in one launch.  Blocks 0 .. NBK/64-1: the
+// key-range bucket counts cnt[3 + e] = sum_b bpart[b][e] (zero without
+// bpart; integer sums in fixed order).  The last block: cnt[0] = below,
+// cnt[1] = candidates (true count), cnt[2] = overflowed regions (all sums, so
+// one all-reduce serves every rank), cnt[CNT_LO..CNT_HI] = the bracket for
+// the host.
+constexpr int BSUM_SLICES = 16; // partial slices per 64-bucket group (k_counts_reduce)
+__global__ __launch_bounds__(256) void k_counts_reduce(const unsigned long long *__restrict__ below,
+                                                      const uint32_t *__restrict__ counts,
+                                                      int64_t nblk, int64_t cap,
+                                                      const SelState *__restrict__ st,
+                                                      const uint32_t *__restrict__ bpart,
+                                                      int64_t nbpart,
+                                                      unsigned long long *__restrict__ cnt)
 {
     __shared__ unsigned long long s0[256], s1[256], s2[256];
-    for (int e = threadIdx.x; e < NBK; e += 256) cnt[3 + e] = 0; // k_bucket_sum adds into these
+    if ((int)blockIdx.x < NBK / 64 * BSUM_SLICES) {
+        // bucket group blockIdx % (NBK/64), partial slice blockIdx / (NBK/64);
+        // cnt[3 .. 3 + NBK) was zeroed this step (k_center / the bracket scan)
+        if (!bpart) return;
+        const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+        const int grp = blockIdx.x % (NBK / 64), sl = blockIdx.x / (NBK / 64);
+        const int e = grp * 64 + lane;
+        const int64_t per = (nbpart + BSUM_SLICES - 1) / BSUM_SLICES;
+        const int64_t p0 = sl * per, p1 = min(nbpart, p0 + per);
+        unsigned long long acc = 0;
+        for (int64_t b0 = p0 + g; b0 < p1; b0 += 32) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t b = b0 + 4 * u;
+                v[u] = b < p1 ? bpart[b * NBK + e] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc += v[u];
+        }
+        s0[threadIdx.x] = acc;
+        __syncthreads();
+        if (g == 0) {
+            const unsigned long long t = s0[lane] + s0[64 + lane] + s0[128 + lane] + s0[192 + lane];
+            if (t) atomicAdd(&cnt[3 + e], t);
+        }
+        return;
+    }
     unsigned long long b = 0, c = 0, o = 0;
     for (int64_t e = threadIdx.x; e < nblk; e += 256) {
         b += below[e];
@@ -1287,23 +1380,12 @@ __global__ void k_counts_reduce(const unsigned long long *__restrict__ below,
     }
 }
 
-// After the truncated sample select: bracket [lo_key, hi_key) from the
-// bucket of selection 0 (lower edge) and of selection 1 (upper edge).
-__global__ void k_bracket(SelState *st)
-{
-    const int sh = st->shift + st->width; // bits below the resolved digits
-    st->lo_key = st->prefix[0];
-    const uint64_t top = st->prefix[1] + (sh >= 64 ? 0ull : (1ull << sh));
-    st->hi_key = (top < st->prefix[1]) ? ~0ull : top;
-    st->binv = (double)NBK / (double)(st->hi_key - st->lo_key);
-}
-
 // med = (sqrt(u_lo) + sqrt(u_hi)) / 2 (or the single middle value);
 // a = ln(n) / med^2  (GaussianRBFKernel.hpp:187, ComputeMedian :222-254).
 // src_lo / src_hi: selection slot holding each order statistic, -1 for a
 // diagonal zero of the full n^2 list.
-__global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
-                           double *a_out, double *med_out)
+__device__ __forceinline__ void finalize_scale(const SelState *st, int navg, int src_lo, int src_hi,
+                                               double logn, double *a_out, double *med_out)
 {
     const double u0 =
         src_lo < 0 ? 0.0 : sqrt(__longlong_as_double((long long)st->prefix[src_lo]));
@@ -1317,6 +1399,11 @@ __global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi,
     }
     *med_out = med;
     *a_out = logn / (med * med);
+}
+__global__ void k_finalize(const SelState *st, int navg, int src_lo, int src_hi, double logn,
+                           double *a_out, double *med_out)
+{
+    finalize_scale(st, navg, src_lo, src_hi, logn, a_out, med_out);
 }
 
 // ===================================================== row-stream kernels ==
@@ -1753,7 +1840,7 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
 // A block owns PHI_RED_ROWS rows: their (d+1)-element partial rows are
 // contiguous in every split s, so the sums are read coalesced into LDS, then
 // phi is written coalesced from LDS.
-constexpr int PHI_RED_ROWS = 128;
+constexpr int PHI_RED_ROWS = 32; // rows per block (enough blocks to fill the chip at small N)
 __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ part,
                                                     const double *__restrict__ rec,
                                                     const double *__restrict__ a_ptr, int64_t row0,
@@ -2574,14 +2661,14 @@ hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
-                              hipStream_t stream)
+                              unsigned long long *bzero, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial,
                        xf ? nmax_bits : nullptr);
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_center, dim3(g), dim3(256), 0, stream, X, n, d, KP, partial, nparts, np,
-                       xc, nrm, nrm_in_slot, xf, med_f32_stride(d), nmax_bits);
+                       xc, nrm, nrm_in_slot, xf, med_f32_stride(d), nmax_bits, bzero);
     return hipGetLastError();
 }
 
@@ -2599,30 +2686,32 @@ hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, c
 hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
                              int64_t cnt, int d, double lr, double b1, double b2, double eps,
                              double c1, double c2, const double *lower, const double *upper,
-                             hipStream_t stream)
+                             double *bak, hipStream_t stream)
 {
     if (cnt <= 0) return hipSuccess;
     int64_t grid = (cnt + 255) / 256;
     if (grid > 8192) grid = 8192;
     hipLaunchKernelGGL(k_opt_update, dim3(grid), dim3(256), 0, stream, kind, g, m, v, X, cnt, d,
-                       lr, b1, b2, eps, c1, c2, lower, upper);
+                       lr, b1, b2, eps, c1, c2, lower, upper, bak);
     return hipGetLastError();
 }
 
 #define SVGD_SAMPLE_CASE(Dv)                                                                 \
     case Dv:                                                                                 \
-        hipLaunchKernelGGL((k_sample_keys_f32<Dv>), dim3(g), dim3(256), 0, stream, xf, n, g0, S, keys); \
+        hipLaunchKernelGGL((k_sample_keys_f32<Dv>), dim3(g), dim3(256), 0, stream, xf, n, g0, S, keys, \
+                           init, st_out);                                                    \
         break;
 
 hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *xf, int64_t n,
                               int d, int KP, int64_t g0, int64_t S, uint64_t *keys,
-                              hipStream_t stream)
+                              const SelState &init, SelState *st_out, hipStream_t stream)
 {
     int64_t g = (S + 255) / 256;
     if (g > 4096) g = 4096;
+    if (g < 1) g = 1; // (writes st_out even for an empty sample shard)
     if (!xf) {
         hipLaunchKernelGGL(k_sample_keys, dim3(g), dim3(256), 0, stream, xc, nrm, n, d, KP, g0, S,
-                           keys);
+                           keys, init, st_out);
         return hipGetLastError();
     }
     switch (d) {
@@ -2637,7 +2726,7 @@ hipError_t launch_sample_keys(const double *xc, const double *nrm, const float *
 }
 
 hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                               int64_t cap, int max_blocks, const SelState *st, uint32_t *gpart,
+                               int64_t cap, int max_blocks, const SelState *st,
                                unsigned long long *ghist, hipStream_t stream)
 {
     if (nreg <= 0) return hipSuccess;
@@ -2646,8 +2735,6 @@ hipError_t launch_hist_regions(const uint64_t *keys, const uint32_t *counts, int
     if (nreg < G) G = (G / nreg) * nreg; // whole slices per region
     if (G < 1) G = 1;
     hipLaunchKernelGGL(k_hist_regions, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap, st,
-                       gpart);
-    hipLaunchKernelGGL(k_hist_sum, dim3(2 * RADIX / 64), dim3(256), 0, stream, gpart, (int)G,
                        ghist);
     return hipGetLastError();
 }
@@ -2674,17 +2761,17 @@ hipError_t launch_select_tail(SelState *st, const uint64_t *cbuf, const unsigned
 }
 
 hipError_t launch_hist_count(const uint64_t *keys, const unsigned long long *ccount, int64_t cap,
-                             const SelState *st, uint32_t *gpart, unsigned long long *ghist,
-                             hipStream_t stream)
+                             const SelState *st, unsigned long long *ghist, hipStream_t stream)
 {
     // one region whose count lives on the device (compacted keys; < 2^32)
     return launch_hist_regions(keys, reinterpret_cast<const uint32_t *>(ccount), 1, cap, 64, st,
-                               gpart, ghist, stream);
+                               ghist, stream);
 }
 
-hipError_t launch_select_scan(SelState *st, unsigned long long *ghist, hipStream_t stream)
+hipError_t launch_select_scan(SelState *st, unsigned long long *ghist, int make_bracket,
+                              unsigned long long *bzero, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_select_scan, dim3(1), dim3(256), 0, stream, st, ghist);
+    hipLaunchKernelGGL(k_select_scan, dim3(1), dim3(256), 0, stream, st, ghist, make_bracket, bzero);
     return hipGetLastError();
 }
 
@@ -2693,12 +2780,8 @@ hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t 
                                 const uint32_t *bpart, int64_t nbpart,
                                 unsigned long long *cnt, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_counts_reduce, dim3(1), dim3(256), 0, stream, below, counts, nblk, cap,
-                       st, cnt);
-    // (k_counts_reduce cleared the bucket counts cnt[3 .. 3 + NBK))
-    if (bpart && nbpart > 0)
-        hipLaunchKernelGGL(k_bucket_sum, dim3(NBK / 64, BSUM_SLICES), dim3(256), 0, stream, bpart,
-                           (int)nbpart, cnt + 3);
+    hipLaunchKernelGGL(k_counts_reduce, dim3(NBK / 64 * BSUM_SLICES + 1), dim3(256), 0, stream, below,
+                       counts, nblk, cap, st, bpart, nbpart, cnt);
     return hipGetLastError();
 }
 
@@ -2723,25 +2806,30 @@ hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int 
 
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                   int64_t cap, const SelState *st, uint64_t *seg, int64_t seg_cap,
-                                  hipStream_t stream)
+                                  const int *status, hipStream_t stream)
 {
     if (nreg <= 0) return hipSuccess;
     const int64_t G = nreg < 512 ? nreg : 512;
     hipLaunchKernelGGL(k_compact_buckets, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap,
-                       st, seg, seg_cap);
+                       st, seg, seg_cap, status);
     return hipGetLastError();
 }
 
 hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
-                               hipStream_t stream)
+                               int navg, int src_lo, int src_hi, double logn, double *scal,
+                               const int *status, hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg, seg_cap);
+    hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg, seg_cap,
+                       navg, src_lo, src_hi, logn, scal, status);
     return hipGetLastError();
 }
 
-hipError_t launch_bracket(SelState *st, hipStream_t stream)
+hipError_t launch_plan_select(const unsigned long long *cnt, SelState *st, int nsel, uint64_t r0,
+                              uint64_t r1, int64_t capr, uint64_t *seg, int *status,
+                              hipStream_t stream)
 {
-    hipLaunchKernelGGL(k_bracket, dim3(1), dim3(1), 0, stream, st);
+    hipLaunchKernelGGL(k_plan_select, dim3(1), dim3(256), 0, stream, cnt, st, nsel, r0, r1, capr,
+                       seg, status);
     return hipGetLastError();
 }
 
