@@ -168,8 +168,8 @@ struct svgd_ctx {
     bool last_fast = false;    // the last resolved median could have been speculative
     bool pending = false;      // a speculative step awaits its status
     bool scal_fresh = true;    // h_scal holds the last scale (fetch_scale)
-    int *d_status = nullptr, *h_status = nullptr;
-    hipEvent_t ev_plan = nullptr, ev_status = nullptr;
+    int *d_status = nullptr, *h_status = nullptr, *h_status_dev = nullptr; // (h_status as seen by kernels)
+    hipEvent_t ev_status = nullptr;
     double *bak = nullptr; // [X_t | m_t | v_t] of this rank's rows for the pending step
 };
 
@@ -546,14 +546,14 @@ int collect_counts(svgd_ctx *c)
 int median_finish_spec(svgd_ctx *c, double logn)
 {
     uint64_t *seg = c->gseg + (size_t)c->rank * (CAPR + 1);
+    // the plan also stores its status straight into pinned host memory: no
+    // copy on the copy stream (a small copy there turned the X shard copies
+    // into blit kernels competing with the median kernels)
     HIPCHK(c, launch_plan_select(c->cnt3, c->st, c->nsel, (uint64_t)c->sel_rank[0],
                                  (uint64_t)c->sel_rank[c->nsel - 1],
-                                 std::min<int64_t>(c->bucket_cap, CAPR), seg, c->d_status, c->stream));
-    HIPCHK(c, hipEventRecord(c->ev_plan, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_plan, 0));
-    HIPCHK(c, hipMemcpyAsync(c->h_status, c->d_status, sizeof(int), hipMemcpyDeviceToHost,
-                             c->cstream));
-    HIPCHK(c, hipEventRecord(c->ev_status, c->cstream));
+                                 std::min<int64_t>(c->bucket_cap, CAPR), seg, c->d_status,
+                                 c->h_status_dev, c->stream));
+    HIPCHK(c, hipEventRecord(c->ev_status, c->stream));
     HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
                                      c->d_status, c->stream));
     CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
@@ -1019,11 +1019,11 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming));
-    HIPCHK(c, hipEventCreateWithFlags(&c->ev_plan, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_status, hipEventDisableTiming));
     CHK(dalloc(c, &c->d_status, 1));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_status, sizeof(int), hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_status, sizeof(int), hipHostMallocCoherent));
     *c->h_status = 0;
+    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_status_dev, c->h_status, 0));
     if (const char *e = std::getenv("SVGD_SPECULATE")) c->spec_allowed = std::atoi(e) != 0;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SVGD_OK;
@@ -1118,7 +1118,6 @@ int svgd_destroy(svgd_ctx *c)
     if (c->ev_cnt) (void)hipEventDestroy(c->ev_cnt);
     if (c->ev_scal) (void)hipEventDestroy(c->ev_scal);
     if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);
-    if (c->ev_plan) (void)hipEventDestroy(c->ev_plan);
     if (c->ev_status) (void)hipEventDestroy(c->ev_status);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);

@@ -128,11 +128,12 @@ hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int
                                const int *status, hipStream_t stream);
 // Device-side bucket plan from the all-reduced counts (speculative step): the
 // select state, seg[0] = 0 and *status = 0, or *status = 1 (bracket miss),
-// 2 (overflowed region), 3 (selected buckets hold > capr keys).  The two
+// 2 (overflowed region), 3 (selected buckets hold > capr keys), also stored to
+// host_status (device view of pinned host memory; optional).  The two
 // launchers above do nothing unless *status == 0 (status nullptr: always run).
 hipError_t launch_plan_select(const unsigned long long *cnt, SelState *st, int nsel, uint64_t r0,
                               uint64_t r1, int64_t capr, uint64_t *seg, int *status,
-                              hipStream_t stream);
+                              int *host_status, hipStream_t stream);
 // per-rank segment capacity of the speculative bucket select
 constexpr int CAPR = 4096;
 

@@ -910,18 +910,28 @@ __global__ __launch_bounds__(1024) void k_select_tail(SelState *st, const uint64
 // *status = 1 (bracket miss), 2 (overflowed region) or 3 (selected buckets
 // above capr) and the selection kernels do nothing -- the host redoes the step
 // on its synchronous path.
+// The status also goes to host_status (pinned host memory, read after the
+// launch's completion event).
 __global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *__restrict__ cnt,
                                                     SelState *st, int nsel, uint64_t r0,
                                                     uint64_t r1, int64_t capr, uint64_t *seg,
-                                                    int *status)
+                                                    int *status_arg, int *host_status)
 {
+    struct Status {
+        int *d, *h;
+        __device__ void operator=(int v) const
+        {
+            *d = v;
+            if (h) *h = v;
+        }
+    } status{status_arg, host_status};
     __shared__ unsigned long long sPart[256];
     __shared__ int sB[2];
     __shared__ unsigned long long sIn[2];
     const int tid = threadIdx.x;
     const unsigned long long below = cnt[0], cand = cnt[1], ovf = cnt[2];
     if (ovf || r0 < below || r1 >= below + cand) {
-        if (tid == 0) *status = ovf ? 2 : 1;
+        if (tid == 0) status = ovf ? 2 : 1;
         return;
     }
     const unsigned long long q[2] = {r0 - below, r1 - below};
@@ -955,13 +965,13 @@ __global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *_
     __syncthreads();
     if (tid != 0) return;
     if (sB[0] < 0 || (ns > 1 && sB[1] < 0)) {
-        *status = 1;
+        status = 1;
         return;
     }
     const int b0 = sB[0], b1 = ns > 1 ? sB[1] : sB[0];
     const unsigned long long tot = cnt[3 + b0] + (b1 != b0 ? cnt[3 + b1] : 0ull);
     if (tot > (unsigned long long)capr) {
-        *status = 3;
+        status = 3;
         return;
     }
     st->nsel = nsel;
@@ -972,7 +982,7 @@ __global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *_
     st->prefix[0] = st->prefix[1] = 0;
     st->error = 0;
     seg[0] = 0; // compaction counter of this rank's segment
-    *status = 0;
+    status = 0;
 }
 
 // Whole select state / scale from kernel arguments (captured at launch, so the
@@ -2826,10 +2836,10 @@ hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int
 
 hipError_t launch_plan_select(const unsigned long long *cnt, SelState *st, int nsel, uint64_t r0,
                               uint64_t r1, int64_t capr, uint64_t *seg, int *status,
-                              hipStream_t stream)
+                              int *host_status, hipStream_t stream)
 {
     hipLaunchKernelGGL(k_plan_select, dim3(1), dim3(256), 0, stream, cnt, st, nsel, r0, r1, capr,
-                       seg, status);
+                       seg, status, host_status);
     return hipGetLastError();
 }
 
