@@ -85,7 +85,7 @@ struct svgd_ctx {
     double bracket_sigma = 3.0; // sample-quantile standard deviations either side
     bool shard_sample = true;   // P > 1: ranks draw disjoint parts of the sample
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
-    bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol)
+    bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol / _tcol)
     double band_est = 1.0;         // this step's bracket: expected share of the pairs
     bool samp_shard = false;    // this step's sample is sharded
     int64_t samp_local = 0;     // sample keys held by this rank
@@ -461,7 +461,11 @@ int median_begin(svgd_ctx *c)
         c->samp_S = S;
         c->samp_qlo = (double)c->sel_rank[0] / (double)M;
         c->samp_qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;
-        const SelState init = sample_state(c, c->bracket_sigma);
+        // whole-tile samples are correlated (a far particle shifts its tile's
+        // 64 x 64 keys together): 3 sigma of S independent draws missed the
+        // bracket on ~40 % of cfg5 steps (each miss: a second collect pass);
+        // 12 measured none at no cost (the band stays ~1 % of the pairs)
+        const SelState init = sample_state(c, tile_sample ? 4.0 * c->bracket_sigma : c->bracket_sigma);
         if (!tile_sample)
             HIPCHK(c, launch_sample_keys(c->xc, c->nrm, c->xf, n, c->dim, c->KP, g0, c->samp_local,
                                          c->sample_keys, init, c->st, c->stream));
@@ -529,6 +533,11 @@ int collect_counts(svgd_ctx *c)
         HIPCHK(c, launch_pair_mcol(c->dim, c->collect_grid, c->xc, c->xf, c->nmax, c->n, c->pnb,
                                    c->tile0, c->tile0 + c->own_tiles, c->regions, c->reg_cap,
                                    c->counts, c->below, c->st, c->bpart, c->stream));
+    else if (!c->rowpath && c->dtype == SVGD_F32 && c->mcol)
+        // fp32 tile path: k_pair_tiles' keys, rows held in VGPRs, no LDS
+        HIPCHK(c, launch_pair_tcol(c->KP, c->collect_grid, c->xcf, c->nrmf, c->n, c->pnb, c->tile0,
+                                   c->tile0 + c->own_tiles, c->regions, c->reg_cap, c->counts,
+                                   c->below, c->st, c->bpart, c->stream));
     else
         HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
@@ -948,6 +957,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->nrm, c->np));
     CHK(dalloc(c, &c->cvec, c->np));
     c->rowpath = dim <= ROWS_MAX_D && !f32;
+    // k_pair_tcol holds 3 blocks per CU (152 VGPRs at d = 64): one full round
+    if (f32) c->collect_blocks = 768;
     if (f32) {
         CHK(dalloc(c, &c->xcf, c->np * c->KP));
         CHK(dalloc(c, &c->nrmf, c->np));
@@ -1001,7 +1012,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     if (const char *e = std::getenv("SVGD_COLLECT_BLOCKS")) // buffers hold <= MAX_COLLECT_BLOCKS
         c->collect_blocks = std::min<int64_t>(MAX_COLLECT_BLOCKS, std::max(1, std::atoi(e)));
     if (const char *e = std::getenv("SVGD_SAMPLE_SHARD")) c->shard_sample = std::atoi(e) != 0;
-    // A/B and test knob: the all-fp64 collect pass (k_pair_rows MODE 0) instead
+    // A/B and test knob: the reference collect passes (k_pair_rows / k_pair_tiles
+    // MODE 0) instead of the matrix-core ones (k_pair_mcol / k_pair_tcol)
     if (const char *e = std::getenv("SVGD_COLLECT_FP64")) c->mcol = std::atoi(e) == 0;
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));

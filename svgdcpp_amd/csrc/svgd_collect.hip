@@ -359,7 +359,277 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 }
 
 
+// ============================== fp32 tile-path collect (d > 16, SVGD_F32) ==
+//
+// The bracket collect pass (MODE 0 of k_pair_tiles<float>) with the same
+// arithmetic, so every pass (sample tiles, radix fallback, this) forms the
+// same fp32 key: dot = the MFMA chain over k ascending from 0 (A = 16
+// columns j, B = 16 rows i, lane l: x[.. + l%16][4kk + l/16]), then
+// s = max(fma(-2, dot, n_i + n_j), 0) (GaussianRBFKernel.hpp:179-187).  Here
+// the sign is flipped, v = min(fma(2, dot, (-n_i) + (-n_j)), 0) = -s exactly
+// (negation commutes with round-to-nearest), so the lane-mask classifier of
+// k_pair_mcol applies unchanged: below <=> s < loT <=> v > -loT, candidate <=>
+// v > -hiT; the key of a candidate is key_of(|v|) = key_of(s).
+//
+// A wave owns one 16-column block of every tile of its block and keeps the
+// tile's 64 rows (4 row blocks of B operands, KP floats each) in VGPRs across
+// the run of tiles that share them (~nb/2); the next tile's columns load
+// during the current one's 4 x KP/4 MFMAs.  No LDS traffic, no barriers in
+// the loop: the pass is MFMA-issue bound (16 x 16 x KP pairs per 4KP MFMA
+// cycles).  Candidates (the band, ~0.3 %) go straight to the block's region.
+// Rows / columns >= n carry norm -inf: never below, never candidates.
+template <int KP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_pair_tcol(
+    const float *__restrict__ xc, const float *__restrict__ nrm, int64_t n, int64_t nb, int64_t t0,
+    int64_t t1, SinkCollect sc)
+{
+    constexpr int KK = KP / 4;
+    __shared__ uint32_t sBk[NBK];
+    __shared__ uint32_t sCnt;
+    __shared__ unsigned long long sBelow[4];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kq = lane >> 4, ql = lane & 15;
+
+    const uint64_t lo_key = sc.st->lo_key, hi_key = sc.st->hi_key;
+    const double binv = sc.st->binv;
+    const double lo_d = __longlong_as_double((long long)lo_key);
+    const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
+                                                        : __longlong_as_double((long long)hi_key);
+    // the smallest floats >= the bracket's doubles (as k_pair_tiles), negated
+    float loT = (float)lo_d, hiT = (float)hi_d;
+    if ((double)loT < lo_d) loT = __int_as_float(__float_as_int(loT) + 1);
+    if ((double)hiT < hi_d) hiT = __int_as_float(__float_as_int(hiT) + 1);
+    const float tl = -loT, th = -hiT;
+    if (tid == 0) sCnt = 0;
+    if (sc.bpart)
+        for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
+    __syncthreads();
+
+    uint64_t *region = sc.region + (int64_t)blockIdx.x * sc.cap;
+    uint32_t below = 0; // scalar
+    const int xl = 4 * kq - ql; // j - i = xl + r + 16 (w - rb) on diagonal tiles
+    const float ninf = -__builtin_inff();
+
+    // A column block: the MFMA A operands and the raw norms, loaded
+    // unconditionally (rows < np) and masked at use -- a select right after
+    // the load would make the compiler wait for it (and the whole prefetch)
+    struct Cols {
+        float A[KK];
+        f4 nv;
+    };
+    auto load_cols = [&](int J, Cols &c) {
+        const int64_t j0 = (int64_t)J * TB + 16 * w;
+        const float *xcol = xc + (j0 + ql) * KP + kq;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) c.A[kk] = xcol[4 * kk];
+        c.nv = *reinterpret_cast<const f4 *>(nrm + j0 + 4 * kq);
+    };
+
+    // Schedule (L2 locality; the plan's tile SET [t0, t1) is unchanged): the
+    // rank's tile rows I (plan.cpp: row I holds slots 0..cnt(I)-1, J = I +
+    // slot mod nb) are cut into bands of R rows, dealt round-robin to the
+    // nG = 8 XCDs (block b runs on XCD b % 8).  Inside a band the XCD's P
+    // blocks sweep the slots together: block q keeps row I = band + q % R
+    // (its rows stay in VGPRs for the whole band) and takes slots q / R,
+    // q / R + S, ... (S = P / R).  At any moment the XCD's blocks read ~R + S
+    // neighbouring column blocks, each shared by ~R blocks through its L2,
+    // instead of P unrelated column streams (15 % L2 hits measured).
+    const int G = gridDim.x;
+    const int nG = (G % 8 == 0) ? 8 : 1;
+    const int P = G / nG, g = blockIdx.x % nG, q = blockIdx.x / nG;
+    int R = 16;
+    while (P % R) R >>= 1;
+    const int S = P / R, rr = q % R, ph = q / R;
+    const int nb32 = (int)nb, n32 = (int)min<int64_t>(n, 0x7fffffff);
+    const int64_t H = (nb - 1) / 2;
+    const int64_t half = (nb & 1) == 0 ? nb / 2 : 0, c1 = H + 2, c2 = H + 1;
+    int Ia = 0, Ib = -1;
+    if (t1 > t0) {
+        int64_t I64, Jd;
+        tile_coords(nb, t0, &I64, &Jd);
+        Ia = (int)I64;
+        tile_coords(nb, t1 - 1, &I64, &Jd);
+        Ib = (int)I64;
+    }
+    const int nbands = (Ib - Ia + 1 + R - 1) / R;
+    // scalar position in the schedule; slots s < hi of row I, column block J
+    struct Pos {
+        int k, I, s, J, hi;
+    };
+    // the first tile at or after band p.k (64-bit plan arithmetic once per row)
+    auto enter_row = [&](Pos &p) {
+        for (; p.k < nbands; p.k += nG) {
+            const int I = Ia + p.k * R + rr;
+            if (I > Ib) continue;
+            const int64_t rs = I < half ? I * c1 : half * c1 + (I - half) * c2;
+            const int lo = (int)max<int64_t>(0, t0 - rs);
+            const int hi = (int)min<int64_t>(I < half ? c1 : c2, t1 - rs);
+            const int s = lo <= ph ? ph : ph + (lo - ph + S - 1) / S * S;
+            if (s < hi) {
+                p.I = I;
+                p.s = s;
+                p.hi = hi;
+                p.J = I + s >= nb32 ? I + s - nb32 : I + s;
+                return true;
+            }
+        }
+        return false;
+    };
+    auto advance = [&](Pos &p) {
+        p.s += S;
+        if (p.s < p.hi) {
+            p.J = p.I + p.s >= nb32 ? p.I + p.s - nb32 : p.I + p.s;
+            return true;
+        }
+        p.k += nG;
+        return enter_row(p);
+    };
+
+    float B[4][KK], hr[4];
+    // one tile (I, J): 4 x KK MFMAs, then the classification
+    auto tile = [&](const Pos &p, const Cols &c) {
+        const int j0 = p.J * TB + 16 * w + 4 * kq;
+        float hc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hc[r] = j0 + r < n32 ? -c.nv[r] : ninf;
+        f4 acc[4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(c.A[kk], B[rb][kk], acc[rb], 0, 0, 0);
+        const bool diag = p.s == 0;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+            f4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = fminf(fmaf(2.0f, acc[rb][r], hr[rb] + hc[r]), 0.0f);
+            unsigned long long h[4], any = 0;
+            uint32_t nbl = 0;
+            if (diag) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    h[r] = mcol_classify_diag(v[r], tl, th, xl, 16 * rb - 16 * w - r, nbl);
+                    any |= h[r];
+                }
+            } else {
+                any = mcol_classify4(v, tl, th, nbl, h);
+            }
+            below += nbl;
+            if (__builtin_expect(any != 0, 0)) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const unsigned long long m = h[r];
+                    if (!m) continue;
+                    uint32_t base = 0;
+                    if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(m));
+                    base = __shfl(base, 0);
+                    if ((m >> lane) & 1ull) {
+                        const uint64_t key = key_of((double)fabsf(v[r]));
+                        const int64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                        if (pos < sc.cap) region[pos] = key;
+                        if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
+                    }
+                }
+            }
+        }
+    };
+    auto rows = [&](int I) {
+        const int ib = I * TB;
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+            const int i = ib + 16 * rb + ql;
+            const float *xr = xc + (int64_t)i * KP + kq;
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) B[rb][kk] = xr[4 * kk];
+            const float nv = nrm[i];
+            hr[rb] = i < n32 ? -nv : ninf;
+        }
+        // all loads done (vmcnt(0) expcnt(7) lgkmcnt(15)): the waits inside
+        // the slot loop then only ever cover the current column buffer
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+    };
+
+    // Per row: its B operands, then its slots two at a time over two column
+    // buffers (no register copies in the loop): the next tile's columns load
+    // during the current tile's MFMAs.  The prefetch is issued on every path
+    // (block 0 when there is no next tile) so the compiler's wait for the
+    // current buffer never includes it.
+    Pos p0{g, 0, 0, 0, 0};
+    if (enter_row(p0)) {
+        Cols c0, c1;
+        load_cols(p0.J, c0);
+        for (bool live = true; live;) {
+            rows(p0.I);
+            for (;;) {
+                Pos p1 = p0;
+                const bool m1 = advance(p1);
+                load_cols(m1 ? p1.J : 0, c1);
+                tile(p0, c0);
+                if (!m1) {
+                    live = false;
+                    break;
+                }
+                if (p1.I != p0.I) { // next row: its first columns are in c1
+                    p0 = p1;
+                    c0 = c1;
+                    break;
+                }
+                Pos p2 = p1;
+                const bool m2 = advance(p2);
+                load_cols(m2 ? p2.J : 0, c0);
+                tile(p1, c1);
+                if (!m2) {
+                    live = false;
+                    break;
+                }
+                const bool row_end = p2.I != p1.I;
+                p0 = p2;
+                if (row_end) break;
+            }
+        }
+    }
+
+    if (lane == 0) sBelow[w] = below;
+    __syncthreads();
+    if (tid == 0) {
+        sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
+        sc.count_out[blockIdx.x] = sCnt;
+    }
+    if (sc.bpart)
+        for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
+}
+
 // ============================================================ launcher ==
+
+#define SVGD_TCOL_CASE(KPv)                                                                  \
+    case KPv:                                                                                \
+        hipLaunchKernelGGL((k_pair_tcol<KPv>), dim3(grid), dim3(256), 0, stream, xc, nrm, n, nb, \
+                           t0, t1, sc);                                                      \
+        break;
+
+hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, int64_t n,
+                            int64_t nb, int64_t t0, int64_t t1, uint64_t *regions, int64_t cap,
+                            uint32_t *counts, unsigned long long *below, const SelState *st,
+                            uint32_t *bpart, hipStream_t stream)
+{
+    if (grid <= 0 || t1 <= t0) return hipSuccess;
+    SinkCollect sc{st, regions, cap, counts, below, nullptr, nullptr, bpart};
+    switch (KP) {
+        SVGD_TCOL_CASE(4)
+        SVGD_TCOL_CASE(8)
+        SVGD_TCOL_CASE(12)
+        SVGD_TCOL_CASE(16)
+        SVGD_TCOL_CASE(32)
+        SVGD_TCOL_CASE(64)
+    default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
 
 #define SVGD_MCOL_CASE(Dv)                                                                   \
     case Dv:                                                                                 \

@@ -11,6 +11,7 @@ namespace svgd_amd {
 typedef float f4_t __attribute__((ext_vector_type(4)));
 
 constexpr int PBLK = 256; // row/column block of the row-stream median tile plan (plan.cpp)
+constexpr int TB = 64;    // particles per tile of the MFMA tile kernels (rows and columns)
 
 // --------------------------------------------------------------- median --
 //

@@ -29,7 +29,6 @@ namespace svgd_amd {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int TB = 64;   // particles per tile (rows and columns)
 constexpr int LDP = TB + 16; // padded LDS row stride (doubles) of the k-major X tiles
 
 typedef float f4 __attribute__((ext_vector_type(4)));

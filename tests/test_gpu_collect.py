@@ -96,3 +96,76 @@ def test_mcol_large_matches_fp64_collect(oracle, monkeypatch, n, d):
         assert c.last_scale()[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
         c.close()
     assert res[0] == res[1]
+
+
+# ---------------------------------------------------------------- fp32 tiles --
+# k_pair_tcol: the fp32 tile path's collect (SVGD_F32, any d) on the matrix
+# cores with k_pair_tiles<float>'s own key arithmetic.  Its median must be
+# BIT-IDENTICAL to k_pair_tiles MODE 0 (SVGD_COLLECT_FP64=1) and to the exact
+# order statistics of the device's own fp32 keys.
+
+def _median32(X, monkeypatch, ref, sample=0, direct=None):
+    monkeypatch.setenv("SVGD_COLLECT_FP64", "1" if ref else "0")
+    n, d = X.shape
+    c = S.Context(d, n, dtype=C.SVGD_F32)
+    c.set_particles(X)
+    kw = {"direct_max_pairs": 0} if direct is None else {"direct_max_pairs": direct}
+    if sample:
+        kw["sample_size"] = sample
+    c.set_median_tuning(**kw)
+    a, med = c.median_scale()
+    return c, (a, med, c.last_scale()[2], c.last_median_keys())
+
+
+@pytest.mark.parametrize("d", [2, 7, 16, 20, 33, 64])
+@pytest.mark.parametrize("n", [300, 1000, 4097])
+def test_tcol_matches_tile_collect_and_exact(oracle, monkeypatch, n, d):
+    X = oracle.splitmix((n, d), 3.0, 11 * n + d)
+    c, got = _median32(X, monkeypatch, ref=False)
+    exp = _exact_median(c, n)
+    c.close()
+    f, ref = _median32(X, monkeypatch, ref=True)
+    f.close()
+    assert got == ref  # same keys and counts: the same path, bit for bit
+    assert got[1] == exp
+
+
+@pytest.mark.parametrize("kind", ["ties", "zeros", "outlier", "direct"])
+def test_tcol_edge_inputs_exact(oracle, monkeypatch, kind):
+    """Ties (a wide band of equal keys), all-zero distances (lo key 0), one far
+    particle, and the direct path (every pair a candidate: bracket [0, inf))."""
+    n, d = 1500, 64
+    X = oracle.splitmix((n, d), 1.0, 5)
+    direct = None
+    if kind == "ties":
+        X = np.repeat(X[:6], n // 6, axis=0)
+    elif kind == "zeros":
+        X = np.zeros((n, d))
+        X[:10] = 1.0
+    elif kind == "outlier":
+        X[17] = 1e6
+    else:
+        direct = 1 << 40
+    n = X.shape[0]
+    c, got = _median32(X, monkeypatch, ref=False, direct=direct)
+    exp = _exact_median(c, n)
+    c.close()
+    f, ref = _median32(X, monkeypatch, ref=True, direct=direct)
+    f.close()
+    assert got[1] == exp
+    assert got[:2] == ref[:2]
+
+
+def test_tcol_full_size_matches_tile_collect(oracle, monkeypatch):
+    """cfg5's shape (N = 65536, d = 64, fp32) with the default tuning."""
+    n, d = 65536, 64
+    X = oracle.splitmix((n, d), 3.0, 64)
+    res = []
+    for ref in (False, True):
+        monkeypatch.setenv("SVGD_COLLECT_FP64", "1" if ref else "0")
+        c = S.Context(d, n, dtype=C.SVGD_F32)
+        c.set_particles(X)
+        res.append(c.median_scale() + (c.last_median_keys(),))
+        assert c.last_scale()[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
+        c.close()
+    assert res[0] == res[1]
