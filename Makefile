@@ -32,7 +32,7 @@ $(SRC_DIR)/plan.o: $(SRC_DIR)/plan.cpp $(HDRS)
 $(SRC_DIR)/hostcomm.o: $(SRC_DIR)/hostcomm.cpp $(SRC_DIR)/hostcomm.h
 	$(HIPCC) -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
-$(SRC_DIR)/host_models.o: $(SRC_DIR)/host_models.cpp $(HDRS)
+$(SRC_DIR)/host_models.o: $(SRC_DIR)/host_models.cpp $(SRC_DIR)/host_grad_block.inc $(HDRS)
 	$(CXX) -O3 -std=c++17 -fPIC -fopenmp -Wall -c $< -o $@
 
 $(LIB): $(OBJS)

@@ -957,8 +957,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     CHK(dalloc(c, &c->nrm, c->np));
     CHK(dalloc(c, &c->cvec, c->np));
     c->rowpath = dim <= ROWS_MAX_D && !f32;
-    // k_pair_tcol holds 3 blocks per CU (152 VGPRs at d = 64): one full round
-    if (f32) c->collect_blocks = 768;
     if (f32) {
         CHK(dalloc(c, &c->xcf, c->np * c->KP));
         CHK(dalloc(c, &c->nrmf, c->np));

@@ -378,8 +378,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // the loop: the pass is MFMA-issue bound (16 x 16 x KP pairs per 4KP MFMA
 // cycles).  Candidates (the band, ~0.3 %) go straight to the block's region.
 // Rows / columns >= n carry norm -inf: never below, never candidates.
+constexpr int TC_STG = 512; // staged band values per wave (k_pair_tcol)
+
 template <int KP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_pair_tcol(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_tcol(
     const float *__restrict__ xc, const float *__restrict__ nrm, int64_t n, int64_t nb, int64_t t0,
     int64_t t1, SinkCollect sc)
 {
@@ -400,7 +402,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
     float loT = (float)lo_d, hiT = (float)hi_d;
     if ((double)loT < lo_d) loT = __int_as_float(__float_as_int(loT) + 1);
     if ((double)hiT < hi_d) hiT = __int_as_float(__float_as_int(hiT) + 1);
-    const float tl = -loT, th = -hiT;
+    // v = fma(2, dot, -n_i - n_j) = -(the unclamped s): min(v, 0) > -T <=>
+    // v > -T for T > 0, and never for T = 0 (+inf then), so the clamp is left
+    // to the key of the staged band values
+    const float tl = loT > 0.0f ? -loT : __builtin_inff();
+    const float th = hiT > 0.0f ? -hiT : __builtin_inff();
+    __shared__ float sStage[4][TC_STG];
+    float *stage = sStage[w];
+    int scnt = 0; // staged band values of this wave
     if (tid == 0) sCnt = 0;
     if (sc.bpart)
         for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
@@ -420,9 +429,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
     };
     auto load_cols = [&](int J, Cols &c) {
         const int64_t j0 = (int64_t)J * TB + 16 * w;
-        const float *xcol = xc + (j0 + ql) * KP + kq;
+        if constexpr (KP % 16 == 0) { // kslot order: 16-byte loads
+            const float *xcol = xc + (j0 + ql) * KP + 4 * kq;
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) c.A[kk] = xcol[4 * kk];
+            for (int u = 0; u < KK / 4; ++u) {
+                const f4 t = *reinterpret_cast<const f4 *>(xcol + 16 * u);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) c.A[4 * u + e] = t[e];
+            }
+        } else {
+            const float *xcol = xc + (j0 + ql) * KP;
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) c.A[kk] = xcol[kslot<float, KP>(kk, kq)];
+        }
         c.nv = *reinterpret_cast<const f4 *>(nrm + j0 + 4 * kq);
     };
 
@@ -438,7 +457,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
     const int G = gridDim.x;
     const int nG = (G % 8 == 0) ? 8 : 1;
     const int P = G / nG, g = blockIdx.x % nG, q = blockIdx.x / nG;
-    int R = 16;
+    int R = 32;
     while (P % R) R >>= 1;
     const int S = P / R, rr = q % R, ph = q / R;
     const int nb32 = (int)nb, n32 = (int)min<int64_t>(n, 0x7fffffff);
@@ -486,7 +505,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         return enter_row(p);
     };
 
-    float B[4][KK], hr[4];
+    // staged band values -> keys (s = max(-v, 0), as k_pair_tiles' fmax) in
+    // the block's region (one LDS atomic per 64) and the bucket histogram
+    auto flush = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // other lanes' staging stores
+        for (int q0 = 0; q0 < scnt; q0 += 64) {
+            const int c = min(64, scnt - q0);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)c);
+            base = __shfl(base, 0);
+            if (lane < c) {
+                const float v = stage[q0 + lane];
+                const uint64_t key = key_of((double)(v >= 0.0f ? 0.0f : -v));
+                const int64_t pos = (int64_t)base + lane;
+                if (pos < sc.cap) region[pos] = key;
+                if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
+            }
+        }
+        scnt = 0;
+    };
+
+    // the tile row's B operands, shared by the block's 4 waves (written at a
+    // row change, between barriers: every wave follows the same schedule)
+    __shared__ float sB[4 * KK * 64];
+    float hr[4];
     // one tile (I, J): 4 x KK MFMAs, then the classification
     auto tile = [&](const Pos &p, const Cols &c) {
         const int j0 = p.J * TB + 16 * w + 4 * kq;
@@ -500,13 +542,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
             for (int rb = 0; rb < 4; ++rb)
-                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(c.A[kk], B[rb][kk], acc[rb], 0, 0, 0);
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(c.A[kk], sB[(rb * KK + kk) * 64 + lane],
+                                                               acc[rb], 0, 0, 0);
         const bool diag = p.s == 0;
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
-            f4 v;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = fminf(fmaf(2.0f, acc[rb][r], hr[rb] + hc[r]), 0.0f);
+            // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): the same roundings,
+            // half the instructions
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 hh = {hr[rb], hr[rb]}, two = {2.0f, 2.0f};
+            const f2 t01 = hh + f2{hc[0], hc[1]}, t23 = hh + f2{hc[2], hc[3]};
+            const f2 v01 = __builtin_elementwise_fma(two, f2{acc[rb][0], acc[rb][1]}, t01);
+            const f2 v23 = __builtin_elementwise_fma(two, f2{acc[rb][2], acc[rb][3]}, t23);
+            const f4 v = {v01[0], v01[1], v23[0], v23[1]};
+            // lane masks: below counted on the scalar unit, band lanes OR-ed
+            // (measured faster than per-lane vector counters: 2.7 vs 3.2 ms)
             unsigned long long h[4], any = 0;
             uint32_t nbl = 0;
             if (diag) {
@@ -519,35 +569,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
                 any = mcol_classify4(v, tl, th, nbl, h);
             }
             below += nbl;
+            // band values (~1 % of the pairs) are staged; their keys are
+            // formed and written in batches of 64 (flush).  A row block adds
+            // at most 256 (a bracket holding every pair: the direct path)
             if (__builtin_expect(any != 0, 0)) {
+                if (scnt > TC_STG - 256) flush();
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const unsigned long long m = h[r];
                     if (!m) continue;
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(m));
-                    base = __shfl(base, 0);
-                    if ((m >> lane) & 1ull) {
-                        const uint64_t key = key_of((double)fabsf(v[r]));
-                        const int64_t pos = base + __popcll(m & ((1ull << lane) - 1ull));
-                        if (pos < sc.cap) region[pos] = key;
-                        if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
-                    }
+                    if ((m >> lane) & 1ull) stage[scnt + __popcll(m & ((1ull << lane) - 1ull))] = v[r];
+                    scnt += __popcll(m);
                 }
             }
         }
     };
     auto rows = [&](int I) {
         const int ib = I * TB;
+        __syncthreads(); // every wave is done with the previous row
+        for (int e = tid; e < 4 * KK * 64; e += 256) {
+            const int l = e & 63, kk = (e >> 6) % KK, rb = (e >> 6) / KK;
+            sB[e] = xc[(int64_t)(ib + 16 * rb + (l & 15)) * KP + kslot<float, KP>(kk, l >> 4)];
+        }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
             const int i = ib + 16 * rb + ql;
-            const float *xr = xc + (int64_t)i * KP + kq;
-#pragma unroll
-            for (int kk = 0; kk < KK; ++kk) B[rb][kk] = xr[4 * kk];
             const float nv = nrm[i];
             hr[rb] = i < n32 ? -nv : ninf;
         }
+        __syncthreads();
         // all loads done (vmcnt(0) expcnt(7) lgkmcnt(15)): the waits inside
         // the slot loop then only ever cover the current column buffer
         __builtin_amdgcn_s_waitcnt(0x0F70);
@@ -568,6 +618,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
                 Pos p1 = p0;
                 const bool m1 = advance(p1);
                 load_cols(m1 ? p1.J : 0, c1);
+                __builtin_amdgcn_sched_barrier(0); // the prefetch issues before the MFMAs
                 tile(p0, c0);
                 if (!m1) {
                     live = false;
@@ -581,6 +632,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
                 Pos p2 = p1;
                 const bool m2 = advance(p2);
                 load_cols(m2 ? p2.J : 0, c0);
+                __builtin_amdgcn_sched_barrier(0);
                 tile(p1, c1);
                 if (!m2) {
                     live = false;
@@ -593,6 +645,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         }
     }
 
+    if (scnt) flush();
     if (lane == 0) sBelow[w] = below;
     __syncthreads();
     if (tid == 0) {

@@ -13,6 +13,20 @@ typedef float f4_t __attribute__((ext_vector_type(4)));
 constexpr int PBLK = 256; // row/column block of the row-stream median tile plan (plan.cpp)
 constexpr int TB = 64;    // particles per tile of the MFMA tile kernels (rows and columns)
 
+// Coordinate k taken by MFMA step kk and lane group q (= lane / 16) in the
+// pair-key Gram of the tile kernels (k_pair_tiles, k_pair_tcol; every pass
+// over the keys uses the same order, so they agree bit for bit).  fp32 with
+// KP % 16 == 0: the steps 4u..4u+3 of lane group q read coordinates
+// 16u + 4q .. 16u + 4q + 3, i.e. one 16-byte load per 4 steps and 64
+// contiguous bytes per row for the 4 groups; otherwise 4 kk + q.
+template <class T, int KP> __device__ __forceinline__ constexpr int kslot(int kk, int q)
+{
+    if constexpr (sizeof(T) == 4 && KP % 16 == 0)
+        return 16 * (kk >> 2) + 4 * q + (kk & 3);
+    else
+        return 4 * kk + q;
+}
+
 // --------------------------------------------------------------- median --
 //
 // Keys: squared distances s = max((|xc_i|^2 + |xc_j|^2) - 2 xc_i.xc_j, 0)

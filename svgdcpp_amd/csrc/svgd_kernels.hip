@@ -554,7 +554,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
         const bool full = Ic != Jc && (Ic + 1) * TB <= n && (Jc + 1) * TB <= n;
         T bI[KP / 4];
 #pragma unroll
-        for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = sXI[(4 * kk + hi) * LDP + w * 16 + lo];
+        for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = sXI[kslot<T, KP>(kk, hi) * LDP + w * 16 + lo];
         const int il = w * 16 + lo;
         const int64_t i = Ic * TB + il;
         const T ni = sNI[il];
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
             A4 dot = {0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < KP / 4; ++kk)
-                dot = mfma16(sXJ[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
+                dot = mfma16(sXJ[kslot<T, KP>(kk, hi) * LDP + js * 16 + lo], bI[kk], dot);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int jl = js * 16 + acc_row<T>(hi, r);
