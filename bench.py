@@ -291,9 +291,15 @@ def main():
             "roofline": {
                 # fp64 d <= 16: VALU row stream (f64 MFMA shares the VALU issue
                 # slots on gfx950); otherwise the MFMA tile kernel
+                # avg_launch_ms: HIP events around the phi phase on the
+                # context's stream -- record prep + the phi kernel + its reduce
+                # (with the fused optimizer update on the row path); the phi
+                # kernel is > 99 % of it at cfg3 (profiles/r02_*kernel_stats*)
                 "kernel": ("k_phi_rows (fused RBF + grad + phi contraction, fp64 VALU row stream)"
                            if dtype == "f64" and d <= 16 else
                            "k_phi (fused RBF + grad + phi contraction, MFMA tiles)"),
+                "timed_span": "k_prep_rec + k_phi_rows + k_phi_reduce (fused update)"
+                              if dtype == "f64" and d <= 16 else "k_prep_v + k_phi (+ cvt)",
                 "bound": "valu" if dtype == "f64" and d <= 16 else "mfma",
                 "achieved": achieved,
                 "peak": peak,

@@ -165,6 +165,7 @@ struct svgd_ctx {
     // backups and redoes the step on the synchronous path.
     bool spec_allowed = true;  // SVGD_SPECULATE=0 disables
     bool spec_step = false;    // this step's median is speculative
+    bool med_ev_done = false;  // this step's median end event is recorded
     bool last_fast = false;    // the last resolved median could have been speculative
     bool pending = false;      // a speculative step awaits its status
     bool scal_fresh = true;    // h_scal holds the last scale (fetch_scale)
@@ -385,6 +386,7 @@ constexpr double MCOL_MAX_BAND = 0.02;
 SelState sample_state(svgd_ctx *c, double sigma);
 int sample_bracket(svgd_ctx *c, bool preset);
 int collect_counts(svgd_ctx *c);
+int median_finish_spec(svgd_ctx *c, double logn);
 
 // Phase 1 of the median: candidate bracket + collect pass + counts.
 // Leaves the reduced counts in c->h_cnt (ready at c->ev_cnt).
@@ -543,7 +545,10 @@ int collect_counts(svgd_ctx *c)
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
                                    c->collect_grid, c->cnt3, c->stream));
     CHK(allreduce_cnt3(c));
-    if (c->spec_step) return SVGD_OK; // the device plan reads the counts
+    // speculative: the device plan and the selection are queued right behind
+    // the counts (while the device still runs the collect pass), not when the
+    // host comes back from the gradient -- no launch gaps between them
+    if (c->spec_step) return median_finish_spec(c, std::log((double)c->n));
     HIPCHK(c, hipMemcpyAsync(c->h_cnt, c->cnt3, CNT_LEN * sizeof(unsigned long long),
                              hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_cnt, c->stream));
@@ -562,14 +567,20 @@ int median_finish_spec(svgd_ctx *c, double logn)
                                  (uint64_t)c->sel_rank[c->nsel - 1],
                                  std::min<int64_t>(c->bucket_cap, CAPR), seg, c->d_status,
                                  c->h_status_dev, c->stream));
-    HIPCHK(c, hipEventRecord(c->ev_status, c->stream));
     HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
                                      c->d_status, c->stream));
     CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
     HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, CAPR, c->navg, c->src_lo, c->src_hi, logn,
                                   c->scal, c->d_status, c->stream));
-    c->pending = true;
-    c->last_path = c->med_path;
+    // the plan's status is final once this completes (recorded after the
+    // selection: an event between two kernels costs a ~5 us dispatch gap)
+    HIPCHK(c, hipEventRecord(c->ev_status, c->stream));
+    // (c->pending -- the plan's status to check -- is set when the step is
+    // complete, by median_finish: resolve_pending never redoes half a step)
+    if (c->timing && !c->ev_med.empty()) {
+        HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+        c->med_ev_done = true;
+    }
     return SVGD_OK;
 }
 
@@ -587,7 +598,11 @@ int median_finish(svgd_ctx *c)
         c->last_path = SVGD_MEDIAN_DIRECT;
         return SVGD_OK;
     }
-    if (c->spec_step) return median_finish_spec(c, logn);
+    if (c->spec_step) { // queued by collect_counts
+        c->pending = true;
+        c->last_path = c->med_path;
+        return SVGD_OK;
+    }
     c->last_fast = false;
     HIPCHK(c, hipEventSynchronize(c->ev_cnt));
     const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
@@ -741,8 +756,17 @@ bool matrix_scale(const svgd_ctx *c)
     return c->scale_method == SVGD_SCALE_MATRIX || c->scale_method == SVGD_SCALE_HESSIAN;
 }
 
-int run_phi(svgd_ctx *c)
+int run_phi(svgd_ctx *c, const OptArgs *opt)
 {
+    // phi phase: the record preparation (V = G - 2a xc, part of the
+    // reference's ComputePhi) through the reduce (+ the fused update); the
+    // start event goes before the preparation -- an event between two
+    // kernels costs a dispatch gap
+    EvPair ev{};
+    if (c->timing) {
+        ev = take_pair(c);
+        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+    }
     const bool mat = matrix_scale(c);
     if (mat) {
         // M = factor * src, L = chol(M), a_eff = 1 (GaussianRBFKernel.hpp:189-210)
@@ -779,15 +803,10 @@ int run_phi(svgd_ctx *c)
         HIPCHK(c, launch_cvt_f32(c->cvec, c->np, c->cvf, c->stream));
         if (mat) HIPCHK(c, launch_cvt_f32(c->zc, c->np * c->KP, c->zcf, c->stream));
     }
-    EvPair ev{};
-    if (c->timing) {
-        ev = take_pair(c);
-        HIPCHK(c, hipEventRecord(ev.a, c->stream));
-    }
     if (c->rowpath)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
-                                  mat ? c->sc_sgn : nullptr, c->phi, c->stream));
+                                  mat ? c->sc_sgn : nullptr, c->phi, opt, c->stream));
     else if (c->dtype == SVGD_F32)
         HIPCHK(c, launch_phi_f32(c->KP, c->NCB, mat ? c->zcf : c->xcf, c->cvf, c->Vf, c->scal,
                                  c->row0, c->nrows, (c->n + TB - 1) / TB, c->dim,
@@ -804,7 +823,8 @@ int run_phi(svgd_ctx *c)
     return SVGD_OK;
 }
 
-int run_opt(svgd_ctx *c)
+// This step's optimizer arguments (advances t: call once per step).
+int opt_args(svgd_ctx *c, OptArgs *o)
 {
     if (c->opt_kind < 0)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
@@ -815,11 +835,25 @@ int run_opt(svgd_ctx *c)
         c2 = 1.0 - std::pow(c->b2, (double)c->t);
     }
     const size_t off = (size_t)c->row0 * c->dim;
-    HIPCHK(c, launch_opt_update(c->opt_kind, c->phi, c->m, c->v, c->X + off, c->nrows * c->dim,
-                                c->dim, c->lr, c->b1, c->b2, c->eps, c1, c2,
-                                c->bounded ? c->lower : nullptr, c->bounded ? c->upper : nullptr,
-                                // X_t, m_t, v_t of this rank's rows for a redo if the device plan failed
-                                c->spec_step ? c->bak : nullptr, c->stream));
+    *o = OptArgs{c->opt_kind, c->dim, c->nrows * c->dim, c->m, c->v, c->X + off, c->lr, c->b1,
+                 c->b2, c->eps, c1, c2, c->bounded ? c->lower : nullptr,
+                 c->bounded ? c->upper : nullptr,
+                 // X_t, m_t, v_t of this rank's rows for a redo if the device plan failed
+                 c->spec_step ? c->bak : nullptr};
+    return SVGD_OK;
+}
+
+// The step's phi and optimizer update: on the row path the update is applied
+// by the phi reduce itself (one launch fewer), else by k_opt_update.
+int run_phi_opt(svgd_ctx *c)
+{
+    if (c->opt_kind < 0)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
+    OptArgs o;
+    CHK(opt_args(c, &o));
+    const bool fused = c->rowpath;
+    CHK(run_phi(c, fused ? &o : nullptr));
+    if (!fused) HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
     CHK(allgather_rows(c, c->X));
     HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
     return SVGD_OK;
@@ -828,14 +862,16 @@ int run_opt(svgd_ctx *c)
 int scale_begin(svgd_ctx *c)
 {
     HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0)); // the last [a, med] copy has read scal
-    CHK(center(c));
-    if (c->scale_method == SVGD_SCALE_FIXED || matrix_scale(c)) return SVGD_OK;
-    EvPair ev{};
-    if (c->timing) {
-        ev = take_pair(c);
+    const bool med = !(c->scale_method == SVGD_SCALE_FIXED || matrix_scale(c));
+    // the median phase's start event goes before the centring (which it
+    // needs): an event between two kernels costs a dispatch gap
+    if (c->timing && med) {
+        EvPair ev = take_pair(c);
         HIPCHK(c, hipEventRecord(ev.a, c->stream));
         c->ev_med.push_back(ev);
     }
+    CHK(center(c));
+    if (!med) return SVGD_OK;
     return median_begin(c);
 }
 
@@ -857,7 +893,9 @@ int scale_finish(svgd_ctx *c)
         return SVGD_OK;
     }
     CHK(median_finish(c));
-    if (c->timing && !c->ev_med.empty()) HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+    if (c->timing && !c->ev_med.empty() && !c->med_ev_done)
+        HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+    c->med_ev_done = false;
     // [a, med] reach the host only when asked (fetch_scale): no copy on the
     // step's path; the event marks where this step's scale is final
     HIPCHK(c, hipEventRecord(c->ev_fin, c->stream));
@@ -905,8 +943,7 @@ int resolve_pending(svgd_ctx *c)
     c->last_fast = false;
     CHK(scale_begin(c));
     CHK(scale_finish(c));
-    CHK(run_phi(c));
-    CHK(run_opt(c));
+    CHK(run_phi_opt(c));
     return SVGD_OK;
 }
 
@@ -1341,7 +1378,7 @@ int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
     CHK(center(c));
     HIPCHK(c, launch_set_scal(a, NAN, c->scal, c->stream));
     CHK(upload_g(c, G_shard));
-    CHK(run_phi(c));
+    CHK(run_phi(c, nullptr));
     if (phi_out && c->nrows > 0) {
         HIPCHK(c, hipMemcpyAsync(phi_out, c->phi, sizeof(double) * (size_t)c->nrows * c->dim,
                                  hipMemcpyDeviceToHost, c->stream));
@@ -1381,8 +1418,7 @@ int svgd_finish_step(svgd_ctx *c, const double *G_shard)
     // (scale_finish), so the device runs it during that round trip
     CHK(upload_g_finish(c));
     CHK(scale_finish(c));
-    CHK(run_phi(c));
-    CHK(run_opt(c));
+    CHK(run_phi_opt(c));
     return SVGD_OK;
 }
 
@@ -1402,8 +1438,7 @@ int svgd_step(svgd_ctx *c, const double *G_shard)
                                 c->dm_mu, c->dm_prec, c->G + (size_t)c->row0 * c->dim, c->stream));
     CHK(scale_finish(c));
     CHK(allgather_rows(c, c->G));
-    CHK(run_phi(c));
-    CHK(run_opt(c));
+    CHK(run_phi_opt(c));
     return SVGD_OK;
 }
 

@@ -66,10 +66,17 @@ hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, cons
                                const float *nrmf, int64_t n, int64_t ntiles, uint64_t *keys,
                                hipStream_t stream);
 // bak (optional, 3 cnt doubles): X_t, m_t, v_t of the cnt elements, saved in the pass
-hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
-                             int64_t cnt, int d, double lr, double b1, double b2, double eps,
-                             double c1, double c2, const double *lower, const double *upper,
-                             double *bak, hipStream_t stream);
+// One optimizer step over cnt = rows x d elements of this rank (X, m, v at
+// the rank's rows): Adam (kind 0) / AdaGrad (1) / RMSProp (2) + clamp.
+struct OptArgs {
+    int kind, d;
+    int64_t cnt;
+    double *m, *v, *X;
+    double lr, b1, b2, eps, c1, c2;
+    const double *lower, *upper; // clamp bounds (both or neither)
+    double *bak;                 // X_t, m_t, v_t saved here when set (speculative step)
+};
+hipError_t launch_opt_update(const OptArgs &o, const double *g, hipStream_t stream);
 // mode 0: collect keys in [st->lo_key, st->hi_key) into per-block regions and count
 // keys below lo_key; mode 1: radix histogram pass over all pairs (fallback);
 // mode 2: debug dump of every key in (i<j) row-major order.
@@ -148,10 +155,12 @@ constexpr int med_f32_stride(int d) { return ((d + 1 + 7) / 8) * 8; }
 hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
                            double *rec, hipStream_t stream);
+// opt (optional): the optimizer step applied to each phi element as the
+// reduce writes it (the step path: one launch fewer than launch_opt_update)
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
-                           double *phi, hipStream_t stream);
+                           double *phi, const OptArgs *opt, hipStream_t stream);
 // full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,
 // or an eigendecomposition when M is indefinite and d <= ROWS_MAX_D);
 // err = 0 positive definite, 2 indefinite, 1 non-finite / no convergence.

@@ -378,45 +378,45 @@ __global__ __launch_bounds__(256) void k_phi(const T *__restrict__ xg, const T *
 
 // bak (optional, the speculative step): bak[0..cnt) = X_t, bak[cnt..2cnt) =
 // m_t, bak[2cnt..3cnt) = v_t of these elements, written in the same pass.
-__global__ void k_opt_update(int kind, const double *__restrict__ g, double *__restrict__ m,
-                             double *__restrict__ v, double *__restrict__ X, int64_t cnt, int d,
-                             double lr, double b1, double b2, double eps, double c1, double c2,
-                             const double *__restrict__ lower, const double *__restrict__ upper,
-                             double *__restrict__ bak)
+__device__ __forceinline__ void opt_elem(const OptArgs &o, int64_t e, double ge)
 {
 #pragma clang fp contract(off)
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cnt;
-         e += (int64_t)gridDim.x * blockDim.x) {
-        const double ge = g[e];
-        if (bak) {
-            bak[e] = X[e];
-            bak[cnt + e] = m[e];
-            bak[2 * cnt + e] = v[e];
-        }
-        double delta;
-        if (kind == 0) { // Adam.hpp:75-83
-            const double me = b1 * m[e] + (1 - b1) * ge;
-            const double ve = b2 * v[e] + (1 - b2) * (ge * ge);
-            m[e] = me;
-            v[e] = ve;
-            delta = (lr * (1.0 / (eps + sqrt(ve / c2)))) * (me / c1);
-        } else if (kind == 1) { // AdaGrad.hpp:60-65
-            const double ve = v[e] + ge * ge;
-            v[e] = ve;
-            delta = (lr * (1.0 / (eps + sqrt(ve)))) * ge;
-        } else { // RMSProp.hpp:69-74 (beta passed as b1)
-            const double ve = b1 * v[e] + (1 - b1) * (ge * ge);
-            v[e] = ve;
-            delta = (lr * (1.0 / (eps + sqrt(ve)))) * ge;
-        }
-        double x = X[e] + delta; // SVGD.hpp:393
-        if (lower) {             // SVGD.hpp:396-399: min(upper) then max(lower)
-            const int k = (int)(e % d);
-            x = x < upper[k] ? x : upper[k];
-            x = x > lower[k] ? x : lower[k];
-        }
-        X[e] = x;
+    double *__restrict__ m = o.m, *__restrict__ v = o.v, *__restrict__ X = o.X;
+    if (o.bak) {
+        o.bak[e] = X[e];
+        o.bak[o.cnt + e] = m[e];
+        o.bak[2 * o.cnt + e] = v[e];
     }
+    double delta;
+    if (o.kind == 0) { // Adam.hpp:75-83
+        const double me = o.b1 * m[e] + (1 - o.b1) * ge;
+        const double ve = o.b2 * v[e] + (1 - o.b2) * (ge * ge);
+        m[e] = me;
+        v[e] = ve;
+        delta = (o.lr * (1.0 / (o.eps + sqrt(ve / o.c2)))) * (me / o.c1);
+    } else if (o.kind == 1) { // AdaGrad.hpp:60-65
+        const double ve = v[e] + ge * ge;
+        v[e] = ve;
+        delta = (o.lr * (1.0 / (o.eps + sqrt(ve)))) * ge;
+    } else { // RMSProp.hpp:69-74 (beta passed as b1)
+        const double ve = o.b1 * v[e] + (1 - o.b1) * (ge * ge);
+        v[e] = ve;
+        delta = (o.lr * (1.0 / (o.eps + sqrt(ve)))) * ge;
+    }
+    double x = X[e] + delta; // SVGD.hpp:393
+    if (o.lower) {           // SVGD.hpp:396-399: min(upper) then max(lower)
+        const int k = (int)(e % o.d);
+        x = x < o.upper[k] ? x : o.upper[k];
+        x = x > o.lower[k] ? x : o.lower[k];
+    }
+    X[e] = x;
+}
+
+__global__ void k_opt_update(OptArgs o, const double *__restrict__ g)
+{
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < o.cnt;
+         e += (int64_t)gridDim.x * blockDim.x)
+        opt_elem(o, e, g[e]);
 }
 
 // --------------------------------------------------------------- median --
@@ -1855,7 +1855,7 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
                                                     const double *__restrict__ a_ptr, int64_t row0,
                                                     int64_t nrows, int d, int RS, int S, int64_t ldp,
                                                     double inv_n, const double *__restrict__ wv,
-                                                    double *__restrict__ phi)
+                                                    double *__restrict__ phi, OptArgs opt, int do_opt)
 {
     __shared__ double sm[PHI_RED_ROWS * 17];
     const double two_a = 2.0 * (*a_ptr);
@@ -1874,7 +1874,9 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
         const int r = o / d, k = o - r * d;
         const int64_t li = rb + r;
         const double w = wv ? wv[(row0 + li) * d + k] : two_a * rec[(row0 + li) * RS + k];
-        phi[li * d + k] = inv_n * (sm[r * DP + k] + w * sm[r * DP + d]);
+        const double ph = inv_n * (sm[r * DP + k] + w * sm[r * DP + d]);
+        phi[li * d + k] = ph;
+        if (do_opt) opt_elem(opt, li * d + k, ph);
     }
 }
 
@@ -2509,7 +2511,7 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
-                           double *phi, hipStream_t stream)
+                           double *phi, const OptArgs *opt, hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
     const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
@@ -2520,7 +2522,8 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
     if (d > 16) return hipErrorInvalidValue; // k_phi_reduce's LDS holds d + 1 <= 17
     const int64_t g = (nrows + PHI_RED_ROWS - 1) / PHI_RED_ROWS;
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
-                       d, phi_rec_stride(d), S, ldp, inv_n, wv, phi);
+                       d, phi_rec_stride(d), S, ldp, inv_n, wv, phi, opt ? *opt : OptArgs{},
+                       opt ? 1 : 0);
     return hipGetLastError();
 }
 
@@ -2692,16 +2695,12 @@ hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, c
     return hipGetLastError();
 }
 
-hipError_t launch_opt_update(int kind, const double *g, double *m, double *v, double *X,
-                             int64_t cnt, int d, double lr, double b1, double b2, double eps,
-                             double c1, double c2, const double *lower, const double *upper,
-                             double *bak, hipStream_t stream)
+hipError_t launch_opt_update(const OptArgs &o, const double *g, hipStream_t stream)
 {
-    if (cnt <= 0) return hipSuccess;
-    int64_t grid = (cnt + 255) / 256;
+    if (o.cnt <= 0) return hipSuccess;
+    int64_t grid = (o.cnt + 255) / 256;
     if (grid > 8192) grid = 8192;
-    hipLaunchKernelGGL(k_opt_update, dim3(grid), dim3(256), 0, stream, kind, g, m, v, X, cnt, d,
-                       lr, b1, b2, eps, c1, c2, lower, upper, bak);
+    hipLaunchKernelGGL(k_opt_update, dim3(grid), dim3(256), 0, stream, o, g);
     return hipGetLastError();
 }
 

@@ -1,12 +1,12 @@
 """Print the kernel timeline (start offset, gap, duration) of the last full
-step in a rocprofv3 kernel trace (steps end at k_opt_update)."""
+step in a rocprofv3 kernel trace (steps start at k_mean_partial)."""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-idx = [i for i, r in enumerate(rows) if 'k_opt_update' in r['Kernel_Name']]
-a, b = idx[-2] + 1, idx[-1] + 1
+idx = [i for i, r in enumerate(rows) if 'k_mean_partial' in r['Kernel_Name']]
+a, b = idx[-2], idx[-1]
 t0 = int(rows[a]['Start_Timestamp'])
 prev = None
 for r in rows[a:b]:
