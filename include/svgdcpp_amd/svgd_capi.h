@@ -201,6 +201,17 @@ int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G)
  * of the Hessian scale (GaussianRBFKernel.hpp:197-205, Model.hpp:366-370). */
 int svgd_model_neg_hess_sum(void *model, const double *X, int64_t nrows, double *H);
 
+/* One SVGD::Step (SVGD.hpp:373-400) with grad log p from a host model
+ * (svgd_model_create; Model::EvaluateLogModelGrad, Model.hpp:335-338,
+ * evaluated per particle as SVGD.hpp:412-416 does): svgd_begin_step +
+ * svgd_model_logp_grad + svgd_finish_step with the X_t copy, the host
+ * gradient and the G upload pipelined in row chunks (chunk i's gradient
+ * overlaps chunk i+1's copy down and chunk i-1's copy up), so the whole host
+ * round trip hides behind the device median.  Same result as the split
+ * calls.  Not for SVGD_SCALE_HESSIAN (that step also needs the caller's
+ * Hessian sum). */
+int svgd_step_host_model(svgd_ctx *ctx, const void *model);
+
 /* Mirror a built-in Gaussian-sum model (svgd_model_create) on the device
  * (MultivariateNormal.hpp:56-61, Model.hpp:55-92):
  * afterwards svgd_step(ctx, NULL) evaluates grad log p on the device and the

@@ -61,6 +61,7 @@ SIGNATURES = {
     "svgd_step": (ctypes.c_int, [_P, _D]),
     "svgd_begin_step": (ctypes.c_int, [_P, _D]),
     "svgd_finish_step": (ctypes.c_int, [_P, _D]),
+    "svgd_step_host_model": (ctypes.c_int, [_P, ctypes.c_void_p]),
     "svgd_host_buffers": (ctypes.c_int, [_P, ctypes.POINTER(_D), ctypes.POINTER(_D)]),
     "svgd_sync": (ctypes.c_int, [_P]),
     "svgd_last_scale": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(ctypes.c_int)]),

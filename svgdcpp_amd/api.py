@@ -582,10 +582,16 @@ class Context:
         self.check(self.lib.svgd_set_median_tuning(self.h, int(direct_max_pairs), int(sample_size),
                                                    int(candidate_capacity)))
 
-    def step_with_model(self, model, hessian=False):
+    def step_with_model(self, model, hessian=False, pipelined=True):
         """One SVGD::Step with host gradients from `model` (overlapped with the
         device median via begin/finish).  hessian=True: the Hessian kernel
-        scale, with this shard's sum of -hess log p supplied from `model`."""
+        scale, with this shard's sum of -hess log p supplied from `model`.
+        A built-in GaussianSum runs through svgd_step_host_model (the X_t copy,
+        the gradient and the G upload pipelined in row chunks, all in C);
+        pipelined=False takes the split begin / gradient / finish calls."""
+        if pipelined and not hessian and isinstance(model, GaussianSum):
+            self.check(self.lib.svgd_step_host_model(self.h, model._handle))
+            return
         self.check(self.lib.svgd_begin_step(self.h, self.x_host_ptr))
         nr = self.row1 - self.row0
         if hessian:

@@ -27,6 +27,7 @@ using namespace svgd_amd;
 namespace {
 
 constexpr int64_t TB = 64;
+constexpr int XCH = 8; // row chunks of the pipelined host-gradient step
 
 struct EvPair {
     hipEvent_t a, b;
@@ -130,6 +131,7 @@ struct svgd_ctx {
     // communicator, one issue order on every rank)
     hipStream_t cstream = nullptr;
     hipEvent_t ev_xready = nullptr, ev_g = nullptr;
+    hipEvent_t ev_xch[XCH] = {};     // X_t row chunks on the host (svgd_step_host_model)
 
     // optimizer
     int opt_kind = -1;
@@ -1063,6 +1065,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_x, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_xready, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_g, hipEventDisableTiming));
+    for (auto &e : c->ev_xch) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_cnt, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_scal, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming));
@@ -1162,6 +1165,8 @@ int svgd_destroy(svgd_ctx *c)
     if (c->ev_x) (void)hipEventDestroy(c->ev_x);
     if (c->ev_xready) (void)hipEventDestroy(c->ev_xready);
     if (c->ev_g) (void)hipEventDestroy(c->ev_g);
+    for (auto &e : c->ev_xch)
+        if (e) (void)hipEventDestroy(e);
     if (c->ev_cnt) (void)hipEventDestroy(c->ev_cnt);
     if (c->ev_scal) (void)hipEventDestroy(c->ev_scal);
     if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);
@@ -1416,6 +1421,61 @@ int svgd_finish_step(svgd_ctx *c, const double *G_shard)
     CHK(upload_g_begin(c, G_shard));
     // the G all-gather is queued before the host waits for the median counts
     // (scale_finish), so the device runs it during that round trip
+    CHK(upload_g_finish(c));
+    CHK(scale_finish(c));
+    CHK(run_phi_opt(c));
+    return SVGD_OK;
+}
+
+int svgd_step_host_model(svgd_ctx *c, const void *model)
+{
+    CHK(check_ready(c));
+    const svgd_amd::HostModel *m = static_cast<const svgd_amd::HostModel *>(model);
+    if (!m || m->d != c->dim)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Host model missing or of another dimension.");
+    if (c->scale_method == SVGD_SCALE_HESSIAN)
+        return fail(c, SVGD_ERR_ARG,
+                    "[Argument Error] svgd_step_host_model does not supply the Hessian scale's sum; "
+                    "use svgd_begin_step / svgd_set_step_hessian_sum / svgd_finish_step.");
+    CHK(resolve_pending(c));
+    if (c->opt_kind < 0)
+        return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
+    const int d = c->dim;
+    const int64_t rows = c->nrows;
+    // row chunks of >= 1 MiB (a chunk's copy, event and OpenMP region cost
+    // ~10 us: smaller chunks lose more than they overlap), at most XCH
+    const int64_t min_rows = std::max<int64_t>(1, (int64_t(1) << 20) / (8 * d));
+    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(XCH, rows / min_rows));
+    auto chunk = [&](int q, int64_t *r0, int64_t *r1) {
+        *r0 = rows * q / nch;
+        *r1 = rows * (q + 1) / nch;
+    };
+    HIPCHK(c, hipEventSynchronize(c->ev_g)); // the previous step's upload has left h_g
+    if (rows > 0) {
+        // X_t is final once the previous step's update (and all-gather) ran
+        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_xready, 0));
+        for (int q = 0; q < nch; ++q) {
+            int64_t r0, r1;
+            chunk(q, &r0, &r1);
+            HIPCHK(c, hipMemcpyAsync(c->h_x + r0 * d, c->X + (size_t)(c->row0 + r0) * d,
+                                     sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyDeviceToHost,
+                                     c->cstream));
+            HIPCHK(c, hipEventRecord(c->ev_xch[q], c->cstream));
+        }
+    }
+    CHK(plan_step(c));
+    CHK(scale_begin(c));
+    for (int q = 0; q < nch && rows > 0; ++q) {
+        int64_t r0, r1;
+        chunk(q, &r0, &r1);
+        HIPCHK(c, hipEventSynchronize(c->ev_xch[q]));
+        if (svgd_model_logp_grad(const_cast<void *>(model), c->h_x + r0 * d, r1 - r0, c->h_g + r0 * d))
+            return fail(c, SVGD_ERR_ARG, "[Argument Error] Host model evaluation failed.");
+        HIPCHK(c, hipMemcpyAsync(c->G + (size_t)(c->row0 + r0) * d, c->h_g + r0 * d,
+                                 sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyHostToDevice,
+                                 c->cstream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_g, c->cstream));
     CHK(upload_g_finish(c));
     CHK(scale_finish(c));
     CHK(run_phi_opt(c));
