@@ -12,7 +12,7 @@ libsvgdcpp_amd.so and numpy + the oracle as the arithmetic:
         sample sequence; two 11-bit radix passes over the sample keys, each
         with ONE all-reduce of the two selections' histograms, resolve the
         sample order statistics sigma either side of the target quantiles to
-        22 bits -> bracket [lo, hi) (k_bracket);
+        22 bits -> bracket [lo, hi) (set by the last k_select_scan);
      b. collect over this rank's svgd_plan_pair_tiles tiles: keys below lo are
         counted, keys in [lo, hi) kept and histogrammed in NBK key-range
         buckets; ONE all-reduce of [below, candidates, NBK bucket counts];
@@ -20,7 +20,11 @@ libsvgdcpp_amd.so and numpy + the oracle as the arithmetic:
         names the bucket(s) of the order statistics; each rank compacts its
         keys in them, ONE all-gather of the segments, every rank selects the
         same keys; bracket miss: streamed radix select over every key (one
-        all-reduce per 11-bit digit) -- the library's fallback;
+        all-reduce per 11-bit digit) -- the library's fallback.  (The library
+        usually plans the buckets on the device instead -- k_plan_select, the
+        same scan over the same all-reduced counts, so every rank reaches the
+        same plan without the host round trip; this re-enactment keeps the
+        host planner, which the synchronous path and redo still use);
   3. phi_hat, Adam and clamp for own rows; all-gather the new X.
 """
 import ctypes
