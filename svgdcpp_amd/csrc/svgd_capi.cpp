@@ -1433,10 +1433,11 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     const svgd_amd::HostModel *m = static_cast<const svgd_amd::HostModel *>(model);
     if (!m || m->d != c->dim)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Host model missing or of another dimension.");
-    if (c->scale_method == SVGD_SCALE_HESSIAN)
-        return fail(c, SVGD_ERR_ARG,
-                    "[Argument Error] svgd_step_host_model does not supply the Hessian scale's sum; "
-                    "use svgd_begin_step / svgd_set_step_hessian_sum / svgd_finish_step.");
+    if (c->scale_method == SVGD_SCALE_HESSIAN) // (the split calls carry the caller's sum)
+        return fail(c, SVGD_ERR_UNSET,
+                    "[Unset Error] Hessian scale: svgd_set_step_hessian_sum was not called this step "
+                    "(svgd_step_host_model does not supply it; use svgd_begin_step / "
+                    "svgd_set_step_hessian_sum / svgd_finish_step).");
     CHK(resolve_pending(c));
     if (c->opt_kind < 0)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");

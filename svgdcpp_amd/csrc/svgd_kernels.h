@@ -141,8 +141,11 @@ hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int
 hipError_t launch_plan_select(const unsigned long long *cnt, SelState *st, int nsel, uint64_t r0,
                               uint64_t r1, int64_t capr, uint64_t *seg, int *status,
                               int *host_status, hipStream_t stream);
-// per-rank segment capacity of the speculative bucket select
-constexpr int CAPR = 4096;
+// per-rank segment capacity of the speculative bucket select.  At cfg3 a
+// bucket holds ~3k keys: 4096 made ~1 in 5 early steps fail the plan (each
+// failure redoes the step); the selection reads only the keys present, and
+// the all-gather (P > 1) moves 128 KiB per rank
+constexpr int CAPR = 16384;
 
 // Row-stream path (d <= 16): particle records rec_j = [xc_j | G_j - 2a xc_j | c_j | 0..],
 // stride phi_rec_stride(d).  phi partials over S column splits -> part[S][ldp][d+1].

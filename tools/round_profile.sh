@@ -19,11 +19,11 @@ python3 tools/kstats.py $OUT/rocprof_kernel_stats.csv > $OUT/rocprof_kernel_stat
 python3 tools/ktimed.py gpurun_out/prof_round/run_kernel_trace.csv 3 > $OUT/rocprof_kernel_timed.txt
 python3 tools/step_timeline.py gpurun_out/prof_round/run_kernel_trace.csv > $OUT/step_timeline.txt
 TAG=_round bash tools/pmc.sh FETCH_SIZE WRITE_SIZE || exit 1
-timeout -k 10 400 python bench.py --config cfg5 --steps 5 --warmup 1 --no-cpu > $OUT/bench_cfg5.log 2>&1 || exit 1
+timeout -k 10 400 python bench.py --config cfg5 --steps 20 --warmup 3 --no-cpu > $OUT/bench_cfg5.log 2>&1 || exit 1
 fault_guard $OUT/bench_cfg5.log
 tail -1 $OUT/bench_cfg5.log > $OUT/bench_cfg5.json
-STEPS=5 WARMUP=1 TAG=_cfg5 BENCH_ARGS="--config cfg5" bash tools/profile.sh > /dev/null || exit 1
-python3 tools/ktimed.py gpurun_out/prof_cfg5/run_kernel_trace.csv 1 > $OUT/rocprof_cfg5_kernel_timed.txt
+STEPS=10 WARMUP=3 TAG=_cfg5 BENCH_ARGS="--config cfg5" bash tools/profile.sh > /dev/null || exit 1
+python3 tools/ktimed.py gpurun_out/prof_cfg5/run_kernel_trace.csv 3 > $OUT/rocprof_cfg5_kernel_timed.txt
 timeout -k 10 400 python bench.py --config cfg2 --steps 20 --warmup 3 --no-cpu > $OUT/bench_cfg2.log 2>&1 || exit 1
 tail -1 $OUT/bench_cfg2.log > $OUT/bench_cfg2.json
 echo round profile done
