@@ -87,11 +87,13 @@ GradBlockFn pick_grad_block()
                                                                            : gb_base::logp_grad_block;
 }
 
-static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, double *G)
+static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, double *G,
+                           int nthreads)
 {
     static const GradBlockFn block = pick_grad_block();
     const int d = m->d, k = m->k;
-#pragma omp parallel
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel num_threads(nthreads)
     {
         std::vector<double> diff((size_t)GB_NP * d), gc((size_t)GB_NP * k * d), q((size_t)GB_NP * k);
         const int64_t nblk = (nrows + GB_NP - 1) / GB_NP;
@@ -103,6 +105,16 @@ static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, d
         }
     }
 }
+
+namespace svgd_amd {
+int model_logp_grad_threads(const HostModel *m, const double *X, int64_t nrows, double *G,
+                            int nthreads)
+{
+    if (!m || (!X && nrows > 0) || (!G && nrows > 0)) return SVGD_ERR_ARG;
+    logp_grad_rows(m, X, nrows, G, nthreads);
+    return SVGD_OK;
+}
+} // namespace svgd_amd
 
 extern "C" {
 
@@ -139,7 +151,7 @@ int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G)
 {
     const HostModel *m = static_cast<const HostModel *>(model);
     if (!m || (!X && nrows > 0) || (!G && nrows > 0)) return SVGD_ERR_ARG;
-    logp_grad_rows(m, X, nrows, G);
+    logp_grad_rows(m, X, nrows, G, 0);
     return SVGD_OK;
 }
 

@@ -1,6 +1,7 @@
 // Internal layout of the built-in Gaussian-sum model handle (host_models.cpp),
 // shared with the C ABI so a context can mirror the model on the device.
 #pragma once
+#include <cstdint>
 #include <vector>
 
 namespace svgd_amd {
@@ -10,4 +11,7 @@ struct HostModel {
     std::vector<double> prec; // k x d x d (row-major), inverse covariances
     std::vector<double> precT; // the same, each transposed (prec[c][r][l] at [c][l][r])
 };
+// svgd_model_logp_grad on nthreads OpenMP threads (<= 0: the OpenMP default)
+int model_logp_grad_threads(const HostModel *m, const double *X, int64_t nrows, double *G,
+                            int nthreads);
 } // namespace svgd_amd
