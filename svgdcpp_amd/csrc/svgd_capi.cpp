@@ -29,6 +29,7 @@ namespace {
 
 constexpr int64_t TB = 64;
 constexpr int XCH = 8; // row chunks of the pipelined host-gradient step
+constexpr int64_t TBJ_COLS = 32; // column tile of k_phi_f32s (TBJ in svgd_kernels.hip)
 
 struct EvPair {
     hipEvent_t a, b;
@@ -69,6 +70,7 @@ struct svgd_ctx {
     double *scal = nullptr; // [0] a, [1] med
     // SVGD_F32: fp32 copies feeding the tile kernels
     float *xcf = nullptr, *nrmf = nullptr, *cvf = nullptr, *Vf = nullptr, *zcf = nullptr;
+    float *XS = nullptr, *VS = nullptr; // operand-ordered column copies (k_phi_f32s)
 
     // row-stream path (d <= ROWS_MAX_D)
     bool rowpath = false;
@@ -806,8 +808,16 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     else
         HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
                                 c->V, c->cvec, c->stream));
+    // F32: the streamed kernel's operand-ordered column copies (k_swz_f32), or
+    // the row-major fp32 copies of the generic tile kernel
+    const bool phis = c->dtype == SVGD_F32 && c->XS && c->row0 % 16 == 0;
+    const int64_t ntl = (c->n + TBJ_COLS - 1) / TBJ_COLS;
     if (c->dtype == SVGD_F32) {
-        HIPCHK(c, launch_cvt_f32(c->V, c->np * c->VW, c->Vf, c->stream));
+        if (phis)
+            HIPCHK(c, launch_swz_f32(mat ? c->zc : c->xc, c->KP, c->V, c->VW, c->cvec, ntl, c->XS,
+                                     c->VS, c->stream));
+        else
+            HIPCHK(c, launch_cvt_f32(c->V, c->np * c->VW, c->Vf, c->stream));
         HIPCHK(c, launch_cvt_f32(c->cvec, c->np, c->cvf, c->stream));
         if (mat) HIPCHK(c, launch_cvt_f32(c->zc, c->np * c->KP, c->zcf, c->stream));
     }
@@ -815,6 +825,10 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
                                   mat ? c->sc_sgn : nullptr, c->phi, opt, c->stream));
+    else if (phis)
+        HIPCHK(c, launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
+                                  c->row0, c->nrows, ntl, c->dim, 1.0 / (double)c->n,
+                                  mat ? c->wv : nullptr, c->xc, c->KP, c->phi, c->stream));
     else if (c->dtype == SVGD_F32)
         HIPCHK(c, launch_phi_f32(c->KP, c->NCB, mat ? c->zcf : c->xcf, c->cvf, c->Vf, c->scal,
                                  c->row0, c->nrows, (c->n + TB - 1) / TB, c->dim,
@@ -1037,6 +1051,11 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
+        if (f32 && phi_f32s_supported(c->KP, c->NCB) && !std::getenv("SVGD_PHI_TILE_GENERIC")) {
+            // np is a multiple of 2 TBJ_COLS: ceil(n / TBJ_COLS) tiles fit
+            CHK(dalloc(c, &c->XS, c->np * c->KP));
+            CHK(dalloc(c, &c->VS, c->np * 16 * (c->NCB + 1)));
+        }
     }
     CHK(dalloc(c, &c->phi, std::max<int64_t>(1, c->nrows) * dim));
     CHK(dalloc(c, &c->m, std::max<int64_t>(1, c->nrows) * dim));
@@ -1152,7 +1171,7 @@ int svgd_destroy(svgd_ctx *c)
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
                        c->sc_sgn,  c->sc_work, c->bak};
-    float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf};
+    float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf, c->XS, c->VS};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
     for (double *p : dbufs)

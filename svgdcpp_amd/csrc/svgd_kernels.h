@@ -196,6 +196,19 @@ hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm,
                             int64_t nb, int64_t t0, int64_t t1, uint64_t *regions, int64_t cap,
                             uint32_t *counts, unsigned long long *below, const SelState *st,
                             uint32_t *bpart, hipStream_t stream);
+// F32 tile phi, streamed (k_phi_f32s): operand-ordered fp32 copies of the
+// columns (XS, VS: ntiles = ceil(n / 32) tiles of 32 particles; XS holds
+// ntiles * 32 * KP floats, VS ntiles * 2 * (VW/16 + 1) * 256) made by
+// launch_swz_f32 from the fp64 coordinates x (stride KP), V (stride VW) and
+// cvec; rows from the row-major fp32 copy xrow (stride KP) and crow.
+// KP % 16 == 0 (phi_f32s_supported); row0 % 16 == 0.
+hipError_t launch_swz_f32(const double *x, int KP, const double *V, int VW, const double *cvec,
+                          int64_t ntiles, float *XS, float *VS, hipStream_t stream);
+bool phi_f32s_supported(int KP, int NCB);
+hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, const float *xrow,
+                           const float *crow, const double *a_ptr, int64_t row0, int64_t nrows,
+                           int64_t ntiles, int d, double inv_n, const double *wv, const double *xc,
+                           int xc_stride, double *phi, hipStream_t stream);
 int phi_rows_blocks_per_cu(int d, int R);
 // G = grad log p of the Gaussian-sum model for `rows` particle rows (d <= 64)
 hipError_t launch_gauss_grad(const double *X, int64_t rows, int d, int k, const double *mu,

@@ -1844,6 +1844,148 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     }
 }
 
+// ------------------------------------------- fp32 tile phi, streamed (F32) --
+//
+// k_phi<float>'s arithmetic (Gram on v_mfma_f32_16x16x4f32, P = 2^t by
+// v_exp_f32, acc += P V on the MFMA), restructured for the fp32 MFMA rate:
+// the column tiles (32 particles) stream through two LDS buffers by
+// global_load_lds DMA -- the next tile lands while the current one is
+// computed, one barrier per tile -- from operand-ordered copies made once per
+// step (k_swz_f32), so every LDS read is a conflict-free 16-byte read of 64
+// consecutive lanes:
+//   XS[t][js][u][lane][e]  = x[32t + 16js + lane%16][16u + 4(lane/16) + e]
+//                           (the Gram A operand of MFMA step 4u+e, kslot order)
+//   VS[t][js][cb][lane][r] = V[32t + 16js + 4(lane/16) + r][16cb + lane%16]
+//                           (the P.V B operand of step r), plane NCB: c_j
+// Rows (B operand of the Gram) come from the row-major fp32 copy in the same
+// kslot order.  Wave w owns rows 16w..16w+15 of the block's 64.
+constexpr int TBJ = 32; // columns per streamed tile
+
+__global__ void k_swz_f32(const double *__restrict__ x, int KP, const double *__restrict__ V,
+                          int VW, const double *__restrict__ cvec, int64_t ntiles,
+                          float *__restrict__ XS, float *__restrict__ VS)
+{
+    const int KU = KP / 16, NCB = VW / 16;
+    const int64_t nx = ntiles * TBJ * KP, nv = ntiles * 2 * (NCB + 1) * 256;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nx + nv;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < nx) {
+            const int q4 = (int)(e & 3), lane = (int)((e >> 2) & 63);
+            int64_t r = e >> 8;
+            const int u = (int)(r % KU);
+            r /= KU;
+            const int js = (int)(r & 1);
+            const int64_t t = r >> 1;
+            const int64_t j = t * TBJ + 16 * js + (lane & 15);
+            XS[e] = (float)x[j * KP + 16 * u + 4 * (lane >> 4) + q4];
+        } else {
+            const int64_t f = e - nx;
+            const int rr = (int)(f & 3), lane = (int)((f >> 2) & 63);
+            int64_t r = f >> 8;
+            const int cb = (int)(r % (NCB + 1));
+            r /= (NCB + 1);
+            const int js = (int)(r & 1);
+            const int64_t t = r >> 1;
+            const int64_t j = t * TBJ + 16 * js + 4 * (lane >> 4) + rr;
+            VS[f] = cb < NCB ? (float)V[j * VW + 16 * cb + (lane & 15)] : (float)cvec[j];
+        }
+    }
+}
+
+template <int KP, int NCB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_phi_f32s(
+    const float *__restrict__ XS, const float *__restrict__ VS, const float *__restrict__ xrow,
+    const float *__restrict__ crow, const double *__restrict__ a_ptr, int64_t row0, int64_t nrows,
+    int64_t ntiles, int d, double inv_n, const double *__restrict__ wv,
+    const double *__restrict__ xc, int xc_stride, double *__restrict__ phi)
+{
+    constexpr int KK = KP / 4, KU = KP / 16;
+    constexpr int VW = 16 * NCB;
+    constexpr int PX = 2 * KU, PV = 2 * (NCB + 1); // 1 KiB pieces per tile
+    constexpr int BUF = (PX + PV) * 256;            // floats per LDS buffer
+    __shared__ __attribute__((aligned(16))) float sbuf[2 * BUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lo = lane & 15, hi = lane >> 4;
+    const double a = *a_ptr;
+    const float alpha = (float)(2.0 * a * LOG2E);
+
+    const int64_t ibase = row0 + (int64_t)blockIdx.x * 64 + w * 16;
+    float bI[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) bI[kk] = xrow[(ibase + lo) * KP + kslot<float, KP>(kk, hi)];
+    const float ci = crow[ibase + lo];
+
+    f4_t acc[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
+
+    // this wave's share of tile t's DMA pieces into buffer b
+    auto issue = [&](int64_t t, int b) {
+        const char *gx = reinterpret_cast<const char *>(XS + t * (PX * 256));
+        const char *gv = reinterpret_cast<const char *>(VS + t * (PV * 256));
+        char *lb = reinterpret_cast<char *>(sbuf + b * BUF);
+#pragma unroll
+        for (int p = w; p < PX + PV; p += 4) {
+            const char *g = p < PX ? gx + p * 1024 : gv + (p - PX) * 1024;
+            __builtin_amdgcn_global_load_lds((gbl_void *)(g + lane * 16), (lds_void *)(lb + p * 1024), 16, 0, 0);
+        }
+    };
+    if (ntiles > 0) issue(0, 0);
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int b = (int)(t & 1);
+        wait_vmcnt<0>();  // this wave's pieces of tile t
+        __syncthreads(); // everyone's pieces; everyone is done with buffer b ^ 1
+        if (t + 1 < ntiles) issue(t + 1, b ^ 1);
+        const float *lx = sbuf + b * BUF, *lv = lx + PX * 256;
+#pragma unroll
+        for (int js = 0; js < 2; ++js) {
+            float A[KK];
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const f4_t q = *reinterpret_cast<const f4_t *>(lx + (js * KU + u) * 256 + lane * 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) A[4 * u + e] = q[e];
+            }
+            f4_t dot = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk)
+                dot = __builtin_amdgcn_mfma_f32_16x16x4f32(A[kk], bI[kk], dot, 0, 0, 0);
+            const f4_t cj = *reinterpret_cast<const f4_t *>(lv + (js * (NCB + 1) + NCB) * 256 + lane * 4);
+            f4_t vv[NCB];
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+                vv[cb] = *reinterpret_cast<const f4_t *>(lv + (js * (NCB + 1) + cb) * 256 + lane * 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float p = exp2_nonpos(fmaf(alpha, dot[r], ci + cj[r]));
+#pragma unroll
+                for (int cb = 0; cb < NCB; ++cb)
+                    acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(p, vv[cb][r], acc[cb], 0, 0, 0);
+            }
+        }
+    }
+
+    // epilogue (fp64), through LDS (the tile buffers are free after the barrier)
+    __syncthreads();
+    float *sAcc = sbuf + w * 16 * (VW + 1);
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sAcc[(4 * hi + q) * (VW + 1) + cb * 16 + lo] = acc[cb][q];
+    __syncthreads();
+    const double two_a = 2.0 * a;
+    for (int e = lane; e < 16 * d; e += 64) {
+        const int il = e / d, c = e - il * d;
+        const int64_t i = ibase + il;
+        if (i - row0 < nrows) {
+            const double s1 = (double)sAcc[il * (VW + 1) + d];
+            const double wgt = wv ? wv[i * d + c] : two_a * xc[i * xc_stride + c];
+            phi[(i - row0) * d + c] = inv_n * ((double)sAcc[il * (VW + 1) + c] + wgt * s1);
+        }
+    }
+}
+
 // phi_i = (sum_s acc_s + 2a xc_i sum_s acc1_s) / N, partials summed in s order.
 // wv (full-matrix scale): 2 M xc_i per particle, in place of 2 a xc_i.
 // A block owns PHI_RED_ROWS rows: their (d+1)-element partial rows are
@@ -2660,6 +2802,42 @@ hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, cons
     return launch_pair_tiles_t<double>(KP, 3, grid, xc, nrm, n, 0, 0, ntiles, nullptr, 0, nullptr,
                                        nullptr, nullptr, nullptr, nullptr, nullptr, stream, keys);
 }
+
+hipError_t launch_swz_f32(const double *x, int KP, const double *V, int VW, const double *cvec,
+                          int64_t ntiles, float *XS, float *VS, hipStream_t stream)
+{
+    if (KP % 16 || VW % 16 || ntiles <= 0) return hipErrorInvalidValue;
+    const int64_t tot = ntiles * TBJ * KP + ntiles * 2 * (VW / 16 + 1) * 256;
+    int64_t g = (tot + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(k_swz_f32, dim3(g), dim3(256), 0, stream, x, KP, V, VW, cvec, ntiles, XS, VS);
+    return hipGetLastError();
+}
+
+#define SVGD_PHIS_CASE(KPv, NCBv)                                                            \
+    if (KP == KPv && NCB == NCBv) {                                                          \
+        hipLaunchKernelGGL((k_phi_f32s<KPv, NCBv>), dim3(grid), dim3(256), 0, stream, XS, VS, xrow, \
+                           crow, a_ptr, row0, nrows, ntiles, d, inv_n, wv, xc, xc_stride, phi); \
+        return hipGetLastError();                                                            \
+    }
+
+bool phi_f32s_supported(int KP, int NCB) { return KP % 16 == 0 && KP <= 64 && NCB >= 1 && NCB <= 5; }
+
+hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, const float *xrow,
+                           const float *crow, const double *a_ptr, int64_t row0, int64_t nrows,
+                           int64_t ntiles, int d, double inv_n, const double *wv, const double *xc,
+                           int xc_stride, double *phi, hipStream_t stream)
+{
+    if (nrows <= 0) return hipSuccess;
+    if (row0 % 16) return hipErrorInvalidValue; // (waves own 16-row groups of the padded rows)
+    const int64_t grid = (nrows + 63) / 64;
+    SVGD_PHIS_CASE(16, 1) SVGD_PHIS_CASE(16, 2)
+    SVGD_PHIS_CASE(32, 1) SVGD_PHIS_CASE(32, 2) SVGD_PHIS_CASE(32, 3)
+    SVGD_PHIS_CASE(64, 1) SVGD_PHIS_CASE(64, 2) SVGD_PHIS_CASE(64, 3) SVGD_PHIS_CASE(64, 4)
+    SVGD_PHIS_CASE(64, 5)
+    return hipErrorInvalidValue;
+}
+#undef SVGD_PHIS_CASE
 
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream)
 {

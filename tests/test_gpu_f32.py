@@ -115,3 +115,24 @@ def test_f32_matrix_scale(oracle):
     ph = c.phi(G, 0.0)
     ref = oracle.phi_matrix(X, G, M)
     assert np.max(np.abs(ph - ref)) <= REL * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("n,d", [(300, 13), (1000, 20), (2049, 33), (4096, 64), (777, 64)])
+def test_streamed_tile_phi_matches_generic(oracle, monkeypatch, n, d):
+    """k_phi_f32s (operand-ordered streamed columns) against the generic fp32
+    tile kernel (SVGD_PHI_TILE_GENERIC=1) and the fp64 oracle."""
+    X = oracle.splitmix((n, d), 2.0, n + 7 * d)
+    G = oracle.splitmix((n, d), 1.0, n + d + 1)
+    out = []
+    for generic in (False, True):
+        if generic:
+            monkeypatch.setenv("SVGD_PHI_TILE_GENERIC", "1")
+        c = S.Context(d, n, dtype=C.SVGD_F32)
+        c.set_particles(X)
+        a = 0.7 / d
+        out.append(c.phi(G, a))
+        c.close()
+    ref = oracle.phi(X, G, a)
+    scale = np.max(np.abs(ref))
+    assert np.max(np.abs(out[0] - ref)) <= 1e-4 * scale
+    assert np.max(np.abs(out[0] - out[1])) <= 1e-4 * scale
