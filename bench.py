@@ -297,9 +297,13 @@ def main():
                 # kernel is > 99 % of it at cfg3 (profiles/r02_*kernel_stats*)
                 "kernel": ("k_phi_rows (fused RBF + grad + phi contraction, fp64 VALU row stream)"
                            if dtype == "f64" and d <= 16 else
+                           "k_phi_f32s (fused RBF + grad + phi contraction, streamed fp32 MFMA tiles)"
+                           if dtype == "f32" and d > 12 else
                            "k_phi (fused RBF + grad + phi contraction, MFMA tiles)"),
-                "timed_span": "k_prep_rec + k_phi_rows + k_phi_reduce (fused update)"
-                              if dtype == "f64" and d <= 16 else "k_prep_v + k_phi (+ cvt)",
+                "timed_span": ("k_prep_rec + k_phi_rows + k_phi_reduce (fused update)"
+                               if dtype == "f64" and d <= 16 else
+                               "k_prep_v + k_swz_f32 + k_cvt_f32 + k_phi_f32s"
+                               if dtype == "f32" and d > 12 else "k_prep_v + k_phi (+ cvt)"),
                 "bound": "valu" if dtype == "f64" and d <= 16 else "mfma",
                 "achieved": achieved,
                 "peak": peak,
