@@ -766,6 +766,12 @@ bool matrix_scale(const svgd_ctx *c)
     return c->scale_method == SVGD_SCALE_MATRIX || c->scale_method == SVGD_SCALE_HESSIAN;
 }
 
+// F32 with the streamed tile phi (operand-ordered copies allocated, 16-aligned rows)
+bool phi_streamed(const svgd_ctx *c)
+{
+    return c->dtype == SVGD_F32 && c->XS && c->row0 % 16 == 0;
+}
+
 int run_phi(svgd_ctx *c, const OptArgs *opt)
 {
     // phi phase: the record preparation (V = G - 2a xc, part of the
@@ -810,7 +816,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
                                 c->V, c->cvec, c->stream));
     // F32: the streamed kernel's operand-ordered column copies (k_swz_f32), or
     // the row-major fp32 copies of the generic tile kernel
-    const bool phis = c->dtype == SVGD_F32 && c->XS && c->row0 % 16 == 0;
+    const bool phis = phi_streamed(c);
     const int64_t ntl = (c->n + TBJ_COLS - 1) / TBJ_COLS;
     if (c->dtype == SVGD_F32) {
         if (phis)
@@ -828,7 +834,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     else if (phis)
         HIPCHK(c, launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
                                   c->row0, c->nrows, ntl, c->dim, 1.0 / (double)c->n,
-                                  mat ? c->wv : nullptr, c->xc, c->KP, c->phi, c->stream));
+                                  mat ? c->wv : nullptr, c->xc, c->KP, c->phi, opt, c->stream));
     else if (c->dtype == SVGD_F32)
         HIPCHK(c, launch_phi_f32(c->KP, c->NCB, mat ? c->zcf : c->xcf, c->cvf, c->Vf, c->scal,
                                  c->row0, c->nrows, (c->n + TB - 1) / TB, c->dim,
@@ -865,15 +871,16 @@ int opt_args(svgd_ctx *c, OptArgs *o)
     return SVGD_OK;
 }
 
-// The step's phi and optimizer update: on the row path the update is applied
-// by the phi reduce itself (one launch fewer), else by k_opt_update.
+// The step's phi and optimizer update: on the row path and the streamed F32
+// tile path the phi kernel's epilogue applies it (one launch fewer, no phi
+// re-read), else k_opt_update.
 int run_phi_opt(svgd_ctx *c)
 {
     if (c->opt_kind < 0)
         return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid Optimizer object pointer.");
     OptArgs o;
     CHK(opt_args(c, &o));
-    const bool fused = c->rowpath;
+    const bool fused = c->rowpath || phi_streamed(c);
     CHK(run_phi(c, fused ? &o : nullptr));
     if (!fused) HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
     CHK(allgather_rows(c, c->X));

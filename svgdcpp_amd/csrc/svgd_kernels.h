@@ -208,7 +208,7 @@ bool phi_f32s_supported(int KP, int NCB);
 hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, const float *xrow,
                            const float *crow, const double *a_ptr, int64_t row0, int64_t nrows,
                            int64_t ntiles, int d, double inv_n, const double *wv, const double *xc,
-                           int xc_stride, double *phi, hipStream_t stream);
+                           int xc_stride, double *phi, const OptArgs *opt, hipStream_t stream);
 int phi_rows_blocks_per_cu(int d, int R);
 // G = grad log p of the Gaussian-sum model for `rows` particle rows (d <= 64)
 hipError_t launch_gauss_grad(const double *X, int64_t rows, int d, int k, const double *mu,

@@ -225,19 +225,21 @@ __global__ void k_prep_v(const double *__restrict__ xc, const double *__restrict
                          int64_t n, int64_t np, int d, int KP, int VW,
                          double *__restrict__ V, double *__restrict__ cvec)
 {
+    // one thread per element of V (coalesced stores; a thread per particle
+    // wrote 16 NCB-strided doubles: 76 -> ~20 us at N = 65536, d = 64)
     const double a = *a_ptr;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < np;
-         j += (int64_t)gridDim.x * blockDim.x) {
-        const bool live = j < n;
-        for (int c = 0; c < VW; ++c) {
-            double v = 0.0;
-            if (live) {
-                if (c < d) v = G[j * d + c] - 2.0 * a * xc[j * KP + c];
-                else if (c == d) v = 1.0;
-            }
-            V[j * VW + c] = v;
+    const int64_t tot = np * VW;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = e / VW;
+        const int c = (int)(e - j * VW);
+        double v = 0.0;
+        if (j < n) {
+            if (c < d) v = G[j * d + c] - 2.0 * a * xc[j * KP + c];
+            else if (c == d) v = 1.0;
         }
-        cvec[j] = live ? -a * LOG2E * nrm[j] : 0.0;
+        V[e] = v;
+        if (c == 0) cvec[j] = j < n ? -a * LOG2E * nrm[j] : 0.0;
     }
 }
 
@@ -1897,7 +1899,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const float *__restrict__ XS, const float *__restrict__ VS, const float *__restrict__ xrow,
     const float *__restrict__ crow, const double *__restrict__ a_ptr, int64_t row0, int64_t nrows,
     int64_t ntiles, int d, double inv_n, const double *__restrict__ wv,
-    const double *__restrict__ xc, int xc_stride, double *__restrict__ phi)
+    const double *__restrict__ xc, int xc_stride, double *__restrict__ phi, OptArgs opt, int do_opt)
 {
     constexpr int KK = KP / 4, KU = KP / 16;
     constexpr int VW = 16 * NCB;
@@ -1981,7 +1983,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         if (i - row0 < nrows) {
             const double s1 = (double)sAcc[il * (VW + 1) + d];
             const double wgt = wv ? wv[i * d + c] : two_a * xc[i * xc_stride + c];
-            phi[(i - row0) * d + c] = inv_n * ((double)sAcc[il * (VW + 1) + c] + wgt * s1);
+            const double ph = inv_n * ((double)sAcc[il * (VW + 1) + c] + wgt * s1);
+            phi[(i - row0) * d + c] = ph;
+            if (do_opt) opt_elem(opt, (i - row0) * d + c, ph);
         }
     }
 }
@@ -2817,7 +2821,8 @@ hipError_t launch_swz_f32(const double *x, int KP, const double *V, int VW, cons
 #define SVGD_PHIS_CASE(KPv, NCBv)                                                            \
     if (KP == KPv && NCB == NCBv) {                                                          \
         hipLaunchKernelGGL((k_phi_f32s<KPv, NCBv>), dim3(grid), dim3(256), 0, stream, XS, VS, xrow, \
-                           crow, a_ptr, row0, nrows, ntiles, d, inv_n, wv, xc, xc_stride, phi); \
+                           crow, a_ptr, row0, nrows, ntiles, d, inv_n, wv, xc, xc_stride, phi, \
+                           opt ? *opt : OptArgs{}, opt ? 1 : 0);                            \
         return hipGetLastError();                                                            \
     }
 
@@ -2826,7 +2831,7 @@ bool phi_f32s_supported(int KP, int NCB) { return KP % 16 == 0 && KP <= 64 && NC
 hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, const float *xrow,
                            const float *crow, const double *a_ptr, int64_t row0, int64_t nrows,
                            int64_t ntiles, int d, double inv_n, const double *wv, const double *xc,
-                           int xc_stride, double *phi, hipStream_t stream)
+                           int xc_stride, double *phi, const OptArgs *opt, hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
     if (row0 % 16) return hipErrorInvalidValue; // (waves own 16-row groups of the padded rows)
@@ -2866,8 +2871,8 @@ hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, c
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream)
 {
-    int64_t g = (np + 255) / 256;
-    if (g > 4096) g = 4096;
+    int64_t g = (np * VW + 255) / 256;
+    if (g > 8192) g = 8192;
     hipLaunchKernelGGL(k_prep_v, dim3(g), dim3(256), 0, stream, xc, G, nrm, a_ptr, n, np, d, KP,
                        VW, V, cvec);
     return hipGetLastError();
