@@ -17,6 +17,13 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
 
 #include "../../include/svgdcpp_amd/svgd_capi.h"
 #include "svgd_kernels.h"
@@ -33,6 +40,75 @@ constexpr int64_t TBJ_COLS = 32; // column tile of k_phi_f32s (TBJ in svgd_kerne
 
 struct EvPair {
     hipEvent_t a, b;
+    hipEvent_t spare = nullptr; // a's own event when a is a shared mark (back to the pool)
+};
+
+// One persistent host thread per context that runs the host-gradient half of
+// svgd_step_host_model (X_t chunks down -> grad log p -> G chunks up) while
+// the calling thread enqueues the step's median chain: the ~14 launches
+// (~5 us each) no longer sit in front of the gradient on one thread.  The
+// worker spins ~1 ms after a job (the next step usually follows within it),
+// then sleeps on the condition variable.
+class HostWorker {
+  public:
+    ~HostWorker()
+    {
+        if (!th_.joinable()) return;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        cv_.notify_one();
+        th_.join();
+    }
+    void post(std::function<int(std::string &)> job)
+    {
+        if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = std::move(job);
+            state_.store(1, std::memory_order_release);
+        }
+        cv_.notify_one();
+    }
+    // wait for the posted job; its return code (and message in err on failure)
+    int wait(std::string &err)
+    {
+        for (int spin = 0; state_.load(std::memory_order_acquire) != 2; ++spin)
+            if (spin > 64) std::this_thread::yield();
+        state_.store(0, std::memory_order_relaxed);
+        if (rc_) err = msg_;
+        return rc_;
+    }
+
+  private:
+    void loop()
+    {
+        for (;;) {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (state_.load(std::memory_order_acquire) != 1 &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(1))
+                std::this_thread::yield();
+            std::function<int(std::string &)> job;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [this] { return quit_ || state_.load() == 1; });
+                if (quit_) return;
+                job = std::move(job_);
+            }
+            msg_.clear();
+            rc_ = job(msg_);
+            state_.store(2, std::memory_order_release);
+        }
+    }
+    std::thread th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::function<int(std::string &)> job_;
+    std::atomic<int> state_{0}; // 0 idle, 1 posted, 2 done
+    int rc_ = 0;
+    std::string msg_;
+    bool quit_ = false;
 };
 
 } // namespace
@@ -176,11 +252,21 @@ struct svgd_ctx {
     // box whose CPU quota equals OMP_NUM_THREADS, all of them tripped the
     // cgroup throttle in ~1 of 3 runs (+0.45 ms/step at cfg3)
     int host_threads = 0;
+    std::unique_ptr<HostWorker> worker; // svgd_step_host_model's gradient thread
     bool last_fast = false;    // the last resolved median could have been speculative
     bool pending = false;      // a speculative step awaits its status
     bool scal_fresh = true;    // h_scal holds the last scale (fetch_scale)
     int *d_status = nullptr, *h_status = nullptr, *h_status_dev = nullptr; // (h_status as seen by kernels)
     hipEvent_t ev_status = nullptr;
+    // Every event record between two kernels costs a ~5 us dispatch gap, so
+    // the end of the median records ONE event that serves as the plan status
+    // (ev_status_use), the scale-final mark (ev_fin_use), the median phase's
+    // end and -- while no work was queued after it (mark) -- the phi phase's
+    // start.
+    hipEvent_t ev_status_use = nullptr, ev_fin_use = nullptr, mark = nullptr;
+    // likewise at the step's end: the phi phase's end event (timing) doubles
+    // as X_t-final for the copy stream (ev_xready_use) when nothing follows it
+    hipEvent_t phi_end = nullptr, ev_xready_use = nullptr;
     double *bak = nullptr; // [X_t | m_t | v_t] of this rank's rows for the pending step
 };
 
@@ -261,6 +347,7 @@ int64_t upper_pairs(int64_t n) { return n * (n - 1) / 2; }
 int allgather_rows(svgd_ctx *c, double *buf)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
+    c->mark = c->phi_end = nullptr; // work queued after the median's / phi's end event
     const size_t cnt = (size_t)c->chunk * c->dim;
     if (c->hcomm) {
         if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(double),
@@ -584,13 +671,16 @@ int median_finish_spec(svgd_ctx *c, double logn)
                                   c->scal, c->d_status, c->stream));
     // the plan's status is final once this completes (recorded after the
     // selection: an event between two kernels costs a ~5 us dispatch gap)
-    HIPCHK(c, hipEventRecord(c->ev_status, c->stream));
     // (c->pending -- the plan's status to check -- is set when the step is
     // complete, by median_finish: resolve_pending never redoes half a step)
     if (c->timing && !c->ev_med.empty()) {
-        HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+        c->ev_status_use = c->ev_med.back().b; // also the median phase's end
         c->med_ev_done = true;
+        c->mark = c->ev_status_use;
+    } else {
+        c->ev_status_use = c->ev_status;
     }
+    HIPCHK(c, hipEventRecord(c->ev_status_use, c->stream));
     return SVGD_OK;
 }
 
@@ -750,7 +840,10 @@ int upload_g_begin(svgd_ctx *c, const double *G_shard)
 // ... and, on the compute stream once it needs G, the all-gather of the shards.
 int upload_g_finish(svgd_ctx *c)
 {
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_g, 0));
+    // a G copy that has already landed needs no cross-queue barrier (a wait
+    // on the copy stream's signal cost a ~25 us dispatch gap before the
+    // record prep even when the copy had finished long before)
+    if (hipEventQuery(c->ev_g) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_g, 0));
     CHK(allgather_rows(c, c->G));
     return SVGD_OK;
 }
@@ -781,8 +874,14 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     EvPair ev{};
     if (c->timing) {
         ev = take_pair(c);
-        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+        if (c->mark) { // the median's end event, nothing queued since
+            ev.spare = ev.a;
+            ev.a = c->mark;
+        } else {
+            HIPCHK(c, hipEventRecord(ev.a, c->stream));
+        }
     }
+    c->mark = nullptr;
     const bool mat = matrix_scale(c);
     if (mat) {
         // M = factor * src, L = chol(M), a_eff = 1 (GaussianRBFKernel.hpp:189-210)
@@ -830,7 +929,8 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     if (c->rowpath)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
-                                  mat ? c->sc_sgn : nullptr, c->phi, opt, c->stream));
+                                  mat ? c->sc_sgn : nullptr, mat ? nullptr : c->nmax, c->phi, opt,
+                                  c->stream));
     else if (phis)
         HIPCHK(c, launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
                                   c->row0, c->nrows, ntl, c->dim, 1.0 / (double)c->n,
@@ -847,6 +947,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     if (c->timing) {
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         c->ev_phi.push_back(ev);
+        c->phi_end = ev.b;
     }
     return SVGD_OK;
 }
@@ -881,16 +982,27 @@ int run_phi_opt(svgd_ctx *c)
     OptArgs o;
     CHK(opt_args(c, &o));
     const bool fused = c->rowpath || phi_streamed(c);
+    c->phi_end = nullptr;
     CHK(run_phi(c, fused ? &o : nullptr));
-    if (!fused) HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
+    if (!fused) {
+        HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
+        c->phi_end = nullptr;
+    }
     CHK(allgather_rows(c, c->X));
-    HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
+    if (c->phi_end) {
+        c->ev_xready_use = c->phi_end;
+    } else {
+        HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
+        c->ev_xready_use = c->ev_xready;
+    }
+    c->phi_end = nullptr;
     return SVGD_OK;
 }
 
 int scale_begin(svgd_ctx *c)
 {
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0)); // the last [a, med] copy has read scal
+    if (hipEventQuery(c->ev_scal) != hipSuccess) // the last [a, med] copy has read scal
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0));
     const bool med = !(c->scale_method == SVGD_SCALE_FIXED || matrix_scale(c));
     // the median phase's start event goes before the centring (which it
     // needs): an event between two kernels costs a dispatch gap
@@ -922,12 +1034,19 @@ int scale_finish(svgd_ctx *c)
         return SVGD_OK;
     }
     CHK(median_finish(c));
-    if (c->timing && !c->ev_med.empty() && !c->med_ev_done)
-        HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
-    c->med_ev_done = false;
     // [a, med] reach the host only when asked (fetch_scale): no copy on the
-    // step's path; the event marks where this step's scale is final
-    HIPCHK(c, hipEventRecord(c->ev_fin, c->stream));
+    // step's path; the event marks where this step's scale is final (on the
+    // speculative path the status event, recorded right after the selection)
+    if (c->med_ev_done) {
+        c->ev_fin_use = c->ev_status_use;
+    } else {
+        if (c->timing && !c->ev_med.empty())
+            HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+        HIPCHK(c, hipEventRecord(c->ev_fin, c->stream));
+        c->ev_fin_use = c->ev_fin;
+        c->mark = nullptr;
+    }
+    c->med_ev_done = false;
     c->scal_fresh = false;
     return SVGD_OK;
 }
@@ -936,7 +1055,7 @@ int scale_finish(svgd_ctx *c)
 int fetch_scale(svgd_ctx *c)
 {
     if (c->scal_fresh) return SVGD_OK;
-    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_fin, 0));
+    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_fin_use ? c->ev_fin_use : c->ev_fin, 0));
     HIPCHK(c, hipMemcpyAsync(c->h_scal, c->scal, 2 * sizeof(double), hipMemcpyDeviceToHost,
                              c->cstream));
     HIPCHK(c, hipEventRecord(c->ev_scal, c->cstream));
@@ -953,7 +1072,7 @@ int resolve_pending(svgd_ctx *c)
 {
     if (!c->pending) return SVGD_OK;
     c->pending = false;
-    HIPCHK(c, hipEventSynchronize(c->ev_status));
+    HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
     if (*c->h_status == 0) return SVGD_OK;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipStreamSynchronize(c->cstream));
@@ -1170,6 +1289,7 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
 int svgd_destroy(svgd_ctx *c)
 {
     if (!c) return SVGD_OK;
+    c->worker.reset(); // idle between steps: joins the gradient thread
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -1193,7 +1313,7 @@ int svgd_destroy(svgd_ctx *c)
         if (p) (void)hipHostFree(p);
     for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})
         for (auto &e : *v) {
-            (void)hipEventDestroy(e.a);
+            (void)hipEventDestroy(e.spare ? e.spare : e.a); // (a shared mark is ev_med's b)
             (void)hipEventDestroy(e.b);
         }
     if (c->ev_x) (void)hipEventDestroy(c->ev_x);
@@ -1362,6 +1482,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     HIPCHK(c, hipMemcpyAsync(c->X, X, sizeof(double) * (size_t)c->n * c->dim,
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
+    c->ev_xready_use = c->ev_xready;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_particles = true;
     return SVGD_OK;
@@ -1413,7 +1534,8 @@ int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
     CHK(check_ready(c));
     CHK(resolve_pending(c));
     c->spec_step = false;
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0)); // the last [a, med] copy has read scal
+    if (hipEventQuery(c->ev_scal) != hipSuccess) // the last [a, med] copy has read scal
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0));
     CHK(center(c));
     HIPCHK(c, launch_set_scal(a, NAN, c->scal, c->stream));
     CHK(upload_g(c, G_shard));
@@ -1435,7 +1557,7 @@ int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
     const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
     if (X_shard_out && c->nrows > 0) {
         // X_t is final once the previous step's update (and all-gather) ran
-        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_xready, 0));
+        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_xready_use ? c->ev_xready_use : c->ev_xready, 0));
         HIPCHK(c, hipMemcpyAsync(c->h_x, c->X + (size_t)c->row0 * c->dim, bytes,
                                  hipMemcpyDeviceToHost, c->cstream));
         HIPCHK(c, hipEventRecord(c->ev_x, c->cstream));
@@ -1488,7 +1610,7 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     HIPCHK(c, hipEventSynchronize(c->ev_g)); // the previous step's upload has left h_g
     if (rows > 0) {
         // X_t is final once the previous step's update (and all-gather) ran
-        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_xready, 0));
+        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_xready_use ? c->ev_xready_use : c->ev_xready, 0));
         for (int q = 0; q < nch; ++q) {
             int64_t r0, r1;
             chunk(q, &r0, &r1);
@@ -1498,19 +1620,52 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
             HIPCHK(c, hipEventRecord(c->ev_xch[q], c->cstream));
         }
     }
-    CHK(plan_step(c));
-    CHK(scale_begin(c));
-    for (int q = 0; q < nch && rows > 0; ++q) {
-        int64_t r0, r1;
-        chunk(q, &r0, &r1);
-        HIPCHK(c, hipEventSynchronize(c->ev_xch[q]));
-        if (model_logp_grad_threads(m, c->h_x + r0 * d, r1 - r0, c->h_g + r0 * d, c->host_threads))
-            return fail(c, SVGD_ERR_ARG, "[Argument Error] Host model evaluation failed.");
-        HIPCHK(c, hipMemcpyAsync(c->G + (size_t)(c->row0 + r0) * d, c->h_g + r0 * d,
-                                 sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyHostToDevice,
-                                 c->cstream));
+    // the gradient thread: each chunk waits for its X_t copy, evaluates the
+    // model and queues its G copy on the copy stream (the calling thread only
+    // touches `stream` until it waits for this job)
+    if (!c->worker) c->worker.reset(new HostWorker());
+    c->worker->post([c, m, d, rows, nch, chunk](std::string &msg) -> int {
+        for (int q = 0; q < nch && rows > 0; ++q) {
+            int64_t r0, r1;
+            chunk(q, &r0, &r1);
+            hipError_t e = hipEventSynchronize(c->ev_xch[q]);
+            if (e != hipSuccess) {
+                msg = std::string("SVGDCpp: [HIP Error] X_t chunk copy: ") + hipGetErrorString(e);
+                return SVGD_ERR_HIP;
+            }
+            if (model_logp_grad_threads(m, c->h_x + r0 * d, r1 - r0, c->h_g + r0 * d,
+                                        c->host_threads)) {
+                msg = "SVGDCpp: [Argument Error] Host model evaluation failed.";
+                return SVGD_ERR_ARG;
+            }
+            e = hipMemcpyAsync(c->G + (size_t)(c->row0 + r0) * d, c->h_g + r0 * d,
+                               sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyHostToDevice,
+                               c->cstream);
+            if (e != hipSuccess) {
+                msg = std::string("SVGDCpp: [HIP Error] G chunk copy: ") + hipGetErrorString(e);
+                return SVGD_ERR_HIP;
+            }
+        }
+        hipError_t e = hipEventRecord(c->ev_g, c->cstream);
+        // the gradient thread waits for its copies to land (the device is
+        // still in the median): the compute stream then needs no barrier on
+        // the copy stream (upload_g_finish)
+        if (e == hipSuccess) e = hipEventSynchronize(c->ev_g);
+        if (e != hipSuccess) {
+            msg = std::string("SVGDCpp: [HIP Error] G event: ") + hipGetErrorString(e);
+            return SVGD_ERR_HIP;
+        }
+        return SVGD_OK;
+    });
+    int rc = plan_step(c);
+    if (rc == SVGD_OK) rc = scale_begin(c);
+    std::string wmsg;
+    const int wrc = c->worker->wait(wmsg); // always joined before returning
+    CHK(rc);
+    if (wrc != SVGD_OK) {
+        c->err = wmsg;
+        return wrc;
     }
-    HIPCHK(c, hipEventRecord(c->ev_g, c->cstream));
     CHK(upload_g_finish(c));
     CHK(scale_finish(c));
     CHK(run_phi_opt(c));
@@ -1531,6 +1686,7 @@ int svgd_step(svgd_ctx *c, const double *G_shard)
     CHK(svgd_begin_step(c, nullptr));
     HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
                                 c->dm_mu, c->dm_prec, c->G + (size_t)c->row0 * c->dim, c->stream));
+    c->mark = nullptr; // (the gradient kernel runs after the median's end event)
     CHK(scale_finish(c));
     CHK(allgather_rows(c, c->G));
     CHK(run_phi_opt(c));
@@ -1638,12 +1794,15 @@ int svgd_get_timing(svgd_ctx *c, double *phi_ms, double *median_ms, int64_t *cou
     if (!c) return SVGD_ERR_ARG;
     CHK(resolve_pending(c));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    // the events go back to the pool: the status / scale-final marks may be
+    // among them (everything they mark is complete now)
+    c->ev_status_use = c->ev_fin_use = c->mark = c->phi_end = c->ev_xready_use = nullptr;
     for (auto &e : c->ev_phi) {
         float ms = 0;
         HIPCHK(c, hipEventElapsedTime(&ms, e.a, e.b));
         c->phi_ms += ms;
         c->tcount += 1;
-        c->ev_pool.push_back(e);
+        c->ev_pool.push_back(e.spare ? EvPair{e.spare, e.b} : EvPair{e.a, e.b});
     }
     c->ev_phi.clear();
     for (auto &e : c->ev_med) {

@@ -163,7 +163,8 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
-                           double *phi, const OptArgs *opt, hipStream_t stream);
+                           const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
+                           hipStream_t stream);
 // full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,
 // or an eigendecomposition when M is indefinite and d <= ROWS_MAX_D);
 // err = 0 positive definite, 2 indefinite, 1 non-finite / no convergence.

@@ -1637,6 +1637,22 @@ __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restri
     }
 }
 
+// The row stream's LDS table holds T[m] = 2^(m/4096) with its high word
+// biased by -(m << 8) (integer arithmetic mod 2^32).  For u = 4096 q + m
+// (m = u & 4095) the high word plus (u << 8) is T[m]'s high word plus
+// (q << 20): 2^q T[m] with ONE v_lshl_add_u32 -- in place of the shift and
+// v_ldexp_f64 -- valid while 1023 + q stays inside the exponent field
+// (callers keep q in [-1001, 1000]).
+__device__ __forceinline__ double tab_biased(double t, int m)
+{
+    return __hiloint2double(__double2hiint(t) - (m << 8), __double2loint(t));
+}
+__device__ __forceinline__ double tab_scale(double tb, int ki)
+{
+    return __hiloint2double(__double2hiint(tb) + (ki << 8), __double2loint(tb));
+}
+constexpr double EXP_U_CLAMP = 1000.0 * EXP_TB; // |u| bound of the clamped (plain) form
+
 // One column record of the phi row stream, held in registers.
 template <int D> struct ColRec {
     double x[D], v[D], c;
@@ -1653,7 +1669,11 @@ template <int D> struct ColRec {
 
 // acc_i += K_ij [V_j, 1] for the lane's R rows against one column j.
 // FOLD: the row term c_i is left out of u (one add fewer per pair) and the
-// row's sums are scaled by 2^(c_i/4096) once at the end (k_phi_rows).
+// row's sums are scaled by 2^(c_i/4096) once at the end (k_phi_rows); the
+// kernel takes it only where u provably stays inside [-1001, 400] x 4096, so
+// no clamp either.  Plain form: u clamped to +-EXP_U_CLAMP (K within
+// [2^-1000, 2^1000] instead of [0, inf]: below any fp64 sum that holds the
+// diagonal K_ii = 1).
 template <int D, int R, bool FOLD>
 __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (&xs)[R][D],
                                               const double (&ci)[R], double (&acc)[R][D],
@@ -1667,6 +1687,10 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
     for (int k = 0; k < D; ++k)
 #pragma unroll
         for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], q.x[k], u[r]);
+    if constexpr (!FOLD) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) u[r] = fmin(fmax(u[r], -EXP_U_CLAMP), EXP_U_CLAMP);
+    }
     // exp2_256 in stages: the R table reads are issued together and their
     // LDS latency hides behind the R polynomials
     double f[R], T[R];
@@ -1683,7 +1707,7 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
     for (int r = 0; r < R; ++r) K[r] = exp2_4096_poly(f[r]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < R; ++r) K[r] = __builtin_ldexp(K[r] * T[r], ki[r] >> 12);
+    for (int r = 0; r < R; ++r) K[r] = K[r] * tab_scale(T[r], ki[r]);
 #pragma unroll
     for (int k = 0; k < D; ++k)
 #pragma unroll
@@ -1699,7 +1723,8 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
                                                  const double *__restrict__ a_ptr, int64_t row0,
                                                  int64_t nrows, int64_t n, int S,
                                                  double *__restrict__ part, int64_t ldp,
-                                                 const double *__restrict__ sgn)
+                                                 const double *__restrict__ sgn,
+                                                 const unsigned long long *__restrict__ nmax_bits)
 {
     constexpr int RS = RecLayout<D>::RS;
     constexpr int CHB = CH_PHI * RS * 8; // bytes per column chunk (multiple of 1 KiB)
@@ -1710,7 +1735,8 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + EXP_TB * 8];
     double *tab = reinterpret_cast<double *>(smem + 4 * 2 * CHB);
 #pragma unroll
-    for (int e = 0; e < EXP_TB / 256; ++e) tab[e * 256 + threadIdx.x] = EXP2_TAB4096[e * 256 + threadIdx.x];
+    for (int e = 0; e < EXP_TB / 256; ++e)
+        tab[e * 256 + threadIdx.x] = tab_biased(EXP2_TAB4096[e * 256 + threadIdx.x], e * 256 + threadIdx.x);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -1751,8 +1777,13 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     // to stay far from overflow (with N |V| on top): whole waves whose rows
     // all have -c_i/4096 = a log2e |xc_i|^2 <= FOLD_MAX take it (the usual
     // case: particles within ~sqrt(400/a) of the mean), others the plain form.
+    // The fold's u = -4096 a log2e (|x_j|^2 - 2 x_i.x_j) >= -4096 (y + 2 sqrt(400 y))
+    // for y = a log2e max_j |x_j|^2: y <= 300 keeps it above -1000 x 4096, so
+    // the folded form needs no clamp (nmax_bits: k_center's max |xc|^2).
     constexpr double FOLD_MAX = 400.0;
-    bool fold_ok = sgn == nullptr; // an indefinite S can make K_ij > 1: no fold
+    const bool nowrap =
+        nmax_bits && LOG2E * (*a_ptr) * __longlong_as_double((long long)*nmax_bits) <= 300.0;
+    bool fold_ok = sgn == nullptr && nowrap; // an indefinite S can make K_ij > 1: no fold
 #pragma unroll
     for (int r = 0; r < R; ++r) fold_ok = fold_ok && ci[r] >= -4096.0 * FOLD_MAX;
     const bool fold = __all(fold_ok);
@@ -1823,9 +1854,8 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const double k = __builtin_rint(ci[r]);
-            const int ki = (int)k;
-            const double g = __builtin_ldexp(exp2_4096_poly(ci[r] - k) * tab[ki & (EXP_TB - 1)],
-                                             ki >> 12);
+            const int ki = (int)k; // in [-400 x 4096, 0]
+            const double g = exp2_4096_poly(ci[r] - k) * tab_scale(tab[ki & (EXP_TB - 1)], ki);
 #pragma unroll
             for (int k2 = 0; k2 < D; ++k2) acc[r][k2] *= g;
             acc1[r] *= g;
@@ -1992,10 +2022,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 
 // phi_i = (sum_s acc_s + 2a xc_i sum_s acc1_s) / N, partials summed in s order.
 // wv (full-matrix scale): 2 M xc_i per particle, in place of 2 a xc_i.
-// A block owns PHI_RED_ROWS rows: their (d+1)-element partial rows are
-// contiguous in every split s, so the sums are read coalesced into LDS, then
-// phi is written coalesced from LDS.
-constexpr int PHI_RED_ROWS = 32; // rows per block (enough blocks to fill the chip at small N)
+// A block owns phi_red_rows(d) = 256 / (d+1) rows: their (d+1)-element
+// partial rows are contiguous in every split s, so each thread sums ONE
+// element over the splits (loads issued 8 splits at a time, added in s
+// order), the sums go to LDS and phi is written coalesced from LDS.
+__host__ __device__ constexpr int phi_red_rows(int d) { return 256 / (d + 1); }
 __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ part,
                                                     const double *__restrict__ rec,
                                                     const double *__restrict__ a_ptr, int64_t row0,
@@ -2003,16 +2034,27 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
                                                     double inv_n, const double *__restrict__ wv,
                                                     double *__restrict__ phi, OptArgs opt, int do_opt)
 {
-    __shared__ double sm[PHI_RED_ROWS * 17];
+    __shared__ double sm[256];
     const double two_a = 2.0 * (*a_ptr);
     const int DP = d + 1;
-    const int64_t rb = (int64_t)blockIdx.x * PHI_RED_ROWS;
-    const int rows = (int)min<int64_t>(PHI_RED_ROWS, nrows - rb);
+    const int RB = phi_red_rows(d);
+    const int64_t rb = (int64_t)blockIdx.x * RB;
+    const int rows = (int)min<int64_t>(RB, nrows - rb);
     if (rows <= 0) return;
-    const int E = rows * DP;
-    for (int e = threadIdx.x; e < E; e += blockDim.x) {
+    const int e = threadIdx.x;
+    if (e < rows * DP) {
+        const double *p = part + rb * DP + e;
+        const int64_t st = ldp * DP;
         double acc = 0.0;
-        for (int s = 0; s < S; ++s) acc += part[((int64_t)s * ldp + rb) * DP + e];
+        int s = 0;
+        for (; s + 8 <= S; s += 8) {
+            double v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = p[(s + q) * st];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc += v[q];
+        }
+        for (; s < S; ++s) acc += p[s * st];
         sm[e] = acc;
     }
     __syncthreads();
@@ -2595,13 +2637,13 @@ __global__ __launch_bounds__(256) void k_gauss_grad(const double *__restrict__ X
     case Dv:                                                                                 \
         if (kind == 0 && R == 1)                                                             \
             hipLaunchKernelGGL((k_phi_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn);               \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
         else if (kind == 0 && R == 2)                                                        \
             hipLaunchKernelGGL((k_phi_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn);               \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
         else if (kind == 0)                                                                  \
             hipLaunchKernelGGL((k_phi_rows<Dv, 4>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn);               \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
         else if (kind == 10)                                                                 \
             hipLaunchKernelGGL((k_pair_rows<Dv, 0>), dim3(grid), dim3(256), 0, stream, xc, KP, \
                                nrm, n, nb, t0, t1, sc, sh, sd);                              \
@@ -2616,7 +2658,7 @@ __global__ __launch_bounds__(256) void k_gauss_grad(const double *__restrict__ X
 static hipError_t launch_rows_kernel(int kind, int D, int R, int grid, const double *rec,
                                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t n,
                                      int S, double *part, int64_t ldp, const double *sgn,
-                                     const double *xc, int KP,
+                                     const unsigned long long *nmax, const double *xc, int KP,
                                      const double *nrm, int64_t nb, int64_t t0, int64_t t1,
                                      SinkCollect sc, SinkHist sh, SinkDebug sd, hipStream_t stream)
 {
@@ -2657,16 +2699,17 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
-                           double *phi, const OptArgs *opt, hipStream_t stream)
+                           const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
+                           hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
     const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
     hipError_t e = launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
-                                      nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
+                                      nmax_bits, nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
                                       SinkDebug{}, stream);
     if (e != hipSuccess) return e;
     if (d > 16) return hipErrorInvalidValue; // k_phi_reduce's LDS holds d + 1 <= 17
-    const int64_t g = (nrows + PHI_RED_ROWS - 1) / PHI_RED_ROWS;
+    const int64_t g = (nrows + phi_red_rows(d) - 1) / phi_red_rows(d);
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
                        d, phi_rec_stride(d), S, ldp, inv_n, wv, phi, opt ? *opt : OptArgs{},
                        opt ? 1 : 0);
@@ -2685,7 +2728,7 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
     SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, mode == 0 ? bpart : nullptr};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n};
-    return launch_rows_kernel(10 + mode, d, 1, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, nullptr, xc,
+    return launch_rows_kernel(10 + mode, d, 1, grid, nullptr, nullptr, 0, 0, n, 1, nullptr, 0, nullptr, nullptr, xc,
                               KP, nrm, nb, t0, t1, sc, sh, sd, stream);
 }
 

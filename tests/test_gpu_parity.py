@@ -74,14 +74,34 @@ def test_phi_far_from_origin(oracle):
 
 @pytest.mark.parametrize("d", [2, 8])
 def test_phi_outliers_mixed_fold(oracle, d):
-    """A few particles far out (a log2e |x_i - mean|^2 >> 400): their waves keep
-    the row term inside the pair loop, every other wave folds it into one
-    factor per row (k_phi_rows FOLD); both agree with the oracle."""
+    """A few particles far out (a log2e max|x_i - mean|^2 >> 300): the whole
+    launch takes k_phi_rows' plain form, whose exponent is clamped to
+    +-1000 x 4096 (pairs with the outliers lie far beyond it: K ~ 2^-9000
+    becomes 2^-1000); it agrees with the oracle."""
     n = 1500
     X = oracle.splitmix((n, d), 1.0, 77 + d)
     X[[5, 700, 1499]] += 40.0
     G = oracle.splitmix((n, d), 1.0, 78 + d)
     a = 2.0
+    ref = oracle.phi(X, G, a)
+    ph = _ctx(X).phi(G, a)
+    assert np.max(np.abs(ph - ref)) <= PHI_TOL
+
+
+@pytest.mark.parametrize("y", [150.0, 299.0, 301.0, 2000.0])
+@pytest.mark.parametrize("d", [2, 8])
+def test_phi_fold_exponent_bound(oracle, d, y):
+    """k_phi_rows folds the row term and scales 2^q T[m] by an integer add to
+    the exponent field (no clamp) only while y = a log2e max|xc|^2 <= 300
+    keeps every folded exponent above -1001; one far particle puts y just
+    either side of the bound (and far beyond it).  A wrapped exponent would
+    show up as huge phi values; every case matches the oracle."""
+    n = 1200
+    X = oracle.splitmix((n, d), 1.0, 31 + d)
+    X[17] += 6.0
+    G = oracle.splitmix((n, d), 1.0, 32 + d)
+    xc = X - X.mean(axis=0)
+    a = y / (np.log2(np.e) * np.max(np.sum(xc * xc, axis=1)))
     ref = oracle.phi(X, G, a)
     ph = _ctx(X).phi(G, a)
     assert np.max(np.abs(ph - ref)) <= PHI_TOL

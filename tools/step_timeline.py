@@ -1,5 +1,7 @@
 """Print the kernel timeline (start offset, gap, duration) of the last full
-step in a rocprofv3 kernel trace (steps start at k_mean_partial)."""
+step in a rocprofv3 kernel trace (steps start at k_mean_partial).  With a
+second argument (the run's memory-copy trace CSV) the copies that start
+inside the step are listed too, marked 'copy'."""
 import csv
 import sys
 
@@ -8,6 +10,7 @@ rows.sort(key=lambda r: int(r['Start_Timestamp']))
 idx = [i for i, r in enumerate(rows) if 'k_mean_partial' in r['Kernel_Name']]
 a, b = idx[-2], idx[-1]
 t0 = int(rows[a]['Start_Timestamp'])
+t1 = int(rows[b]['Start_Timestamp'])
 prev = None
 for r in rows[a:b]:
     s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
@@ -15,3 +18,9 @@ for r in rows[a:b]:
     print(f"{(s - t0) / 1e3:9.1f} {gap:7.1f} {(e - s) / 1e3:8.1f}  {r['Kernel_Name'][:60]}")
     prev = e
 print('step span us', (int(rows[b - 1]['End_Timestamp']) - t0) / 1e3)
+if len(sys.argv) > 2:
+    for r in sorted(csv.DictReader(open(sys.argv[2])), key=lambda r: int(r['Start_Timestamp'])):
+        s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
+        if t0 - 200000 <= s < t1:
+            what = r.get('Direction') or r.get('Operation') or ''
+            print(f"{(s - t0) / 1e3:9.1f} {'copy':>7} {(e - s) / 1e3:8.1f}  {what} {r.get('Size', r.get('Bytes', ''))}")
