@@ -195,18 +195,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         scnt = 0;
     };
 
-    const int64_t T = t1 - t0;
-    const int64_t tb = t0 + T * blockIdx.x / gridDim.x, te = t0 + T * (blockIdx.x + 1) / gridDim.x;
     // lane-constant part of "j > i" inside a 16 x 16 block (diagonal tiles):
     // j - i = (4 kq - ql) + r + (jl0 - il0)
     const int xl = 4 * kq - ql;
-    if (tb < te) {
-        const int64_t H = (nb - 1) / 2;
-        int64_t I, J;
-        tile_coords(nb, tb, &I, &J);
-        int64_t slot = (J - I + nb) % nb;
+    // Schedule (L2 locality, as k_pair_tcol; the plan's tile SET [t0, t1) is
+    // unchanged): the rank's tile rows I (plan.cpp: row I holds slots
+    // 0..cnt(I)-1, J = I + slot mod nb) are cut into bands of R rows dealt
+    // round-robin to the nG = 8 XCDs (block b runs on XCD b % 8).  Inside a
+    // band the XCD's P blocks sweep the slots together: block q keeps row
+    // I = band + q % R (its rows stay in LDS for the whole band) and takes
+    // slots q / R, q / R + S, ... (S = P / R), so at any moment the XCD's
+    // blocks read ~R + S neighbouring column tiles, each shared by ~R blocks
+    // through the XCD's L2 -- instead of P unrelated column streams (each XCD
+    // re-fetched the fp32 records ~17 times per pass: 430 MB at cfg3).
+    const int G = gridDim.x;
+    const int nG = (G % 8 == 0) ? 8 : 1;
+    const int P = G / nG, gx = blockIdx.x % nG, q = blockIdx.x / nG;
+    const int64_t H = (nb - 1) / 2;
+    const int64_t half = (nb & 1) == 0 ? nb / 2 : 0, c1 = H + 2, c2 = H + 1;
+    int64_t Ia = 0, Ib = -1;
+    if (t1 > t0) {
+        int64_t Jd;
+        tile_coords(nb, t0, &Ia, &Jd);
+        tile_coords(nb, t1 - 1, &Ib, &Jd);
+    }
+    int R = 32;
+    while (P % R) R >>= 1;
+    while (R > 1 && Ib - Ia + 1 < (int64_t)nG * R) R >>= 1; // every XCD gets a band
+    const int S = P / R, rr = q % R, ph = q / R;
+    const int64_t nbands = (Ib - Ia + 1 + R - 1) / R;
+    struct Pos {
+        int64_t k, I, s, J, hi;
+    };
+    // the first tile at or after band p.k of this block's row and phase
+    auto enter_row = [&](Pos &p) {
+        for (; p.k < nbands; p.k += nG) {
+            const int64_t I = Ia + p.k * R + rr;
+            if (I > Ib) continue;
+            const int64_t rs = I < half ? I * c1 : half * c1 + (I - half) * c2;
+            const int64_t lo = max<int64_t>(0, t0 - rs);
+            const int64_t hi = min<int64_t>(I < half ? c1 : c2, t1 - rs);
+            const int64_t sl = lo <= ph ? ph : ph + (lo - ph + S - 1) / S * S;
+            if (sl < hi) {
+                p.I = I;
+                p.s = sl;
+                p.hi = hi;
+                p.J = I + sl >= nb ? I + sl - nb : I + sl;
+                return true;
+            }
+        }
+        return false;
+    };
+    auto advance = [&](Pos &p) {
+        p.s += S;
+        if (p.s < p.hi) {
+            p.J = p.I + p.s >= nb ? p.I + p.s - nb : p.I + p.s;
+            return true;
+        }
+        p.k += nG;
+        return enter_row(p);
+    };
+    Pos pos{gx, 0, 0, 0, 0};
+    if (t1 > t0 && enter_row(pos)) {
         int64_t curI = -1;
-        for (int64_t t = tb; t < te; ++t) {
+        do {
+            const int64_t I = pos.I, J = pos.J;
             const int64_t ib = I * PBLK, jbase = J * PBLK;
             if (I != curI) {
                 // the tile's rows: lane slot (b, l) of row ib + 16 b + (l & 15)
@@ -335,15 +388,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             else
                 jloop(std::false_type{});
             if (scnt) flush(ib, jbase);
-            // next tile (plan.cpp order, as k_pair_rows)
-            ++slot;
-            const int64_t cntI = ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
-            if (slot == cntI) {
-                ++I;
-                slot = 0;
-            }
-            J = slot == 0 ? I : (I + slot) % nb;
-        }
+        } while (advance(pos));
     }
 
     if (lane == 0) {
