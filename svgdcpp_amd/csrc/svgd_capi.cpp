@@ -267,6 +267,7 @@ struct svgd_ctx {
     // likewise at the step's end: the phi phase's end event (timing) doubles
     // as X_t-final for the copy stream (ev_xready_use) when nothing follows it
     hipEvent_t phi_end = nullptr, ev_xready_use = nullptr;
+    hipEvent_t last_phi_end = nullptr; // the last phi phase's end (timing): the next median's start
     double *bak = nullptr; // [X_t | m_t | v_t] of this rank's rows for the pending step
 };
 
@@ -947,7 +948,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     if (c->timing) {
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         c->ev_phi.push_back(ev);
-        c->phi_end = ev.b;
+        c->phi_end = c->last_phi_end = ev.b;
     }
     return SVGD_OK;
 }
@@ -1005,12 +1006,21 @@ int scale_begin(svgd_ctx *c)
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0));
     const bool med = !(c->scale_method == SVGD_SCALE_FIXED || matrix_scale(c));
     // the median phase's start event goes before the centring (which it
-    // needs): an event between two kernels costs a dispatch gap
+    // needs): an event between two kernels costs a dispatch gap, so the last
+    // step's phi end (a timing event) serves when there is one -- the phase
+    // then also holds the gap between steps (a diagnostic only: these events
+    // feed svgd_get_timing and nothing else)
     if (c->timing && med) {
         EvPair ev = take_pair(c);
-        HIPCHK(c, hipEventRecord(ev.a, c->stream));
+        if (c->last_phi_end) {
+            ev.spare = ev.a;
+            ev.a = c->last_phi_end;
+        } else {
+            HIPCHK(c, hipEventRecord(ev.a, c->stream));
+        }
         c->ev_med.push_back(ev);
     }
+    c->last_phi_end = nullptr;
     CHK(center(c));
     if (!med) return SVGD_OK;
     return median_begin(c);
@@ -1786,6 +1796,7 @@ int svgd_set_timing(svgd_ctx *c, int enable)
 {
     if (!c) return SVGD_ERR_ARG;
     c->timing = enable != 0;
+    c->last_phi_end = nullptr;
     return SVGD_OK;
 }
 
@@ -1797,6 +1808,7 @@ int svgd_get_timing(svgd_ctx *c, double *phi_ms, double *median_ms, int64_t *cou
     // the events go back to the pool: the status / scale-final marks may be
     // among them (everything they mark is complete now)
     c->ev_status_use = c->ev_fin_use = c->mark = c->phi_end = c->ev_xready_use = nullptr;
+    c->last_phi_end = nullptr;
     for (auto &e : c->ev_phi) {
         float ms = 0;
         HIPCHK(c, hipEventElapsedTime(&ms, e.a, e.b));
@@ -1809,7 +1821,7 @@ int svgd_get_timing(svgd_ctx *c, double *phi_ms, double *median_ms, int64_t *cou
         float ms = 0;
         HIPCHK(c, hipEventElapsedTime(&ms, e.a, e.b));
         c->med_ms += ms;
-        c->ev_pool.push_back(e);
+        c->ev_pool.push_back(e.spare ? EvPair{e.spare, e.b} : EvPair{e.a, e.b});
     }
     c->ev_med.clear();
     if (phi_ms) *phi_ms = c->phi_ms;
