@@ -219,6 +219,116 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
     }
 }
 
+// k_center for d <= 16 with the median record stride KP = med_rec_stride(D):
+// the same values bit for bit, but the row's X loads unrolled (all in flight
+// together instead of one dependent load-store round trip per column: the
+// generic loop was latency-bound at 20 us for N = 65536, d = 8) and the
+// records written with 16-byte stores.
+template <int D>
+__global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, int64_t n,
+                                                  const double *__restrict__ partial, int nparts,
+                                                  int64_t np, double *__restrict__ xc,
+                                                  double *__restrict__ nrm, int nrm_in_slot,
+                                                  float *__restrict__ xf,
+                                                  unsigned long long *nmax_bits,
+                                                  unsigned long long *bzero)
+{
+    constexpr int KP = med_rec_stride(D), KF = med_f32_stride(D);
+    if (bzero && blockIdx.x == 0)
+        for (int e = threadIdx.x; e < NBK; e += blockDim.x) bzero[e] = 0;
+    __shared__ double mu[D];
+    __shared__ double sP[1024];
+    // the first row's X is loaded before the mean (its latency overlaps the
+    // partials'), each later row's one iteration ahead
+    const int64_t jstride = (int64_t)gridDim.x * blockDim.x;
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double xn[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) xn[k] = j < n ? X[j * D + k] : 0.0;
+    if (nparts * D <= 1024) {
+        // every partial loaded at once (one coalesced sweep), then added in
+        // b order from LDS: the same sums as the loop below without its
+        // nparts / 8 dependent global round trips
+        for (int e = threadIdx.x; e < nparts * D; e += blockDim.x) sP[e] = partial[e];
+        __syncthreads();
+        if (threadIdx.x < D) {
+            double s = 0.0;
+            int b = 0;
+            for (; b + 8 <= nparts; b += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = sP[(b + u) * D + threadIdx.x];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s += v[u];
+            }
+            for (; b < nparts; ++b) s += sP[b * D + threadIdx.x];
+            mu[threadIdx.x] = s / (double)n;
+        }
+    } else if (threadIdx.x < D) {
+        const int k = threadIdx.x;
+        double s = 0.0; // partials added in b order, as k_center
+        for (int b0 = 0; b0 < nparts; b0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = b0 + u < nparts ? partial[(b0 + u) * D + k] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + u < nparts) s += v[u];
+        }
+        mu[k] = s / (double)n;
+    }
+    __syncthreads();
+    unsigned long long bmax = 0;
+    for (; j < np; j += jstride) {
+        double v[KP];
+        const bool live = j < n;
+#pragma unroll
+        for (int k = 0; k < D; ++k) v[k] = xn[k];
+        const int64_t jn = j + jstride;
+#pragma unroll
+        for (int k = 0; k < D; ++k) xn[k] = jn < n ? X[jn * D + k] : 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) v[k] = live ? v[k] - mu[k] : 0.0;
+#pragma unroll
+        for (int k = D; k < KP; ++k) v[k] = 0.0;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) s = fma(v[k], v[k], s); // (the zero pads add nothing)
+        nrm[j] = s;
+        float f[KF];
+        if (xf) {
+#pragma unroll
+            for (int k = 0; k < KF; ++k)
+                f[k] = k < D ? (float)v[k] : (k == D ? (live ? (float)(-0.5 * s) : -__builtin_inff()) : 0.0f);
+        }
+        if (nrm_in_slot) v[D] = -0.5 * s;
+        double2 *o = reinterpret_cast<double2 *>(xc + j * KP);
+#pragma unroll
+        for (int q = 0; q < KP / 2; ++q) o[q] = make_double2(v[2 * q], v[2 * q + 1]);
+        if (xf) {
+            float4 *of = reinterpret_cast<float4 *>(xf + j * KF);
+#pragma unroll
+            for (int q = 0; q < KF / 4; ++q) of[q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+            unsigned long long m = (unsigned long long)__double_as_longlong(s);
+            for (int o2 = 32; o2 > 0; o2 >>= 1) {
+                const unsigned long long t = __shfl_xor(m, o2);
+                m = t > m ? t : m;
+            }
+            bmax = m > bmax ? m : bmax;
+        }
+    }
+    if (xf) {
+        __shared__ unsigned long long wmax[4];
+        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bmax;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long m = 0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = wmax[w] > m ? wmax[w] : m;
+            atomicMax(nmax_bits, m);
+        }
+    }
+}
+
 // V_j = [G_j - 2a xc_j, 1, 0...] (row stride 16*NCB), c_j = -a log2e |xc_j|^2.
 __global__ void k_prep_v(const double *__restrict__ xc, const double *__restrict__ G,
                          const double *__restrict__ nrm, const double *__restrict__ a_ptr,
@@ -2905,6 +3015,22 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
                        xf ? nmax_bits : nullptr);
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
+#define SVGD_CENTER_CASE(Dv)                                                                  \
+    case Dv:                                                                                  \
+        hipLaunchKernelGGL((k_center_d<Dv>), dim3(g), dim3(256), 0, stream, X, n, partial,    \
+                           nparts, np, xc, nrm, nrm_in_slot, xf, nmax_bits, bzero);            \
+        return hipGetLastError();
+    if (d <= 16 && KP == med_rec_stride(d)) {
+        switch (d) {
+            SVGD_CENTER_CASE(1) SVGD_CENTER_CASE(2) SVGD_CENTER_CASE(3) SVGD_CENTER_CASE(4)
+            SVGD_CENTER_CASE(5) SVGD_CENTER_CASE(6) SVGD_CENTER_CASE(7) SVGD_CENTER_CASE(8)
+            SVGD_CENTER_CASE(9) SVGD_CENTER_CASE(10) SVGD_CENTER_CASE(11) SVGD_CENTER_CASE(12)
+            SVGD_CENTER_CASE(13) SVGD_CENTER_CASE(14) SVGD_CENTER_CASE(15) SVGD_CENTER_CASE(16)
+        default:
+            break;
+        }
+    }
+#undef SVGD_CENTER_CASE
     hipLaunchKernelGGL(k_center, dim3(g), dim3(256), 0, stream, X, n, d, KP, partial, nparts, np,
                        xc, nrm, nrm_in_slot, xf, med_f32_stride(d), nmax_bits, bzero);
     return hipGetLastError();
