@@ -42,7 +42,7 @@ oracle:
 	$(MAKE) -C oracle
 
 # C++ programs over the SVGDCpp-compatible headers (include/Core, Model, Kernel, Optimizer)
-CPP_FLAGS := -O2 -std=c++17 -Wall -Iinclude
+CPP_FLAGS := -O2 -std=c++17 -Wall -fopenmp -Iinclude
 CPP_LINK := -Lsvgdcpp_amd -lsvgdcpp_amd -Wl,-rpath,'$$ORIGIN/../svgdcpp_amd' -Wl,--allow-shlib-undefined
 CPP_HDRS := $(wildcard include/SVGDCpp/*.hpp include/SVGDCpp/*/*.hpp) include/Core include/Model include/Kernel include/Optimizer
 CPP_BINS := build/mvn_example build/gmm_example build/test_api

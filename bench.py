@@ -10,14 +10,28 @@ inside the timed region, X resident in HBM.  For N GPUs (one process each,
 torchrun) the particles are sharded by rows and the context all-gathers X and
 G over RCCL every step; N is fixed (strong scaling, as the metric specifies).
 
+Protocol: W warm-up steps, then `--repeats` (5) timed runs of
+exactly K steps, each bracketed by barrier + device sync; value/ms_per_step
+are the median run (per run the slowest rank).  Then one untimed diagnostic
+pass of K steps with extra HIP events (the phi kernel alone, the device's
+wait for G, collectives).
+
 The JSON line also carries
-  roofline     -- the phi kernel (dominant) measured with HIP events on the
-                  library's own stream: algorithmic flop per launch
-                  (rows x N x (5d+4)) / average launch time,
-                  against the FP64 peak (78.6 TF/s, MI355X spec; vector = matrix).
-  cpu_baseline -- the CPU oracle (a port of the reference's arithmetic) on the
-                  host cores of this box for a bounded row sample of the same
-                  workload (rank 0, N=1 only).
+  roofline     -- the phi kernel (dominant): algorithmic flop per launch
+                  (rows x N x (5d+4)) / its average launch time
+                  from HIP events around that launch alone (diagnostic pass),
+                  against the FP64 peak (78.6 TF/s, MI355X spec; vector =
+                  matrix); frac_at_load_clock uses the gfx clock amdsmi read
+                  during the same pass.
+  phases / host / diag -- where a step's time goes: the phi and median
+                  phases (timed runs), the host gradient's wall clocks, the
+                  device's wait for G before the phi chain (diagnostic pass).
+  gpu_timed / gpu_diag -- amdsmi clock, power, throttle residency over the
+                  timed runs / the diagnostic pass.
+  cpu_baseline -- the CPU oracle (a port of the reference's arithmetic) on all
+                  host cores this process may use, for a bounded row sample of
+                  the same workload (rank 0, N=1 only), plus a 1-thread number.
+  per_rank     -- (N > 1) every rank's phases, host and diagnostic times.
 """
 import argparse
 import ctypes
@@ -95,6 +109,154 @@ def _host_cpu():
     return model, cores
 
 
+def _cpu_quota():
+    """CPUs this process's cgroup may use (cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                return float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return q / per
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+class GpuMonitor:
+    """Samples the GPU's clock, power and throttle residency through amdsmi
+    (host-side sysfs/SMU reads; nothing is queued on the GPU) in a thread,
+    so the line carries the clock THIS run held, not one from another box."""
+
+    ACC = ("ppt_residency_acc", "socket_thm_residency_acc", "prochot_residency_acc",
+           "hbm_thm_residency_acc", "vr_thm_residency_acc")
+
+    def __init__(self, device, period=0.02):
+        import threading
+
+        self.ok, self.err, self.h, self.samples = False, None, None, []
+        self.period, self.static = period, {}
+        self._stop = threading.Event()
+        self._th = None
+        try:
+            import amdsmi
+
+            self.smi = amdsmi
+            amdsmi.amdsmi_init()
+            bdf = _pci_bus_id(device)
+            hs = amdsmi.amdsmi_get_processor_handles()
+            for h in hs:
+                if bdf and amdsmi.amdsmi_get_gpu_device_bdf(h).lower() == bdf.lower():
+                    self.h = h
+            if self.h is None and len(hs) == 1:
+                self.h = hs[0]
+            if self.h is None:
+                raise RuntimeError(f"no amdsmi handle for {bdf} among {len(hs)}")
+            self.static["bdf"] = bdf
+            try:
+                cap = amdsmi.amdsmi_get_power_cap_info(self.h)
+                self.static["power_cap_w"] = cap["power_cap"] / 1e6
+                self.static["default_power_cap_w"] = cap["default_power_cap"] / 1e6
+            except Exception as e:  # noqa: BLE001 - diagnostics only
+                self.static["power_cap_err"] = str(e)[:80]
+            try:
+                ci = amdsmi.amdsmi_get_clock_info(self.h, amdsmi.AmdSmiClkType.GFX)
+                self.static["gfxclk_max_mhz"] = ci.get("max_clk")
+            except Exception as e:  # noqa: BLE001
+                self.static["clock_info_err"] = str(e)[:80]
+            self.ok = True
+        except Exception as e:  # noqa: BLE001 - no amdsmi: the line says so
+            self.err = f"{type(e).__name__}: {str(e)[:120]}"
+
+    def _read(self):
+        m = self.smi.amdsmi_get_gpu_metrics_info(self.h)
+        clks = m.get("current_gfxclks")
+        if isinstance(clks, (list, tuple)):
+            clks = [c for c in clks if isinstance(c, (int, float)) and 0 < c < 10000]
+        clk = (sum(clks) / len(clks)) if clks else m.get("current_gfxclk")
+        out = {"t": time.perf_counter(), "gfxclk": clk, "power": m.get("current_socket_power"),
+               "hotspot": m.get("temperature_hotspot"), "throttle": m.get("indep_throttle_status"),
+               "acc_count": m.get("accumulation_counter")}
+        for k in self.ACC:
+            out[k] = m.get(k)
+        return out
+
+    def _loop(self):
+        while not self._stop.is_set():
+            try:
+                self.samples.append(self._read())
+            except Exception as e:  # noqa: BLE001
+                self.err = f"{type(e).__name__}: {str(e)[:120]}"
+                return
+            self._stop.wait(self.period)
+
+    def start(self):
+        import threading
+
+        if not self.ok:
+            return self
+        self.samples = []
+        self._stop.clear()
+        self._th = threading.Thread(target=self._loop, daemon=True)
+        self._th.start()
+        return self
+
+    def stop(self):
+        if self._th is not None:
+            self._stop.set()
+            self._th.join()
+            self._th = None
+        return self.summary()
+
+    def summary(self):
+        if not self.ok:
+            return {"source": "amdsmi", "error": self.err}
+        s = [x for x in self.samples if isinstance(x.get("gfxclk"), (int, float))]
+        out = {"source": "amdsmi gpu_metrics (current_gfxclks mean over XCDs), this run",
+               "samples": len(self.samples), **self.static}
+        if s:
+            c = sorted(x["gfxclk"] for x in s)
+            out.update(gfxclk_mhz_median=c[len(c) // 2], gfxclk_mhz_min=c[0], gfxclk_mhz_max=c[-1])
+        p = sorted(x["power"] for x in self.samples if isinstance(x.get("power"), (int, float)))
+        if p:
+            out.update(power_w_median=p[len(p) // 2], power_w_max=p[-1])
+        t = [x["hotspot"] for x in self.samples if isinstance(x.get("hotspot"), (int, float))]
+        if t:
+            out["hotspot_c_max"] = max(t)
+        th = sorted({x["throttle"] for x in self.samples if isinstance(x.get("throttle"), int)})
+        if th:
+            out["indep_throttle_status_seen"] = th
+        # residency accumulators: share of the sampled span spent throttled
+        if len(self.samples) >= 2:
+            a, b = self.samples[0], self.samples[-1]
+            if all(isinstance(x.get("acc_count"), int) for x in (a, b)) and b["acc_count"] > a["acc_count"]:
+                dn = b["acc_count"] - a["acc_count"]
+                for k in self.ACC:
+                    if isinstance(a.get(k), int) and isinstance(b.get(k), int):
+                        out[k.replace("_acc", "_frac")] = (b[k] - a[k]) / dn
+        return out
+
+
+def _pci_bus_id(device):
+    """PCI bus id of a HIP device (hipDeviceGetPCIBusId), for the amdsmi handle."""
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, int(device)) == 0:
+            return buf.value.decode()
+    except OSError:
+        pass
+    return None
+
+
 def _cpu_sample(o, X0, mus, covs, rows):
     n, d = X0.shape
     t0 = time.perf_counter()
@@ -115,19 +277,26 @@ def cpu_baseline(X0, mus, covs, rows, rows_1t):
 
     n, d = X0.shape
     rows, rows_1t = min(rows, n), min(rows_1t, n)
-    threads = int(o.num_threads())
+    # every core this process may use: the affinity mask, capped by the
+    # cgroup's CPU quota when one is set (threads beyond it only get throttled)
+    model, affinity = _host_cpu()
+    quota = _cpu_quota()
+    threads = max(1, min(affinity, int(quota)) if quota else affinity)
+    keep = int(o.num_threads())
+    o.set_threads(threads)
     dt = _cpu_sample(o, X0, mus, covs, rows)
     o.set_threads(1)
     dt1 = _cpu_sample(o, X0, mus, covs, rows_1t)
-    o.set_threads(threads)
-    model, host_cores = _host_cpu()
+    o.set_threads(keep)
     return {
         "value": rows / dt,
         "unit": "particle-updates/s",
         "cores": threads,
         "kind": "port",
         "host_cpu": model,
-        "host_cores": host_cores,
+        "host_cores": affinity,
+        "cpu_quota": quota,
+        "cores_rule": "min(len(sched_getaffinity), cgroup cpu.max quota)",
         "value_1thread": rows_1t / dt1,
         "sample": f"one step of the N={n} d={d} Gaussian-sum(k={len(mus)}) workload restricted to {rows} particle rows "
                   f"(their median pair share, grad log p of all N, phi_hat of {rows} rows against all N, "
@@ -167,6 +336,8 @@ def main():
     ap.add_argument("--cpu-rows", type=int, default=32768)
     ap.add_argument("--cpu-rows-1t", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the median is reported")
+    ap.add_argument("--no-diag", action="store_true", help="skip the untimed diagnostic pass")
     ap.add_argument("--dtype", choices=["f64", "f32"], default=None,
                     help="compute dtype of the O(N^2) work (default: the config's; cfg5 is f32)")
     ap.add_argument("--device-model", action="store_true",
@@ -229,31 +400,85 @@ def main():
         step()
     ctx.sync()
     ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))  # drop warmup events
+    ctx.diagnostics()  # (reset)
     ctx.check(ctx.lib.svgd_set_timing(ctx.h, 1))
 
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    ctx.sync()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-
+    # the median of `repeats` timed runs of exactly K steps, each
+    # bracketed by barrier + device sync; the GPU's clock/power sampled by
+    # amdsmi over the same span
+    mon = GpuMonitor(local_rank).start()
+    runs = []
+    for _ in range(args.repeats):
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        ctx.sync()
+        torch.cuda.synchronize()
+        barrier()
+        runs.append(time.perf_counter() - t0)
+    gpu_timed = mon.stop()
     phi_ms, med_ms, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
     ctx.check(ctx.lib.svgd_get_timing(ctx.h, ctypes.byref(phi_ms), ctypes.byref(med_ms), ctypes.byref(cnt)))
+    host_timed = ctx.diagnostics()  # host-side clocks of the timed steps (always on)
+    nsteps_timed = args.steps * args.repeats
+
+    # diagnostic pass (untimed): the phi kernel alone, the device's wait for
+    # G before the phi chain, collectives -- extra events, so not in the runs
+    diag = None
+    gpu_diag = None
+    if not args.no_diag:
+        ctx.check(ctx.lib.svgd_set_timing(ctx.h, 2))
+        mon.start()
+        for _ in range(args.steps):
+            step()
+        ctx.sync()
+        gpu_diag = mon.stop()
+        diag = ctx.diagnostics()
+        ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))
+        ctx.check(ctx.lib.svgd_set_timing(ctx.h, 0))
+
     a, med, path = ctx.last_scale()
     rows = ctx.row1 - ctx.row0
+    elapsed = sorted(runs)[len(runs) // 2]  # this rank's median run
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        t = torch.tensor(runs, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # per run: the slowest rank
+        runs = [float(x) for x in t.tolist()]
+        elapsed = sorted(runs)[len(runs) // 2]
+
+    def per_step(v, k):
+        return v / k if k else None
+
+    mine = {
+        "rank": rank, "rows": rows,
+        "phases_ms_per_step": {"phi": per_step(phi_ms.value, nsteps_timed),
+                               "median": per_step(med_ms.value, nsteps_timed)},
+        "host_ms_per_step": {"grad": per_step(host_timed["host_grad_ms"], host_timed["steps"]),
+                             "xwait": per_step(host_timed["host_xwait_ms"], host_timed["steps"]),
+                             "job": per_step(host_timed["host_job_ms"], host_timed["steps"]),
+                             "caller_wait": per_step(host_timed["host_wait_ms"], host_timed["steps"]),
+                             "threads": host_timed["host_threads"]},
+    }
+    if diag is not None:
+        mine["diag_ms_per_step"] = {
+            "phi_kernel": per_step(diag["phi_kernel_ms"], diag["phi_kernel_n"]),
+            "phi_wait_for_g": per_step(diag["phi_wait_ms"], diag["phi_wait_n"]),
+            "collectives": per_step(diag["coll_ms"], args.steps),
+            "g_allgather": per_step(diag["gather_g_ms"], args.steps),
+            "host_grad": per_step(diag["host_grad_ms"], diag["steps"]),
+        }
+        mine["n_ranks_seen"] = int(diag["ranks"])
+    per_rank = [mine]
+    if dist is not None:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
     if rank == 0:
-        phi_avg_s = phi_ms.value / max(1, cnt.value) / 1e3
+        phi_kernel_ms = mine.get("diag_ms_per_step", {}).get("phi_kernel")
         flops_launch = float(rows) * n * (5 * d + 4)
-        achieved = flops_launch / phi_avg_s / 1e12 if phi_avg_s > 0 else None
+        achieved = flops_launch / (phi_kernel_ms / 1e3) / 1e12 if phi_kernel_ms else None
         peak = FP32_PEAK_TFLOPS if dtype == "f32" else FP64_PEAK_TFLOPS
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "phi_pmc_traffic.json")
@@ -269,6 +494,7 @@ def main():
                 iss = json.load(f)
             if iss.get("n") == n and iss.get("d") == d and iss.get("world") == world and dtype == "f64":
                 issue = iss
+        row_kernel = dtype == "f64" and d <= 16
         out = {
             "metric": METRIC,
             "value": n * args.steps / elapsed,
@@ -288,48 +514,49 @@ def main():
                             f"{'device' if args.device_model else 'host'} grad log p per step",
                 "n": n, "d": d, "k": k, "parallelism": f"rows{world}",
             },
+            "repeats": {"n": len(runs), "rule": "value/ms_per_step = median run (max over ranks per run)",
+                        "ms_per_step": [r / args.steps * 1e3 for r in runs]},
             "roofline": {
                 # fp64 d <= 16: VALU row stream (f64 MFMA shares the VALU issue
-                # slots on gfx950); otherwise the MFMA tile kernel
-                # avg_launch_ms: HIP events around the phi phase on the
-                # context's stream -- record prep + the phi kernel + its reduce
-                # (with the fused optimizer update on the row path); the phi
-                # kernel is > 99 % of it at cfg3 (profiles/r02_*kernel_stats*)
+                # slots on gfx950); otherwise the MFMA tile kernel.
+                # avg_launch_ms: HIP events around the phi kernel launch alone
+                # (diagnostic pass after the timed runs; k_phi_rows without
+                # its reduce), so it is comparable with rocprof's kernel mean
                 "kernel": ("k_phi_rows (fused RBF + grad + phi contraction, fp64 VALU row stream)"
-                           if dtype == "f64" and d <= 16 else
+                           if row_kernel else
                            "k_phi_f32s (fused RBF + grad + phi contraction, streamed fp32 MFMA tiles)"
                            if dtype == "f32" and d > 12 else
                            "k_phi (fused RBF + grad + phi contraction, MFMA tiles)"),
-                "timed_span": ("k_prep_rec + k_phi_rows + k_phi_reduce (fused update)"
-                               if dtype == "f64" and d <= 16 else
-                               "k_prep_v + k_swz_f32 + k_cvt_f32 + k_phi_f32s"
-                               if dtype == "f32" and d > 12 else "k_prep_v + k_phi (+ cvt)"),
-                "bound": "valu" if dtype == "f64" and d <= 16 else "mfma",
+                "timed_span": "the phi kernel launch alone (HIP events, diagnostic pass)",
+                "bound": "valu" if row_kernel else "mfma",
                 "achieved": achieved,
                 "peak": peak,
                 "unit": "TFLOP/s",
                 "frac": (achieved / peak) if achieved else None,
                 "traffic": traffic,
-                "avg_launch_ms": phi_avg_s * 1e3,
+                "avg_launch_ms": phi_kernel_ms,
                 "flop_per_launch": flops_launch,
             },
-            "phases_ms_per_step": {"phi": phi_ms.value / max(1, args.steps),
-                                   "median": med_ms.value / max(1, args.steps)},
+            "phases_ms_per_step": mine["phases_ms_per_step"],
+            "host_ms_per_step": mine["host_ms_per_step"],
+            "diag_ms_per_step": mine.get("diag_ms_per_step"),
+            "gpu_timed": gpu_timed,
+            "gpu_diag": gpu_diag,
             "median_path": ["direct", "bracket", "fallback", "rebracket"][path],
             "scale_a": a,
         }
+        if world > 1:
+            out["per_rank"] = per_rank
+        clk = (gpu_diag or {}).get("gfxclk_mhz_median")
+        if achieved and clk:
+            # the flop fraction against the peak at the clock this run held
+            # under the phi kernel (amdsmi, same run): the ceiling this
+            # instruction mix can reach on this box
+            out["roofline"]["clock_mhz_under_load"] = clk
+            out["roofline"]["frac_at_load_clock"] = achieved / (peak * clk / 2400.0)
         if issue is not None:
-            # issue-slot view beside the flop fraction: the fp64 VALU pipe's
-            # share of issue slots used, and the clock the chip holds under this
-            # load (DVFS) -- the flop fraction at that clock is the ceiling this
-            # instruction mix can reach
-            clk = issue["clock_ghz_under_load"]
-            out["roofline"].update({
-                "valu_issue_util": issue["valu_issue_util"],
-                "clock_ghz_under_load": clk,
-                "frac_at_load_clock": (achieved / (peak * clk / 2.4)) if achieved else None,
-                "issue_source": issue["source"],
-            })
+            out["roofline"].update({"valu_issue_util": issue["valu_issue_util"],
+                                    "issue_source": issue["source"]})
         if args.config != "cfg3" or args.device_model or dtype != "f64":
             desc = cfg["desc"]
             if dtype != cfg.get("dtype", "f64"):

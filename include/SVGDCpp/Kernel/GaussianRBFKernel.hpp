@@ -46,6 +46,45 @@ public:
         // Step() before it is used (SVGD.hpp:389); the device recomputes it per
         // step, so no O(N^2) host work happens at construction.
         kernel_parameters_ = {Eigen::MatrixXd::Identity(dimension_, dimension_)};
+        // the closed form as the kernel function too (the reference sets its
+        // lambda with UpdateKernel, :75-87), so rbf + k, rbf * k, ... compose
+        // on the generic host path like any other set kernel
+        UpdateKernel(&GaussianRBFKernel::Value, &GaussianRBFKernel::Grad);
+    }
+
+    /** :75-81 -- exp(-(x - loc)^T M (x - loc)), M = params[0]. */
+    static double Value(const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &params,
+                        const Eigen::VectorXd &loc)
+    {
+        const Eigen::MatrixXd &M = params.at(0);
+        const long d = x.rows();
+        double s = 0.0;
+        for (long r = 0; r < d; ++r)
+        {
+            double t = 0.0;
+            for (long c = 0; c < d; ++c)
+                t += M(r, c) * (x(c) - loc(c));
+            s += (x(r) - loc(r)) * t;
+        }
+        return std::exp(-s);
+    }
+
+    /** grad_x: -2 M (x - loc) k(x, loc) (the reference's CppAD Jacobian of :75-81). */
+    static Eigen::VectorXd Grad(const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &params,
+                                const Eigen::VectorXd &loc)
+    {
+        const Eigen::MatrixXd &M = params.at(0);
+        const long d = x.rows();
+        const double kv = Value(x, params, loc);
+        Eigen::VectorXd g(d);
+        for (long r = 0; r < d; ++r)
+        {
+            double t = 0.0;
+            for (long c = 0; c < d; ++c)
+                t += M(r, c) * (x(c) - loc(c));
+            g(r) = -2.0 * t * kv;
+        }
+        return g;
     }
 
     std::unique_ptr<Kernel> CloneUniquePointer() const override { return std::make_unique<GaussianRBFKernel>(*this); }
@@ -80,34 +119,12 @@ public:
     }
 
     /** exp(-(x - location)^T M (x - location)) */
-    double EvaluateKernel(const Eigen::VectorXd &x) override
-    {
-        const Eigen::MatrixXd &M = GetScaleMatrix();
-        double s = 0.0;
-        for (long r = 0; r < dimension_; ++r)
-        {
-            double t = 0.0;
-            for (long c = 0; c < dimension_; ++c)
-                t += M(r, c) * (x(c) - location_(c));
-            s += (x(r) - location_(r)) * t;
-        }
-        return std::exp(-s);
-    }
+    double EvaluateKernel(const Eigen::VectorXd &x) override { return Value(x, kernel_parameters_, location_); }
 
     /** -2 M (x - location) k(x, location) */
     Eigen::VectorXd EvaluateKernelGrad(const Eigen::VectorXd &x) override
     {
-        const Eigen::MatrixXd &M = GetScaleMatrix();
-        const double kv = EvaluateKernel(x);
-        Eigen::VectorXd g(dimension_);
-        for (long r = 0; r < dimension_; ++r)
-        {
-            double t = 0.0;
-            for (long c = 0; c < dimension_; ++c)
-                t += M(r, c) * (x(c) - location_(c));
-            g(r) = -2.0 * t * kv;
-        }
-        return g;
+        return Grad(x, kernel_parameters_, location_);
     }
 
     /** :141-156 -- host restatement; the SVGD driver computes the scale on the device. */

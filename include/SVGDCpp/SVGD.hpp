@@ -33,6 +33,7 @@
 #define SVGDCPP_AMD_SVGD_HPP
 
 #include <fstream>
+#include <exception>
 #include <sstream>
 
 #include "Core.hpp"
@@ -286,13 +287,50 @@ protected:
 #ifdef _OPENMP
         if (parallel_)
         {
+            // an exception may not leave an OpenMP region (std::terminate):
+            // the first one is kept and rethrown after it, as the serial path
+            // would throw it
+            std::exception_ptr first;
 #pragma omp parallel
             {
-                std::unique_ptr<Kernel> k = kernel_ptr_->CloneUniquePointer();
+                try
+                {
+                    std::unique_ptr<Kernel> k = kernel_ptr_->CloneUniquePointer();
 #pragma omp for schedule(static)
-                for (long i = 0; i < n; ++i)
-                    row(*k, i);
+                    for (long i = 0; i < n; ++i)
+                    {
+                        bool skip;
+#pragma omp atomic read
+                        skip = failed_;
+                        if (!skip)
+                        {
+                            try
+                            {
+                                row(*k, i);
+                            }
+                            catch (...)
+                            {
+#pragma omp critical(svgdcpp_host_step)
+                                if (!first)
+                                    first = std::current_exception();
+#pragma omp atomic write
+                                failed_ = true;
+                            }
+                        }
+                    }
+                }
+                catch (...) // the clone itself
+                {
+#pragma omp critical(svgdcpp_host_step)
+                    if (!first)
+                        first = std::current_exception();
+#pragma omp atomic write
+                    failed_ = true;
+                }
             }
+            failed_ = false;
+            if (first)
+                std::rethrow_exception(first);
         }
         else
 #endif
@@ -419,6 +457,7 @@ protected:
     size_t num_iterations_;
     size_t num_particles_ = 0;
     const bool parallel_ = false;
+    bool failed_ = false; // parallel HostStep: a row threw, the others stop
     bool check_bounds_ = false;
     bool log_intermediate_matrices_ = false;
     bool initialized_ = false;

@@ -173,10 +173,48 @@ int svgd_last_scale(const svgd_ctx *ctx, double *a_out, double *med_out, int *me
  * size-independent rank checks of the selection at full size. */
 int svgd_last_median_keys(svgd_ctx *ctx, double *sq_lo, double *sq_hi, int64_t *rank_lo,
                           int64_t *rank_hi);
-/* Enable HIP-event timing of the phi kernel and the median phase on the
- * context stream; get returns accumulated milliseconds and launch count. */
-int svgd_set_timing(svgd_ctx *ctx, int enable);
+/* HIP-event timing on the context stream.  level 1: the phi phase (median
+ * end -> record prep .. reduce + update) and the median phase (previous phi
+ * end -> scale final), with events only at phase boundaries; get returns the
+ * accumulated milliseconds and the phi-phase count (and resets them).
+ * level 2 adds the diagnostic events read by svgd_get_diagnostics -- the phi
+ * kernel alone, the device's wait between the median's end and the phi chain,
+ * every collective -- each one a ~5 us dispatch gap (a diagnostic pass, not
+ * the timed one).  0 disables. */
+int svgd_set_timing(svgd_ctx *ctx, int level);
 int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *count);
+/* Accumulated diagnostics since the last call (then reset); writes
+ * min(cap, SVGD_DIAG_LEN) doubles, returns that count or an error:
+ *   STEPS            svgd_step_host_model calls
+ *   PHI_KERNEL_MS/N  phi kernel alone (k_phi_rows without its reduce, or the
+ *                    tile kernel), HIP events (level 2)
+ *   PHI_WAIT_MS/N    device idle between the median's end and the phi chain:
+ *                    waiting for the host gradient / G copies / G all-gather (level 2)
+ *   COLL_MS/N        collectives on the compute stream (level 2, P > 1)
+ *   GATHER_G_MS/N    the G all-gather on its own stream (level 2, P > 1)
+ *   HOST_GRAD_MS     host grad log p wall time (worker thread, all chunks)
+ *   HOST_XWAIT_MS    worker waiting for X_t chunk copies
+ *   HOST_JOB_MS      worker job: post -> last G chunk landed
+ *   HOST_WAIT_MS     calling thread waiting for the worker after queuing the median
+ *   RANKS            ranks in the communicator (1 without one)
+ *   HOST_THREADS     OpenMP threads of the host gradient */
+#define SVGD_DIAG_STEPS 0
+#define SVGD_DIAG_PHI_KERNEL_MS 1
+#define SVGD_DIAG_PHI_KERNEL_N 2
+#define SVGD_DIAG_PHI_WAIT_MS 3
+#define SVGD_DIAG_PHI_WAIT_N 4
+#define SVGD_DIAG_COLL_MS 5
+#define SVGD_DIAG_COLL_N 6
+#define SVGD_DIAG_GATHER_G_MS 7
+#define SVGD_DIAG_GATHER_G_N 8
+#define SVGD_DIAG_HOST_GRAD_MS 9
+#define SVGD_DIAG_HOST_XWAIT_MS 10
+#define SVGD_DIAG_HOST_JOB_MS 11
+#define SVGD_DIAG_HOST_WAIT_MS 12
+#define SVGD_DIAG_RANKS 13
+#define SVGD_DIAG_HOST_THREADS 14
+#define SVGD_DIAG_LEN 15
+int svgd_get_diagnostics(svgd_ctx *ctx, double *out, int cap);
 /* Median tuning knobs (tests force each path): pair count at or below which
  * all keys are stored (direct path), sample size, candidate capacity.
  * Values <= 0 keep the current setting. */

@@ -34,6 +34,11 @@ SVGD_MEDIAN_DIRECT = 0
 SVGD_MEDIAN_BRACKET = 1
 SVGD_MEDIAN_FALLBACK = 2
 SVGD_MEDIAN_REBRACKET = 3
+# svgd_get_diagnostics slots (svgd_capi.h SVGD_DIAG_*)
+DIAG_NAMES = ("steps", "phi_kernel_ms", "phi_kernel_n", "phi_wait_ms", "phi_wait_n", "coll_ms",
+              "coll_n", "gather_g_ms", "gather_g_n", "host_grad_ms", "host_xwait_ms",
+              "host_job_ms", "host_wait_ms", "ranks", "host_threads")
+SVGD_DIAG_LEN = len(DIAG_NAMES)
 
 _D = ctypes.POINTER(ctypes.c_double)
 _I64 = ctypes.c_int64
@@ -68,6 +73,7 @@ SIGNATURES = {
     "svgd_last_median_keys": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     "svgd_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "svgd_get_timing": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(_I64)]),
+    "svgd_get_diagnostics": (ctypes.c_int, [_P, _D, ctypes.c_int]),
     "svgd_set_median_tuning": (ctypes.c_int, [_P, _I64, _I64, _I64]),
     "svgd_debug_pair_keys": (ctypes.c_int, [_P, _D, _I64]),
     "svgd_set_scale_matrix": (ctypes.c_int, [_P, _D]),

@@ -216,6 +216,21 @@ class MultivariateNormal(GaussianSum):
         return 1.0 / ((2.0 * math.pi) ** (self.dimension_ / 2.0) * math.sqrt(np.linalg.det(self.covs_[0])))
 
 
+def _builtin_grad(model):
+    """The model's gradient is the built-in C++ one: a GaussianSum whose
+    subclass (if any) overrides neither gradient method -- only then may the
+    C handle evaluate it (an override must run as the user wrote it)."""
+    t = type(model)
+    return (isinstance(model, GaussianSum) and t.log_model_grad is GaussianSum.log_model_grad
+            and t.EvaluateLogModelGrad is GaussianSum.EvaluateLogModelGrad)
+
+
+def _builtin_hess(model):
+    t = type(model)
+    return (isinstance(model, GaussianSum) and t.neg_hess_sum is GaussianSum.neg_hess_sum
+            and t.EvaluateLogModelHessian is GaussianSum.EvaluateLogModelHessian)
+
+
 def _gaussian_components(m):
     if isinstance(m, GaussianSum):
         return list(m.means_), list(m.covs_)
@@ -331,6 +346,23 @@ class GaussianRBFKernel(Kernel):
         self.target_model_ = model
         self.scale_ = float(scale)
         self.scale_matrix_ = None  # full M for ScaleMethod.Constant
+        self.kernel_parameters_ = [self.scale_matrix()]
+        # the closed form as the kernel function too (the reference sets its
+        # lambda with UpdateKernel, GaussianRBFKernel.hpp:75-87), so rbf + k,
+        # rbf * k, ... compose on the generic host path like any set kernel
+        self._fun = GaussianRBFKernel._value
+        self._grad = GaussianRBFKernel._gradient
+
+    @staticmethod
+    def _value(x, params, loc):  # :75-81, M = params[0]
+        diff = np.asarray(x, dtype=np.float64) - loc
+        return float(np.exp(-diff @ np.asarray(params[0]) @ diff))
+
+    @staticmethod
+    def _gradient(x, params, loc):
+        diff = np.asarray(x, dtype=np.float64) - loc
+        M = np.asarray(params[0])
+        return -2.0 * (M @ diff) * np.exp(-diff @ M @ diff)
 
     def scale_matrix(self):
         """M of k(x, x') = exp(-(x-x')^T M (x-x'))."""
@@ -339,26 +371,24 @@ class GaussianRBFKernel(Kernel):
         return self.scale_ * np.eye(self.dimension_)
 
     def EvaluateKernel(self, x):  # GaussianRBFKernel.hpp:75-81
-        diff = np.asarray(x, dtype=np.float64) - self.location_
-        return float(np.exp(-diff @ self.scale_matrix() @ diff))
+        return self._value(x, [self.scale_matrix()], self.location_)
 
     def EvaluateKernelGrad(self, x):
-        diff = np.asarray(x, dtype=np.float64) - self.location_
-        M = self.scale_matrix()
-        return -2.0 * (M @ diff) * np.exp(-diff @ M @ diff)
+        return self._gradient(x, [self.scale_matrix()], self.location_)
 
     def UpdateParameters(self, params):
         M = np.asarray(params[0], dtype=np.float64)
         if M.ndim == 0:
             self.scale_, self.scale_matrix_ = float(M), None
-            return
-        if M.shape != (self.dimension_, self.dimension_):
+        elif M.shape != (self.dimension_, self.dimension_):
             raise DimensionMismatchException("Kernel scale matrix has incorrect dimensions.")
-        a = float(M[0, 0])
-        if np.array_equal(M, a * np.eye(M.shape[0])):
-            self.scale_, self.scale_matrix_ = a, None
         else:
-            self.scale_matrix_ = M.copy()
+            a = float(M[0, 0])
+            if np.array_equal(M, a * np.eye(M.shape[0])):
+                self.scale_, self.scale_matrix_ = a, None
+            else:
+                self.scale_matrix_ = M.copy()
+        self.kernel_parameters_ = [self.scale_matrix()]
 
 
 # -------------------------------------------------------------- optimizers --
@@ -589,16 +619,16 @@ class Context:
         A built-in GaussianSum runs through svgd_step_host_model (the X_t copy,
         the gradient and the G upload pipelined in row chunks, all in C);
         pipelined=False takes the split begin / gradient / finish calls."""
-        if pipelined and not hessian and isinstance(model, GaussianSum):
+        if pipelined and not hessian and _builtin_grad(model):
             self.check(self.lib.svgd_step_host_model(self.h, model._handle))
             return
         self.check(self.lib.svgd_begin_step(self.h, self.x_host_ptr))
         nr = self.row1 - self.row0
         if hessian:
-            H = (model.neg_hess_sum_ptr(self.x_host_ptr, nr) if isinstance(model, GaussianSum)
+            H = (model.neg_hess_sum_ptr(self.x_host_ptr, nr) if _builtin_hess(model)
                  else model.neg_hess_sum(self.x_host[:nr]))
             self.set_step_hessian_sum(H)
-        if isinstance(model, GaussianSum):
+        if _builtin_grad(model):
             model.log_model_grad_ptr(self.x_host_ptr, nr, self.g_host_ptr)
         elif nr > 0:
             self.g_host[:nr] = model.log_model_grad(self.x_host[:nr])
@@ -620,7 +650,7 @@ class Context:
     def set_device_model(self, model):
         """Mirror a GaussianSum on the device; then
         step_device() runs the whole step, grad log p included, in HBM."""
-        if model is not None and not isinstance(model, GaussianSum):
+        if model is not None and not _builtin_grad(model):
             raise TypeError("only the built-in Gaussian-sum models have a device form")
         self.check(self.lib.svgd_set_device_model(self.h, model._handle if model is not None else None))
         self._device_model = model  # keep the host handle alive
@@ -635,6 +665,14 @@ class Context:
 
     def sync(self):
         self.check(self.lib.svgd_sync(self.h))
+
+    def diagnostics(self):
+        """svgd_get_diagnostics as a dict (accumulated since the last call, then reset)."""
+        buf = (ctypes.c_double * C.SVGD_DIAG_LEN)()
+        rc = self.lib.svgd_get_diagnostics(self.h, buf, C.SVGD_DIAG_LEN)
+        if rc < 0:
+            self.check(rc)
+        return dict(zip(C.DIAG_NAMES, list(buf)))
 
 
 class SVGD:
@@ -750,7 +788,7 @@ class SVGD:
                 c.check(c.lib.svgd_begin_step(c.h, c.x_host_ptr))
                 nr = c.row1 - c.row0
                 c.set_step_hessian_sum(hmodel.neg_hess_sum(c.x_host[:nr]))
-                if isinstance(self.model_, GaussianSum):
+                if _builtin_grad(self.model_):
                     self.model_.log_model_grad_ptr(c.x_host_ptr, nr, c.g_host_ptr)
                 elif nr > 0:
                     c.g_host[:nr] = self.model_.log_model_grad(c.x_host[:nr])

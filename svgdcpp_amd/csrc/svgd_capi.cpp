@@ -122,6 +122,13 @@ struct svgd_ctx {
     int device = 0;
     int world = 1, rank = 0;
     ncclComm_t comm = nullptr;
+    // a second communicator (ncclCommSplit of comm) for the G all-gather on
+    // its own stream: it overlaps the median chain's kernels and collectives
+    // (one communicator's operations would run in issue order behind them)
+    ncclComm_t gcomm = nullptr;
+    hipStream_t gstream = nullptr;
+    hipEvent_t ev_gg = nullptr;   // G all-gathered (gstream)
+    bool gg_pending = false;      // phi must wait for ev_gg
     HostComm *hcomm = nullptr; // SVGD_HOSTCOMM rehearsal backend (ranks sharing one GPU)
     // device mirror of a built-in Gaussian-sum model (svgd_set_device_model)
     int dm_k = 0;
@@ -228,12 +235,29 @@ struct svgd_ctx {
     std::vector<double> h_mat;
     bool have_particles = false;
 
-    // timing
+    // timing (svgd_set_timing): level 1 = phase events at the phase
+    // boundaries only; level 2 adds the diagnostic events (phi kernel alone,
+    // the wait for G before the phi chain, every collective) -- each one a
+    // dispatch gap, so a diagnostic pass, never the timed one
     bool timing = false;
+    int tlevel = 0;
     std::vector<EvPair> ev_phi, ev_med;
     std::vector<EvPair> ev_pool;
     double phi_ms = 0, med_ms = 0;
     int64_t tcount = 0;
+    struct DiagEv {
+        hipEvent_t a, b;
+        int kind;    // DG_* below
+        bool own_a;  // a came from the pool (else it is a phase event)
+    };
+    std::vector<DiagEv> ev_diag;
+    std::vector<hipEvent_t> ev_single; // pool of the diagnostic events
+    hipEvent_t med_end_ev = nullptr;    // this step's median-end phase event
+    double dg_ms[4] = {0, 0, 0, 0};
+    int64_t dg_cnt[4] = {0, 0, 0, 0};
+    // host-side wall clocks of svgd_step_host_model (always on: steady_clock)
+    double h_grad_ms = 0, h_xwait_ms = 0, h_job_ms = 0, h_wait_ms = 0;
+    int64_t h_steps = 0;
 
     int last_path = SVGD_MEDIAN_DIRECT;
     std::string err;
@@ -343,33 +367,73 @@ EvPair take_pair(svgd_ctx *c)
 
 int64_t upper_pairs(int64_t n) { return n * (n - 1) / 2; }
 
+// diagnostic event kinds (svgd_set_timing level 2; svgd_get_diagnostics)
+enum { DG_PHI_KERNEL = 0, DG_PHI_WAIT = 1, DG_COLL = 2, DG_GATHER_G = 3 };
+
+// level-2 diagnostic span on stream s: begin records a pooled event, end its
+// partner; begin returns nullptr below level 2 and end then does nothing
+hipEvent_t take_ev(svgd_ctx *c)
+{
+    hipEvent_t e = nullptr;
+    if (!c->ev_single.empty()) {
+        e = c->ev_single.back();
+        c->ev_single.pop_back();
+    } else {
+        (void)hipEventCreate(&e);
+    }
+    return e;
+}
+hipEvent_t diag_begin(svgd_ctx *c, hipStream_t s)
+{
+    if (c->tlevel < 2) return nullptr;
+    hipEvent_t e = take_ev(c);
+    (void)hipEventRecord(e, s);
+    c->mark = c->phi_end = nullptr; // work (an event) queued after those marks
+    return e;
+}
+void diag_end(svgd_ctx *c, hipStream_t s, hipEvent_t a, int kind, bool own_a = true)
+{
+    if (!a) return;
+    hipEvent_t b = take_ev(c);
+    (void)hipEventRecord(b, s);
+    c->ev_diag.push_back({a, b, kind, own_a});
+    c->mark = c->phi_end = nullptr;
+}
+
 // ---------------------------------------------------------- collectives --
 
-int allgather_rows(svgd_ctx *c, double *buf)
+int allgather_rows_on(svgd_ctx *c, double *buf, ncclComm_t comm, hipStream_t s, int kind)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
     c->mark = c->phi_end = nullptr; // work queued after the median's / phi's end event
     const size_t cnt = (size_t)c->chunk * c->dim;
+    hipEvent_t d0 = diag_begin(c, s);
     if (c->hcomm) {
-        if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(double),
-                               c->stream))
+        if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(double), s))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-gather failed.");
-        return SVGD_OK;
+    } else {
+        NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclDouble, comm, s));
     }
-    NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclDouble, c->comm,
-                             c->stream));
+    diag_end(c, s, d0, kind);
     return SVGD_OK;
+}
+
+int allgather_rows(svgd_ctx *c, double *buf)
+{
+    return allgather_rows_on(c, buf, c->comm, c->stream, DG_COLL);
 }
 
 int allreduce_u64(svgd_ctx *c, unsigned long long *buf, size_t cnt)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
+    hipEvent_t d0 = diag_begin(c, c->stream);
     if (c->hcomm) {
         if (hostcomm_allreduce_u64(c->hcomm, buf, cnt, c->stream))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
-        return SVGD_OK;
+    } else {
+        NCCLCHK(c, ncclAllReduce(buf, buf, cnt, ncclUint64, ncclSum, c->comm, c->stream));
     }
-    NCCLCHK(c, ncclAllReduce(buf, buf, cnt, ncclUint64, ncclSum, c->comm, c->stream));
+    diag_end(c, c->stream, d0, DG_COLL);
     return SVGD_OK;
 }
 
@@ -384,14 +448,16 @@ int allreduce_cnt3(svgd_ctx *c)
 int allgather_u64(svgd_ctx *c, uint64_t *buf, size_t cnt)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
+    hipEvent_t d0 = diag_begin(c, c->stream);
     if (c->hcomm) {
         if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(uint64_t),
                                c->stream))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-gather failed.");
-        return SVGD_OK;
+    } else {
+        NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclUint64, c->comm,
+                                 c->stream));
     }
-    NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclUint64, c->comm,
-                             c->stream));
+    diag_end(c, c->stream, d0, DG_COLL);
     return SVGD_OK;
 }
 
@@ -676,6 +742,7 @@ int median_finish_spec(svgd_ctx *c, double logn)
     // complete, by median_finish: resolve_pending never redoes half a step)
     if (c->timing && !c->ev_med.empty()) {
         c->ev_status_use = c->ev_med.back().b; // also the median phase's end
+        c->med_end_ev = c->ev_status_use;
         c->med_ev_done = true;
         c->mark = c->ev_status_use;
     } else {
@@ -838,9 +905,19 @@ int upload_g_begin(svgd_ctx *c, const double *G_shard)
     return SVGD_OK;
 }
 
-// ... and, on the compute stream once it needs G, the all-gather of the shards.
+// ... and the all-gather of the shards.  With a G communicator (P > 1 over
+// RCCL) it runs on its own stream as soon as the shard has landed, beside the
+// median chain, and the phi chain waits for it (run_phi); otherwise on the
+// compute stream once it needs G.
 int upload_g_finish(svgd_ctx *c)
 {
+    if (c->gcomm) {
+        if (hipEventQuery(c->ev_g) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(c->gstream, c->ev_g, 0));
+        CHK(allgather_rows_on(c, c->G, c->gcomm, c->gstream, DG_GATHER_G));
+        HIPCHK(c, hipEventRecord(c->ev_gg, c->gstream));
+        c->gg_pending = true;
+        return SVGD_OK;
+    }
     // a G copy that has already landed needs no cross-queue barrier (a wait
     // on the copy stream's signal cost a ~25 us dispatch gap before the
     // record prep even when the copy had finished long before)
@@ -882,7 +959,16 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
             HIPCHK(c, hipEventRecord(ev.a, c->stream));
         }
     }
+    // level 2: the device's wait between the median's end and the phi chain
+    // (the host gradient, the G copies and, P > 1, the G all-gather)
+    hipEvent_t med_end = c->tlevel >= 2 ? c->med_end_ev : nullptr;
+    c->med_end_ev = nullptr;
     c->mark = nullptr;
+    if (c->gg_pending) {
+        if (hipEventQuery(c->ev_gg) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gg, 0));
+        c->gg_pending = false;
+    }
+    if (med_end) diag_end(c, c->stream, med_end, DG_PHI_WAIT, false);
     const bool mat = matrix_scale(c);
     if (mat) {
         // M = factor * src, L = chol(M), a_eff = 1 (GaussianRBFKernel.hpp:189-210)
@@ -927,11 +1013,14 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         HIPCHK(c, launch_cvt_f32(c->cvec, c->np, c->cvf, c->stream));
         if (mat) HIPCHK(c, launch_cvt_f32(c->zc, c->np * c->KP, c->zcf, c->stream));
     }
+    // level 2: the phi kernel alone (k_phi_rows before its reduce, or the tile kernel)
+    hipEvent_t k0 = diag_begin(c, c->stream), k1 = nullptr;
+    if (k0) k1 = take_ev(c);
     if (c->rowpath)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
                                   mat ? c->sc_sgn : nullptr, mat ? nullptr : c->nmax, c->phi, opt,
-                                  c->stream));
+                                  c->stream, k1));
     else if (phis)
         HIPCHK(c, launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
                                   c->row0, c->nrows, ntl, c->dim, 1.0 / (double)c->n,
@@ -945,6 +1034,10 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         HIPCHK(c, launch_phi(c->KP, c->NCB, mat ? c->zc : c->xc, c->cvec, c->V, c->scal, c->row0,
                              c->nrows, (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n,
                              mat ? c->wv : nullptr, c->phi, c->stream));
+    if (k0) {
+        if (!c->rowpath) HIPCHK(c, hipEventRecord(k1, c->stream));
+        c->ev_diag.push_back({k0, k1, DG_PHI_KERNEL, true});
+    }
     if (c->timing) {
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         c->ev_phi.push_back(ev);
@@ -989,13 +1082,15 @@ int run_phi_opt(svgd_ctx *c)
         HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
         c->phi_end = nullptr;
     }
-    CHK(allgather_rows(c, c->X));
+    // this rank's rows of X_{t+1} are final here: the next step's X_t copy
+    // down (host gradient) need not wait for the X all-gather (P > 1)
     if (c->phi_end) {
         c->ev_xready_use = c->phi_end;
     } else {
         HIPCHK(c, hipEventRecord(c->ev_xready, c->stream));
         c->ev_xready_use = c->ev_xready;
     }
+    CHK(allgather_rows(c, c->X));
     c->phi_end = nullptr;
     return SVGD_OK;
 }
@@ -1050,8 +1145,10 @@ int scale_finish(svgd_ctx *c)
     if (c->med_ev_done) {
         c->ev_fin_use = c->ev_status_use;
     } else {
-        if (c->timing && !c->ev_med.empty())
+        if (c->timing && !c->ev_med.empty()) {
             HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
+            c->med_end_ev = c->ev_med.back().b;
+        }
         HIPCHK(c, hipEventRecord(c->ev_fin, c->stream));
         c->ev_fin_use = c->ev_fin;
         c->mark = nullptr;
@@ -1292,6 +1389,10 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
         ncclUniqueId id;
         std::memcpy(&id, unique_id128, sizeof(id));
         NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
+        // the G all-gather's communicator and stream (upload_g_finish)
+        NCCLCHK(c, ncclCommSplit(c->comm, 0, rank, &c->gcomm, nullptr));
+        HIPCHK(c, hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_gg, hipEventDisableTiming));
     }
     return SVGD_OK;
 }
@@ -1302,6 +1403,8 @@ int svgd_destroy(svgd_ctx *c)
     c->worker.reset(); // idle between steps: joins the gradient thread
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    if (c->gstream) (void)hipStreamSynchronize(c->gstream);
+    if (c->gcomm) (void)ncclCommDestroy(c->gcomm);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->hcomm) hostcomm_destroy(c->hcomm);
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
@@ -1337,6 +1440,13 @@ int svgd_destroy(svgd_ctx *c)
     if (c->ev_status) (void)hipEventDestroy(c->ev_status);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->gstream) (void)hipStreamDestroy(c->gstream);
+    if (c->ev_gg) (void)hipEventDestroy(c->ev_gg);
+    for (auto &e : c->ev_diag) {
+        if (e.own_a) (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    for (hipEvent_t e : c->ev_single) (void)hipEventDestroy(e);
     delete c;
     return SVGD_OK;
 }
@@ -1548,6 +1658,11 @@ int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_scal, 0));
     CHK(center(c));
     HIPCHK(c, launch_set_scal(a, NAN, c->scal, c->stream));
+    // the host copy of [a, med] follows (svgd_last_scale after svgd_phi)
+    HIPCHK(c, hipEventSynchronize(c->ev_scal)); // no D2H into h_scal pending
+    c->h_scal[0] = a;
+    c->h_scal[1] = NAN;
+    c->scal_fresh = true;
     CHK(upload_g(c, G_shard));
     CHK(run_phi(c, nullptr));
     if (phi_out && c->nrows > 0) {
@@ -1634,20 +1749,29 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     // model and queues its G copy on the copy stream (the calling thread only
     // touches `stream` until it waits for this job)
     if (!c->worker) c->worker.reset(new HostWorker());
-    c->worker->post([c, m, d, rows, nch, chunk](std::string &msg) -> int {
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t0, clk::time_point t1) {
+        return std::chrono::duration<double, std::milli>(t1 - t0).count();
+    };
+    const clk::time_point t_post = clk::now();
+    c->worker->post([c, m, d, rows, nch, chunk, ms_since, t_post](std::string &msg) -> int {
         for (int q = 0; q < nch && rows > 0; ++q) {
             int64_t r0, r1;
             chunk(q, &r0, &r1);
+            const clk::time_point tw = clk::now();
             hipError_t e = hipEventSynchronize(c->ev_xch[q]);
             if (e != hipSuccess) {
                 msg = std::string("SVGDCpp: [HIP Error] X_t chunk copy: ") + hipGetErrorString(e);
                 return SVGD_ERR_HIP;
             }
+            const clk::time_point tg = clk::now();
             if (model_logp_grad_threads(m, c->h_x + r0 * d, r1 - r0, c->h_g + r0 * d,
                                         c->host_threads)) {
                 msg = "SVGDCpp: [Argument Error] Host model evaluation failed.";
                 return SVGD_ERR_ARG;
             }
+            c->h_xwait_ms += ms_since(tw, tg);
+            c->h_grad_ms += ms_since(tg, clk::now());
             e = hipMemcpyAsync(c->G + (size_t)(c->row0 + r0) * d, c->h_g + r0 * d,
                                sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyHostToDevice,
                                c->cstream);
@@ -1665,12 +1789,16 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
             msg = std::string("SVGDCpp: [HIP Error] G event: ") + hipGetErrorString(e);
             return SVGD_ERR_HIP;
         }
+        c->h_job_ms += ms_since(t_post, clk::now());
         return SVGD_OK;
     });
     int rc = plan_step(c);
     if (rc == SVGD_OK) rc = scale_begin(c);
     std::string wmsg;
+    const clk::time_point tw0 = clk::now();
     const int wrc = c->worker->wait(wmsg); // always joined before returning
+    c->h_wait_ms += ms_since(tw0, clk::now());
+    c->h_steps += 1;
     CHK(rc);
     if (wrc != SVGD_OK) {
         c->err = wmsg;
@@ -1796,8 +1924,49 @@ int svgd_set_timing(svgd_ctx *c, int enable)
 {
     if (!c) return SVGD_ERR_ARG;
     c->timing = enable != 0;
+    c->tlevel = enable < 0 ? 0 : enable;
     c->last_phi_end = nullptr;
     return SVGD_OK;
+}
+
+int svgd_get_diagnostics(svgd_ctx *c, double *out, int cap)
+{
+    if (!c || (!out && cap > 0)) return SVGD_ERR_ARG;
+    CHK(resolve_pending(c));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->gstream) HIPCHK(c, hipStreamSynchronize(c->gstream));
+    for (auto &e : c->ev_diag) {
+        float ms = 0;
+        HIPCHK(c, hipEventElapsedTime(&ms, e.a, e.b));
+        c->dg_ms[e.kind] += ms;
+        c->dg_cnt[e.kind] += 1;
+        if (e.own_a) c->ev_single.push_back(e.a);
+        c->ev_single.push_back(e.b);
+    }
+    c->ev_diag.clear();
+    int ranks = 1;
+    if (c->comm) (void)ncclCommCount(c->comm, &ranks);
+    else if (c->hcomm) ranks = c->world;
+    const double v[SVGD_DIAG_LEN] = {(double)c->h_steps,
+                                     c->dg_ms[DG_PHI_KERNEL],
+                                     (double)c->dg_cnt[DG_PHI_KERNEL],
+                                     c->dg_ms[DG_PHI_WAIT],
+                                     (double)c->dg_cnt[DG_PHI_WAIT],
+                                     c->dg_ms[DG_COLL],
+                                     (double)c->dg_cnt[DG_COLL],
+                                     c->dg_ms[DG_GATHER_G],
+                                     (double)c->dg_cnt[DG_GATHER_G],
+                                     c->h_grad_ms,
+                                     c->h_xwait_ms,
+                                     c->h_job_ms,
+                                     c->h_wait_ms,
+                                     (double)ranks,
+                                     (double)c->host_threads};
+    for (int i = 0; i < cap && i < SVGD_DIAG_LEN; ++i) out[i] = v[i];
+    for (int k = 0; k < 4; ++k) c->dg_ms[k] = 0, c->dg_cnt[k] = 0;
+    c->h_grad_ms = c->h_xwait_ms = c->h_job_ms = c->h_wait_ms = 0;
+    c->h_steps = 0;
+    return cap < SVGD_DIAG_LEN ? cap : SVGD_DIAG_LEN;
 }
 
 int svgd_get_timing(svgd_ctx *c, double *phi_ms, double *median_ms, int64_t *count)

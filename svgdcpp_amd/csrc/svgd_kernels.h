@@ -159,12 +159,13 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            const double *a_ptr, int64_t n, int64_t np, int d, int KP, int RS,
                            double *rec, hipStream_t stream);
 // opt (optional): the optimizer step applied to each phi element as the
-// reduce writes it (the step path: one launch fewer than launch_opt_update)
+// reduce writes it (the step path: one launch fewer than launch_opt_update).
+// ev_mid (optional): recorded between k_phi_rows and its reduce (diagnostics)
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
-                           hipStream_t stream);
+                           hipStream_t stream, hipEvent_t ev_mid = nullptr);
 // full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,
 // or an eigendecomposition when M is indefinite and d <= ROWS_MAX_D);
 // err = 0 positive definite, 2 indefinite, 1 non-finite / no convergence.

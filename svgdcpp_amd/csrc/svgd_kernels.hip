@@ -2810,14 +2810,18 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
-                           hipStream_t stream)
+                           hipStream_t stream, hipEvent_t ev_mid)
 {
-    if (nrows <= 0) return hipSuccess;
+    if (nrows <= 0) {
+        if (ev_mid) return hipEventRecord(ev_mid, stream);
+        return hipSuccess;
+    }
     const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
     hipError_t e = launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                       nmax_bits, nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
                                       SinkDebug{}, stream);
     if (e != hipSuccess) return e;
+    if (ev_mid && (e = hipEventRecord(ev_mid, stream)) != hipSuccess) return e;
     if (d > 16) return hipErrorInvalidValue; // k_phi_reduce's LDS holds d + 1 <= 17
     const int64_t g = (nrows + phi_red_rows(d) - 1) / phi_red_rows(d);
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,

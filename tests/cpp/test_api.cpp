@@ -442,6 +442,64 @@ static void TestGenericKernelHostPath()
     CHECK(Throws<DimensionMismatchException>([&] { Kernel s = a + k3; }));
     Kernel unset(2);
     CHECK(Throws<UnsetException>([&] { Kernel s = a + unset; }));
+
+    // a GaussianRBFKernel composes like any set kernel (its constructor sets
+    // the closed form, as the reference's sets its lambda,
+    // GaussianRBFKernel.hpp:75-87): rbf (+ - * /) b against the operands
+    {
+        auto xr = std::make_shared<Eigen::MatrixXd>(Eigen::MatrixXd::Random(2, 4));
+        GaussianRBFKernel rbf(xr, GaussianRBFKernel::ScaleMethod::Constant);
+        Eigen::Matrix2d M;
+        M << 0.5, 0.1, 0.1, 0.8;
+        rbf.UpdateParameters({Eigen::MatrixXd(M)});
+        Kernel rops[4] = {rbf + b, rbf - b, rbf * b, rbf / b};
+        rbf.UpdateLocation(loc);
+        const Eigen::VectorXd d1 = x1 - loc;
+        const double kr = std::exp(-(d1(0) * (M(0, 0) * d1(0) + M(0, 1) * d1(1)) +
+                                     d1(1) * (M(1, 0) * d1(0) + M(1, 1) * d1(1))));
+        CHECK(std::fabs(rbf.EvaluateKernel(x1) - kr) < 1e-15);
+        const double rexp[4] = {kr + kb, kr - kb, kr * kb, kr / kb};
+        for (int q = 0; q < 4; ++q)
+        {
+            Kernel &k = rops[q];
+            CHECK(k.GetParameters().size() == 2);
+            k.UpdateLocation(loc);
+            CHECK(std::fabs(k.EvaluateKernel(x1) - rexp[q]) < 1e-15);
+            const Eigen::VectorXd g = k.EvaluateKernelGrad(x1);
+            for (long c = 0; c < 2; ++c)
+            {
+                Eigen::VectorXd xp = x1, xm = x1;
+                xp(c) += 1e-6;
+                xm(c) -= 1e-6;
+                CHECK(std::fabs(g(c) - (k.EvaluateKernel(xp) - k.EvaluateKernel(xm)) / 2e-6) < 1e-8);
+            }
+        }
+    }
+
+    // Parallel = true: the composed kernel on OpenMP threads matches the
+    // serial run, and an unset kernel surfaces UnsetException from Run()
+    // instead of terminating inside the parallel region
+    {
+        std::srand(3);
+        auto xs = std::make_shared<Eigen::MatrixXd>(Eigen::MatrixXd::Random(2, 12));
+        auto xp = std::make_shared<Eigen::MatrixXd>(*xs);
+        auto model = std::make_shared<CosineModel>();
+        auto mk = [&](const std::shared_ptr<Eigen::MatrixXd> &x, bool par) {
+            auto k = std::make_shared<Kernel>(*UnitRBF(2) * *UnitRBF(2) + *UnitRBF(2));
+            auto opt = std::make_shared<Adam>(2, 12, 1.0e-1, 0.9, 0.999);
+            SVGD s(2, 5, x, k, model, opt, par);
+            s.Initialize();
+            s.Run();
+        };
+        mk(xs, false);
+        mk(xp, true);
+        CHECK(MaxAbsDiff(*xs, *xp) == 0.0);
+        std::shared_ptr<Kernel> plain = std::make_shared<Kernel>(2);
+        auto opt = std::make_shared<Adam>(2, 12, 1.0e-1, 0.9, 0.999);
+        SVGD s(2, 1, xs, plain, model, opt, true);
+        s.Initialize();
+        CHECK(Throws<UnsetException>([&] { s.Run(); }));
+    }
 }
 
 // Logged-matrix runs for tests/test_cpp_api.py (value parity of the

@@ -147,6 +147,62 @@ def test_kernel_composition_rules():
         S.Kernel(2).EvaluateKernel(x)
 
 
+def test_rbf_kernel_composes_like_a_set_kernel():
+    """A GaussianRBFKernel sets its closed form as the kernel function (the
+    reference's constructor calls UpdateKernel, GaussianRBFKernel.hpp:75-87),
+    so rbf (+ - * /) k composes and runs on the generic host path."""
+    X = np.random.default_rng(0).uniform(-1, 1, (2, 5))
+    rbf = S.GaussianRBFKernel(X, S.GaussianRBFKernel.ScaleMethod.Constant)
+    M = np.array([[0.5, 0.1], [0.1, 0.8]])
+    rbf.UpdateParameters([M])
+    b = S.Kernel(2)
+    b.UpdateKernel(lambda x, p, loc: 1.0 + p[0][0, 0] * np.sum((x - loc) ** 2),
+                   lambda x, p, loc: 2.0 * p[0][0, 0] * (x - loc))
+    b.UpdateParameters([np.array([[0.7]])])
+    loc, x = np.array([0.2, -0.4]), np.array([0.5, 0.3])
+    d = x - loc
+    kr = float(np.exp(-d @ M @ d))
+    rbf.UpdateLocation(loc)
+    b.UpdateLocation(loc)
+    assert rbf.EvaluateKernel(x) == pytest.approx(kr, rel=1e-15)
+    kb = b.EvaluateKernel(x)
+    for k, want in ((rbf + b, kr + kb), (rbf - b, kr - kb), (rbf * b, kr * kb), (rbf / b, kr / kb)):
+        assert type(k) is S.Kernel and len(k.GetParameters()) == 2
+        k.UpdateLocation(loc)
+        assert k.EvaluateKernel(x) == pytest.approx(want, rel=1e-15)
+        g = k.EvaluateKernelGrad(x)
+        for c in range(2):
+            e = np.zeros(2)
+            e[c] = 1e-6
+            assert abs(g[c] - (k.EvaluateKernel(x + e) - k.EvaluateKernel(x - e)) / 2e-6) < 1e-8
+    # an isotropic scale set later is what the composition sees
+    rbf.UpdateParameters([np.array(0.3)])
+    k = rbf + b
+    k.UpdateLocation(loc)
+    assert k.EvaluateKernel(x) == pytest.approx(np.exp(-0.3 * d @ d) + kb, rel=1e-15)
+
+
+def test_gaussian_sum_subclass_gradient_override_is_honoured():
+    """A GaussianSum subclass that overrides its gradient never reaches the C
+    model's gradient (svgd_step_host_model / the device mirror)."""
+    from svgdcpp_amd.api import _builtin_grad, _builtin_hess
+
+    class Tempered(S.MultivariateNormal):
+        def log_model_grad(self, X, out=None):
+            return 0.5 * super().log_model_grad(X)
+
+    class Plain(S.MultivariateNormal):
+        pass
+
+    mvn = S.MultivariateNormal(np.zeros(2), np.eye(2))
+    assert _builtin_grad(mvn) and _builtin_hess(mvn)
+    assert _builtin_grad(Plain(np.zeros(2), np.eye(2)))
+    assert not _builtin_grad(Tempered(np.zeros(2), np.eye(2)))
+    with pytest.raises(TypeError):
+        ctx = object.__new__(S.Context)  # set_device_model rejects it before any C call
+        S.Context.set_device_model(ctx, Tempered(np.zeros(2), np.eye(2)))
+
+
 @pytest.mark.gpu
 def test_device_log_matches_oracle(oracle, golden_dir, tmp_path):
     """The device path's log (median-scaled RBF, MVN) vs the oracle at the
