@@ -164,6 +164,7 @@ struct svgd_ctx {
     unsigned long long *nmax = nullptr; // max |xc|^2 (double bits)
     int S = 1;
     int R = 2; // rows per lane of k_phi_rows
+    int phi_kind = 0; // 0 k_phi_rows (LDS columns), 1 k_phi_rows_s (scalar columns)
     int64_t ldp = 0;
 
     // median
@@ -1020,7 +1021,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
                                   mat ? c->sc_sgn : nullptr, mat ? nullptr : c->nmax, c->phi, opt,
-                                  c->stream, k1));
+                                  c->stream, k1, mat ? 0 : c->phi_kind));
     else if (phis)
         HIPCHK(c, launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
                                   c->row0, c->nrows, ntl, c->dim, 1.0 / (double)c->n,
@@ -1264,7 +1265,15 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
             const int r = std::atoi(e);
             if (r == 1 || r == 2 || r == 4) c->R = r;
         }
-        const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim, c->R) * ncu;
+        // A/B knob: the scalar-column variant of the phi row stream (R rows per lane)
+        if (const char *e = std::getenv("SVGD_PHI_SMEM")) {
+            const int r = std::atoi(e);
+            if (phi_rows_s_supported(dim, r)) {
+                c->phi_kind = 1;
+                c->R = r;
+            }
+        }
+        const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim, c->R, c->phi_kind) * ncu;
         const int64_t iblocks = std::max<int64_t>(1, (c->nrows + 256 * c->R - 1) / (256 * c->R));
         int64_t S = std::max<int64_t>(1, (resident + iblocks - 1) / iblocks);
         // 2 blocks per resident slot: one block wave per slot left a tail of

@@ -160,12 +160,14 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
                            double *rec, hipStream_t stream);
 // opt (optional): the optimizer step applied to each phi element as the
 // reduce writes it (the step path: one launch fewer than launch_opt_update).
-// ev_mid (optional): recorded between k_phi_rows and its reduce (diagnostics)
+// ev_mid (optional): recorded between k_phi_rows and its reduce (diagnostics).
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
-                           hipStream_t stream, hipEvent_t ev_mid = nullptr);
+                           hipStream_t stream, hipEvent_t ev_mid = nullptr, int kind = 0);
+// kind 1: the scalar-column variant k_phi_rows_s (phi_rows_s_supported)
+bool phi_rows_s_supported(int d, int R);
 // full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,
 // or an eigendecomposition when M is indefinite and d <= ROWS_MAX_D);
 // err = 0 positive definite, 2 indefinite, 1 non-finite / no convergence.
@@ -211,7 +213,7 @@ hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, co
                            const float *crow, const double *a_ptr, int64_t row0, int64_t nrows,
                            int64_t ntiles, int d, double inv_n, const double *wv, const double *xc,
                            int xc_stride, double *phi, const OptArgs *opt, hipStream_t stream);
-int phi_rows_blocks_per_cu(int d, int R);
+int phi_rows_blocks_per_cu(int d, int R, int kind = 0);
 // G = grad log p of the Gaussian-sum model for `rows` particle rows (d <= 64)
 hipError_t launch_gauss_grad(const double *X, int64_t rows, int d, int k, const double *mu,
                              const double *prec, double *G, hipStream_t stream);
