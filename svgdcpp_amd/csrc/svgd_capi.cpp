@@ -165,6 +165,12 @@ struct svgd_ctx {
     int S = 1;
     int R = 2; // rows per lane of k_phi_rows
     int phi_kind = 0; // 0 k_phi_rows (LDS columns), 1 k_phi_rows_s (scalar columns)
+    // symmetric phi pass (k_phi_sym, one rank, d <= 8): geometry and buffers
+    bool sym = false;
+    int symB = 0, symSRS = 0, symNSUB = 0, sym_grid = 0, sym_rslots = 0;
+    int64_t sym_nb = 0, sym_units = 0;
+    double *srec = nullptr, *rowpart = nullptr, *colpart = nullptr;
+    int *symok = nullptr;
     int64_t ldp = 0;
 
     // median
@@ -1014,10 +1020,24 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         HIPCHK(c, launch_cvt_f32(c->cvec, c->np, c->cvf, c->stream));
         if (mat) HIPCHK(c, launch_cvt_f32(c->zc, c->np * c->KP, c->zcf, c->stream));
     }
-    // level 2: the phi kernel alone (k_phi_rows before its reduce, or the tile kernel)
-    hipEvent_t k0 = diag_begin(c, c->stream), k1 = nullptr;
-    if (k0) k1 = take_ev(c);
-    if (c->rowpath)
+    // level 2: the phi kernel alone (k_phi_rows before its reduce, k_phi_sym,
+    // or the tile kernel)
+    const bool sym = c->sym && !mat;
+    hipEvent_t k0 = sym ? (c->tlevel >= 2 ? take_ev(c) : nullptr) : diag_begin(c, c->stream);
+    hipEvent_t k1 = k0 ? take_ev(c) : nullptr;
+    if (sym) {
+        c->mark = c->phi_end = nullptr;
+        SymArgs sa{c->dim,    c->xc,        c->KP,          c->G,        c->nrm,       c->scal,
+                   c->nmax,   c->n,         c->sym_nb,      c->sym_units, c->srec,     c->symok,
+                   c->rowpart, c->sym_rslots, c->colpart,   c->sym_grid, c->row0,      c->nrows,
+                   1.0 / (double)c->n, c->phi};
+        HIPCHK(c, launch_phi_sym(sa, opt, k0, k1, c->stream));
+        // the row stream takes the step instead when the records' flag says
+        // the symmetric form would leave its range (symok = 0)
+        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
+                                  c->ldp, 1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, opt,
+                                  c->stream, nullptr, c->phi_kind, c->symok));
+    } else if (c->rowpath)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
                                   mat ? c->sc_sgn : nullptr, mat ? nullptr : c->nmax, c->phi, opt,
@@ -1039,6 +1059,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         if (!c->rowpath) HIPCHK(c, hipEventRecord(k1, c->stream));
         c->ev_diag.push_back({k0, k1, DG_PHI_KERNEL, true});
     }
+    if (sym) c->mark = c->phi_end = nullptr;
     if (c->timing) {
         HIPCHK(c, hipEventRecord(ev.b, c->stream));
         c->ev_phi.push_back(ev);
@@ -1290,6 +1311,36 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
         CHK(dalloc(c, &c->nmax, 1));
         CHK(dalloc(c, &c->part, (int64_t)c->S * c->ldp * (dim + 1)));
+        // symmetric phi pass: one rank (a pair feeds two particles, which
+        // ranks would have to exchange), isotropic scales, d <= 8
+        bool want_sym = c->world == 1 && phi_sym_supported(dim);
+        if (const char *e = std::getenv("SVGD_PHI_SYM")) want_sym = want_sym && std::atoi(e) != 0;
+        else want_sym = false; // (opt-in until measured)
+        if (want_sym && phi_sym_geom(dim, &c->symB, &c->symSRS, &c->symNSUB)) {
+            const int64_t B = c->symB;
+            c->sym_nb = (n + B - 1) / B;
+            const int64_t T = c->sym_nb * (c->sym_nb + 1) / 2;
+            c->sym_units = T * c->symNSUB;
+            const int64_t slots = (int64_t)phi_sym_blocks_per_cu(dim) * ncu;
+            c->sym_grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->sym_units, slots));
+            // row blocks a work-group visits (its unit range is contiguous in
+            // the plan's row-major tile order)
+            int rs = 1;
+            for (int64_t g = 0; g < c->sym_grid; ++g) {
+                const int64_t u0 = c->sym_units * g / c->sym_grid, u1 = c->sym_units * (g + 1) / c->sym_grid;
+                if (u1 <= u0) continue;
+                int64_t I0, J0, I1, J1;
+                svgd_plan_pair_tile(n, (int)B, 1, 0, u0 / c->symNSUB, &I0, &J0);
+                svgd_plan_pair_tile(n, (int)B, 1, 0, (u1 - 1) / c->symNSUB, &I1, &J1);
+                rs = std::max<int>(rs, (int)(I1 - I0 + 1));
+            }
+            c->sym_rslots = rs;
+            CHK(dalloc(c, &c->srec, c->sym_nb * B * c->symSRS));
+            CHK(dalloc(c, &c->rowpart, (int64_t)c->sym_grid * rs * B * (dim + 1)));
+            CHK(dalloc(c, &c->colpart, T * B * (dim + 1)));
+            CHK(dalloc(c, &c->symok, 1));
+            c->sym = true;
+        }
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
@@ -1419,7 +1470,7 @@ int svgd_destroy(svgd_ctx *c)
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
-                       c->sc_sgn,  c->sc_work, c->bak};
+                       c->sc_sgn,  c->sc_work, c->bak, c->srec, c->rowpart, c->colpart};
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf, c->XS, c->VS};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
@@ -1427,7 +1478,7 @@ int svgd_destroy(svgd_ctx *c)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
                      c->xf,          c->nmax,    c->sc_err, c->cbuf, c->ccount, c->d_status,
-                     c->bpart,       c->gseg};
+                     c->bpart,       c->gseg, c->symok};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err, c->h_status};

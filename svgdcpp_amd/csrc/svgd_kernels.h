@@ -165,7 +165,38 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
-                           hipStream_t stream, hipEvent_t ev_mid = nullptr, int kind = 0);
+                           hipStream_t stream, hipEvent_t ev_mid = nullptr, int kind = 0,
+                           const int *skip = nullptr);
+// skip (optional): the row stream and its reduce do nothing while *skip != 0
+// (the symmetric pass below took the step)
+
+// Symmetric phi pass (d <= 8, one rank): each unordered pair's kernel value
+// feeds both particles (k_phi_sym), then k_sym_finish sums the partials in a
+// fixed order, forms phi and applies the optimizer.  Runs only while *symok
+// (set by its record prep: a log2e max|xc|^2 <= 300); otherwise the row
+// stream, launched after it with skip = symok, takes the step.
+struct SymArgs {
+    int d;
+    const double *xc;
+    int KP;
+    const double *G, *nrm, *a_ptr;
+    const unsigned long long *nmax;
+    int64_t n, nbs, units; // particles, blocks of B, (tile, sub-tile) units
+    double *srec;          // nbs * B records of SRS doubles
+    int *symok;
+    double *rowpart;       // grid x rslots x B x (d+1)
+    int rslots;
+    double *colpart;       // tiles x B x (d+1)
+    int grid;
+    int64_t row0, nrows;
+    double inv_n;
+    double *phi;
+};
+bool phi_sym_supported(int d);
+bool phi_sym_geom(int d, int *B, int *SRS, int *NSUB);
+int phi_sym_blocks_per_cu(int d);
+hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0, hipEvent_t ev_k1,
+                          hipStream_t stream);
 // kind 1: the scalar-column variant k_phi_rows_s (phi_rows_s_supported)
 bool phi_rows_s_supported(int d, int R);
 // full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,

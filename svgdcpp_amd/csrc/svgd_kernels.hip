@@ -1834,10 +1834,12 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
                                                  int64_t nrows, int64_t n, int S,
                                                  double *__restrict__ part, int64_t ldp,
                                                  const double *__restrict__ sgn,
-                                                 const unsigned long long *__restrict__ nmax_bits)
+                                                 const unsigned long long *__restrict__ nmax_bits,
+                                                 const int *__restrict__ skip)
 {
     constexpr int RS = RecLayout<D>::RS;
     constexpr int CHB = CH_PHI * RS * 8; // bytes per column chunk (multiple of 1 KiB)
+    if (skip && *skip) return; // the symmetric pass took this step
     // register double buffer of the column record only where it fits without
     // spilling (row state R(2D+2) + two records 2(2D+1) doubles)
     constexpr bool PIPE = (R * (2 * D + 2) + 2 * (2 * D + 1)) * 2 <= 232;
@@ -1986,6 +1988,376 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     }
 }
 
+// ==================================================== symmetric phi pass ==
+//
+// K_ij = K_ji: each unordered pair's kernel value feeds both particles.  With
+// w_j = 2^(c_j/4096) = exp(-a |xc_j|^2) and E_ij = 2^(u_ij/4096),
+// u_ij = 8192 a log2e xc_i.xc_j (= E_ji), K_ij = w_i w_j E_ij, so
+//   S_i = sum_j E_ij W_j,   W_j = w_j [V_j, 1]   (V_j = G_j - 2a xc_j)
+//   phi_i = (1/N) w_i (S_i[0..d) + 2a xc_i S_i[d])        (SVGD.hpp:453)
+// and the pair (i, j) adds E_ij W_j to S_i and E_ij W_i to S_j: per
+// unordered pair one Gram (d FMA), one exp and 2(d+1) FMA -- instead of twice
+// the Gram and the exp.  Valid while y = a log2e max|xc|^2 <= 300 (the row
+// stream's fold condition): then |u| <= 600 x 4096 and w >= 2^-300, far from
+// overflow; otherwise (flag symok = 0) the row stream runs instead.
+//
+// Work: the row-stream median's block-pair plan (tile_coords) over blocks of
+// B = 256 R particles, each tile cut into B / 64 sub-tiles of 64 columns; a
+// work-group takes a contiguous range of (tile, sub-tile) units, holds the
+// tile's B rows in registers (R per lane, 4 waves) and streams the sub-tiles
+// through two LDS buffers (global_load_lds DMA).  Inside a sub-tile each
+// 16-lane group walks a 16-column set in 16 steps on a skewed schedule --
+// lane t meets column (t + s) mod 16 at step s, reading that record from LDS
+// (a conflict-free 16-lane pattern) -- and the column accumulators rotate one
+// lane per step (DPP row_ror:15), so BOTH sums stay in registers; after the
+// 16 steps lane t holds its column's sum over the group's rows.  4 phases
+// give every group every set.  Diagonal tiles take the ordered form (row
+// sums only).  Row sums go to rowpart when the work-group's row block
+// changes; a sub-tile's column sums (4 waves added in fixed order) to
+// colpart.  k_sym_finish adds every partial of a particle in a fixed order
+// (deterministic), forms phi and applies the optimizer (opt_elem).
+constexpr int SYM_SUB = 64; // columns per sub-tile (4 sets of 16)
+template <int D> struct SymGeom {
+    // rows per lane: as many as fit 256 VGPRs (2 waves/SIMD) without spilling
+    static constexpr int R = D == 1 ? 8 : D == 2 ? 6 : D == 3 ? 5 : D == 4 ? 4 : D <= 6 ? 3 : 2;
+    static constexpr int B = 4 * 64 * R;                 // block: a work-group's rows
+    static constexpr int NSUB = B / SYM_SUB;
+    static constexpr int DP = D + 1;
+    // record [xc (D) | W (D+1) | pad], stride 2H doubles, H odd: the 16
+    // per-lane 16-byte reads of a set hit 16 distinct 4-bank groups
+    static constexpr int H = (DP % 2 == 1) ? DP : DP + 1;
+    static constexpr int SRS = 2 * H;
+    static constexpr int SUBB = SYM_SUB * SRS * 8; // bytes per sub-tile (whole KiB)
+};
+
+__device__ __forceinline__ int64_t sym_cnt(int64_t nb, int64_t I)
+{
+    const int64_t H = (nb - 1) / 2;
+    return ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
+}
+__device__ __forceinline__ int64_t sym_base(int64_t nb, int64_t I)
+{
+    const int64_t H = (nb - 1) / 2;
+    if ((nb & 1) == 0) {
+        const int64_t half = nb / 2;
+        return I < half ? I * (H + 2) : half * (H + 2) + (I - half) * (H + 1);
+    }
+    return I * (H + 1);
+}
+
+__device__ __forceinline__ double dpp_ror15(double v)
+{
+    // lane t <- lane t + 1 (mod 16) within each row of 16 lanes; old = src
+    // (every lane has a source in a full-row rotation)
+    const int l = __double2loint(v), h = __double2hiint(v);
+    const int lo = __builtin_amdgcn_update_dpp(l, l, 0x12F, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(h, h, 0x12F, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// vmcnt wait with a wave-uniform count (0..3)
+__device__ __forceinline__ void wait_vmcnt_upto3(int n)
+{
+    if (n >= 3) wait_vmcnt<3>();
+    else if (n == 2) wait_vmcnt<2>();
+    else if (n == 1) wait_vmcnt<1>();
+    else wait_vmcnt<0>();
+}
+
+// Barrier that drains only LDS operations (a __syncthreads() would also wait
+// for the next sub-tile's in-flight DMA).
+__device__ __forceinline__ void sym_lds_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// records: srec_j = [xc_j | w_j (G_j - 2a xc_j) | w_j | 0..] (zero past n),
+// w_j = exp(-a |xc_j|^2); symok = (a log2e max|xc|^2 <= 300)
+template <int D>
+__global__ void k_prep_sym(const double *__restrict__ xc, int KP, const double *__restrict__ G,
+                           const double *__restrict__ nrm, const double *__restrict__ a_ptr,
+                           const unsigned long long *__restrict__ nmax_bits, int64_t n, int64_t npad,
+                           double *__restrict__ srec, int *__restrict__ symok)
+{
+    using Gm = SymGeom<D>;
+    const double a = *a_ptr;
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        *symok = LOG2E * a * __longlong_as_double((long long)*nmax_bits) <= 300.0 ? 1 : 0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < npad;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        double *o = srec + j * Gm::SRS;
+        if (j < n) {
+            const double w = exp2(-a * LOG2E * nrm[j]);
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const double x = xc[j * KP + k];
+                o[k] = x;
+                o[D + k] = w * (G[j * D + k] - 2.0 * a * x);
+            }
+            o[2 * D] = w;
+        } else {
+#pragma unroll
+            for (int k = 0; k <= 2 * D; ++k) o[k] = 0.0;
+        }
+#pragma unroll
+        for (int k = 2 * D + 1; k < Gm::SRS; ++k) o[k] = 0.0;
+    }
+}
+
+template <int D, int R, bool SYMM>
+__device__ __forceinline__ void sym_step(const double *__restrict__ rj, const double (&xs)[R][D],
+                                         const double (&wi)[R][D + 1], double (&acc)[R][D + 1],
+                                         double (&cacc)[D + 1], const double *tab)
+{
+    // the column's coordinates first, its weights only once the Gram is done
+    // (sched_barrier: the two never hold registers at the same time)
+    double u[R], f[R], T[R], E[R];
+    int ki[R];
+    {
+        double xj[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) xj[k] = rj[k];
+#pragma unroll
+        for (int r = 0; r < R; ++r) u[r] = xs[r][0] * xj[0];
+#pragma unroll
+        for (int k = 1; k < D; ++k)
+#pragma unroll
+            for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], xj[k], u[r]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double wj[D + 1];
+#pragma unroll
+    for (int k = 0; k <= D; ++k) wj[k] = rj[D + k];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double kk = __builtin_rint(u[r]);
+        f[r] = u[r] - kk;
+        ki[r] = (int)kk;
+        T[r] = tab[ki[r] & (EXP_TB - 1)];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) E[r] = exp2_4096_poly(f[r]) * tab_scale(T[r], ki[r]);
+#pragma unroll
+    for (int k = 0; k <= D; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][k] = fma(E[r], wj[k], acc[r][k]);
+    if constexpr (SYMM) {
+#pragma unroll
+        for (int k = 0; k <= D; ++k)
+#pragma unroll
+            for (int r = 0; r < R; ++r) cacc[k] = fma(E[r], wi[r][k], cacc[k]);
+#pragma unroll
+        for (int k = 0; k <= D; ++k) cacc[k] = dpp_ror15(cacc[k]);
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_phi_sym(const double *__restrict__ srec,
+                                                 const double *__restrict__ a_ptr, int64_t nb,
+                                                 int64_t U, const int *__restrict__ symok,
+                                                 double *__restrict__ rowpart, int rslots,
+                                                 double *__restrict__ colpart)
+{
+    using Gm = SymGeom<D>;
+    constexpr int R = Gm::R, B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP,
+                  SUBB = Gm::SUBB, NP = SUBB / 1024;
+    __shared__ __attribute__((aligned(16))) char smem[2 * SUBB + 4 * SYM_SUB * DP * 8 + EXP_TB * 8];
+    if (!*symok) return; // uniform: the row stream runs instead
+    double *sCol = reinterpret_cast<double *>(smem + 2 * SUBB);
+    double *tab = sCol + 4 * SYM_SUB * DP;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = lane >> 4, tl = lane & 15;
+#pragma unroll
+    for (int e = 0; e < EXP_TB / 256; ++e)
+        tab[e * 256 + tid] = tab_biased(EXP2_TAB4096[e * 256 + tid], e * 256 + tid);
+    for (int e = tid; e < 4 * SYM_SUB * DP; e += 256) sCol[e] = 0.0;
+    __syncthreads();
+
+    const double alpha = 8192.0 * LOG2E * (*a_ptr);
+    const int64_t Gn = gridDim.x;
+    const int64_t u0 = U * (int64_t)blockIdx.x / Gn, u1 = U * ((int64_t)blockIdx.x + 1) / Gn;
+    const int npw = (NP - w + 3) / 4; // this wave's DMA pieces per sub-tile
+    // (tile, sub-tile) cursor: the plan's tile t = (I, J), J = I + slot mod nb
+    // (plan.cpp); advanced incrementally (no 64-bit divisions per sub-tile)
+    struct Cur {
+        int64_t t, I, J, slot, cnt;
+        int q;
+    };
+    auto cur_at = [&](int64_t u) {
+        Cur c;
+        c.t = u / NSUB;
+        c.q = (int)(u - c.t * NSUB);
+        tile_coords(nb, c.t, &c.I, &c.J);
+        c.slot = c.J >= c.I ? c.J - c.I : c.J + nb - c.I;
+        c.cnt = sym_cnt(nb, c.I);
+        return c;
+    };
+    auto cur_next = [&](Cur &c) {
+        if (++c.q < NSUB) return;
+        c.q = 0;
+        ++c.t;
+        if (++c.slot == c.cnt) {
+            ++c.I;
+            c.slot = 0;
+            c.cnt = sym_cnt(nb, c.I);
+        }
+        c.J = c.I + c.slot >= nb ? c.I + c.slot - nb : c.I + c.slot;
+    };
+    auto issue = [&](const Cur &c, int buf) {
+        const char *src =
+            reinterpret_cast<const char *>(srec + (c.J * B + (int64_t)c.q * SYM_SUB) * SRS);
+        char *dst = smem + buf * SUBB;
+        for (int p = w; p < NP; p += 4)
+            __builtin_amdgcn_global_load_lds((gbl_void *)(src + p * 1024 + lane * 16),
+                                             (lds_void *)(dst + p * 1024), 16, 0, 0);
+    };
+
+    double xs[R][D], wi[R][DP], acc[R][DP];
+    int64_t curI = -1, firstI = 0;
+    auto flush_rows = [&]() {
+        const int slot = (int)(curI - firstI);
+        double *o = rowpart + ((int64_t)blockIdx.x * rslots + slot) * B * DP;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int lr = w * 64 * R + r * 64 + lane;
+#pragma unroll
+            for (int k = 0; k < DP; ++k) o[lr * DP + k] = acc[r][k];
+        }
+    };
+
+    if (u0 >= u1) return;
+    Cur cu = cur_at(u0), cn = cu;
+    issue(cu, 0);
+    for (int64_t u = u0; u < u1; ++u) {
+        const int buf = (int)((u - u0) & 1);
+        if (u + 1 < u1) {
+            cur_next(cn);
+            issue(cn, buf ^ 1);
+            wait_vmcnt_upto3(npw); // this wave's pieces of sub-tile u have landed
+        } else {
+            wait_vmcnt<0>();
+        }
+        sym_lds_barrier(); // every wave's pieces of sub-tile u are in LDS
+        const int64_t t = cu.t, I = cu.I, J = cu.J;
+        const int q = cu.q;
+        cur_next(cu);
+        if (I != curI) {
+            if (curI >= 0) flush_rows();
+            else firstI = I;
+            curI = I;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double *ri = srec + (I * B + w * 64 * R + r * 64 + lane) * SRS;
+#pragma unroll
+                for (int k = 0; k < D; ++k) xs[r][k] = alpha * ri[k];
+#pragma unroll
+                for (int k = 0; k < DP; ++k) {
+                    wi[r][k] = ri[D + k];
+                    acc[r][k] = 0.0;
+                }
+            }
+            wait_vmcnt<0>(); // (rare: once per row block) also drains the next sub-tile's DMA
+        }
+        const double *cb = reinterpret_cast<const double *>(smem + buf * SUBB);
+        auto phases = [&](auto symm_tag) {
+            constexpr bool SYMM = decltype(symm_tag)::value;
+#pragma unroll 1
+            for (int ph = 0; ph < 4; ++ph) {
+                const int set = (grp + ph) & 3;
+                const double *cset = cb + set * 16 * SRS;
+                double cacc[DP];
+#pragma unroll
+                for (int k = 0; k < DP; ++k) cacc[k] = 0.0;
+#pragma unroll 1
+                for (int s = 0; s < 16; ++s)
+                    sym_step<D, R, SYMM>(cset + ((tl + s) & 15) * SRS, xs, wi, acc, cacc, tab);
+                if constexpr (SYMM) {
+                    // lane tl holds column set*16 + tl; the 4 phases of a set
+                    // come from different groups of this wave, in phase order
+                    double *sc = sCol + (w * SYM_SUB + set * 16 + tl) * DP;
+#pragma unroll
+                    for (int k = 0; k < DP; ++k) sc[k] += cacc[k];
+                }
+            }
+        };
+        if (I == J) phases(std::false_type{});
+        else phases(std::true_type{});
+        sym_lds_barrier(); // every wave is done with buffer buf and its column slots
+        if (I != J) {
+            double *o = colpart + (t * B + (int64_t)q * SYM_SUB) * DP;
+            for (int e = tid; e < SYM_SUB * DP; e += 256) {
+                double v = sCol[e];
+#pragma unroll
+                for (int ww = 1; ww < 4; ++ww) v += sCol[ww * SYM_SUB * DP + e];
+                o[e] = v;
+#pragma unroll
+                for (int ww = 0; ww < 4; ++ww) sCol[ww * SYM_SUB * DP + e] = 0.0;
+            }
+        }
+    }
+    if (curI >= 0) flush_rows();
+}
+
+// phi_p = (1/N) w_p (S_p[0..d) + 2a xc_p S_p[d]) for this rank's rows, S_p =
+// every row and column partial of p in a fixed order, then the optimizer.
+// A block owns 256 / (d+1) particles, one thread per (particle, component).
+template <int D>
+__global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ rowpart,
+                                                    const double *__restrict__ colpart, int rslots,
+                                                    const double *__restrict__ srec,
+                                                    const double *__restrict__ a_ptr, int64_t nb,
+                                                    int64_t U, int G, const int *__restrict__ symok,
+                                                    int64_t row0, int64_t nrows, double inv_n,
+                                                    double *__restrict__ phi, OptArgs opt, int do_opt)
+{
+    using Gm = SymGeom<D>;
+    constexpr int B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP, RB = 256 / DP;
+    if (!*symok) return;
+    __shared__ double sm[256];
+    const int64_t rb = (int64_t)blockIdx.x * RB;
+    const int rows = (int)min<int64_t>(RB, nrows - rb);
+    if (rows <= 0) return;
+    const int e = threadIdx.x;
+    if (e < rows * DP) {
+        const int pl_ = e / DP, k = e - pl_ * DP;
+        const int64_t p = row0 + rb + pl_;
+        const int64_t P = p / B, pl = p - P * B;
+        double acc = 0.0;
+        // row role: the work-groups whose unit range meets row block P's units
+        const int64_t ub = sym_base(nb, P) * NSUB, ue = ub + sym_cnt(nb, P) * NSUB;
+        int64_t g = ub * G / U;
+        while (g > 0 && U * g / G > ub) --g;
+        while (g + 1 < G && U * (g + 1) / G <= ub) ++g;
+        for (; g < G; ++g) {
+            const int64_t gu0 = U * g / G, gu1 = U * (g + 1) / G;
+            if (gu0 >= ue) break;
+            if (gu1 <= ub || gu0 >= gu1) continue;
+            int64_t I0, J0;
+            tile_coords(nb, gu0 / NSUB, &I0, &J0);
+            acc += rowpart[(((int64_t)g * rslots + (P - I0)) * B + pl) * DP + k];
+        }
+        // column role: tiles (I, P), slot s >= 1
+        for (int64_t sl = 1; sl <= (nb - 1) / 2 + 1; ++sl) {
+            const int64_t I = ((P - sl) % nb + nb) % nb;
+            if (I == P || sl >= sym_cnt(nb, I)) continue;
+            const int64_t t = sym_base(nb, I) + sl;
+            acc += colpart[(t * B + pl) * DP + k];
+        }
+        sm[e] = acc;
+    }
+    __syncthreads();
+    const double two_a = 2.0 * (*a_ptr);
+    for (int o = threadIdx.x; o < rows * D; o += blockDim.x) {
+        const int r = o / D, k = o - r * D;
+        const int64_t li = rb + r, p = row0 + li;
+        const double *rec = srec + p * SRS;
+        const double ph = inv_n * (rec[2 * D] * (sm[r * DP + k] + two_a * rec[k] * sm[r * DP + D]));
+        phi[li * D + k] = ph;
+        if (do_opt) opt_elem(opt, li * D + k, ph);
+    }
+}
+
 // ------------------------------------ phi row stream, scalar column loads --
 //
 // k_phi_rows with the column records read by the scalar unit (s_load into
@@ -2052,10 +2424,12 @@ __global__ __launch_bounds__(256) void k_phi_rows_s(const double *__restrict__ r
                                                    int64_t nrows, int64_t n, int S,
                                                    double *__restrict__ part, int64_t ldp,
                                                    const double *__restrict__ sgn,
-                                                   const unsigned long long *__restrict__ nmax_bits)
+                                                   const unsigned long long *__restrict__ nmax_bits,
+                                                   const int *__restrict__ skip)
 {
     constexpr int RS = RecLayout<D>::RS;
     __shared__ double tab[EXP_TB];
+    if (skip && *skip) return;
 #pragma unroll
     for (int e = 0; e < EXP_TB / 256; ++e)
         tab[e * 256 + threadIdx.x] = tab_biased(EXP2_TAB4096[e * 256 + threadIdx.x], e * 256 + threadIdx.x);
@@ -2292,8 +2666,10 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
                                                     const double *__restrict__ a_ptr, int64_t row0,
                                                     int64_t nrows, int d, int RS, int S, int64_t ldp,
                                                     double inv_n, const double *__restrict__ wv,
-                                                    double *__restrict__ phi, OptArgs opt, int do_opt)
+                                                    double *__restrict__ phi, OptArgs opt, int do_opt,
+                                                    const int *__restrict__ skip)
 {
+    if (skip && *skip) return;
     __shared__ double sm[256];
     const double two_a = 2.0 * (*a_ptr);
     const int DP = d + 1;
@@ -2897,13 +3273,13 @@ __global__ __launch_bounds__(256) void k_gauss_grad(const double *__restrict__ X
     case Dv:                                                                                 \
         if (kind == 0 && R == 1)                                                             \
             hipLaunchKernelGGL((k_phi_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);         \
         else if (kind == 0 && R == 2)                                                        \
             hipLaunchKernelGGL((k_phi_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);         \
         else if (kind == 0)                                                                  \
             hipLaunchKernelGGL((k_phi_rows<Dv, 4>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);         \
         else if (kind == 10)                                                                 \
             hipLaunchKernelGGL((k_pair_rows<Dv, 0>), dim3(grid), dim3(256), 0, stream, xc, KP, \
                                nrm, n, nb, t0, t1, sc, sh, sd);                              \
@@ -2920,7 +3296,8 @@ static hipError_t launch_rows_kernel(int kind, int D, int R, int grid, const dou
                                      int S, double *part, int64_t ldp, const double *sgn,
                                      const unsigned long long *nmax, const double *xc, int KP,
                                      const double *nrm, int64_t nb, int64_t t0, int64_t t1,
-                                     SinkCollect sc, SinkHist sh, SinkDebug sd, hipStream_t stream)
+                                     SinkCollect sc, SinkHist sh, SinkDebug sd, hipStream_t stream,
+                                     const int *skip = nullptr)
 {
     switch (D) {
         SVGD_ROWS_CASE(1)
@@ -2960,14 +3337,14 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
 static hipError_t launch_rows_s(int d, int R, int grid, const double *rec, const double *a_ptr,
                                 int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                                 int64_t ldp, const double *sgn, const unsigned long long *nmax,
-                                hipStream_t stream)
+                                hipStream_t stream, const int *skip)
 {
     if (d == 8 && R == 4)
         hipLaunchKernelGGL((k_phi_rows_s<8, 4>), dim3(grid), dim3(256), 0, stream, rec, a_ptr, row0,
-                           nrows, n, S, part, ldp, sgn, nmax);
+                           nrows, n, S, part, ldp, sgn, nmax, skip);
     else if (d == 8 && R == 5)
         hipLaunchKernelGGL((k_phi_rows_s<8, 5>), dim3(grid), dim3(256), 0, stream, rec, a_ptr, row0,
-                           nrows, n, S, part, ldp, sgn, nmax);
+                           nrows, n, S, part, ldp, sgn, nmax, skip);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -2979,7 +3356,7 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
-                           hipStream_t stream, hipEvent_t ev_mid, int kind)
+                           hipStream_t stream, hipEvent_t ev_mid, int kind, const int *skip)
 {
     if (nrows <= 0) {
         if (ev_mid) return hipEventRecord(ev_mid, stream);
@@ -2987,17 +3364,17 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
     }
     const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
     hipError_t e = kind == 1 ? launch_rows_s(d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
-                                             nmax_bits, stream)
+                                             nmax_bits, stream, skip)
                              : launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                       nmax_bits, nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
-                                      SinkDebug{}, stream);
+                                      SinkDebug{}, stream, skip);
     if (e != hipSuccess) return e;
     if (ev_mid && (e = hipEventRecord(ev_mid, stream)) != hipSuccess) return e;
     if (d > 16) return hipErrorInvalidValue; // k_phi_reduce's LDS holds d + 1 <= 17
     const int64_t g = (nrows + phi_red_rows(d) - 1) / phi_red_rows(d);
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
                        d, phi_rec_stride(d), S, ldp, inv_n, wv, phi, opt ? *opt : OptArgs{},
-                       opt ? 1 : 0);
+                       opt ? 1 : 0, skip);
     return hipGetLastError();
 }
 
@@ -3432,6 +3809,77 @@ hipError_t launch_finalize(const SelState *st, int navg, int src_lo, int src_hi,
 } // namespace svgd_amd
 
 namespace svgd_amd {
+
+bool phi_sym_supported(int d) { return d >= 1 && d <= 8; }
+
+#define SVGD_SYM_GEOM(Dv)                                                                    \
+    case Dv:                                                                                 \
+        *B = SymGeom<Dv>::B;                                                                 \
+        *SRS = SymGeom<Dv>::SRS;                                                             \
+        *NSUB = SymGeom<Dv>::NSUB;                                                           \
+        return true;
+bool phi_sym_geom(int d, int *B, int *SRS, int *NSUB)
+{
+    switch (d) {
+        SVGD_SYM_GEOM(1) SVGD_SYM_GEOM(2) SVGD_SYM_GEOM(3) SVGD_SYM_GEOM(4)
+        SVGD_SYM_GEOM(5) SVGD_SYM_GEOM(6) SVGD_SYM_GEOM(7) SVGD_SYM_GEOM(8)
+    default:
+        return false;
+    }
+}
+
+int phi_sym_blocks_per_cu(int d)
+{
+    int nb = 0;
+    hipError_t e = hipErrorInvalidValue;
+    switch (d) {
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<1>, 256, 0); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<2>, 256, 0); break;
+    case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<3>, 256, 0); break;
+    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<4>, 256, 0); break;
+    case 5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<5>, 256, 0); break;
+    case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<6>, 256, 0); break;
+    case 7: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<7>, 256, 0); break;
+    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<8>, 256, 0); break;
+    default: break;
+    }
+    return (e == hipSuccess && nb > 0) ? nb : 1;
+}
+
+#define SVGD_SYM_CASE(Dv)                                                                     \
+    case Dv: {                                                                                \
+        using Gm = SymGeom<Dv>;                                                               \
+        const int64_t npad = a.nbs * Gm::B;                                                   \
+        int64_t g = (npad + 255) / 256;                                                       \
+        if (g > 4096) g = 4096;                                                               \
+        hipLaunchKernelGGL((k_prep_sym<Dv>), dim3(g), dim3(256), 0, stream, a.xc, a.KP, a.G,   \
+                           a.nrm, a.a_ptr, a.nmax, a.n, npad, a.srec, a.symok);               \
+        if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
+        if (ev_k0 && (e = hipEventRecord(ev_k0, stream)) != hipSuccess) return e;             \
+        hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(256), 0, stream, a.srec, a.a_ptr, \
+                           a.nbs, a.units, a.symok, a.rowpart, a.rslots, a.colpart);          \
+        if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
+        if (ev_k1 && (e = hipEventRecord(ev_k1, stream)) != hipSuccess) return e;             \
+        constexpr int RB = 256 / Gm::DP;                                                      \
+        hipLaunchKernelGGL((k_sym_finish<Dv>), dim3((a.nrows + RB - 1) / RB), dim3(256), 0,    \
+                           stream, a.rowpart, a.colpart, a.rslots, a.srec, a.a_ptr, a.nbs,     \
+                           a.units, a.grid, a.symok, a.row0, a.nrows, a.inv_n, a.phi,          \
+                           opt ? *opt : OptArgs{}, opt ? 1 : 0);                              \
+        return hipGetLastError();                                                             \
+    }
+
+hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0, hipEvent_t ev_k1,
+                          hipStream_t stream)
+{
+    hipError_t e = hipSuccess;
+    if (a.nrows <= 0) return hipSuccess;
+    switch (a.d) {
+        SVGD_SYM_CASE(1) SVGD_SYM_CASE(2) SVGD_SYM_CASE(3) SVGD_SYM_CASE(4)
+        SVGD_SYM_CASE(5) SVGD_SYM_CASE(6) SVGD_SYM_CASE(7) SVGD_SYM_CASE(8)
+    default:
+        return hipErrorInvalidValue;
+    }
+}
 
 #define SVGD_OCC_CASE(Dv)                                                                    \
     case Dv:                                                                                 \
