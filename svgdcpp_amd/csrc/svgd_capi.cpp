@@ -714,7 +714,8 @@ int collect_counts(svgd_ctx *c)
     else
         HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
-                                   c->collect_grid, c->cnt3, c->stream));
+                                   c->collect_grid, c->cnt3, c->stream,
+                                   c->spec_step ? c->gseg + (size_t)c->rank * (CAPR + 1) : nullptr));
     CHK(allreduce_cnt3(c));
     // speculative: the device plan and the selection are queued right behind
     // the counts (while the device still runs the collect pass), not when the
@@ -734,12 +735,11 @@ int median_finish_spec(svgd_ctx *c, double logn)
     // the plan also stores its status straight into pinned host memory: no
     // copy on the copy stream (a small copy there turned the X shard copies
     // into blit kernels competing with the median kernels)
-    HIPCHK(c, launch_plan_select(c->cnt3, c->st, c->nsel, (uint64_t)c->sel_rank[0],
-                                 (uint64_t)c->sel_rank[c->nsel - 1],
-                                 std::min<int64_t>(c->bucket_cap, CAPR), seg, c->d_status,
-                                 c->h_status_dev, c->stream));
+    // (the compaction's blocks derive the bucket plan themselves: no plan launch)
+    const PlanArgs pa{c->cnt3, c->nsel, (uint64_t)c->sel_rank[0], (uint64_t)c->sel_rank[c->nsel - 1],
+                      std::min<int64_t>(c->bucket_cap, CAPR), c->d_status, c->h_status_dev};
     HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
-                                     c->d_status, c->stream));
+                                     c->d_status, c->stream, &pa));
     CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
     HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, CAPR, c->navg, c->src_lo, c->src_hi, logn,
                                   c->scal, c->d_status, c->stream));

@@ -114,7 +114,9 @@ constexpr int CNT_LO = 3 + NBK, CNT_HI = 4 + NBK, CNT_LEN = 5 + NBK;
 hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
                                 int64_t nblk, int64_t cap, const SelState *st,
                                 const uint32_t *bpart, int64_t nbpart,
-                                unsigned long long *cnt, hipStream_t stream);
+                                unsigned long long *cnt, hipStream_t stream,
+                                uint64_t *seg_zero = nullptr);
+// (seg_zero, optional: zeroed -- the speculative compaction's counter)
 // device state from kernel arguments (no host staging buffer)
 hipError_t launch_set_state(const SelState &s, SelState *st, hipStream_t stream);
 hipError_t launch_set_scal(double a, double med, double *scal, hipStream_t stream);
@@ -123,10 +125,21 @@ hipError_t launch_set_scal(double a, double med, double *scal, hipStream_t strea
 hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int b0, int b1,
                           uint64_t *seg, hipStream_t stream);
 // keys of the selected buckets st->bsel[] -> seg = [count, keys (<= seg_cap)]
-// (seg[0] must be zero on entry)
+// (seg[0] must be zero on entry).  plan (optional, the speculative step):
+// every block derives the bucket plan from the all-reduced counts itself
+// (as launch_plan_select would) and block 0 publishes it (select state,
+// *status, *host_status) -- one launch fewer per step.
+struct PlanArgs {
+    const unsigned long long *cnt; // nullptr: the plan is already in st
+    int nsel;
+    uint64_t r0, r1;
+    int64_t capr;
+    int *status, *host_status;
+};
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                                  int64_t cap, const SelState *st, uint64_t *seg, int64_t seg_cap,
-                                  const int *status, hipStream_t stream);
+                                  int64_t cap, SelState *st, uint64_t *seg, int64_t seg_cap,
+                                  const int *status, hipStream_t stream,
+                                  const PlanArgs *plan = nullptr);
 // exact selection of st->rank[s] within bucket st->bsel[s] over nseg gathered
 // segments [count, keys...] of stride seg_cap + 1 -> st->prefix[s] = that key,
 // then the scale as launch_finalize

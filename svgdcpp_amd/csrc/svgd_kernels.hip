@@ -1023,27 +1023,26 @@ __global__ __launch_bounds__(1024) void k_select_tail(SelState *st, const uint64
 // on its synchronous path.
 // The status also goes to host_status (pinned host memory, read after the
 // launch's completion event).
-__global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *__restrict__ cnt,
-                                                    SelState *st, int nsel, uint64_t r0,
-                                                    uint64_t r1, int64_t capr, uint64_t *seg,
-                                                    int *status_arg, int *host_status)
+// The bucket plan of the speculative step, computed by one 256-thread block
+// from the all-reduced counts: the buckets holding the order statistics and
+// their ranks inside them, or status 1 (bracket miss), 2 (overflowed region),
+// 3 (selected buckets above capr).  Block-uniform results.
+struct PlanOut {
+    int status, b0, b1, ns;
+    unsigned long long in0, in1;
+};
+__device__ PlanOut plan_block(const unsigned long long *__restrict__ cnt, int nsel, uint64_t r0,
+                              uint64_t r1, int64_t capr)
 {
-    struct Status {
-        int *d, *h;
-        __device__ void operator=(int v) const
-        {
-            *d = v;
-            if (h) *h = v;
-        }
-    } status{status_arg, host_status};
     __shared__ unsigned long long sPart[256];
     __shared__ int sB[2];
     __shared__ unsigned long long sIn[2];
     const int tid = threadIdx.x;
+    PlanOut o{0, -1, -1, 1, 0, 0};
     const unsigned long long below = cnt[0], cand = cnt[1], ovf = cnt[2];
     if (ovf || r0 < below || r1 >= below + cand) {
-        if (tid == 0) status = ovf ? 2 : 1;
-        return;
+        o.status = ovf ? 2 : 1;
+        return o;
     }
     const unsigned long long q[2] = {r0 - below, r1 - below};
     const int ns = (nsel > 1 && q[1] != q[0]) ? 2 : 1;
@@ -1053,8 +1052,8 @@ __global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *_
     sPart[tid] = loc;
     if (tid < 2) sB[tid] = -1;
     __syncthreads();
-    for (int o = 1; o < 256; o <<= 1) {
-        const unsigned long long v = tid >= o ? sPart[tid - o] : 0ull;
+    for (int off = 1; off < 256; off <<= 1) {
+        const unsigned long long v = tid >= off ? sPart[tid - off] : 0ull;
         __syncthreads();
         sPart[tid] += v;
         __syncthreads();
@@ -1074,26 +1073,46 @@ __global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *_
             }
         }
     __syncthreads();
-    if (tid != 0) return;
     if (sB[0] < 0 || (ns > 1 && sB[1] < 0)) {
-        status = 1;
-        return;
+        o.status = 1;
+        return o;
     }
-    const int b0 = sB[0], b1 = ns > 1 ? sB[1] : sB[0];
-    const unsigned long long tot = cnt[3 + b0] + (b1 != b0 ? cnt[3 + b1] : 0ull);
-    if (tot > (unsigned long long)capr) {
-        status = 3;
-        return;
+    o.ns = ns;
+    o.b0 = sB[0];
+    o.b1 = ns > 1 ? sB[1] : sB[0];
+    o.in0 = sIn[0];
+    o.in1 = ns > 1 ? sIn[1] : sIn[0];
+    const unsigned long long tot = cnt[3 + o.b0] + (o.b1 != o.b0 ? cnt[3 + o.b1] : 0ull);
+    if (tot > (unsigned long long)capr) o.status = 3;
+    return o;
+}
+
+// The plan's select state and status (one thread); seg[0] (this rank's
+// compaction counter) is zeroed by k_counts_reduce.
+__device__ void plan_publish(const PlanOut &o, SelState *st, int nsel, int *status_d, int *status_h)
+{
+    if (o.status == 0) {
+        st->nsel = nsel;
+        st->rank[0] = o.in0;
+        st->rank[1] = nsel > 1 ? o.in1 : o.in0;
+        st->bsel[0] = o.b0;
+        st->bsel[1] = o.b1;
+        st->prefix[0] = st->prefix[1] = 0;
+        st->error = 0;
     }
-    st->nsel = nsel;
-    st->rank[0] = sIn[0];
-    st->rank[1] = nsel > 1 ? sIn[ns - 1] : sIn[0];
-    st->bsel[0] = b0;
-    st->bsel[1] = b1;
-    st->prefix[0] = st->prefix[1] = 0;
-    st->error = 0;
-    seg[0] = 0; // compaction counter of this rank's segment
-    status = 0;
+    *status_d = o.status;
+    if (status_h) *status_h = o.status;
+}
+
+__global__ __launch_bounds__(256) void k_plan_select(const unsigned long long *__restrict__ cnt,
+                                                    SelState *st, int nsel, uint64_t r0,
+                                                    uint64_t r1, int64_t capr, uint64_t *seg,
+                                                    int *status_arg, int *host_status)
+{
+    const PlanOut o = plan_block(cnt, nsel, r0, r1, capr);
+    if (threadIdx.x != 0) return;
+    if (o.status == 0) seg[0] = 0;
+    plan_publish(o, st, nsel, status_arg, host_status);
 }
 
 // Whole select state / scale from kernel arguments (captured at launch, so the
@@ -1127,15 +1146,29 @@ constexpr int CB_LDS = 4096; // keys buffered per block between flushes
 __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restrict__ keys,
                                                         const uint32_t *__restrict__ counts,
                                                         int64_t nreg, int64_t cap,
-                                                        const SelState *__restrict__ st,
+                                                        SelState *__restrict__ st,
                                                         uint64_t *__restrict__ seg, int64_t seg_cap,
-                                                        const int *__restrict__ status)
+                                                        const int *__restrict__ status, PlanArgs pa)
 {
-    if (status && *status != 0) return; // the device plan found no bucket path
+    int nsel, b0, b1;
+    if (pa.cnt) {
+        // speculative step: every block derives the bucket plan from the
+        // all-reduced counts itself (no plan launch); block 0 publishes it
+        const PlanOut o = plan_block(pa.cnt, pa.nsel, pa.r0, pa.r1, pa.capr);
+        if (blockIdx.x == 0 && threadIdx.x == 0) plan_publish(o, st, pa.nsel, pa.status, pa.host_status);
+        if (o.status != 0) return;
+        nsel = pa.nsel;
+        b0 = o.b0;
+        b1 = nsel > 1 ? o.b1 : -1;
+    } else {
+        if (status && *status != 0) return; // the device plan found no bucket path
+        nsel = st->nsel;
+        b0 = st->bsel[0];
+        b1 = nsel > 1 ? st->bsel[1] : -1;
+    }
     __shared__ uint64_t sK[CB_LDS];
     __shared__ int sN;
     __shared__ unsigned long long sBase;
-    const int nsel = st->nsel, b0 = st->bsel[0], b1 = nsel > 1 ? st->bsel[1] : -1;
     const uint64_t lo = st->lo_key;
     const double binv = st->binv;
     unsigned long long *ctr = reinterpret_cast<unsigned long long *>(seg);
@@ -1443,7 +1476,8 @@ __global__ __launch_bounds__(256) void k_counts_reduce(const unsigned long long 
                                                       const SelState *__restrict__ st,
                                                       const uint32_t *__restrict__ bpart,
                                                       int64_t nbpart,
-                                                      unsigned long long *__restrict__ cnt)
+                                                      unsigned long long *__restrict__ cnt,
+                                                      uint64_t *__restrict__ seg_zero)
 {
     __shared__ unsigned long long s0[256], s1[256], s2[256];
     if ((int)blockIdx.x < NBK / 64 * BSUM_SLICES) {
@@ -1498,6 +1532,7 @@ __global__ __launch_bounds__(256) void k_counts_reduce(const unsigned long long 
         cnt[2] = s2[0];
         cnt[CNT_LO] = st->lo_key;
         cnt[CNT_HI] = st->hi_key;
+        if (seg_zero) seg_zero[0] = 0; // the speculative compaction's counter
     }
 }
 
@@ -3690,10 +3725,10 @@ hipError_t launch_select_scan(SelState *st, unsigned long long *ghist, int make_
 hipError_t launch_counts_reduce(const unsigned long long *below, const uint32_t *counts,
                                 int64_t nblk, int64_t cap, const SelState *st,
                                 const uint32_t *bpart, int64_t nbpart,
-                                unsigned long long *cnt, hipStream_t stream)
+                                unsigned long long *cnt, hipStream_t stream, uint64_t *seg_zero)
 {
     hipLaunchKernelGGL(k_counts_reduce, dim3(NBK / 64 * BSUM_SLICES + 1), dim3(256), 0, stream, below,
-                       counts, nblk, cap, st, bpart, nbpart, cnt);
+                       counts, nblk, cap, st, bpart, nbpart, cnt, seg_zero);
     return hipGetLastError();
 }
 
@@ -3717,13 +3752,14 @@ hipError_t launch_set_sel(SelState *st, int nsel, uint64_t r0, uint64_t r1, int 
 }
 
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
-                                  int64_t cap, const SelState *st, uint64_t *seg, int64_t seg_cap,
-                                  const int *status, hipStream_t stream)
+                                  int64_t cap, SelState *st, uint64_t *seg, int64_t seg_cap,
+                                  const int *status, hipStream_t stream, const PlanArgs *plan)
 {
-    if (nreg <= 0) return hipSuccess;
-    const int64_t G = nreg < 512 ? nreg : 512;
+    if (nreg <= 0 && !plan) return hipSuccess;
+    int64_t G = nreg < 512 ? nreg : 512;
+    if (G < 1) G = 1; // (with a plan the launch publishes it even without regions)
     hipLaunchKernelGGL(k_compact_buckets, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap,
-                       st, seg, seg_cap, status);
+                       st, seg, seg_cap, status, plan ? *plan : PlanArgs{});
     return hipGetLastError();
 }
 

@@ -12,7 +12,7 @@ through size-independent properties:
     N = 262144 has 3.4e10 pairs, past 2^32):  count(D^2 < s(1-eps)) <= rank <
     count(D^2 < s(1+eps)), eps = 1e-12 (fp64; the centred Gram form differs in
     the last bits) or 1e-5 (fp32 keys);
-  * phi_hat on 512 sampled rows (the first and last 256) vs the oracle's phi
+  * phi_hat on 1024 sampled rows (the first and last 256, 512 around n / 2) vs the oracle's phi
     for those rows against all N columns (SVGD.hpp:407-454): max-abs <= 1e-10
     (fp64) or <= 1e-4 max|phi_hat| (fp32, cfg5);
   * one full step (scale + host grad log p + phi_hat + Adam) on the sampled
@@ -53,7 +53,10 @@ def _ctx(X, dtype):
 
 
 def _sample_rows(n):
-    return [(0, 256), (n - 256, n)]
+    # both ends and 512 mid-range rows straddling n / 2: a k_phi_rows row
+    # block boundary (1024 rows at d = 8), a symmetric-pass block boundary
+    # and, on one rank, the middle of the column-split range
+    return [(0, 256), (n // 2 - 256, n // 2 + 256), (n - 256, n)]
 
 
 @pytest.mark.parametrize("name,n,d,dtype", CASES, ids=[c[0] for c in CASES])
@@ -133,3 +136,54 @@ def test_fullsize_rebracket_path_exact(monkeypatch):
     r.close()
     assert got == ref
     assert path in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
+
+
+def test_fullsize_plain_form_with_outlier(oracle):
+    """cfg3 plus one far outlier: a log2e max|xc|^2 >> 300, so every wave of
+    the phi row stream takes the plain (unfolded, clamped-exponent) form and
+    the symmetric pass hands the step over -- sampled rows, the outlier's own
+    row included, against the oracle."""
+    X, model = _workload("cfg3", 65536, 8)
+    X = X.copy()
+    X[70] += 60.0
+    G = model.log_model_grad(X)
+    c = _ctx(X, C.SVGD_F64)
+    a, _ = c.median_scale()
+    ph = c.phi(G, a)
+    c.close()
+    assert np.all(np.isfinite(ph))
+    for r0, r1 in [(0, 256)] + _sample_rows(65536)[1:]:
+        ref = oracle.phi(X, G, a, rows=(r0, r1))
+        assert np.max(np.abs(ph[r0:r1] - ref)) <= 1e-10, (r0, r1)
+
+
+def test_fullsize_five_speculative_steps(oracle):
+    """cfg3, 5 steps: queued back to back (speculative device plan, no host
+    round trip inside a step) they end bit-identical to 5 steps run one at a
+    time, and every one of those steps matches the oracle's step on the
+    sampled rows from the device's scale of that X_t (<= 1e-9)."""
+    X0, model = _workload("cfg3", 65536, 8)
+    b2b = _ctx(X0, C.SVGD_F64)
+    b2b.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+    for _ in range(5):
+        b2b.step_with_model(model)
+    X5 = b2b.get_particles()
+    b2b.close()
+    c = _ctx(X0, C.SVGD_F64)
+    c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+    rows = _sample_rows(65536)
+    opts = {r: oracle.Adam((r[1] - r[0], 8), 0.1, 0.9, 0.999) for r in rows}
+    Xt = X0
+    for _ in range(5):
+        c.step_with_model(model)
+        a = c.last_scale()[0]
+        X1 = c.get_particles()
+        G = model.log_model_grad(Xt)
+        for r0, r1 in rows:
+            ph = oracle.phi(Xt, G, a, rows=(r0, r1))
+            Xr = Xt[r0:r1].copy()
+            oracle.apply_update(Xr, opts[(r0, r1)].step(ph))
+            assert np.max(np.abs(X1[r0:r1] - Xr)) <= 1e-9
+        Xt = X1
+    c.close()
+    assert np.array_equal(Xt, X5)
