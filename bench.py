@@ -337,6 +337,9 @@ def main():
     ap.add_argument("--cpu-rows-1t", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the median is reported")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="measurement only: time rank 0's share of a P-rank step on one GPU "
+                         "(no collectives; results are not the step's) -- not a headline line")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed diagnostic pass")
     ap.add_argument("--dtype", choices=["f64", "f32"], default=None,
                     help="compute dtype of the O(N^2) work (default: the config's; cfg5 is f32)")
@@ -347,6 +350,8 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
 
+    if args.sim_world > 1:
+        os.environ["SVGD_SIM_WORLD"] = str(args.sim_world)
     import torch
     import svgdcpp_amd as S
     from svgdcpp_amd import _capi as C
@@ -453,8 +458,12 @@ def main():
 
     mine = {
         "rank": rank, "rows": rows,
-        "phases_ms_per_step": {"phi": per_step(phi_ms.value, nsteps_timed),
-                               "median": per_step(med_ms.value, nsteps_timed)},
+        # phase events sit at phase boundaries only (svgd_set_timing level 1):
+        # "phi" runs from the median's end (so it holds any wait for G) to the
+        # update's end, "median" from the previous step's end (so it holds the
+        # gap between steps) to the scale; the diagnostic pass separates both
+        "phases_ms_per_step": {"phi_incl_wait_for_g": per_step(phi_ms.value, nsteps_timed),
+                               "median_incl_step_gap": per_step(med_ms.value, nsteps_timed)},
         "host_ms_per_step": {"grad": per_step(host_timed["host_grad_ms"], host_timed["steps"]),
                              "xwait": per_step(host_timed["host_xwait_ms"], host_timed["steps"]),
                              "job": per_step(host_timed["host_job_ms"], host_timed["steps"]),
@@ -557,7 +566,12 @@ def main():
         if issue is not None:
             out["roofline"].update({"valu_issue_util": issue["valu_issue_util"],
                                     "issue_source": issue["source"]})
-        if args.config != "cfg3" or args.device_model or dtype != "f64":
+        if args.sim_world > 1:
+            out["metric"] = (f"per-rank step time of a {args.sim_world}-GPU run, simulated on one GPU "
+                             f"(rank 0's rows and pair share, no collectives; not the headline)")
+            out["value"] = None
+            out["sim_world"] = args.sim_world
+        elif args.config != "cfg3" or args.device_model or dtype != "f64":
             desc = cfg["desc"]
             if dtype != cfg.get("dtype", "f64"):
                 desc = desc.replace("fp32 compute", "fp64 compute") + (", fp32 compute" if dtype == "f32" and "fp32" not in desc else "")

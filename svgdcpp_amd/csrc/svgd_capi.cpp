@@ -121,6 +121,7 @@ struct svgd_ctx {
     int dtype = SVGD_F64;
     int device = 0;
     int world = 1, rank = 0;
+    int sim_world = 1; // SVGD_SIM_WORLD (measurement only): rank 0's share of a P-rank step
     ncclComm_t comm = nullptr;
     // a second communicator (ncclCommSplit of comm) for the G all-gather on
     // its own stream: it overlaps the median chain's kernels and collectives
@@ -177,7 +178,12 @@ struct svgd_ctx {
     int64_t direct_max_pairs = int64_t(1) << 24;
     int64_t sample_size = 0; // 0: auto, clamp(M / 256, 2^18, 2^22) for M pairs
     double bracket_sigma = 3.0; // sample-quantile standard deviations either side
-    bool shard_sample = true;   // P > 1: ranks draw disjoint parts of the sample
+    // P > 1: every rank draws the whole (smaller, <= 2^20) bracket sample of
+    // the one counter-based sequence and derives the same bracket locally --
+    // no histogram all-reduces in the step (two RCCL calls cost more than
+    // sampling 2^20 pairs); SVGD_SAMPLE_SHARD=1: ranks draw disjoint parts of
+    // a full-size sample and all-reduce its two radix histograms instead
+    bool shard_sample = false;
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
     bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol / _tcol)
     double band_est = 1.0;         // this step's bracket: expected share of the pairs
@@ -566,6 +572,11 @@ int median_begin(svgd_ctx *c)
     const int64_t n = c->n;
     int64_t rlo, rhi;
     c->navg = svgd_plan_median_ranks(n, &rlo, &rhi);
+    if (c->sim_world > 1) { // the same quantile of this rank's share of the pairs
+        const int64_t d = rhi - rlo;
+        rlo = rlo >= 0 ? rlo / c->sim_world : rlo;
+        rhi = rlo + d;
+    }
     // distinct non-negative upper ranks to select
     c->nsel = 0;
     c->src_lo = c->src_hi = -1;
@@ -615,7 +626,11 @@ int median_begin(svgd_ctx *c)
                     : tile_path       ? int64_t(1) << 22
                                       : std::min<int64_t>(std::max<int64_t>(M / 256, int64_t(1) << 18),
                                                           int64_t(1) << 22);
+        const bool multi = c->comm || c->hcomm || c->sim_world > 1;
+        if (multi && !c->shard_sample && c->sample_size <= 0)
+            S = std::min<int64_t>(S, int64_t(1) << 20); // every rank draws all of it
         S = std::min<int64_t>(S, M);
+        if (c->sim_world > 1 && c->shard_sample) S = std::max<int64_t>(1, S / c->sim_world); // a rank's share
         const bool tile_sample = tile_path && S >= TB * TB;
         if (tile_sample) S = S / (TB * TB) * (TB * TB);
         if (c->sample_alloc < S) {
@@ -632,8 +647,9 @@ int median_begin(svgd_ctx *c)
         const int64_t g0 = c->samp_shard ? S * c->rank / c->world : 0;
         c->samp_local = c->samp_shard ? S * (c->rank + 1) / c->world - g0 : S;
         c->samp_S = S;
-        c->samp_qlo = (double)c->sel_rank[0] / (double)M;
-        c->samp_qhi = (double)c->sel_rank[c->nsel - 1] / (double)M;
+        const double Mq = c->sim_world > 1 ? (double)M / c->sim_world : (double)M;
+        c->samp_qlo = (double)c->sel_rank[0] / Mq;
+        c->samp_qhi = (double)c->sel_rank[c->nsel - 1] / Mq;
         // whole-tile samples are correlated (a far particle shifts its tile's
         // 64 x 64 keys together): 3 sigma of S independent draws missed the
         // bracket on ~40 % of cfg5 steps (each miss: a second collect pass);
@@ -1252,14 +1268,23 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     c->nb = (n + TB - 1) / TB;
     c->np = c->nb * TB + TB;
     c->chunk = (n + c->world - 1) / c->world;
-    svgd_plan_rows(n, c->world, c->rank, &c->row0, &c->row1);
+    // SVGD_SIM_WORLD=P (measurement only, one rank): run rank 0's share of a
+    // P-rank step -- its rows of phi and the optimizer, 1/P of the median's
+    // pair tiles with the order statistics' ranks scaled to that share -- on
+    // one GPU without collectives, to time the per-rank kernels of a P-GPU
+    // run.  The results are NOT the step's (no data from the other ranks).
+    const int plan_world = c->world == 1 && std::getenv("SVGD_SIM_WORLD")
+                               ? std::max(1, std::atoi(std::getenv("SVGD_SIM_WORLD")))
+                               : c->world;
+    c->sim_world = plan_world != c->world ? plan_world : 1;
+    svgd_plan_rows(n, plan_world, c->rank, &c->row0, &c->row1);
     c->nrows = c->row1 - c->row0;
     c->pblock = SVGD_PAIR_BLOCK_DT(dim, dtype);
     c->pnb = (n + c->pblock - 1) / c->pblock;
-    c->own_tiles = svgd_plan_pair_tiles(n, c->pblock, c->world, c->rank);
+    c->own_tiles = svgd_plan_pair_tiles(n, c->pblock, plan_world, c->rank);
     {
         const int64_t T = c->pnb * (c->pnb + 1) / 2;
-        c->tile0 = T * c->rank / c->world;
+        c->tile0 = T * c->rank / plan_world;
     }
     HIPCHK(c, hipSetDevice(device));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
