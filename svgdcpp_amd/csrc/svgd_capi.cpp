@@ -122,6 +122,7 @@ struct svgd_ctx {
     int device = 0;
     int world = 1, rank = 0;
     int sim_world = 1; // SVGD_SIM_WORLD (measurement only): rank 0's share of a P-rank step
+    int64_t sim_pairs = 0; // the unordered pairs in that share's tiles
     ncclComm_t comm = nullptr;
     // a second communicator (ncclCommSplit of comm) for the G all-gather on
     // its own stream: it overlaps the median chain's kernels and collectives
@@ -572,9 +573,9 @@ int median_begin(svgd_ctx *c)
     const int64_t n = c->n;
     int64_t rlo, rhi;
     c->navg = svgd_plan_median_ranks(n, &rlo, &rhi);
-    if (c->sim_world > 1) { // the same quantile of this rank's share of the pairs
+    if (c->sim_world > 1 && rlo >= 0) { // the same quantile of this rank's share of the pairs
         const int64_t d = rhi - rlo;
-        rlo = rlo >= 0 ? rlo / c->sim_world : rlo;
+        rlo = (int64_t)((long double)rlo * (long double)c->sim_pairs / (long double)upper_pairs(n));
         rhi = rlo + d;
     }
     // distinct non-negative upper ranks to select
@@ -647,7 +648,7 @@ int median_begin(svgd_ctx *c)
         const int64_t g0 = c->samp_shard ? S * c->rank / c->world : 0;
         c->samp_local = c->samp_shard ? S * (c->rank + 1) / c->world - g0 : S;
         c->samp_S = S;
-        const double Mq = c->sim_world > 1 ? (double)M / c->sim_world : (double)M;
+        const double Mq = c->sim_world > 1 ? (double)c->sim_pairs : (double)M;
         c->samp_qlo = (double)c->sel_rank[0] / Mq;
         c->samp_qhi = (double)c->sel_rank[c->nsel - 1] / Mq;
         // whole-tile samples are correlated (a far particle shifts its tile's
@@ -1286,6 +1287,15 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
         const int64_t T = c->pnb * (c->pnb + 1) / 2;
         c->tile0 = T * c->rank / plan_world;
     }
+    if (c->sim_world > 1) { // real pairs of the share's tiles (diagonal tiles: upper half)
+        for (int64_t t = 0; t < c->own_tiles; ++t) {
+            int64_t I, J;
+            svgd_plan_pair_tile(n, c->pblock, plan_world, c->rank, t, &I, &J);
+            const int64_t ri = std::min<int64_t>(c->pblock, n - I * c->pblock);
+            const int64_t rj = std::min<int64_t>(c->pblock, n - J * c->pblock);
+            c->sim_pairs += I == J ? ri * (ri - 1) / 2 : ri * rj;
+        }
+    }
     HIPCHK(c, hipSetDevice(device));
     HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(c, hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
@@ -1319,8 +1329,11 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
                 c->R = r;
             }
         }
+        if (const char *e = std::getenv("SVGD_PHI_T8K"))
+            if (std::atoi(e) != 0 && c->phi_kind == 0 && phi_rows_t8k_supported(dim, c->R)) c->phi_kind = 2;
         const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim, c->R, c->phi_kind) * ncu;
-        const int64_t iblocks = std::max<int64_t>(1, (c->nrows + 256 * c->R - 1) / (256 * c->R));
+        const int64_t rows_wg = (c->phi_kind == 2 ? 512 : 256) * (int64_t)c->R;
+        const int64_t iblocks = std::max<int64_t>(1, (c->nrows + rows_wg - 1) / rows_wg);
         int64_t S = std::max<int64_t>(1, (resident + iblocks - 1) / iblocks);
         // 2 blocks per resident slot: one block wave per slot left a tail of
         // idle CUs (measured at cfg3, phi launch: S x1 4.00 ms, x2 3.83-3.93,

@@ -212,6 +212,8 @@ hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0
                           hipStream_t stream);
 // kind 1: the scalar-column variant k_phi_rows_s (phi_rows_s_supported)
 bool phi_rows_s_supported(int d, int R);
+// kind 2: k_phi_rows with 8-wave work-groups and the mask-free 8192-entry exp table
+bool phi_rows_t8k_supported(int d, int R);
 // full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,
 // or an eigendecomposition when M is indefinite and d <= ROWS_MAX_D);
 // err = 0 positive definite, 2 indefinite, 1 non-finite / no convergence.

@@ -1819,7 +1819,17 @@ template <int D> struct ColRec {
 // no clamp either.  Plain form: u clamped to +-EXP_U_CLAMP (K within
 // [2^-1000, 2^1000] instead of [0, inf]: below any fp64 sum that holds the
 // diagonal K_ii = 1).
-template <int D, int R, bool FOLD>
+// Byte offset of table entry (ki mod 8192) in ONE instruction: the 16-bit
+// shift zeroes the destination's high half on gfx9 (tools/check_b16.hip
+// checks it on the device), so (ki << 3) & 0xffff needs no separate mask.
+__device__ __forceinline__ uint32_t tab8k_offset(int ki)
+{
+    uint32_t a;
+    asm("v_lshlrev_b16 %0, 3, %1" : "=v"(a) : "v"(ki));
+    return a;
+}
+
+template <int D, int R, bool FOLD, int TABN = EXP_TB>
 __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (&xs)[R][D],
                                               const double (&ci)[R], double (&acc)[R][D],
                                               double (&acc1)[R], const double *tab)
@@ -1845,7 +1855,10 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
         const double k = __builtin_rint(u[r]);
         f[r] = u[r] - k;
         ki[r] = (int)k;
-        T[r] = tab[ki[r] & (EXP_TB - 1)];
+        if constexpr (TABN == 8192)
+            T[r] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(tab) + tab8k_offset(ki[r]));
+        else
+            T[r] = tab[ki[r] & (EXP_TB - 1)];
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1863,8 +1876,12 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
 
 // sgn (matrix scale, M = L S L^T): the row coordinates are scaled by S so
 // the pair term is z_i^T S z_j; nullptr = the isotropic scale (S = I).
-template <int D, int R>
-__global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec,
+// NW waves per work-group; TABN = 4096 (the 32 KiB table, 4 waves) or 8192
+// (a 64 KiB table -- two octaves, T[m + 4096] = 2 T[m] exactly -- whose
+// address needs no mask, tab8k_offset; 8 waves share it so the LDS still
+// fits 8 waves per CU)
+template <int D, int R, int NW = 4, int TABN = EXP_TB>
+__global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__ rec,
                                                  const double *__restrict__ a_ptr, int64_t row0,
                                                  int64_t nrows, int64_t n, int S,
                                                  double *__restrict__ part, int64_t ldp,
@@ -1879,11 +1896,14 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     // spilling (row state R(2D+2) + two records 2(2D+1) doubles)
     constexpr bool PIPE = (R * (2 * D + 2) + 2 * (2 * D + 1)) * 2 <= 232;
     // per-wave double-buffered column chunks, then the 2^(i/4096) table
-    __shared__ __attribute__((aligned(16))) char smem[4 * 2 * CHB + EXP_TB * 8];
-    double *tab = reinterpret_cast<double *>(smem + 4 * 2 * CHB);
+    __shared__ __attribute__((aligned(16))) char smem[NW * 2 * CHB + TABN * 8];
+    double *tab = reinterpret_cast<double *>(smem + NW * 2 * CHB);
 #pragma unroll
-    for (int e = 0; e < EXP_TB / 256; ++e)
-        tab[e * 256 + threadIdx.x] = tab_biased(EXP2_TAB4096[e * 256 + threadIdx.x], e * 256 + threadIdx.x);
+    for (int e = 0; e < TABN / (NW * 64); ++e) {
+        const int m = e * NW * 64 + threadIdx.x;
+        const double t = EXP2_TAB4096[m & (EXP_TB - 1)];
+        tab[m] = tab_biased(m >= EXP_TB ? 2.0 * t : t, m);
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -1891,7 +1911,7 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
     char *wbuf = smem + w * 2 * CHB;
     const int64_t iblk = blockIdx.x / S;
     const int s = (int)(blockIdx.x - iblk * S);
-    const int64_t rbase = iblk * (256 * R) + w * (64 * R); // local row of this wave's lane 0
+    const int64_t rbase = iblk * (NW * 64 * R) + w * (64 * R); // local row of this wave's lane 0
     // u_ij = c_i + c_j + 8192 a log2e xc_i.xc_j = -4096 a log2e |xc_i - xc_j|^2;
     // the row coordinates are pre-scaled by 8192 a log2e
     const double alpha = 8192.0 * LOG2E * (*a_ptr);
@@ -1967,30 +1987,30 @@ __global__ __launch_bounds__(256) void k_phi_rows(const double *__restrict__ rec
         for (; jj + 4 <= cnt; jj += 4) {
             qb.load(cb + (jj + 1) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD, TABN>(qa, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
             qa.load(cb + (jj + 2) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R, FOLD>(qb, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD, TABN>(qb, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
             qb.load(cb + (jj + 3) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD, TABN>(qa, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
             qa.load(cb + (jj + 4) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R, FOLD>(qb, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD, TABN>(qb, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
         }
         for (; jj < cnt; jj += 2) {
             qb.load(cb + (jj + 1) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD, TABN>(qa, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
             if (jj + 1 >= cnt) break;
             qa.load(cb + (jj + 2) * RS);
             __builtin_amdgcn_sched_barrier(0);
-            phi_rows_pair<D, R, FOLD>(qb, xs, ci, acc, acc1, tab);
+            phi_rows_pair<D, R, FOLD, TABN>(qb, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -3387,6 +3407,24 @@ static hipError_t launch_rows_s(int d, int R, int grid, const double *rec, const
 
 bool phi_rows_s_supported(int d, int R) { return d == 8 && (R == 4 || R == 5); }
 
+// kind 2: k_phi_rows with 8 waves and the 8192-entry table (d in {2, 8}, R = 4)
+bool phi_rows_t8k_supported(int d, int R) { return (d == 2 || d == 8) && R == 4; }
+static hipError_t launch_rows_t8k(int d, int grid, const double *rec, const double *a_ptr,
+                                  int64_t row0, int64_t nrows, int64_t n, int S, double *part,
+                                  int64_t ldp, const double *sgn, const unsigned long long *nmax,
+                                  hipStream_t stream, const int *skip)
+{
+    if (d == 8)
+        hipLaunchKernelGGL((k_phi_rows<8, 4, 8, 8192>), dim3(grid), dim3(512), 0, stream, rec, a_ptr,
+                           row0, nrows, n, S, part, ldp, sgn, nmax, skip);
+    else if (d == 2)
+        hipLaunchKernelGGL((k_phi_rows<2, 4, 8, 8192>), dim3(grid), dim3(512), 0, stream, rec, a_ptr,
+                           row0, nrows, n, S, part, ldp, sgn, nmax, skip);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
@@ -3397,8 +3435,11 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
         if (ev_mid) return hipEventRecord(ev_mid, stream);
         return hipSuccess;
     }
-    const int grid = (int)(((nrows + 256 * R - 1) / (256 * R)) * S);
-    hipError_t e = kind == 1 ? launch_rows_s(d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
+    const int rows_wg = (kind == 2 ? 512 : 256) * R;
+    const int grid = (int)(((nrows + rows_wg - 1) / rows_wg) * S);
+    hipError_t e = kind == 2 ? launch_rows_t8k(d, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
+                                               nmax_bits, stream, skip)
+                   : kind == 1 ? launch_rows_s(d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                              nmax_bits, stream, skip)
                              : launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                       nmax_bits, nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
@@ -3928,6 +3969,11 @@ int phi_rows_blocks_per_cu(int d, int R, int kind)
 {
     int nb = 0;
     hipError_t e = hipErrorInvalidValue;
+    if (kind == 2) {
+        if (d == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<8, 4, 8, 8192>, 512, 0);
+        if (d == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<2, 4, 8, 8192>, 512, 0);
+        return (e == hipSuccess && nb > 0) ? nb : 1;
+    }
     if (kind == 1) {
         if (d == 8 && R == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows_s<8, 4>, 256, 0);
         if (d == 8 && R == 5) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows_s<8, 5>, 256, 0);
