@@ -490,18 +490,19 @@ def main():
         achieved = flops_launch / (phi_kernel_ms / 1e3) / 1e12 if phi_kernel_ms else None
         peak = FP32_PEAK_TFLOPS if dtype == "f32" else FP64_PEAK_TFLOPS
         traffic = None
+        wkey = args.sim_world if args.sim_world > 1 else world  # the profiles' world
         pmc_path = os.path.join(ROOT, "profiles", "phi_pmc_traffic.json")
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("n") == n and pmc.get("d") == d and pmc.get("world") == world:
+            if pmc.get("n") == n and pmc.get("d") == d and pmc.get("world") == wkey:
                 traffic = pmc.get("bytes_per_launch")
         issue = None  # SQ counters of the same kernel (committed profile, not this run)
         issue_path = os.path.join(ROOT, "profiles", "phi_pmc_issue.json")
         if os.path.exists(issue_path):
             with open(issue_path) as f:
                 iss = json.load(f)
-            if iss.get("n") == n and iss.get("d") == d and iss.get("world") == world and dtype == "f64":
+            if iss.get("n") == n and iss.get("d") == d and iss.get("world") == wkey and dtype == "f64":
                 issue = iss
         row_kernel = dtype == "f64" and d <= 16
         out = {

@@ -166,7 +166,7 @@ struct svgd_ctx {
     unsigned long long *nmax = nullptr; // max |xc|^2 (double bits)
     int S = 1;
     int R = 2; // rows per lane of k_phi_rows
-    int phi_kind = 0; // 0 k_phi_rows (LDS columns), 1 k_phi_rows_s (scalar columns)
+    int phi_kind = 0; // 0 k_phi_rows (4 waves), 1 k_phi_rows_s (scalar columns), 2 k_phi_rows (8 waves, column-split)
     // symmetric phi pass (k_phi_sym, one rank, d <= 8): geometry and buffers
     bool sym = false;
     int symB = 0, symSRS = 0, symNSUB = 0, sym_grid = 0, sym_rslots = 0;
@@ -754,7 +754,8 @@ int median_finish_spec(svgd_ctx *c, double logn)
     // into blit kernels competing with the median kernels)
     // (the compaction's blocks derive the bucket plan themselves: no plan launch)
     const PlanArgs pa{c->cnt3, c->nsel, (uint64_t)c->sel_rank[0], (uint64_t)c->sel_rank[c->nsel - 1],
-                      std::min<int64_t>(c->bucket_cap, CAPR), c->d_status, c->h_status_dev};
+                      std::min<int64_t>(c->bucket_cap, CAPR), c->d_status, c->h_status_dev,
+                      c->sim_world > 1 ? 1 : 0};
     HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
                                      c->d_status, c->stream, &pa));
     CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
@@ -797,6 +798,13 @@ int median_finish(svgd_ctx *c)
     }
     c->last_fast = false;
     HIPCHK(c, hipEventSynchronize(c->ev_cnt));
+    if (c->sim_world > 1 && !c->h_cnt[2] && c->h_cnt[1] > 0) {
+        // measurement mode: the share is selected alone -- re-anchor the
+        // ranks inside its candidates (the device plan does the same)
+        const int64_t dr = c->sel_rank[c->nsel - 1] - c->sel_rank[0];
+        c->sel_rank[0] = (int64_t)(c->h_cnt[0] + c->h_cnt[1] / 2);
+        if (c->nsel > 1) c->sel_rank[1] = c->sel_rank[0] + dr;
+    }
     const uint64_t r0 = (uint64_t)c->sel_rank[0], r1 = (uint64_t)c->sel_rank[c->nsel - 1];
     auto in_bracket = [&]() {
         return !c->h_cnt[2] && r0 >= c->h_cnt[0] && r1 < c->h_cnt[0] + c->h_cnt[1];
@@ -1329,10 +1337,13 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
                 c->R = r;
             }
         }
-        if (const char *e = std::getenv("SVGD_PHI_T8K"))
-            if (std::atoi(e) != 0 && c->phi_kind == 0 && phi_rows_t8k_supported(dim, c->R)) c->phi_kind = 2;
+        // default: 8-wave work-groups, 8192-entry table, columns split over the
+        // waves (kind 2); SVGD_PHI_T8K=0 selects the 4-wave kernel (kind 0)
+        bool t8k = true;
+        if (const char *e = std::getenv("SVGD_PHI_T8K")) t8k = std::atoi(e) != 0;
+        if (t8k && c->phi_kind == 0 && phi_rows_t8k_supported(dim, c->R)) c->phi_kind = 2;
         const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim, c->R, c->phi_kind) * ncu;
-        const int64_t rows_wg = (c->phi_kind == 2 ? 512 : 256) * (int64_t)c->R;
+        const int64_t rows_wg = c->phi_kind == 2 ? phi_rows_t8k_rows(c->R) : 256 * (int64_t)c->R;
         const int64_t iblocks = std::max<int64_t>(1, (c->nrows + rows_wg - 1) / rows_wg);
         int64_t S = std::max<int64_t>(1, (resident + iblocks - 1) / iblocks);
         // 2 blocks per resident slot: one block wave per slot left a tail of

@@ -135,6 +135,9 @@ struct PlanArgs {
     uint64_t r0, r1;
     int64_t capr;
     int *status, *host_status;
+    // SVGD_SIM_WORLD measurement mode: one rank's share is selected alone, so
+    // r0 is re-anchored at the middle of its candidates (r1 keeps r1 - r0)
+    int sim = 0;
 };
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                   int64_t cap, SelState *st, uint64_t *seg, int64_t seg_cap,
@@ -214,6 +217,7 @@ hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0
 bool phi_rows_s_supported(int d, int R);
 // kind 2: k_phi_rows with 8-wave work-groups and the mask-free 8192-entry exp table
 bool phi_rows_t8k_supported(int d, int R);
+int phi_rows_t8k_rows(int R); // rows per work-group of kind 2
 // full-matrix kernel scale: M = factor * sym(src) = L diag(sgn) L^T (Cholesky,
 // or an eigendecomposition when M is indefinite and d <= ROWS_MAX_D);
 // err = 0 positive definite, 2 indefinite, 1 non-finite / no convergence.

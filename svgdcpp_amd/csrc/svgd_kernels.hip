@@ -1032,7 +1032,7 @@ struct PlanOut {
     unsigned long long in0, in1;
 };
 __device__ PlanOut plan_block(const unsigned long long *__restrict__ cnt, int nsel, uint64_t r0,
-                              uint64_t r1, int64_t capr)
+                              uint64_t r1, int64_t capr, int sim = 0)
 {
     __shared__ unsigned long long sPart[256];
     __shared__ int sB[2];
@@ -1040,6 +1040,11 @@ __device__ PlanOut plan_block(const unsigned long long *__restrict__ cnt, int ns
     const int tid = threadIdx.x;
     PlanOut o{0, -1, -1, 1, 0, 0};
     const unsigned long long below = cnt[0], cand = cnt[1], ovf = cnt[2];
+    if (sim) { // measurement mode (PlanArgs::sim)
+        const uint64_t dr = r1 - r0;
+        r0 = below + cand / 2;
+        r1 = r0 + dr;
+    }
     if (ovf || r0 < below || r1 >= below + cand) {
         o.status = ovf ? 2 : 1;
         return o;
@@ -1154,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restr
     if (pa.cnt) {
         // speculative step: every block derives the bucket plan from the
         // all-reduced counts itself (no plan launch); block 0 publishes it
-        const PlanOut o = plan_block(pa.cnt, pa.nsel, pa.r0, pa.r1, pa.capr);
+        const PlanOut o = plan_block(pa.cnt, pa.nsel, pa.r0, pa.r1, pa.capr, pa.sim);
         if (blockIdx.x == 0 && threadIdx.x == 0) plan_publish(o, st, pa.nsel, pa.status, pa.host_status);
         if (o.status != 0) return;
         nsel = pa.nsel;
@@ -1879,8 +1884,12 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
 // NW waves per work-group; TABN = 4096 (the 32 KiB table, 4 waves) or 8192
 // (a 64 KiB table -- two octaves, T[m + 4096] = 2 T[m] exactly -- whose
 // address needs no mask, tab8k_offset; 8 waves share it so the LDS still
-// fits 8 waves per CU)
-template <int D, int R, int NW = 4, int TABN = EXP_TB>
+// fits 8 waves per CU).
+// WC: the waves of a work-group split its column range WC ways (NW / WC row
+// groups of 64 R rows): their partial sums are added in LDS in wave order
+// before one partial per work-group goes out -- WC times fewer partials (HBM
+// writes here, reads in k_phi_reduce) for the same number of waves.
+template <int D, int R, int NW = 4, int TABN = EXP_TB, int WC = 1>
 __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__ rec,
                                                  const double *__restrict__ a_ptr, int64_t row0,
                                                  int64_t nrows, int64_t n, int S,
@@ -1909,9 +1918,12 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     char *wbuf = smem + w * 2 * CHB;
+    static_assert(NW % WC == 0, "WC must divide NW");
+    constexpr int WR = NW / WC; // row groups per work-group
+    const int wr = w % WR, wc = w / WR;
     const int64_t iblk = blockIdx.x / S;
     const int s = (int)(blockIdx.x - iblk * S);
-    const int64_t rbase = iblk * (NW * 64 * R) + w * (64 * R); // local row of this wave's lane 0
+    const int64_t rbase = iblk * (WR * 64 * R) + wr * (64 * R); // local row of this wave's lane 0
     // u_ij = c_i + c_j + 8192 a log2e xc_i.xc_j = -4096 a log2e |xc_i - xc_j|^2;
     // the row coordinates are pre-scaled by 8192 a log2e
     const double alpha = 8192.0 * LOG2E * (*a_ptr);
@@ -1937,7 +1949,9 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
     // latency overlaps the previous column's arithmetic.  rec has >= 64 padded
     // rows past n, so whole chunks may be copied; the look-ahead read past a
     // chunk stays inside smem and is discarded.
-    const int64_t j0 = n * s / S, j1 = n * (s + 1) / S;
+    // column split of this wave: s (the work-group's) refined WC ways
+    const int64_t ST = (int64_t)S * WC, sw = (int64_t)s * WC + wc;
+    const int64_t j0 = n * sw / ST, j1 = n * (sw + 1) / ST;
     const int64_t nch = (j1 - j0 + CH_PHI - 1) / CH_PHI;
     const char *gcol = reinterpret_cast<const char *>(rec + j0 * RS);
     // Folding c_i out of the pair loop needs K_ij 2^(-c_i/4096) <= 2^(-c_i/4096)
@@ -1973,7 +1987,7 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
             for (int jj = 0; jj < cnt; ++jj) {
                 ColRec<D> q;
                 q.load(cb + jj * RS);
-                phi_rows_pair<D, R, FOLD>(q, xs, ci, acc, acc1, tab);
+                phi_rows_pair<D, R, FOLD, TABN>(q, xs, ci, acc, acc1, tab);
             }
             continue;
         }
@@ -2031,6 +2045,34 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
         stream_columns(std::false_type{});
     }
 
+    if constexpr (WC > 1) {
+        // the WC column groups' sums, added in wave order through LDS (the
+        // chunk buffers and the table are free once every wave is here), one
+        // slice of 64 rows per row group at a time; coalesced partial rows
+        constexpr int RB = WR * 64;  // rows of one slice
+        constexpr int EL = RB * (D + 1);
+        static_assert(WC * EL * 8 <= (int)sizeof(smem), "reduction slice exceeds the LDS");
+        double *red = reinterpret_cast<double *>(smem);
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            double *o = red + (wc * RB + wr * 64 + lane) * (D + 1);
+#pragma unroll
+            for (int k = 0; k < D; ++k) o[k] = acc[r][k];
+            o[D] = acc1[r];
+            __syncthreads();
+            for (int e = threadIdx.x; e < EL; e += NW * 64) {
+                double v = red[e];
+#pragma unroll
+                for (int q = 1; q < WC; ++q) v += red[q * EL + e];
+                const int rl = e / (D + 1), k = e - rl * (D + 1);
+                const int64_t li = iblk * (WR * 64 * R) + (rl >> 6) * (64 * R) + 64 * r + (rl & 63);
+                if (li < nrows) part[((int64_t)s * ldp + li) * (D + 1) + k] = v;
+            }
+            __syncthreads();
+        }
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t li = rbase + 64 * r + lane;
@@ -3407,21 +3449,31 @@ static hipError_t launch_rows_s(int d, int R, int grid, const double *rec, const
 
 bool phi_rows_s_supported(int d, int R) { return d == 8 && (R == 4 || R == 5); }
 
-// kind 2: k_phi_rows with 8 waves and the 8192-entry table (d in {2, 8}, R = 4)
-bool phi_rows_t8k_supported(int d, int R) { return (d == 2 || d == 8) && R == 4; }
+// kind 2: k_phi_rows with 8 waves, the 8192-entry table and the columns split
+// over the 8 waves (WC = 8: one 64 R-row group per work-group); R = 4 for
+// d <= 8, 2 above (the register budget)
+constexpr int T8K_NW = 8, T8K_WC = 8;
+bool phi_rows_t8k_supported(int d, int R) { return d >= 1 && d <= 16 && R == (d <= 8 ? 4 : 2); }
+int phi_rows_t8k_rows(int R) { return (T8K_NW / T8K_WC) * 64 * R; }
+#define SVGD_T8K_KERNEL(Dv) k_phi_rows<Dv, ((Dv) <= 8 ? 4 : 2), T8K_NW, 8192, T8K_WC>
+#define SVGD_T8K_CASE(Dv)                                                                       \
+    case Dv:                                                                                    \
+        hipLaunchKernelGGL((SVGD_T8K_KERNEL(Dv)), dim3(grid), dim3(T8K_NW * 64), 0, stream, rec, \
+                           a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);               \
+        break;
 static hipError_t launch_rows_t8k(int d, int grid, const double *rec, const double *a_ptr,
                                   int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                                   int64_t ldp, const double *sgn, const unsigned long long *nmax,
                                   hipStream_t stream, const int *skip)
 {
-    if (d == 8)
-        hipLaunchKernelGGL((k_phi_rows<8, 4, 8, 8192>), dim3(grid), dim3(512), 0, stream, rec, a_ptr,
-                           row0, nrows, n, S, part, ldp, sgn, nmax, skip);
-    else if (d == 2)
-        hipLaunchKernelGGL((k_phi_rows<2, 4, 8, 8192>), dim3(grid), dim3(512), 0, stream, rec, a_ptr,
-                           row0, nrows, n, S, part, ldp, sgn, nmax, skip);
-    else
+    switch (d) {
+        SVGD_T8K_CASE(1) SVGD_T8K_CASE(2) SVGD_T8K_CASE(3) SVGD_T8K_CASE(4)
+        SVGD_T8K_CASE(5) SVGD_T8K_CASE(6) SVGD_T8K_CASE(7) SVGD_T8K_CASE(8)
+        SVGD_T8K_CASE(9) SVGD_T8K_CASE(10) SVGD_T8K_CASE(11) SVGD_T8K_CASE(12)
+        SVGD_T8K_CASE(13) SVGD_T8K_CASE(14) SVGD_T8K_CASE(15) SVGD_T8K_CASE(16)
+    default:
         return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -3435,7 +3487,7 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
         if (ev_mid) return hipEventRecord(ev_mid, stream);
         return hipSuccess;
     }
-    const int rows_wg = (kind == 2 ? 512 : 256) * R;
+    const int rows_wg = kind == 2 ? phi_rows_t8k_rows(R) : 256 * R;
     const int grid = (int)(((nrows + rows_wg - 1) / rows_wg) * S);
     hipError_t e = kind == 2 ? launch_rows_t8k(d, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                                nmax_bits, stream, skip)
@@ -3970,8 +4022,19 @@ int phi_rows_blocks_per_cu(int d, int R, int kind)
     int nb = 0;
     hipError_t e = hipErrorInvalidValue;
     if (kind == 2) {
-        if (d == 8) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<8, 4, 8, 8192>, 512, 0);
-        if (d == 2) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows<2, 4, 8, 8192>, 512, 0);
+#define SVGD_T8K_OCC(Dv)                                                                          \
+    case Dv:                                                                                      \
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, SVGD_T8K_KERNEL(Dv), T8K_NW * 64, 0); \
+        break;
+        switch (d) {
+            SVGD_T8K_OCC(1) SVGD_T8K_OCC(2) SVGD_T8K_OCC(3) SVGD_T8K_OCC(4)
+            SVGD_T8K_OCC(5) SVGD_T8K_OCC(6) SVGD_T8K_OCC(7) SVGD_T8K_OCC(8)
+            SVGD_T8K_OCC(9) SVGD_T8K_OCC(10) SVGD_T8K_OCC(11) SVGD_T8K_OCC(12)
+            SVGD_T8K_OCC(13) SVGD_T8K_OCC(14) SVGD_T8K_OCC(15) SVGD_T8K_OCC(16)
+        default:
+            break;
+        }
+#undef SVGD_T8K_OCC
         return (e == hipSuccess && nb > 0) ? nb : 1;
     }
     if (kind == 1) {

@@ -60,6 +60,28 @@ def test_phi_random_shapes(oracle, n, d):
     assert np.max(np.abs(ph - ref)) <= PHI_TOL
 
 
+@pytest.mark.parametrize("n,d", [(1, 2), (5, 8), (200, 8), (1000, 8), (2049, 8), (4000, 2),
+                                 (777, 3), (130, 12), (70, 16)])
+def test_phi_row_kernel_variants(oracle, monkeypatch, n, d):
+    """The row stream's two work-group shapes: the default (kind 2: 8 waves
+    splitting one row group's columns, their sums added in LDS in wave order)
+    and the 4-wave kernel (SVGD_PHI_T8K=0, one partial per wave's rows).  Both
+    against the oracle; against each other only the summation order differs."""
+    X = oracle.splitmix((n, d), 2.0, 500 + n + d)
+    G = oracle.splitmix((n, d), 1.0, 600 + n + d)
+    a = 0.29
+    ref = oracle.phi(X, G, a)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SVGD_PHI_T8K", v)
+        c = _ctx(X)
+        out[v] = c.phi(G, a)
+        assert np.array_equal(out[v], c.phi(G, a))  # deterministic
+        c.close()
+        assert np.max(np.abs(out[v] - ref)) <= PHI_TOL, v
+    assert np.max(np.abs(out["1"] - out["0"])) <= 1e-12
+
+
 def test_phi_far_from_origin(oracle):
     """Translation: particles around 1e3 (mean-centring keeps the x_i*sum K -
     sum K x_j assembly accurate)."""
