@@ -469,6 +469,10 @@ def main():
                              "job": per_step(host_timed["host_job_ms"], host_timed["steps"]),
                              "caller_wait": per_step(host_timed["host_wait_ms"], host_timed["steps"]),
                              "threads": host_timed["host_threads"]},
+        # speculative steps whose median bracket was predicted from the last
+        # medians (no sample), and of those the ones redone after a miss
+        "tracked_brackets": {"steps": int(host_timed["steps"]), "predicted": int(host_timed["trk_steps"]),
+                             "missed": int(host_timed["trk_miss"])},
     }
     if diag is not None:
         mine["diag_ms_per_step"] = {
@@ -549,6 +553,7 @@ def main():
             },
             "phases_ms_per_step": mine["phases_ms_per_step"],
             "host_ms_per_step": mine["host_ms_per_step"],
+            "tracked_brackets": mine["tracked_brackets"],
             "diag_ms_per_step": mine.get("diag_ms_per_step"),
             "gpu_timed": gpu_timed,
             "gpu_diag": gpu_diag,

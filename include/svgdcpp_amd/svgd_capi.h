@@ -197,7 +197,10 @@ int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *c
  *   HOST_JOB_MS      worker job: post -> last G chunk landed
  *   HOST_WAIT_MS     calling thread waiting for the worker after queuing the median
  *   RANKS            ranks in the communicator (1 without one)
- *   HOST_THREADS     OpenMP threads of the host gradient */
+ *   HOST_THREADS     OpenMP threads of the host gradient
+ *   TRK_STEPS        speculative steps whose median bracket was predicted from
+ *                    the previous steps' medians (no sample, no bracket passes)
+ *   TRK_MISS         of those, steps redone because the bracket missed */
 #define SVGD_DIAG_STEPS 0
 #define SVGD_DIAG_PHI_KERNEL_MS 1
 #define SVGD_DIAG_PHI_KERNEL_N 2
@@ -213,7 +216,9 @@ int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *c
 #define SVGD_DIAG_HOST_WAIT_MS 12
 #define SVGD_DIAG_RANKS 13
 #define SVGD_DIAG_HOST_THREADS 14
-#define SVGD_DIAG_LEN 15
+#define SVGD_DIAG_TRK_STEPS 15
+#define SVGD_DIAG_TRK_MISS 16
+#define SVGD_DIAG_LEN 17
 int svgd_get_diagnostics(svgd_ctx *ctx, double *out, int cap);
 /* Median tuning knobs (tests force each path): pair count at or below which
  * all keys are stored (direct path), sample size, candidate capacity.

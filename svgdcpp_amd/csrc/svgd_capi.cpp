@@ -307,6 +307,25 @@ struct svgd_ctx {
     hipEvent_t phi_end = nullptr, ev_xready_use = nullptr;
     hipEvent_t last_phi_end = nullptr; // the last phi phase's end (timing): the next median's start
     double *bak = nullptr; // [X_t | m_t | v_t] of this rank's rows for the pending step
+
+    // Bracket tracking (speculative steps, row path): the median of D^2 moves
+    // smoothly from step to step, so the collect pass's bracket is predicted
+    // from the last selected keys (linear extrapolation, half-width from the
+    // observed prediction errors) instead of a sample and its two radix
+    // passes.  The selection stays exact; a bracket that misses the order
+    // statistics is a failed plan, and the step is redone with a sample.
+    bool trk_allowed = true;    // SVGD_TRACK_BRACKET=0 disables
+    double trk_min_w = 2e-5;    // SVGD_TRACK_MIN_WIDTH: relative half-width floor
+    double trk_err_mult = 4.0;  // SVGD_TRACK_ERR_MULT: half-width / recent error
+    uint64_t *h_trk = nullptr, *h_trk_dev = nullptr; // pinned [lo, hi, below, cand, key0, key1, err]
+    double trk_m[2] = {0, 0};   // last selected D^2 (lower order statistic), newest first
+    int trk_n = 0;
+    double trk_err[3] = {0, 0, 0}; // recent relative prediction errors
+    int trk_nerr = 0;
+    double trk_dens = 0;        // candidates per unit of D^2 in the last bracket (all ranks)
+    double trk_pred = -1;       // this step's predicted median D^2 (< 0: sampled bracket)
+    bool trk_keys = false;      // this step's k_select_small writes h_trk
+    int64_t trk_steps = 0, trk_miss = 0;
 };
 
 namespace {
@@ -566,10 +585,63 @@ int sample_bracket(svgd_ctx *c, bool preset);
 int collect_counts(svgd_ctx *c);
 int median_finish_spec(svgd_ctx *c, double logn);
 
+double key_value(uint64_t k) { return __builtin_bit_cast(double, k); }
+
+// A resolved selection -> the tracking history: the selected lower key, the
+// error of the prediction the last steps implied, the bracket's density.
+void trk_record(svgd_ctx *c, uint64_t lo_key, uint64_t hi_key, uint64_t cand)
+{
+    const double m = key_value(c->h_trk[4]);
+    if (c->h_trk[6] || !(m > 0.0) || !std::isfinite(m)) {
+        c->trk_n = 0;
+        return;
+    }
+    if (c->trk_n >= 2) {
+        const double p = c->trk_pred >= 0 ? c->trk_pred : 2.0 * c->trk_m[0] - c->trk_m[1];
+        c->trk_err[2] = c->trk_err[1];
+        c->trk_err[1] = c->trk_err[0];
+        c->trk_err[0] = std::fabs(m - p) / m;
+        c->trk_nerr = std::min(c->trk_nerr + 1, 3);
+    }
+    const double lo = key_value(lo_key);
+    const double hi = hi_key >= 0x7ff0000000000000ull ? INFINITY : key_value(hi_key);
+    c->trk_dens = (std::isfinite(hi) && hi > lo) ? (double)cand / (hi - lo) : 0.0;
+    c->trk_m[1] = c->trk_m[0];
+    c->trk_m[0] = m;
+    c->trk_n = std::min(c->trk_n + 1, 2);
+}
+
+// The predicted bracket for this step, or false (sample it): the predicted
+// band must not hold more candidates than the sampled bracket's would
+// (band_samp: its expected share of the pairs).
+bool trk_predict(svgd_ctx *c, double Mq, double band_samp, uint64_t *lo_key, uint64_t *hi_key,
+                 double *band_frac)
+{
+    if (!c->trk_allowed || c->trk_n < 2 || !(c->trk_dens > 0.0)) return false;
+    const double m1 = c->trk_m[0], m2 = c->trk_m[1];
+    double pred = 2.0 * m1 - m2;
+    if (!(pred > 0.0)) pred = m1;
+    double e = 0.0;
+    if (c->trk_nerr == 0) e = std::fabs(m1 - m2) / m1; // no error seen yet: the drift itself
+    for (int k = 0; k < c->trk_nerr; ++k) e = std::max(e, c->trk_err[k]);
+    const double w = std::max(c->trk_err_mult * e, c->trk_min_w);
+    if (!(w < 0.05)) return false;
+    const double lo = pred * (1.0 - w), hi = pred * (1.0 + w);
+    const double band = c->trk_dens * (hi - lo) / Mq;
+    if (!(band <= band_samp)) return false;
+    *lo_key = __builtin_bit_cast(uint64_t, lo);
+    *hi_key = __builtin_bit_cast(uint64_t, hi) + 1;
+    *band_frac = band;
+    c->trk_pred = pred;
+    return true;
+}
+
 // Phase 1 of the median: candidate bracket + collect pass + counts.
 // Leaves the reduced counts in c->h_cnt (ready at c->ev_cnt).
 int median_begin(svgd_ctx *c)
 {
+    c->trk_pred = -1;
+    c->trk_keys = false;
     const int64_t n = c->n;
     int64_t rlo, rhi;
     c->navg = svgd_plan_median_ranks(n, &rlo, &rhi);
@@ -631,6 +703,31 @@ int median_begin(svgd_ctx *c)
         if (multi && !c->shard_sample && c->sample_size <= 0)
             S = std::min<int64_t>(S, int64_t(1) << 20); // every rank draws all of it
         S = std::min<int64_t>(S, M);
+        const double Mq = c->sim_world > 1 ? (double)c->sim_pairs : (double)M;
+        uint64_t tlo = 0, thi = 0;
+        double tband = 0;
+        if (c->spec_step && c->rowpath && c->sample_size <= 0 && c->cand_capacity <= 0) {
+            // the sampled bracket's expected share (sample_state at q = 1/2)
+            const double sig = std::sqrt((double)S * 0.25) + 1.0;
+            const double band_samp = (2.0 * c->bracket_sigma * sig + 3.0) / (double)S;
+            if (trk_predict(c, Mq, band_samp, &tlo, &thi, &tband)) {
+                // predicted bracket: no sample, no radix passes (k_center
+                // zeroed the bucket counts); regions sized for 4x the band
+                c->trk_steps += 1;
+                c->band_est = tband;
+                HIPCHK(c, launch_set_state(make_state(1, &tlo, tlo, thi), c->st, c->stream));
+                const int64_t pairs_own = tiles * c->pblock * c->pblock;
+                const int64_t total = (int64_t)(4.0 * tband * (double)pairs_own) + 2048 * c->nregions;
+                c->reg_cap = std::max<int64_t>(1, total / c->nregions);
+                const int64_t need = c->reg_cap * c->nregions;
+                if (c->regions_alloc < need) {
+                    CHK(dalloc(c, &c->regions, need));
+                    CHK(dalloc(c, &c->cbuf, need));
+                    c->regions_alloc = need;
+                }
+                return collect_counts(c);
+            }
+        }
         if (c->sim_world > 1 && c->shard_sample) S = std::max<int64_t>(1, S / c->sim_world); // a rank's share
         const bool tile_sample = tile_path && S >= TB * TB;
         if (tile_sample) S = S / (TB * TB) * (TB * TB);
@@ -648,7 +745,6 @@ int median_begin(svgd_ctx *c)
         const int64_t g0 = c->samp_shard ? S * c->rank / c->world : 0;
         c->samp_local = c->samp_shard ? S * (c->rank + 1) / c->world - g0 : S;
         c->samp_S = S;
-        const double Mq = c->sim_world > 1 ? (double)c->sim_pairs : (double)M;
         c->samp_qlo = (double)c->sel_rank[0] / Mq;
         c->samp_qhi = (double)c->sel_rank[c->nsel - 1] / Mq;
         // whole-tile samples are correlated (a far particle shifts its tile's
@@ -755,12 +851,13 @@ int median_finish_spec(svgd_ctx *c, double logn)
     // (the compaction's blocks derive the bucket plan themselves: no plan launch)
     const PlanArgs pa{c->cnt3, c->nsel, (uint64_t)c->sel_rank[0], (uint64_t)c->sel_rank[c->nsel - 1],
                       std::min<int64_t>(c->bucket_cap, CAPR), c->d_status, c->h_status_dev,
-                      c->sim_world > 1 ? 1 : 0};
+                      c->sim_world > 1 ? 1 : 0, c->h_trk_dev};
     HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
                                      c->d_status, c->stream, &pa));
     CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
     HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, CAPR, c->navg, c->src_lo, c->src_hi, logn,
-                                  c->scal, c->d_status, c->stream));
+                                  c->scal, c->d_status, c->stream, c->h_trk_dev));
+    c->trk_keys = true;
     // the plan's status is final once this completes (recorded after the
     // selection: an event between two kernels costs a ~5 us dispatch gap)
     // (c->pending -- the plan's status to check -- is set when the step is
@@ -857,7 +954,8 @@ int median_finish(svgd_ctx *c)
                                              seg, scap, nullptr, c->stream));
             CHK(allgather_u64(c, c->gseg, (size_t)scap + 1));
             HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, scap, c->navg, c->src_lo,
-                                          c->src_hi, logn, c->scal, nullptr, c->stream));
+                                          c->src_hi, logn, c->scal, nullptr, c->stream, c->h_trk_dev));
+            c->trk_keys = true;
             c->last_path = path;
             // the next step may take the device plan if this one would have
             c->last_fast = (path == SVGD_MEDIAN_BRACKET || path == SVGD_MEDIAN_DIRECT) &&
@@ -1227,7 +1325,11 @@ int resolve_pending(svgd_ctx *c)
     if (!c->pending) return SVGD_OK;
     c->pending = false;
     HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
-    if (*c->h_status == 0) return SVGD_OK;
+    if (*c->h_status == 0) {
+        if (c->trk_allowed) trk_record(c, c->h_trk[0], c->h_trk[1], c->h_trk[3]);
+        return SVGD_OK;
+    }
+    if (c->trk_pred >= 0) c->trk_miss += 1;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     HIPCHK(c, hipStreamSynchronize(c->cstream));
     // this rank's rows of X_t, m_t, v_t back, then X_t all-gathered again
@@ -1246,6 +1348,13 @@ int resolve_pending(svgd_ctx *c)
     CHK(scale_begin(c));
     CHK(scale_finish(c));
     CHK(run_phi_opt(c));
+    // the redo's selection (synchronous path) continues the tracking history
+    if (c->trk_allowed && c->trk_keys) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        trk_record(c, c->h_cnt[CNT_LO], c->h_cnt[CNT_HI], c->h_cnt[1]);
+    } else {
+        c->trk_n = 0;
+    }
     return SVGD_OK;
 }
 
@@ -1441,7 +1550,13 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     HIPCHK(c, hipHostMalloc((void **)&c->h_status, sizeof(int), hipHostMallocCoherent));
     *c->h_status = 0;
     HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_status_dev, c->h_status, 0));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_trk, 8 * sizeof(uint64_t), hipHostMallocCoherent));
+    std::memset(c->h_trk, 0, 8 * sizeof(uint64_t));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_trk_dev, c->h_trk, 0));
     if (const char *e = std::getenv("SVGD_SPECULATE")) c->spec_allowed = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SVGD_TRACK_BRACKET")) c->trk_allowed = std::atoi(e) != 0;
+    if (const char *e = std::getenv("SVGD_TRACK_MIN_WIDTH")) c->trk_min_w = std::atof(e);
+    if (const char *e = std::getenv("SVGD_TRACK_ERR_MULT")) c->trk_err_mult = std::atof(e);
     c->host_threads = std::max(1, omp_get_max_threads() / 2);
     if (const char *e = std::getenv("SVGD_HOST_THREADS")) c->host_threads = std::max(1, std::atoi(e));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1530,7 +1645,7 @@ int svgd_destroy(svgd_ctx *c)
                      c->bpart,       c->gseg, c->symok};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
-    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err, c->h_status};
+    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
     for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})
@@ -2070,11 +2185,14 @@ int svgd_get_diagnostics(svgd_ctx *c, double *out, int cap)
                                      c->h_job_ms,
                                      c->h_wait_ms,
                                      (double)ranks,
-                                     (double)c->host_threads};
+                                     (double)c->host_threads,
+                                     (double)c->trk_steps,
+                                     (double)c->trk_miss};
     for (int i = 0; i < cap && i < SVGD_DIAG_LEN; ++i) out[i] = v[i];
     for (int k = 0; k < 4; ++k) c->dg_ms[k] = 0, c->dg_cnt[k] = 0;
     c->h_grad_ms = c->h_xwait_ms = c->h_job_ms = c->h_wait_ms = 0;
     c->h_steps = 0;
+    c->trk_steps = c->trk_miss = 0;
     return cap < SVGD_DIAG_LEN ? cap : SVGD_DIAG_LEN;
 }
 

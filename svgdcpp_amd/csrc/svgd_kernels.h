@@ -138,6 +138,9 @@ struct PlanArgs {
     // SVGD_SIM_WORLD measurement mode: one rank's share is selected alone, so
     // r0 is re-anchored at the middle of its candidates (r1 keeps r1 - r0)
     int sim = 0;
+    // bracket tracking (optional, pinned host memory): [0] lo_key, [1] hi_key,
+    // [2] below, [3] candidates of this step's bracket (block 0 of the plan)
+    uint64_t *trk = nullptr;
 };
 hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, int64_t nreg,
                                   int64_t cap, SelState *st, uint64_t *seg, int64_t seg_cap,
@@ -146,9 +149,10 @@ hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, 
 // exact selection of st->rank[s] within bucket st->bsel[s] over nseg gathered
 // segments [count, keys...] of stride seg_cap + 1 -> st->prefix[s] = that key,
 // then the scale as launch_finalize
+// trk (optional, pinned host memory): [4], [5] <- the selected keys, [6] <- error
 hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
                                int navg, int src_lo, int src_hi, double logn, double *scal,
-                               const int *status, hipStream_t stream);
+                               const int *status, hipStream_t stream, uint64_t *trk = nullptr);
 // Device-side bucket plan from the all-reduced counts (speculative step): the
 // select state, seg[0] = 0 and *status = 0, or *status = 1 (bracket miss),
 // 2 (overflowed region), 3 (selected buckets hold > capr keys), also stored to

@@ -1160,7 +1160,15 @@ __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restr
         // speculative step: every block derives the bucket plan from the
         // all-reduced counts itself (no plan launch); block 0 publishes it
         const PlanOut o = plan_block(pa.cnt, pa.nsel, pa.r0, pa.r1, pa.capr, pa.sim);
-        if (blockIdx.x == 0 && threadIdx.x == 0) plan_publish(o, st, pa.nsel, pa.status, pa.host_status);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (pa.trk) { // this step's bracket and counts for the host's bracket tracking
+                pa.trk[0] = st->lo_key;
+                pa.trk[1] = st->hi_key;
+                pa.trk[2] = pa.cnt[0];
+                pa.trk[3] = pa.cnt[1];
+            }
+            plan_publish(o, st, pa.nsel, pa.status, pa.host_status);
+        }
         if (o.status != 0) return;
         nsel = pa.nsel;
         b0 = o.b0;
@@ -1268,7 +1276,8 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
                                                       int nseg, int64_t seg_cap, int navg,
                                                       int src_lo, int src_hi, double logn,
                                                       double *__restrict__ scal,
-                                                      const int *__restrict__ status)
+                                                      const int *__restrict__ status,
+                                                      uint64_t *__restrict__ trk)
 {
     if (status && *status != 0) return; // the device plan found no bucket path
     __shared__ uint32_t sHist[2][RADIX];
@@ -1393,6 +1402,11 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
         st->prefix[0] = prefix[0];
         if (nsel > 1) st->prefix[1] = prefix[1];
         finalize_scale(st, navg, src_lo, src_hi, logn, scal, scal + 1);
+        if (trk) { // the selected keys for the host's bracket tracking
+            trk[4] = prefix[0];
+            trk[5] = nsel > 1 ? prefix[1] : prefix[0];
+            trk[6] = err ? 1 : 0;
+        }
     }
 }
 
@@ -3858,10 +3872,10 @@ hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, 
 
 hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
                                int navg, int src_lo, int src_hi, double logn, double *scal,
-                               const int *status, hipStream_t stream)
+                               const int *status, hipStream_t stream, uint64_t *trk)
 {
     hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg, seg_cap,
-                       navg, src_lo, src_hi, logn, scal, status);
+                       navg, src_lo, src_hi, logn, scal, status, trk);
     return hipGetLastError();
 }
 
