@@ -310,15 +310,15 @@ struct svgd_ctx {
 
     // Bracket tracking (speculative steps, row path): the median of D^2 moves
     // smoothly from step to step, so the collect pass's bracket is predicted
-    // from the last selected keys (linear extrapolation, half-width from the
-    // observed prediction errors) instead of a sample and its two radix
-    // passes.  The selection stays exact; a bracket that misses the order
+    // from the last selected keys (quadratic extrapolation, half-width 4x the
+    // largest of the last 3 prediction errors) instead of a sample and its two
+    // radix passes.  The selection stays exact; a bracket that misses the order
     // statistics is a failed plan, and the step is redone with a sample.
     bool trk_allowed = true;    // SVGD_TRACK_BRACKET=0 disables
     double trk_min_w = 2e-5;    // SVGD_TRACK_MIN_WIDTH: relative half-width floor
     double trk_err_mult = 4.0;  // SVGD_TRACK_ERR_MULT: half-width / recent error
     uint64_t *h_trk = nullptr, *h_trk_dev = nullptr; // pinned [lo, hi, below, cand, key0, key1, err]
-    double trk_m[2] = {0, 0};   // last selected D^2 (lower order statistic), newest first
+    double trk_m[3] = {0, 0, 0}; // last selected D^2 (lower order statistic), newest first
     int trk_n = 0;
     double trk_err[3] = {0, 0, 0}; // recent relative prediction errors
     int trk_nerr = 0;
@@ -587,6 +587,15 @@ int median_finish_spec(svgd_ctx *c, double logn);
 
 double key_value(uint64_t k) { return __builtin_bit_cast(double, k); }
 
+// The next median D^2 from the last 2 or 3 (quadratic through 3 points: on
+// SVGD trajectories its errors are ~5x below the linear one's, 1e-4..5e-4)
+double trk_extrapolate(const svgd_ctx *c)
+{
+    const double *m = c->trk_m;
+    double p = c->trk_n >= 3 ? 3.0 * m[0] - 3.0 * m[1] + m[2] : 2.0 * m[0] - m[1];
+    return p > 0.0 ? p : m[0];
+}
+
 // A resolved selection -> the tracking history: the selected lower key, the
 // error of the prediction the last steps implied, the bracket's density.
 void trk_record(svgd_ctx *c, uint64_t lo_key, uint64_t hi_key, uint64_t cand)
@@ -597,7 +606,7 @@ void trk_record(svgd_ctx *c, uint64_t lo_key, uint64_t hi_key, uint64_t cand)
         return;
     }
     if (c->trk_n >= 2) {
-        const double p = c->trk_pred >= 0 ? c->trk_pred : 2.0 * c->trk_m[0] - c->trk_m[1];
+        const double p = c->trk_pred >= 0 ? c->trk_pred : trk_extrapolate(c);
         c->trk_err[2] = c->trk_err[1];
         c->trk_err[1] = c->trk_err[0];
         c->trk_err[0] = std::fabs(m - p) / m;
@@ -606,9 +615,10 @@ void trk_record(svgd_ctx *c, uint64_t lo_key, uint64_t hi_key, uint64_t cand)
     const double lo = key_value(lo_key);
     const double hi = hi_key >= 0x7ff0000000000000ull ? INFINITY : key_value(hi_key);
     c->trk_dens = (std::isfinite(hi) && hi > lo) ? (double)cand / (hi - lo) : 0.0;
+    c->trk_m[2] = c->trk_m[1];
     c->trk_m[1] = c->trk_m[0];
     c->trk_m[0] = m;
-    c->trk_n = std::min(c->trk_n + 1, 2);
+    c->trk_n = std::min(c->trk_n + 1, 3);
 }
 
 // The predicted bracket for this step, or false (sample it): the predicted
@@ -619,8 +629,7 @@ bool trk_predict(svgd_ctx *c, double Mq, double band_samp, uint64_t *lo_key, uin
 {
     if (!c->trk_allowed || c->trk_n < 2 || !(c->trk_dens > 0.0)) return false;
     const double m1 = c->trk_m[0], m2 = c->trk_m[1];
-    double pred = 2.0 * m1 - m2;
-    if (!(pred > 0.0)) pred = m1;
+    const double pred = trk_extrapolate(c);
     double e = 0.0;
     if (c->trk_nerr == 0) e = std::fabs(m1 - m2) / m1; // no error seen yet: the drift itself
     for (int k = 0; k < c->trk_nerr; ++k) e = std::max(e, c->trk_err[k]);

@@ -36,13 +36,15 @@ def _pair(oracle, monkeypatch, n, d, env):
 def test_tracked_brackets_bit_identical(oracle, monkeypatch, n, d):
     (a, b), model = _pair(oracle, monkeypatch, n, d, {})
     a.diagnostics()
-    for step in range(14):
+    for step in range(16):
         for c in (a, b):
             c.step_with_model(model)
         assert np.array_equal(a.get_particles(), b.get_particles()), step
         assert a.last_scale()[:2] == b.last_scale()[:2], step
     da, db = a.diagnostics(), b.diagnostics()
-    assert da["trk_steps"] >= 5  # predicted from the third speculative step on
+    # predicted once the prediction errors are small enough for a bracket
+    # narrower than the sampled one (quadratic extrapolation needs 3 medians)
+    assert da["trk_steps"] >= 3
     assert db["trk_steps"] == 0
     a.close()
     b.close()
