@@ -324,6 +324,9 @@ struct svgd_ctx {
     int trk_nerr = 0;
     double trk_dens = 0;        // candidates per unit of D^2 in the last bracket (all ranks)
     double trk_pred = -1;       // this step's predicted median D^2 (< 0: sampled bracket)
+    bool trk_go = false;        // this step's bracket is the predicted one (trk_plan)
+    uint64_t trk_lo = 0, trk_hi = 0;
+    double trk_band = 0;        // its expected share of the pairs
     bool trk_keys = false;      // this step's k_select_small writes h_trk
     int64_t trk_steps = 0, trk_miss = 0;
 };
@@ -510,10 +513,16 @@ int allreduce_f64(svgd_ctx *c, double *buf, size_t cnt)
 
 // --------------------------------------------------------------- median --
 
-int center(svgd_ctx *c)
+SelState make_state(int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key,
+                    int known_from = 63, uint64_t prefix = 0);
+
+// st_init (optional): the predicted bracket's select state, written by the
+// centring launch itself (no launch of its own)
+int center(svgd_ctx *c, const SelState *st_init = nullptr)
 {
     HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
-                                 c->nrm, c->rowpath ? 1 : 0, c->xf, c->nmax, c->cnt3 + 3, c->stream));
+                                 c->nrm, c->rowpath ? 1 : 0, c->xf, c->nmax, c->cnt3 + 3, c->stream,
+                                 c->st, st_init));
     if (c->dtype == SVGD_F32) {
         HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
         HIPCHK(c, launch_cvt_f32(c->nrm, c->np, c->nrmf, c->stream));
@@ -525,7 +534,7 @@ int center(svgd_ctx *c)
 // selected key are already known to equal those of `prefix` (64: nothing
 // known; keys are < 2^63); the first digit is the RADIX_BITS below them.
 SelState make_state(int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t hi_key,
-                    int known_from = 63, uint64_t prefix = 0)
+                    int known_from, uint64_t prefix)
 {
     SelState s{};
     s.nsel = nsel;
@@ -645,11 +654,51 @@ bool trk_predict(svgd_ctx *c, double Mq, double band_samp, uint64_t *lo_key, uin
     return true;
 }
 
+// The default sample size of the bracket passes for M unordered pairs.
+int64_t sample_size(const svgd_ctx *c, int64_t M)
+{
+    // sample size: the band it leaves costs the collect pass, sampling and
+    // the two bracket passes cost ~S; measured optimum near M / 256 pairs
+    // (cfg2, M = 1.3e8: 2^19 -> median 0.222 vs 0.262 ms at 2^22), capped
+    // at 2^22 (cfg3, M = 2.1e9)
+    // tile path: whole random 64 x 64 tiles (MFMA Gram, ~1/1000 of the
+    // collect pass) instead of scattered pairs (2 random 8d-byte rows each).
+    // Its keys come in correlated 4096-key tiles, so it keeps 2^22 (1024
+    // tiles) whatever M: the bracket's sigma assumes many independent draws.
+    const bool tile_path = !c->rowpath && c->n / TB >= 2;
+    int64_t S = c->sample_size > 0 ? c->sample_size
+                : tile_path       ? int64_t(1) << 22
+                                  : std::min<int64_t>(std::max<int64_t>(M / 256, int64_t(1) << 18),
+                                                      int64_t(1) << 22);
+    const bool multi = c->comm || c->hcomm || c->sim_world > 1;
+    if (multi && !c->shard_sample && c->sample_size <= 0)
+        S = std::min<int64_t>(S, int64_t(1) << 20); // every rank draws all of it
+    return std::min<int64_t>(S, M);
+}
+
+// This step's bracket, decided before the centring launch (which then also
+// writes the predicted select state): predicted on speculative row-path
+// steps when trk_predict allows it, else sampled in median_begin.
+void trk_plan(svgd_ctx *c)
+{
+    c->trk_go = false;
+    c->trk_pred = -1;
+    const int64_t M = upper_pairs(c->n);
+    if (!c->spec_step || !c->rowpath || c->sample_size > 0 || c->cand_capacity > 0 ||
+        M <= c->direct_max_pairs)
+        return;
+    const int64_t S = sample_size(c, M);
+    const double Mq = c->sim_world > 1 ? (double)c->sim_pairs : (double)M;
+    // the sampled bracket's expected share (sample_state at q = 1/2)
+    const double sig = std::sqrt((double)S * 0.25) + 1.0;
+    const double band_samp = (2.0 * c->bracket_sigma * sig + 3.0) / (double)S;
+    c->trk_go = trk_predict(c, Mq, band_samp, &c->trk_lo, &c->trk_hi, &c->trk_band);
+}
+
 // Phase 1 of the median: candidate bracket + collect pass + counts.
 // Leaves the reduced counts in c->h_cnt (ready at c->ev_cnt).
 int median_begin(svgd_ctx *c)
 {
-    c->trk_pred = -1;
     c->trk_keys = false;
     const int64_t n = c->n;
     int64_t rlo, rhi;
@@ -695,47 +744,25 @@ int median_begin(svgd_ctx *c)
         CHK(upload_state(c, 1, z, 0, ~0ull));
     } else {
         c->med_path = SVGD_MEDIAN_BRACKET;
-        // sample size: the band it leaves costs the collect pass, sampling and
-        // the two bracket passes cost ~S; measured optimum near M / 256 pairs
-        // (cfg2, M = 1.3e8: 2^19 -> median 0.222 vs 0.262 ms at 2^22), capped
-        // at 2^22 (cfg3, M = 2.1e9)
-        // tile path: whole random 64 x 64 tiles (MFMA Gram, ~1/1000 of the
-        // collect pass) instead of scattered pairs (2 random 8d-byte rows each).
-        // Its keys come in correlated 4096-key tiles, so it keeps 2^22 (1024
-        // tiles) whatever M: the bracket's sigma assumes many independent draws.
         const bool tile_path = !c->rowpath && n / TB >= 2;
-        int64_t S = c->sample_size > 0 ? c->sample_size
-                    : tile_path       ? int64_t(1) << 22
-                                      : std::min<int64_t>(std::max<int64_t>(M / 256, int64_t(1) << 18),
-                                                          int64_t(1) << 22);
-        const bool multi = c->comm || c->hcomm || c->sim_world > 1;
-        if (multi && !c->shard_sample && c->sample_size <= 0)
-            S = std::min<int64_t>(S, int64_t(1) << 20); // every rank draws all of it
-        S = std::min<int64_t>(S, M);
+        int64_t S = sample_size(c, M);
         const double Mq = c->sim_world > 1 ? (double)c->sim_pairs : (double)M;
-        uint64_t tlo = 0, thi = 0;
-        double tband = 0;
-        if (c->spec_step && c->rowpath && c->sample_size <= 0 && c->cand_capacity <= 0) {
-            // the sampled bracket's expected share (sample_state at q = 1/2)
-            const double sig = std::sqrt((double)S * 0.25) + 1.0;
-            const double band_samp = (2.0 * c->bracket_sigma * sig + 3.0) / (double)S;
-            if (trk_predict(c, Mq, band_samp, &tlo, &thi, &tband)) {
-                // predicted bracket: no sample, no radix passes (k_center
-                // zeroed the bucket counts); regions sized for 4x the band
-                c->trk_steps += 1;
-                c->band_est = tband;
-                HIPCHK(c, launch_set_state(make_state(1, &tlo, tlo, thi), c->st, c->stream));
-                const int64_t pairs_own = tiles * c->pblock * c->pblock;
-                const int64_t total = (int64_t)(4.0 * tband * (double)pairs_own) + 2048 * c->nregions;
-                c->reg_cap = std::max<int64_t>(1, total / c->nregions);
-                const int64_t need = c->reg_cap * c->nregions;
-                if (c->regions_alloc < need) {
-                    CHK(dalloc(c, &c->regions, need));
-                    CHK(dalloc(c, &c->cbuf, need));
-                    c->regions_alloc = need;
-                }
-                return collect_counts(c);
+        if (c->trk_go) {
+            // predicted bracket (trk_plan; its select state was written by
+            // the centring launch): no sample, no radix passes (k_center
+            // zeroed the bucket counts); regions sized for 4x the band
+            c->trk_steps += 1;
+            c->band_est = c->trk_band;
+            const int64_t pairs_own = tiles * c->pblock * c->pblock;
+            const int64_t total = (int64_t)(4.0 * c->trk_band * (double)pairs_own) + 2048 * c->nregions;
+            c->reg_cap = std::max<int64_t>(1, total / c->nregions);
+            const int64_t need = c->reg_cap * c->nregions;
+            if (c->regions_alloc < need) {
+                CHK(dalloc(c, &c->regions, need));
+                CHK(dalloc(c, &c->cbuf, need));
+                c->regions_alloc = need;
             }
+            return collect_counts(c);
         }
         if (c->sim_world > 1 && c->shard_sample) S = std::max<int64_t>(1, S / c->sim_world); // a rank's share
         const bool tile_sample = tile_path && S >= TB * TB;
@@ -1270,7 +1297,14 @@ int scale_begin(svgd_ctx *c)
         c->ev_med.push_back(ev);
     }
     c->last_phi_end = nullptr;
-    CHK(center(c));
+    c->trk_go = false;
+    if (med) trk_plan(c);
+    if (c->trk_go) {
+        const SelState st = make_state(1, &c->trk_lo, c->trk_lo, c->trk_hi);
+        CHK(center(c, &st));
+    } else {
+        CHK(center(c));
+    }
     if (!med) return SVGD_OK;
     return median_begin(c);
 }

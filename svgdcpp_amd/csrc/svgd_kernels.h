@@ -39,10 +39,12 @@ constexpr int CAPG = 16384;
 // xf (optional, d <= 16): fp32 median records [xc | -|xc|^2/2 | 0..] of stride
 // med_f32_stride(d); nmax_bits: max |xc|^2 as double bits (atomicMax).
 // bzero (optional): NBK counters zeroed (the step's collect-pass bucket counts)
+// st_init (optional): written to *st_out by the launch (a predicted bracket)
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
-                              unsigned long long *bzero, hipStream_t stream);
+                              unsigned long long *bzero, hipStream_t stream,
+                              SelState *st_out = nullptr, const SelState *st_init = nullptr);
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);

@@ -163,10 +163,11 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
                          const double *__restrict__ partial, int nparts, int64_t np,
                          double *__restrict__ xc, double *__restrict__ nrm, int nrm_in_slot,
                          float *__restrict__ xf, int KF, unsigned long long *nmax_bits,
-                         unsigned long long *bzero)
+                         unsigned long long *bzero, SelState *st_out, SelState st_init)
 {
     if (bzero && blockIdx.x == 0) // this step's collect-pass bucket counts
         for (int e = threadIdx.x; e < NBK; e += blockDim.x) bzero[e] = 0;
+    if (st_out && blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_init; // predicted bracket
     __shared__ double mu[256];
     for (int k = threadIdx.x; k < d; k += blockDim.x) {
         // partials added in b order; 8 loads in flight
@@ -231,11 +232,13 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
                                                   double *__restrict__ nrm, int nrm_in_slot,
                                                   float *__restrict__ xf,
                                                   unsigned long long *nmax_bits,
-                                                  unsigned long long *bzero)
+                                                  unsigned long long *bzero, SelState *st_out,
+                                                  SelState st_init)
 {
     constexpr int KP = med_rec_stride(D), KF = med_f32_stride(D);
     if (bzero && blockIdx.x == 0)
         for (int e = threadIdx.x; e < NBK; e += blockDim.x) bzero[e] = 0;
+    if (st_out && blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_init; // predicted bracket
     __shared__ double mu[D];
     __shared__ double sP[1024];
     // the first row's X is loaded before the mean (its latency overlaps the
@@ -1697,6 +1700,14 @@ __device__ __forceinline__ double exp2_4096_poly(double f)
 
 constexpr int CH_PHI = 16; // columns per LDS chunk of the phi row stream
 constexpr int EXP_TB = 4096; // row-stream exp table entries
+// Biased exponent (the 8-wave kernel, TABN = 8192): u' = u + EXP_UB >= 0 on
+// both forms (folded u >= -1001 x 4096, plain |u| <= 1000 x 4096), so
+// floor(u') = the truncating conversion and u' - floor(u') = v_fract_f64:
+// the range reduction takes 2 VALU instead of 3 (rint, sub, cvt).  The table
+// entries carry -(EXP_QB << 20) in their high word to undo the 2^EXP_QB.
+// c_j + EXP_UB is stored in the record's slot 2d + 1 (k_prep_rec).
+constexpr int EXP_QB = 1002;
+constexpr double EXP_UB = (double)EXP_QB * EXP_TB;
 
 // rec_j = [xc_j (D) | V_j = G_j - 2a xc_j (D) | c_j = -4096 a log2e |xc_j|^2 | 0 ...],
 // stride phi_rec_stride(D) = roundup(2D+1, 8) doubles, so CH_PHI records are
@@ -1796,6 +1807,8 @@ __global__ void k_prep_rec(const double *__restrict__ xc, const double *__restri
                 v = G[j * d + (k - d)] - 2.0 * a * xc[j * KP + (k - d)];
             else if (k == 2 * d)
                 v = -4096.0 * a * LOG2E * nrm[j];
+            else if (k == 2 * d + 1)
+                v = -4096.0 * a * LOG2E * nrm[j] + EXP_UB;
         }
         rec[e] = v;
     }
@@ -1816,18 +1829,25 @@ __device__ __forceinline__ double tab_scale(double tb, int ki)
     return __hiloint2double(__double2hiint(tb) + (ki << 8), __double2loint(tb));
 }
 constexpr double EXP_U_CLAMP = 1000.0 * EXP_TB; // |u| bound of the clamped (plain) form
+// 2^(f/4096) on f in [0, 1) (minimax, relative error 2.54e-14; tools/exp_poly_fit.py)
+__device__ __forceinline__ double exp2_4096_poly01(double f)
+{
+    return fma(fma(0x1.ec0687f62a7d5p-27, f, 0x1.62e42fdfa8275p-13), f, 0x1.0000000000071p+0);
+}
 
 // One column record of the phi row stream, held in registers.
+// CS: the slot of c_j (2D: c_j; 2D + 1: c_j + EXP_UB, the biased-exponent
+// kernels' folded form)
 template <int D> struct ColRec {
     double x[D], v[D], c;
-    __device__ __forceinline__ void load(const double *rj)
+    template <int CS = 2 * D> __device__ __forceinline__ void load(const double *rj)
     {
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             x[k] = rj[k];
             v[k] = rj[D + k];
         }
-        c = rj[2 * D];
+        c = rj[CS];
     }
 };
 
@@ -1848,11 +1868,14 @@ __device__ __forceinline__ uint32_t tab8k_offset(int ki)
     return a;
 }
 
+// TABN = 8192: the biased exponent (EXP_UB): q.c is c_j + EXP_UB (folded)
+// and ci is c_i + EXP_UB (plain form), so u >= 0 here.
 template <int D, int R, bool FOLD, int TABN = EXP_TB>
 __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (&xs)[R][D],
                                               const double (&ci)[R], double (&acc)[R][D],
                                               double (&acc1)[R], const double *tab)
 {
+    constexpr bool BIAS = TABN == 8192;
     // the R rows' chains interleaved (independent FMAs back to back)
     double u[R], K[R];
 #pragma unroll
@@ -1862,8 +1885,10 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
 #pragma unroll
         for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], q.x[k], u[r]);
     if constexpr (!FOLD) {
+        constexpr double lo = BIAS ? EXP_UB - EXP_U_CLAMP : -EXP_U_CLAMP;
+        constexpr double hi = BIAS ? EXP_UB + EXP_U_CLAMP : EXP_U_CLAMP;
 #pragma unroll
-        for (int r = 0; r < R; ++r) u[r] = fmin(fmax(u[r], -EXP_U_CLAMP), EXP_U_CLAMP);
+        for (int r = 0; r < R; ++r) u[r] = fmin(fmax(u[r], lo), hi);
     }
     // exp2_256 in stages: the R table reads are issued together and their
     // LDS latency hides behind the R polynomials
@@ -1871,17 +1896,20 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
     int ki[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const double k = __builtin_rint(u[r]);
-        f[r] = u[r] - k;
-        ki[r] = (int)k;
-        if constexpr (TABN == 8192)
+        if constexpr (BIAS) {
+            f[r] = __builtin_amdgcn_fract(u[r]); // u >= 0: u - floor(u)
+            ki[r] = (int)u[r];                    // = floor(u)
             T[r] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(tab) + tab8k_offset(ki[r]));
-        else
+        } else {
+            const double k = __builtin_rint(u[r]);
+            f[r] = u[r] - k;
+            ki[r] = (int)k;
             T[r] = tab[ki[r] & (EXP_TB - 1)];
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < R; ++r) K[r] = exp2_4096_poly(f[r]);
+    for (int r = 0; r < R; ++r) K[r] = BIAS ? exp2_4096_poly01(f[r]) : exp2_4096_poly(f[r]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int r = 0; r < R; ++r) K[r] = K[r] * tab_scale(T[r], ki[r]);
@@ -1925,7 +1953,9 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
     for (int e = 0; e < TABN / (NW * 64); ++e) {
         const int m = e * NW * 64 + threadIdx.x;
         const double t = EXP2_TAB4096[m & (EXP_TB - 1)];
-        tab[m] = tab_biased(m >= EXP_TB ? 2.0 * t : t, m);
+        const double tb = tab_biased(m >= EXP_TB ? 2.0 * t : t, m);
+        // TABN = 8192: also -(EXP_QB << 20), undoing the exponent bias
+        tab[m] = TABN == 8192 ? __hiloint2double(__double2hiint(tb) - (EXP_QB << 20), __double2loint(tb)) : tb;
     }
     __syncthreads();
 
@@ -1983,8 +2013,10 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
     for (int r = 0; r < R; ++r) fold_ok = fold_ok && ci[r] >= -4096.0 * FOLD_MAX;
     const bool fold = __all(fold_ok);
     if (nch > 0) dma_to_lds<CHB>(gcol, wbuf, lane);
+    constexpr bool BIAS = TABN == 8192; // biased exponent (phi_rows_pair)
     auto stream_columns = [&](auto fold_tag) {
     constexpr bool FOLD = decltype(fold_tag)::value;
+    constexpr int CS = (BIAS && FOLD) ? 2 * D + 1 : 2 * D; // c_j (+ EXP_UB) slot
     for (int64_t c = 0; c < nch; ++c) {
         if (c + 1 < nch) {
             dma_to_lds<CHB>(gcol + (c + 1) * CHB, wbuf + ((c + 1) & 1) * CHB, lane);
@@ -2000,43 +2032,43 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
         if constexpr (!PIPE) {
             for (int jj = 0; jj < cnt; ++jj) {
                 ColRec<D> q;
-                q.load(cb + jj * RS);
+                q.template load<CS>(cb + jj * RS);
                 phi_rows_pair<D, R, FOLD, TABN>(q, xs, ci, acc, acc1, tab);
             }
             continue;
         }
         ColRec<D> qa, qb;
-        qa.load(cb);
+        qa.template load<CS>(cb);
         __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0): nothing pending at the loop head
         // (sched_barrier keeps the scheduler from sinking the prefetch reads
         // back down to their first use)
         // 4 columns per iteration without exit tests, then the 0..3 rest
         int jj = 0;
         for (; jj + 4 <= cnt; jj += 4) {
-            qb.load(cb + (jj + 1) * RS);
+            qb.template load<CS>(cb + (jj + 1) * RS);
             __builtin_amdgcn_sched_barrier(0);
             phi_rows_pair<D, R, FOLD, TABN>(qa, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
-            qa.load(cb + (jj + 2) * RS);
+            qa.template load<CS>(cb + (jj + 2) * RS);
             __builtin_amdgcn_sched_barrier(0);
             phi_rows_pair<D, R, FOLD, TABN>(qb, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
-            qb.load(cb + (jj + 3) * RS);
+            qb.template load<CS>(cb + (jj + 3) * RS);
             __builtin_amdgcn_sched_barrier(0);
             phi_rows_pair<D, R, FOLD, TABN>(qa, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
-            qa.load(cb + (jj + 4) * RS);
+            qa.template load<CS>(cb + (jj + 4) * RS);
             __builtin_amdgcn_sched_barrier(0);
             phi_rows_pair<D, R, FOLD, TABN>(qb, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
         }
         for (; jj < cnt; jj += 2) {
-            qb.load(cb + (jj + 1) * RS);
+            qb.template load<CS>(cb + (jj + 1) * RS);
             __builtin_amdgcn_sched_barrier(0);
             phi_rows_pair<D, R, FOLD, TABN>(qa, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
             if (jj + 1 >= cnt) break;
-            qa.load(cb + (jj + 2) * RS);
+            qa.template load<CS>(cb + (jj + 2) * RS);
             __builtin_amdgcn_sched_barrier(0);
             phi_rows_pair<D, R, FOLD, TABN>(qb, xs, ci, acc, acc1, tab);
             __builtin_amdgcn_sched_barrier(0);
@@ -2049,13 +2081,16 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const double k = __builtin_rint(ci[r]);
-            const int ki = (int)k; // in [-400 x 4096, 0]
+            const int ki = (int)k + (BIAS ? EXP_QB * EXP_TB : 0); // k in [-400 x 4096, 0]
             const double g = exp2_4096_poly(ci[r] - k) * tab_scale(tab[ki & (EXP_TB - 1)], ki);
 #pragma unroll
             for (int k2 = 0; k2 < D; ++k2) acc[r][k2] *= g;
             acc1[r] *= g;
         }
     } else {
+        if constexpr (BIAS)
+#pragma unroll
+            for (int r = 0; r < R; ++r) ci[r] += EXP_UB; // u = c_i + c_j + .. >= 0 after the clamp
         stream_columns(std::false_type{});
     }
 
@@ -3703,8 +3738,11 @@ hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
-                              unsigned long long *bzero, hipStream_t stream)
+                              unsigned long long *bzero, hipStream_t stream, SelState *st_out,
+                              const SelState *st_init)
 {
+    const SelState sinit = st_init ? *st_init : SelState{};
+    if (!st_init) st_out = nullptr;
     hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial,
                        xf ? nmax_bits : nullptr);
     int64_t g = (np + 255) / 256;
@@ -3712,7 +3750,7 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
 #define SVGD_CENTER_CASE(Dv)                                                                  \
     case Dv:                                                                                  \
         hipLaunchKernelGGL((k_center_d<Dv>), dim3(g), dim3(256), 0, stream, X, n, partial,    \
-                           nparts, np, xc, nrm, nrm_in_slot, xf, nmax_bits, bzero);            \
+                           nparts, np, xc, nrm, nrm_in_slot, xf, nmax_bits, bzero, st_out, sinit); \
         return hipGetLastError();
     if (d <= 16 && KP == med_rec_stride(d)) {
         switch (d) {
@@ -3726,7 +3764,7 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
     }
 #undef SVGD_CENTER_CASE
     hipLaunchKernelGGL(k_center, dim3(g), dim3(256), 0, stream, X, n, d, KP, partial, nparts, np,
-                       xc, nrm, nrm_in_slot, xf, med_f32_stride(d), nmax_bits, bzero);
+                       xc, nrm, nrm_in_slot, xf, med_f32_stride(d), nmax_bits, bzero, st_out, sinit);
     return hipGetLastError();
 }
 
