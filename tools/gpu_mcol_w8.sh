@@ -1,0 +1,12 @@
+#!/bin/bash
+# k_pair_mcol at 8 waves per SIMD (SVGD_MCOL_W8=1): the collect tests, then
+# A/B against the 4-wave kernel at cfg3 / cfg2 / sim-world 8
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/ab
+source tools/fault_guard.sh
+SVGD_MCOL_W8=1 timeout -k 10 900 python -u -m pytest tests/test_gpu_collect.py tests/test_gpu_fullsize.py tests/test_gpu_median_paths.py tests/test_gpu_track.py -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/ab/pytest_w8.log 2>&1; rc=$?
+echo "pytest w8 rc=$rc"; tail -3 gpurun_out/ab/pytest_w8.log; fault_guard gpurun_out/ab/pytest_w8.log; [ $rc -ne 0 ] && exit $rc
+VARIANTS="base SVGD_MCOL_W8=1" SKIP_PYTEST=1 bash tools/gpu_ab_phi.sh || exit 1
+VARIANTS="base SVGD_MCOL_W8=1" BENCH_ARGS="--config cfg2" SKIP_PYTEST=1 bash tools/gpu_ab_phi.sh || exit 1
+VARIANTS="base SVGD_MCOL_W8=1" BENCH_ARGS="--sim-world 8" SKIP_PYTEST=1 bash tools/gpu_ab_phi.sh || exit 1
+SVGD_MCOL_W8=1 CONFIGS="cfg3" bash tools/gpu_timeline.sh
