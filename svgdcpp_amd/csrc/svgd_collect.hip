@@ -3,7 +3,6 @@
 // kernels are not.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <cstdlib>
 #include <type_traits>
 
 #include "svgd_device.h"
@@ -130,13 +129,8 @@ template <int D> struct McolRow {
 // (B operands and thresholds, written when the row block changes), and wave w
 // takes the 16-column blocks w, w + 4, ...  Each wave stages its own band
 // pairs and owns region blockIdx * 4 + w, as k_pair_rows.
-// W8: 8 waves per SIMD (the kernel is latency-bound at 4: SQ counters show no
-// pipe above half busy) -- the row groups single-buffered (<= 64 VGPRs), the
-// key-range bucket counts as global atomics into the block's own slice of
-// bpart instead of an LDS histogram, 256 staged pairs per wave: 20 KiB of
-// LDS per work-group, 8 work-groups per CU.
-template <int D, bool W8>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4, 8))) void k_pair_mcol(const double *__restrict__ xc,
+template <int D>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_mcol(const double *__restrict__ xc,
                                                   const float *__restrict__ xf, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc)
@@ -146,17 +140,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4,
     constexpr int KK = McolRow<D>::KK;     // MFMA k-steps
     constexpr int RW = McolRow<D>::RW;
     constexpr int NI = PBLK / 16;          // 16-row blocks of a tile
-    constexpr int STG = W8 ? MC_STG / 2 : MC_STG; // staged band pairs per wave
-    constexpr int NG = W8 ? 2 : MC_NG;            // row blocks per classification group
     __shared__ __attribute__((aligned(16))) float sRow[NI * 64 * RW];
-    __shared__ uint32_t sStage[4][STG];
-    __shared__ uint32_t sBkL[W8 ? 1 : NBK];
+    __shared__ uint32_t sStage[4][MC_STG];
+    __shared__ uint32_t sBk[NBK];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int kq = lane >> 4, ql = lane & 15;
     uint32_t *stage = sStage[w];
-    // bucket counts: LDS (written to bpart at the end), or bpart directly (W8)
-    uint32_t *sBk = W8 ? (sc.bpart ? sc.bpart + (int64_t)blockIdx.x * NBK : nullptr) : sBkL;
 
     const uint64_t lo_key = sc.st->lo_key, hi_key = sc.st->hi_key;
     const double binv = sc.st->binv;
@@ -167,7 +157,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4,
     const double delta = nmax <= 0x1p40 ? 4.0 * (D + 4) * 0x1p-24 * nmax + 0x1p-100 : __builtin_inf();
     if (sc.bpart)
         for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
-    if constexpr (W8) __syncthreads(); // (the zeroed slice before any atomic)
 
     const int64_t wreg = (int64_t)blockIdx.x * 4 + w;
     uint64_t *wregion = sc.region + wreg * sc.cap;
@@ -311,17 +300,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4,
 #pragma unroll
                 for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
             };
-            // one group of NG row blocks: its row operands from LDS, its MFMAs
+            // one group of MC_NG row blocks: its row operands from LDS, its MFMAs
             auto group_mfma = [&](int g0, const f4 &hq, const float (&A)[KK],
-                                  float (&Bg)[NG][RW], f4 (&acc)[NG]) {
+                                  float (&Bg)[MC_NG][RW], f4 (&acc)[MC_NG]) {
 #pragma unroll
-                for (int g = 0; g < NG; ++g)
+                for (int g = 0; g < MC_NG; ++g)
 #pragma unroll
                     for (int q = 0; q < RW; q += 4)
                         *reinterpret_cast<f4 *>(&Bg[g][q]) =
                             *reinterpret_cast<const f4 *>(sRow + ((g0 + g) * 64 + lane) * RW + q);
 #pragma unroll
-                for (int g = 0; g < NG; ++g) {
+                for (int g = 0; g < MC_NG; ++g) {
                     acc[g] = hq;
 #pragma unroll
                     for (int kk = 0; kk < KK; ++kk)
@@ -340,20 +329,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4,
                 for (int jb = w; jb < njb; jb += 4) {
                     // (a block of 16 x 256 pairs stages ~10 band pairs; one that
                     // outgrows the area marks the region overflowed)
-                    if (scnt > STG / 2) flush(ib, jbase);
+                    if (scnt > MC_STG / 2) flush(ib, jbase);
                     if (jb + 4 < njb) load_cols(jb + 4, An, hqn);
                     const int jl0 = 16 * jb;
-                    float Bg[NG][RW], Bn[NG][RW];
-                    f4 acc[NG], accn[NG];
-                    if constexpr (!W8) group_mfma(0, hq, A, Bg, acc);
-                    for (int g0 = 0; g0 < NI; g0 += NG) {
-                        if constexpr (W8)
-                            group_mfma(g0, hq, A, Bg, acc); // single-buffered
-                        else if (g0 + NG < NI)
-                            group_mfma(g0 + NG, hq, A, Bn, accn);
+                    float Bg[MC_NG][RW], Bn[MC_NG][RW];
+                    f4 acc[MC_NG], accn[MC_NG];
+                    group_mfma(0, hq, A, Bg, acc);
+                    for (int g0 = 0; g0 < NI; g0 += MC_NG) {
+                        if (g0 + MC_NG < NI) group_mfma(g0 + MC_NG, hq, A, Bn, accn);
                         uint32_t nbelow = 0;
 #pragma unroll
-                        for (int g = 0; g < NG; ++g) {
+                        for (int g = 0; g < MC_NG; ++g) {
                             unsigned long long h[4], any = 0;
                             if constexpr (DIAG) {
 #pragma unroll
@@ -373,7 +359,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4,
                                     const unsigned long long m = h[r];
                                     if (!m) continue;
                                     const int c = __popcll(m);
-                                    if (scnt + c > STG) { // pathological band: give up
+                                    if (scnt + c > MC_STG) { // pathological band: give up
                                         ovf = true;      // (region overflow -> exact fallback)
                                         continue;
                                     }
@@ -385,13 +371,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4,
                             }
                         }
                         below += nbelow;
-                        if constexpr (!W8) {
 #pragma unroll
-                            for (int g = 0; g < NG; ++g) {
-                                acc[g] = accn[g];
+                        for (int g = 0; g < MC_NG; ++g) {
+                            acc[g] = accn[g];
 #pragma unroll
-                                for (int q = 0; q < RW; ++q) Bg[g][q] = Bn[g][q];
-                            }
+                            for (int q = 0; q < RW; ++q) Bg[g][q] = Bn[g][q];
                         }
                     }
 #pragma unroll
@@ -413,7 +397,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 4,
         // then takes the exact streamed fallback
         sc.count_out[wreg] = ovf ? 0xffffffffu : (uint32_t)min<int64_t>(wcnt, 0xffffffffll);
     }
-    if (sc.bpart && !W8) {
+    if (sc.bpart) {
         __syncthreads();
         for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
     }
@@ -747,12 +731,8 @@ hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm,
 
 #define SVGD_MCOL_CASE(Dv)                                                                   \
     case Dv:                                                                                 \
-        if (w8)                                                                              \
-            hipLaunchKernelGGL((k_pair_mcol<Dv, true>), dim3(grid), dim3(256), 0, stream, xc, xf, n, \
-                               nb, t0, t1, sc);                                              \
-        else                                                                                 \
-            hipLaunchKernelGGL((k_pair_mcol<Dv, false>), dim3(grid), dim3(256), 0, stream, xc, xf, n, \
-                               nb, t0, t1, sc);                                              \
+        hipLaunchKernelGGL((k_pair_mcol<Dv>), dim3(grid), dim3(256), 0, stream, xc, xf, n, nb, t0, \
+                           t1, sc);                                                          \
         break;
 
 hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
@@ -764,11 +744,6 @@ hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
     if (grid <= 0 || t1 <= t0) return hipSuccess;
     if (!nmax_bits || !xf) return hipErrorInvalidValue;
     SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, bpart};
-    // A/B knob: the 8-waves-per-SIMD variant (k_pair_mcol<D, true>)
-    static const bool w8 = [] {
-        const char *e = std::getenv("SVGD_MCOL_W8");
-        return e && std::atoi(e) != 0;
-    }();
     switch (d) {
         SVGD_MCOL_CASE(1)
         SVGD_MCOL_CASE(2)
