@@ -15,9 +15,10 @@ for p in (ROOT, os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
 
 
-def run(rank, world, name, n, d, steps, q):
+def run(rank, world, name, n, d, steps, q, env=None):
     try:
         os.environ["SVGD_HOSTCOMM"] = name
+        os.environ.update(env or {})
         import oracle as O
         import svgdcpp_amd as S
         from svgdcpp_amd import _capi as C
@@ -31,12 +32,14 @@ def run(rank, world, name, n, d, steps, q):
         ctx.set_bounds(-np.full(d, 2.5), np.full(d, 2.5))
         model = S.GaussianSum(list(mus), list(covs))
         scales = []
+        ctx.diagnostics()
         for _ in range(steps):
             ctx.step_with_model(model)
             scales.append(ctx.last_scale()[:3])
         X = ctx.get_particles()
         shard = (ctx.row0, ctx.row1)
+        trk = ctx.diagnostics()["trk_steps"]
         ctx.close()
-        q.put(("ok", rank, X, scales, shard))
+        q.put(("ok", rank, X, scales, shard, trk))
     except Exception:
-        q.put(("err", rank, traceback.format_exc(), None, None))
+        q.put(("err", rank, traceback.format_exc(), None, None, None))

@@ -17,19 +17,21 @@ import _gpu_rank_worker as W
 pytestmark = pytest.mark.gpu
 
 
-def _run_ranks(world, n, d, steps):
+def _run_ranks(world, n, d, steps, env=None, trk=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     name = "svgd_" + uuid.uuid4().hex[:12]
-    procs = [ctx.Process(target=W.run, args=(r, world, name, n, d, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=W.run, args=(r, world, name, n, d, steps, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
     try:
         for _ in range(world):
-            status, rank, X, scales, shard = q.get(timeout=300)
+            status, rank, X, scales, shard, ntrk = q.get(timeout=300)
             assert status == "ok", X
             out[rank] = (X, scales, shard)
+            if trk is not None:
+                trk[rank] = ntrk
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -56,3 +58,19 @@ def test_sharded_step_matches_single_rank(world, n):
         np.testing.assert_allclose([s[0] for s in scales], [s[0] for s in s1], rtol=1e-13)
         assert [s[2] for s in scales] == [s[2] for s in s1]
         np.testing.assert_allclose(X, X1, rtol=0, atol=1e-10)
+
+
+def test_sharded_tracked_brackets_bit_identical():
+    """The tracked median bracket on a sharded run (world 2): every rank
+    predicts the same bracket from the same all-reduced counts and selected
+    keys, and the trajectory is bit-identical to sampling every bracket."""
+    n, d, steps = 12007, 5, 14
+    trk = {}
+    tracked = _run_ranks(2, n, d, steps, {"SVGD_TRACK_BRACKET": "1"}, trk)
+    sampled = _run_ranks(2, n, d, steps, {"SVGD_TRACK_BRACKET": "0"})
+    assert min(trk.values()) >= 3 and trk[0] == trk[1]
+    for rank in (0, 1):
+        Xa, sa, _ = tracked[rank]
+        Xb, sb, _ = sampled[rank]
+        assert np.array_equal(Xa, Xb), rank
+        assert sa == sb, rank
