@@ -52,3 +52,13 @@ def test_rccl_one_rank_step_bit_identical(oracle, monkeypatch, n, d, bucket_cap)
     if n * (n - 1) // 2 > (1 << 24):
         assert all(s[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET, C.SVGD_MEDIAN_FALLBACK)
                    for s in sa)
+
+
+def test_rccl_one_rank_tracked_brackets(oracle, monkeypatch):
+    """16 steps through the one-rank RCCL communicator (G all-gather on its
+    own communicator and stream, tracked median brackets from the fourth
+    speculative step on) against the same steps without one: bit-identical."""
+    Xa, sa = _run(oracle, 6000, 8, 16, True, monkeypatch)
+    Xb, sb = _run(oracle, 6000, 8, 16, False, monkeypatch)
+    assert sa == sb
+    assert np.array_equal(Xa, Xb)
