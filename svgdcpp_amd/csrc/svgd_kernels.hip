@@ -1294,6 +1294,70 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
     const int nsel = st->nsel;
     const int bs[2] = {st->bsel[0], nsel > 1 ? st->bsel[1] : st->bsel[0]};
     unsigned long long rank[2] = {st->rank[0], nsel > 1 ? st->rank[1] : st->rank[0]};
+    {
+        // Few keys (the usual case: a tracked or sampled bracket's bucket holds
+        // tens to hundreds): gather each selected bucket's keys into LDS and
+        // take the order statistic by counting, per key, the keys below and
+        // at or below it -- exact, no radix passes.  Otherwise the radix path.
+        constexpr int SEL_FAST = 1024;
+        __shared__ uint64_t sKey[2][SEL_FAST];
+        __shared__ int sN[2];
+        __shared__ uint64_t sSel[2];
+        __shared__ int sHit[2];
+        if (tid < 2) {
+            sN[tid] = 0;
+            sHit[tid] = 0;
+        }
+        __syncthreads();
+        for (int g = 0; g < nseg; ++g) {
+            const uint64_t *sg = segs + (int64_t)g * (seg_cap + 1);
+            const int64_t cnt = min<int64_t>((int64_t)sg[0], seg_cap);
+            for (int64_t e = tid; e < cnt; e += 1024) {
+                const uint64_t key = sg[1 + e];
+                const int kb = kbucket(key, lo, binv);
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (kb == bs[q]) {
+                        const int pos = atomicAdd(&sN[q], 1);
+                        if (pos < SEL_FAST) sKey[q][pos] = key;
+                    }
+            }
+        }
+        __syncthreads();
+        const int n0 = sN[0], n1 = sN[1];
+        if (n0 <= SEL_FAST && n1 <= SEL_FAST) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int nq = q ? n1 : n0;
+                for (int i = tid; i < nq; i += 1024) {
+                    const uint64_t k = sKey[q][i];
+                    unsigned long long lt = 0, le = 0;
+                    for (int j = 0; j < nq; ++j) {
+                        const uint64_t o = sKey[q][j];
+                        lt += o < k;
+                        le += o <= k;
+                    }
+                    if (lt <= rank[q] && rank[q] < le) { // k is the rank[q]-th key (ties: same value)
+                        sSel[q] = k;
+                        sHit[q] = 1;
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                if (!sHit[0] || !sHit[1]) st->error = 1; // rank outside the bucket (should not happen)
+                st->prefix[0] = sSel[0];
+                if (nsel > 1) st->prefix[1] = sSel[1];
+                finalize_scale(st, navg, src_lo, src_hi, logn, scal, scal + 1);
+                if (trk) {
+                    trk[4] = sSel[0];
+                    trk[5] = nsel > 1 ? sSel[1] : sSel[0];
+                    trk[6] = (!sHit[0] || !sHit[1]) ? 1 : 0;
+                }
+            }
+            return;
+        }
+    }
     // min / max key of each selected bucket
     uint64_t mn[2] = {~0ull, ~0ull}, mx[2] = {0, 0};
     for (int g = 0; g < nseg; ++g) {
