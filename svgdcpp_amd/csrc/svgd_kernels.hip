@@ -1182,59 +1182,69 @@ __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restr
         b0 = st->bsel[0];
         b1 = nsel > 1 ? st->bsel[1] : -1;
     }
+    // one region per wave at a time (a region holds tens to hundreds of band
+    // keys: the loads of 4 regions are in flight per block instead of one
+    // region after another); matches gather in LDS, one global reservation
+    // per block at the end (a wave writes straight to the segment if the LDS
+    // buffer is full)
     __shared__ uint64_t sK[CB_LDS];
-    __shared__ int sN;
+    __shared__ int sN, sValid; // reserved slots; the first slot a full buffer left unwritten
     __shared__ unsigned long long sBase;
     const uint64_t lo = st->lo_key;
     const double binv = st->binv;
     unsigned long long *ctr = reinterpret_cast<unsigned long long *>(seg);
     uint64_t *outk = seg + 1;
-    const int lane = threadIdx.x & 63;
-    constexpr int CU = 8; // loads in flight per thread; <= 256 * CU matches per chunk
-    if (threadIdx.x == 0) sN = 0;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    constexpr int CU = 4; // loads in flight per lane
+    if (threadIdx.x == 0) {
+        sN = 0;
+        sValid = CB_LDS;
+    }
     __syncthreads();
-    auto flush = [&]() {
-        __syncthreads();
-        const int m = sN;
-        if (threadIdx.x == 0 && m) sBase = atomicAdd(ctr, (unsigned long long)m);
-        __syncthreads();
-        for (int e = threadIdx.x; e < m; e += 256) {
-            const unsigned long long pos = sBase + e;
-            if (pos < (unsigned long long)seg_cap) outk[pos] = sK[e];
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) sN = 0;
-        __syncthreads();
-    };
-    for (int64_t r = blockIdx.x; r < nreg; r += gridDim.x) {
+    for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < nreg; r += (int64_t)gridDim.x * 4) {
         int64_t cnt = counts ? (int64_t)counts[r] : cap;
         if (cnt > cap) cnt = cap;
         const uint64_t *kr = keys + r * cap;
-        for (int64_t b = 0; b < cnt; b += 256 * CU) {
-            if (sN > CB_LDS - 256 * CU) flush(); // block-uniform (read after a barrier)
+        for (int64_t b = 0; b < cnt; b += 64 * CU) {
             uint64_t kk[CU];
 #pragma unroll
             for (int u = 0; u < CU; ++u) {
-                const int64_t e = b + u * 256 + threadIdx.x;
+                const int64_t e = b + u * 64 + lane;
                 kk[u] = e < cnt ? kr[e] : 0;
             }
 #pragma unroll
             for (int u = 0; u < CU; ++u) {
-                const int64_t e = b + u * 256 + threadIdx.x;
+                const int64_t e = b + u * 64 + lane;
                 const int kb = kbucket(kk[u], lo, binv);
                 const bool m = e < cnt && (kb == b0 || kb == b1);
                 const unsigned long long bal = __ballot(m);
-                if (bal) {
-                    int base = 0;
-                    if (lane == 0) base = atomicAdd(&sN, __popcll(bal));
-                    base = __shfl(base, 0);
-                    if (m) sK[base + __popcll(bal & ((1ull << lane) - 1ull))] = kk[u];
+                if (!bal) continue;
+                const int c = __popcll(bal), off = __popcll(bal & ((1ull << lane) - 1ull));
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&sN, c);
+                base = __shfl(base, 0);
+                if (base + c <= CB_LDS) {
+                    if (m) sK[base + off] = kk[u];
+                } else { // LDS buffer full: this wave reserves and writes directly
+                    unsigned long long g = 0;
+                    if (lane == 0) {
+                        atomicMin(&sValid, base); // slots from base on stay unwritten
+                        g = atomicAdd(ctr, (unsigned long long)c);
+                    }
+                    g = __shfl(g, 0);
+                    if (m && g + off < (unsigned long long)seg_cap) outk[g + off] = kk[u];
                 }
             }
-            __syncthreads();
         }
     }
-    flush();
+    __syncthreads();
+    const int m = min(sN, sValid);
+    if (threadIdx.x == 0 && m) sBase = atomicAdd(ctr, (unsigned long long)m);
+    __syncthreads();
+    for (int e = threadIdx.x; e < m; e += 256) {
+        const unsigned long long pos = sBase + e;
+        if (pos < (unsigned long long)seg_cap) outk[pos] = sK[e];
+    }
 }
 
 // Inclusive prefix sum of v over a 1024-thread block (wave shuffles + one
@@ -3965,7 +3975,8 @@ hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, 
                                   const int *status, hipStream_t stream, const PlanArgs *plan)
 {
     if (nreg <= 0 && !plan) return hipSuccess;
-    int64_t G = nreg < 512 ? nreg : 512;
+    int64_t G = (nreg + 3) / 4; // one region per wave
+    if (G > 512) G = 512;
     if (G < 1) G = 1; // (with a plan the launch publishes it even without regions)
     hipLaunchKernelGGL(k_compact_buckets, dim3(G), dim3(256), 0, stream, keys, counts, nreg, cap,
                        st, seg, seg_cap, status, plan ? *plan : PlanArgs{});
