@@ -308,7 +308,7 @@ struct svgd_ctx {
     hipEvent_t last_phi_end = nullptr; // the last phi phase's end (timing): the next median's start
     double *bak = nullptr; // [X_t | m_t | v_t] of this rank's rows for the pending step
 
-    // Bracket tracking (speculative steps, row path): the median of D^2 moves
+    // Bracket tracking (speculative steps): the median of D^2 moves
     // smoothly from step to step, so the collect pass's bracket is predicted
     // from the last selected keys (quadratic extrapolation, half-width 4x the
     // largest of the last 3 prediction errors) instead of a sample and its two
@@ -677,15 +677,15 @@ int64_t sample_size(const svgd_ctx *c, int64_t M)
 }
 
 // This step's bracket, decided before the centring launch (which then also
-// writes the predicted select state): predicted on speculative row-path
-// steps when trk_predict allows it, else sampled in median_begin.
+// writes the predicted select state): predicted on speculative steps (row
+// and tile paths: keys are D^2 as doubles on both) when trk_predict allows
+// it, else sampled in median_begin.
 void trk_plan(svgd_ctx *c)
 {
     c->trk_go = false;
     c->trk_pred = -1;
     const int64_t M = upper_pairs(c->n);
-    if (!c->spec_step || !c->rowpath || c->sample_size > 0 || c->cand_capacity > 0 ||
-        M <= c->direct_max_pairs)
+    if (!c->spec_step || c->sample_size > 0 || c->cand_capacity > 0 || M <= c->direct_max_pairs)
         return;
     const int64_t S = sample_size(c, M);
     const double Mq = c->sim_world > 1 ? (double)c->sim_pairs : (double)M;

@@ -16,7 +16,7 @@ from svgdcpp_amd import _capi as C
 pytestmark = pytest.mark.gpu
 
 
-def _pair(oracle, monkeypatch, n, d, env):
+def _pair(oracle, monkeypatch, n, d, env, dtype=None):
     X = oracle.splitmix((n, d), 3.0, 11 * n + d)
     mus = oracle.splitmix((3, d), 2.0, 17)
     model = S.GaussianSum(list(mus), [np.eye(d) * (1.0 + 0.25 * k) for k in range(3)])
@@ -25,16 +25,19 @@ def _pair(oracle, monkeypatch, n, d, env):
         monkeypatch.setenv("SVGD_TRACK_BRACKET", tr)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        c = S.Context(d, n)
+        c = S.Context(d, n) if dtype is None else S.Context(d, n, dtype=dtype)
         c.set_particles(X)
         c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
         ctxs.append(c)
     return ctxs, model
 
 
-@pytest.mark.parametrize("n,d", [(6000, 8), (9000, 2), (7000, 5)])
-def test_tracked_brackets_bit_identical(oracle, monkeypatch, n, d):
-    (a, b), model = _pair(oracle, monkeypatch, n, d, {})
+@pytest.mark.parametrize("n,d,dtype", [(6000, 8, None), (9000, 2, None), (7000, 5, None),
+                                       (6000, 24, None), (6000, 64, "f32")])
+def test_tracked_brackets_bit_identical(oracle, monkeypatch, n, d, dtype):
+    """Row path (d <= 16), fp64 tile path (d = 24) and the F32 tile path."""
+    dt = None if dtype is None else C.SVGD_F32
+    (a, b), model = _pair(oracle, monkeypatch, n, d, {}, dt)
     a.diagnostics()
     for step in range(16):
         for c in (a, b):
