@@ -689,9 +689,12 @@ void trk_plan(svgd_ctx *c)
         return;
     const int64_t S = sample_size(c, M);
     const double Mq = c->sim_world > 1 ? (double)c->sim_pairs : (double)M;
-    // the sampled bracket's expected share (sample_state at q = 1/2)
+    // the sampled bracket's expected share (sample_state at q = 1/2; whole-tile
+    // samples take 4x the sigmas, median_begin)
+    const bool tile_sample = !c->rowpath && c->n / TB >= 2 && S >= TB * TB;
+    const double sigma = tile_sample ? 4.0 * c->bracket_sigma : c->bracket_sigma;
     const double sig = std::sqrt((double)S * 0.25) + 1.0;
-    const double band_samp = (2.0 * c->bracket_sigma * sig + 3.0) / (double)S;
+    const double band_samp = (2.0 * sigma * sig + 3.0) / (double)S;
     c->trk_go = trk_predict(c, Mq, band_samp, &c->trk_lo, &c->trk_hi, &c->trk_band);
 }
 
