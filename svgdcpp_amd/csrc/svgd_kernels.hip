@@ -1306,18 +1306,15 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
     unsigned long long rank[2] = {st->rank[0], nsel > 1 ? st->rank[1] : st->rank[0]};
     {
         // Few keys (the usual case: a tracked or sampled bracket's bucket holds
-        // tens to hundreds): gather each selected bucket's keys into LDS and
-        // take the order statistic by counting, per key, the keys below and
-        // at or below it -- exact, no radix passes.  Otherwise the radix path.
+        // tens to hundreds): gather each selected bucket's keys into LDS, sort
+        // them (bitonic, padded to a power of two with ~0) and take the
+        // rank-th -- exact, no radix passes.  Otherwise the radix path.
+        // (Counting each key's rank over all others was O(n^2) on one CU:
+        // 75 us at n = 1024.)
         constexpr int SEL_FAST = 1024;
         __shared__ uint64_t sKey[2][SEL_FAST];
         __shared__ int sN[2];
-        __shared__ uint64_t sSel[2];
-        __shared__ int sHit[2];
-        if (tid < 2) {
-            sN[tid] = 0;
-            sHit[tid] = 0;
-        }
+        if (tid < 2) sN[tid] = 0;
         __syncthreads();
         for (int g = 0; g < nseg; ++g) {
             const uint64_t *sg = segs + (int64_t)g * (seg_cap + 1);
@@ -1336,33 +1333,41 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
         __syncthreads();
         const int n0 = sN[0], n1 = sN[1];
         if (n0 <= SEL_FAST && n1 <= SEL_FAST) {
+            uint64_t sel[2];
+            bool ok = true;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int nq = q ? n1 : n0;
-                for (int i = tid; i < nq; i += 1024) {
-                    const uint64_t k = sKey[q][i];
-                    unsigned long long lt = 0, le = 0;
-                    for (int j = 0; j < nq; ++j) {
-                        const uint64_t o = sKey[q][j];
-                        lt += o < k;
-                        le += o <= k;
+                int p2 = 1;
+                while (p2 < nq) p2 <<= 1;
+                uint64_t *a = sKey[q];
+                if (tid >= nq && tid < p2) a[tid] = ~0ull; // padding sorts last
+                __syncthreads();
+                for (int k = 2; k <= p2; k <<= 1)
+                    for (int j = k >> 1; j > 0; j >>= 1) {
+                        const int ixj = tid ^ j;
+                        if (tid < p2 && ixj > tid) {
+                            const uint64_t x = a[tid], y = a[ixj];
+                            const bool up = (tid & k) == 0;
+                            if ((x > y) == up) {
+                                a[tid] = y;
+                                a[ixj] = x;
+                            }
+                        }
+                        __syncthreads();
                     }
-                    if (lt <= rank[q] && rank[q] < le) { // k is the rank[q]-th key (ties: same value)
-                        sSel[q] = k;
-                        sHit[q] = 1;
-                    }
-                }
+                ok = ok && rank[q] < (unsigned long long)nq;
+                sel[q] = ok ? a[rank[q]] : 0ull;
             }
-            __syncthreads();
             if (tid == 0) {
-                if (!sHit[0] || !sHit[1]) st->error = 1; // rank outside the bucket (should not happen)
-                st->prefix[0] = sSel[0];
-                if (nsel > 1) st->prefix[1] = sSel[1];
+                if (!ok) st->error = 1; // rank outside the bucket (should not happen)
+                st->prefix[0] = sel[0];
+                if (nsel > 1) st->prefix[1] = sel[1];
                 finalize_scale(st, navg, src_lo, src_hi, logn, scal, scal + 1);
                 if (trk) {
-                    trk[4] = sSel[0];
-                    trk[5] = nsel > 1 ? sSel[1] : sSel[0];
-                    trk[6] = (!sHit[0] || !sHit[1]) ? 1 : 0;
+                    trk[4] = sel[0];
+                    trk[5] = nsel > 1 ? sel[1] : sel[0];
+                    trk[6] = ok ? 0 : 1;
                 }
             }
             return;
