@@ -1333,29 +1333,41 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
         __syncthreads();
         const int n0 = sN[0], n1 = sN[1];
         if (n0 <= SEL_FAST && n1 <= SEL_FAST) {
+            // register bitonic sort, one key per thread: partners within a
+            // wave by shuffle (j < 64), across waves through LDS (j >= 64:
+            // 10 of the 55 stages at 1024 keys, two barriers each)
             uint64_t sel[2];
             bool ok = true;
+            const bool same = bs[1] == bs[0];
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const int nq = q ? n1 : n0;
+                uint64_t *a = sKey[q];
+                if (q == 1 && same) { // both order statistics in one bucket: sorted already
+                    ok = ok && rank[1] < (unsigned long long)nq;
+                    sel[1] = ok ? sKey[0][rank[1]] : 0ull;
+                    break;
+                }
                 int p2 = 1;
                 while (p2 < nq) p2 <<= 1;
-                uint64_t *a = sKey[q];
-                if (tid >= nq && tid < p2) a[tid] = ~0ull; // padding sorts last
-                __syncthreads();
+                uint64_t x = tid < nq ? a[tid] : ~0ull; // padding sorts last
                 for (int k = 2; k <= p2; k <<= 1)
                     for (int j = k >> 1; j > 0; j >>= 1) {
-                        const int ixj = tid ^ j;
-                        if (tid < p2 && ixj > tid) {
-                            const uint64_t x = a[tid], y = a[ixj];
-                            const bool up = (tid & k) == 0;
-                            if ((x > y) == up) {
-                                a[tid] = y;
-                                a[ixj] = x;
-                            }
+                        uint64_t y;
+                        if (j >= 64) {
+                            __syncthreads();
+                            if (tid < p2) a[tid] = x;
+                            __syncthreads();
+                            y = tid < p2 ? a[tid ^ j] : x;
+                        } else {
+                            y = __shfl_xor(x, j);
                         }
-                        __syncthreads();
+                        const bool keep_min = ((tid & k) == 0) == ((tid & j) == 0);
+                        x = keep_min ? (x < y ? x : y) : (x < y ? y : x);
                     }
+                __syncthreads();
+                if (tid < p2) a[tid] = x;
+                __syncthreads();
                 ok = ok && rank[q] < (unsigned long long)nq;
                 sel[q] = ok ? a[rank[q]] : 0ull;
             }
