@@ -1875,6 +1875,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     c->ev_xready_use = c->ev_xready;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_particles = true;
+    c->trk_n = c->trk_nerr = 0; // new particles: the median history restarts
     return SVGD_OK;
 }
 
