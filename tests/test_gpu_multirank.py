@@ -60,16 +60,17 @@ def test_sharded_step_matches_single_rank(world, n):
         np.testing.assert_allclose(X, X1, rtol=0, atol=1e-10)
 
 
-def test_sharded_tracked_brackets_bit_identical():
-    """The tracked median bracket on a sharded run (world 2): every rank
-    predicts the same bracket from the same all-reduced counts and selected
-    keys, and the trajectory is bit-identical to sampling every bracket."""
-    n, d, steps = 12007, 5, 14
+@pytest.mark.parametrize("world,n", [(2, 12007), (8, 20011)])
+def test_sharded_tracked_brackets_bit_identical(world, n):
+    """The tracked median bracket on a sharded run: every rank predicts the
+    same bracket from the same all-reduced counts and selected keys, and the
+    trajectory is bit-identical to sampling every bracket."""
+    d, steps = 5, 14
     trk = {}
-    tracked = _run_ranks(2, n, d, steps, {"SVGD_TRACK_BRACKET": "1"}, trk)
-    sampled = _run_ranks(2, n, d, steps, {"SVGD_TRACK_BRACKET": "0"})
-    assert min(trk.values()) >= 3 and trk[0] == trk[1]
-    for rank in (0, 1):
+    tracked = _run_ranks(world, n, d, steps, {"SVGD_TRACK_BRACKET": "1"}, trk)
+    sampled = _run_ranks(world, n, d, steps, {"SVGD_TRACK_BRACKET": "0"})
+    assert min(trk.values()) >= 3 and len(set(trk.values())) == 1
+    for rank in range(world):
         Xa, sa, _ = tracked[rank]
         Xb, sb, _ = sampled[rank]
         assert np.array_equal(Xa, Xb), rank
