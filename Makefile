@@ -33,7 +33,7 @@ $(SRC_DIR)/hostcomm.o: $(SRC_DIR)/hostcomm.cpp $(SRC_DIR)/hostcomm.h
 	$(HIPCC) -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
 $(SRC_DIR)/host_models.o: $(SRC_DIR)/host_models.cpp $(SRC_DIR)/host_grad_block.inc $(HDRS)
-	$(CXX) -O3 -std=c++17 -fPIC -fopenmp -Wall -c $< -o $@
+	$(CXX) -O3 -std=c++17 -fPIC -fopenmp -Wall -Wno-psabi -c $< -o $@
 
 $(LIB): $(OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS) -L/opt/rocm/lib -lrccl -fopenmp -Wl,-rpath,/opt/rocm/lib

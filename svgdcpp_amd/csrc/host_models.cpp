@@ -68,7 +68,7 @@ bool invert(const double *A, int d, double *out)
 // l ascending, whatever the blocking.
 constexpr int GB_NP = 4, GB_RW = 8;
 typedef double v4d __attribute__((vector_size(32)));
-namespace gb_base {
+namespace gb_base { // (-Wno-psabi: exp4_nonpos's v4d return is inlined, no ABI crossing)
 #include "host_grad_block.inc"
 }
 #pragma GCC push_options

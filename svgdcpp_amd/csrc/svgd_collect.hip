@@ -130,7 +130,7 @@ template <int D> struct McolRow {
 // takes the 16-column blocks w, w + 4, ...  Each wave stages its own band
 // pairs and owns region blockIdx * 4 + w, as k_pair_rows.
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_mcol(const double *__restrict__ xc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 : 2, 8))) void k_pair_mcol(const double *__restrict__ xc,
                                                   const float *__restrict__ xf, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc)
