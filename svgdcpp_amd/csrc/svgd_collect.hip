@@ -3,7 +3,6 @@
 // kernels are not.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <cstdlib>
 #include <type_traits>
 
 #include "svgd_device.h"
@@ -99,45 +98,6 @@ __device__ __forceinline__ unsigned long long mcol_classify4(const f4_t &v, floa
                  : "scc");
     return any;
 }
-// The same with the below counts kept per lane in 4 VGPRs (vb[r] += the
-// lane's bit of below mask r: v_addc with the mask as carry-in, 4 independent
-// accumulators and carry-outs, so no dependency chain): 4 VALU in place of 8
-// SALU per 16 x 16 block, off the scalar unit (SQ counters: SALU 47 %, VALU
-// 33 %, MFMA 32 %).  (A first single-accumulator version lost 1-2 %: its
-// v_addc chain serialised on vb and on the shared carry-out.)
-__device__ __forceinline__ unsigned long long mcol_classify4_v(const f4_t &v, float tl, float th,
-                                                               uint32_t (&vb)[4],
-                                                               unsigned long long (&h)[4])
-{
-    unsigned long long l0, l1, l2, l3, any, c0, c1, c2, c3;
-    asm volatile("v_cmp_gt_f32_e64 %[l0], %[v0], %[tl]\n\t"
-                 "v_cmp_gt_f32_e64 %[h0], %[v0], %[th]\n\t"
-                 "v_cmp_gt_f32_e64 %[l1], %[v1], %[tl]\n\t"
-                 "v_cmp_gt_f32_e64 %[h1], %[v1], %[th]\n\t"
-                 "v_cmp_gt_f32_e64 %[l2], %[v2], %[tl]\n\t"
-                 "v_cmp_gt_f32_e64 %[h2], %[v2], %[th]\n\t"
-                 "v_cmp_gt_f32_e64 %[l3], %[v3], %[tl]\n\t"
-                 "v_cmp_gt_f32_e64 %[h3], %[v3], %[th]\n\t"
-                 "v_addc_co_u32_e64 %[b0], %[c0], %[b0], 0, %[l0]\n\t"
-                 "v_addc_co_u32_e64 %[b1], %[c1], %[b1], 0, %[l1]\n\t"
-                 "v_addc_co_u32_e64 %[b2], %[c2], %[b2], 0, %[l2]\n\t"
-                 "v_addc_co_u32_e64 %[b3], %[c3], %[b3], 0, %[l3]\n\t"
-                 "s_andn2_b64 %[h0], %[h0], %[l0]\n\t"
-                 "s_andn2_b64 %[h1], %[h1], %[l1]\n\t"
-                 "s_andn2_b64 %[h2], %[h2], %[l2]\n\t"
-                 "s_andn2_b64 %[h3], %[h3], %[l3]\n\t"
-                 "s_or_b64 %[any], %[h0], %[h1]\n\t"
-                 "s_or_b64 %[any], %[any], %[h2]\n\t"
-                 "s_or_b64 %[any], %[any], %[h3]"
-                 : [b0] "+v"(vb[0]), [b1] "+v"(vb[1]), [b2] "+v"(vb[2]), [b3] "+v"(vb[3]),
-                   [any] "=&s"(any), [c0] "=&s"(c0), [c1] "=&s"(c1), [c2] "=&s"(c2), [c3] "=&s"(c3),
-                   [l0] "=&s"(l0), [l1] "=&s"(l1), [l2] "=&s"(l2), [l3] "=&s"(l3), [h0] "=&s"(h[0]),
-                   [h1] "=&s"(h[1]), [h2] "=&s"(h[2]), [h3] "=&s"(h[3])
-                 : [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]), [tl] "v"(tl),
-                   [th] "v"(th)
-                 : "scc");
-    return any;
-}
 // Diagonal tiles (1 in nb/2 of them): lanes with xl > c (j > i) only.
 // Returns the band lanes of the value.
 __device__ __forceinline__ unsigned long long mcol_classify_diag(float v, float tl, float th, int xl,
@@ -169,7 +129,7 @@ template <int D> struct McolRow {
 // (B operands and thresholds, written when the row block changes), and wave w
 // takes the 16-column blocks w, w + 4, ...  Each wave stages its own band
 // pairs and owns region blockIdx * 4 + w, as k_pair_rows.
-template <int D, bool VB = false>
+template <int D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 : 2, 8))) void k_pair_mcol(const double *__restrict__ xc,
                                                   const float *__restrict__ xf, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
@@ -202,7 +162,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     uint64_t *wregion = sc.region + wreg * sc.cap;
     int64_t wcnt = 0;             // keys written to the region
     unsigned long long below = 0; // below count (scalar: classified + exact)
-    uint32_t vbelow[4] = {0, 0, 0, 0}; // VB: the off-diagonal classified part, per lane
     int scnt = 0;                 // staged band pairs
     bool ovf = false;             // a group outgrew the staging area
 
@@ -390,10 +349,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                     any |= h[r];
                                 }
                             } else {
-                                if constexpr (VB)
-                                    any = mcol_classify4_v(acc[g], Bg[g][KK], Bg[g][KK + 1], vbelow, h);
-                                else
-                                    any = mcol_classify4(acc[g], Bg[g][KK], Bg[g][KK + 1], nbelow, h);
+                                any = mcol_classify4(acc[g], Bg[g][KK], Bg[g][KK + 1], nbelow, h);
                             }
                             // rare (~0.4 of the blocks, ~1 band pair each): stage the band pairs
                             if (__builtin_expect(any != 0, 0)) {
@@ -435,11 +391,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
         } while (advance(pos));
     }
 
-    if constexpr (VB) {
-        unsigned long long vs = (unsigned long long)vbelow[0] + vbelow[1] + vbelow[2] + vbelow[3];
-        for (int o = 32; o > 0; o >>= 1) vs += __shfl_xor(vs, o);
-        below += vs;
-    }
     if (lane == 0) {
         sc.below_out[wreg] = below;
         // an overflowed staging area reports an overflowed region: the host
@@ -780,12 +731,8 @@ hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm,
 
 #define SVGD_MCOL_CASE(Dv)                                                                   \
     case Dv:                                                                                 \
-        if (vb)                                                                              \
-            hipLaunchKernelGGL((k_pair_mcol<Dv, true>), dim3(grid), dim3(256), 0, stream, xc, xf, n, \
-                               nb, t0, t1, sc);                                              \
-        else                                                                                 \
-            hipLaunchKernelGGL((k_pair_mcol<Dv, false>), dim3(grid), dim3(256), 0, stream, xc, xf, n, \
-                               nb, t0, t1, sc);                                              \
+        hipLaunchKernelGGL((k_pair_mcol<Dv>), dim3(grid), dim3(256), 0, stream, xc, xf, n, nb, t0, \
+                           t1, sc);                                                          \
         break;
 
 hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
@@ -797,11 +744,6 @@ hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
     if (grid <= 0 || t1 <= t0) return hipSuccess;
     if (!nmax_bits || !xf) return hipErrorInvalidValue;
     SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, bpart};
-    // A/B knob: per-lane below counters (k_pair_mcol<D, true>)
-    static const bool vb = [] {
-        const char *e = std::getenv("SVGD_MCOL_VCOUNT");
-        return e && std::atoi(e) != 0;
-    }();
     switch (d) {
         SVGD_MCOL_CASE(1)
         SVGD_MCOL_CASE(2)
