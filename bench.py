@@ -341,9 +341,6 @@ def main():
                     help="measurement only: time rank 0's share of a P-rank step on one GPU "
                          "(no collectives; results are not the step's) -- not a headline line")
     ap.add_argument("--no-diag", action="store_true", help="skip the untimed diagnostic pass")
-    ap.add_argument("--phase-events", action="store_true",
-                    help="phase events in the timed runs (svgd_set_timing level 1; default: none -- "
-                         "each is a dispatch gap -- and the phase split comes from the diagnostic pass)")
     ap.add_argument("--dtype", choices=["f64", "f32"], default=None,
                     help="compute dtype of the O(N^2) work (default: the config's; cfg5 is f32)")
     ap.add_argument("--device-model", action="store_true",
@@ -409,7 +406,7 @@ def main():
     ctx.sync()
     ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))  # drop warmup events
     ctx.diagnostics()  # (reset)
-    ctx.check(ctx.lib.svgd_set_timing(ctx.h, 1 if args.phase_events else 0))
+    ctx.check(ctx.lib.svgd_set_timing(ctx.h, 1))
 
     # the median of `repeats` timed runs of exactly K steps, each
     # bracketed by barrier + device sync; the GPU's clock/power sampled by
@@ -444,12 +441,7 @@ def main():
         ctx.sync()
         gpu_diag = mon.stop()
         diag = ctx.diagnostics()
-        if args.phase_events:
-            ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))
-        else:  # the phase split of the diagnostic pass (its events add ~5 us gaps)
-            ctx.check(ctx.lib.svgd_get_timing(ctx.h, ctypes.byref(phi_ms), ctypes.byref(med_ms),
-                                              ctypes.byref(cnt)))
-            nsteps_timed = args.steps
+        ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))
         ctx.check(ctx.lib.svgd_set_timing(ctx.h, 0))
 
     a, med, path = ctx.last_scale()
@@ -466,12 +458,10 @@ def main():
 
     mine = {
         "rank": rank, "rows": rows,
-        # phase events sit at phase boundaries (svgd_set_timing level 1 in the
-        # timed runs with --phase-events, else the diagnostic pass's): "phi"
-        # runs from the median's end (so it holds any wait for G) to the
+        # phase events sit at phase boundaries only (svgd_set_timing level 1):
+        # "phi" runs from the median's end (so it holds any wait for G) to the
         # update's end, "median" from the previous step's end (so it holds the
         # gap between steps) to the scale; the diagnostic pass separates both
-        "phases_source": "timed runs" if args.phase_events else "diagnostic pass",
         "phases_ms_per_step": {"phi_incl_wait_for_g": per_step(phi_ms.value, nsteps_timed),
                                "median_incl_step_gap": per_step(med_ms.value, nsteps_timed)},
         "host_ms_per_step": {"grad": per_step(host_timed["host_grad_ms"], host_timed["steps"]),
@@ -562,7 +552,6 @@ def main():
                 "flop_per_launch": flops_launch,
             },
             "phases_ms_per_step": mine["phases_ms_per_step"],
-            "phases_source": mine["phases_source"],
             "host_ms_per_step": mine["host_ms_per_step"],
             "tracked_brackets": mine["tracked_brackets"],
             "diag_ms_per_step": mine.get("diag_ms_per_step"),

@@ -295,15 +295,6 @@ struct svgd_ctx {
     bool pending = false;      // a speculative step awaits its status
     bool scal_fresh = true;    // h_scal holds the last scale (fetch_scale)
     int *d_status = nullptr, *h_status = nullptr, *h_status_dev = nullptr; // (h_status as seen by kernels)
-    // Polled completion of the speculative selection (timing level 0): the
-    // selection writes seq into pinned memory when its results are final and
-    // resolve_pending spins on it -- no event record between the selection
-    // and the record prep (a ~5.6 us dispatch gap per step).  SVGD_STATUS_POLL=0
-    // records the event instead.
-    bool status_poll = true;
-    unsigned int *h_done = nullptr, *h_done_dev = nullptr;
-    unsigned int poll_seq = 0;
-    bool poll_pending = false;
     hipEvent_t ev_status = nullptr;
     // Every event record between two kernels costs a ~5 us dispatch gap, so
     // the end of the median records ONE event that serves as the plan status
@@ -903,18 +894,9 @@ int median_finish_spec(svgd_ctx *c, double logn)
     HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
                                      c->d_status, c->stream, &pa));
     CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
-    const bool poll = c->status_poll && !c->timing;
-    if (poll) c->poll_seq += 1;
     HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, CAPR, c->navg, c->src_lo, c->src_hi, logn,
-                                  c->scal, c->d_status, c->stream, c->h_trk_dev,
-                                  poll ? c->h_done_dev : nullptr, c->poll_seq));
+                                  c->scal, c->d_status, c->stream, c->h_trk_dev));
     c->trk_keys = true;
-    if (poll) { // resolve_pending spins on h_done; fetch_scale comes after it
-        c->poll_pending = true;
-        c->ev_status_use = nullptr;
-        c->med_ev_done = true;
-        return SVGD_OK;
-    }
     // the plan's status is final once this completes (recorded after the
     // selection: an event between two kernels costs a ~5 us dispatch gap)
     // (c->pending -- the plan's status to check -- is set when the step is
@@ -1380,26 +1362,6 @@ int fetch_scale(svgd_ctx *c)
     return SVGD_OK;
 }
 
-// Wait for the polled selection (h_done == poll_seq).  A kernel fault would
-// never set it: after a while the stream is synchronised (reporting the
-// fault) and the flag checked once more.
-int poll_wait(svgd_ctx *c)
-{
-    c->poll_pending = false;
-    const volatile unsigned int *f = c->h_done;
-    for (long it = 0; *f != c->poll_seq; ++it) {
-        if (it == (1L << 22)) { // ~ a second of polling
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            if (*f != c->poll_seq)
-                return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] The median selection did not complete.");
-            break;
-        }
-        __builtin_ia32_pause();
-    }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    return SVGD_OK;
-}
-
 // Check the pending speculative step; on a failed device plan restore X_t,
 // m_t, v_t, t and redo the step on the synchronous path (G_t is still on the
 // device).  Every rank sees the same status (it derives from all-reduced
@@ -1408,11 +1370,7 @@ int resolve_pending(svgd_ctx *c)
 {
     if (!c->pending) return SVGD_OK;
     c->pending = false;
-    if (c->poll_pending) {
-        CHK(poll_wait(c));
-    } else {
-        HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
-    }
+    HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
     if (*c->h_status == 0) {
         if (c->trk_allowed) trk_record(c, c->h_trk[0], c->h_trk[1], c->h_trk[3]);
         return SVGD_OK;
@@ -1638,15 +1596,11 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     HIPCHK(c, hipHostMalloc((void **)&c->h_status, sizeof(int), hipHostMallocCoherent));
     *c->h_status = 0;
     HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_status_dev, c->h_status, 0));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_done, sizeof(unsigned int), hipHostMallocCoherent));
-    *c->h_done = 0;
-    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_done_dev, c->h_done, 0));
     HIPCHK(c, hipHostMalloc((void **)&c->h_trk, 8 * sizeof(uint64_t), hipHostMallocCoherent));
     std::memset(c->h_trk, 0, 8 * sizeof(uint64_t));
     HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_trk_dev, c->h_trk, 0));
     if (const char *e = std::getenv("SVGD_SPECULATE")) c->spec_allowed = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_TRACK_BRACKET")) c->trk_allowed = std::atoi(e) != 0;
-    if (const char *e = std::getenv("SVGD_STATUS_POLL")) c->status_poll = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_TRACK_MIN_WIDTH")) c->trk_min_w = std::atof(e);
     if (const char *e = std::getenv("SVGD_TRACK_ERR_MULT")) c->trk_err_mult = std::atof(e);
     c->host_threads = std::max(1, omp_get_max_threads() / 2);
@@ -1737,7 +1691,7 @@ int svgd_destroy(svgd_ctx *c)
                      c->bpart,       c->gseg, c->symok};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
-    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk, c->h_done};
+    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
     for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})

@@ -1290,24 +1290,9 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
                                                       int src_lo, int src_hi, double logn,
                                                       double *__restrict__ scal,
                                                       const int *__restrict__ status,
-                                                      uint64_t *__restrict__ trk,
-                                                      unsigned int *__restrict__ done,
-                                                      unsigned int seq)
+                                                      uint64_t *__restrict__ trk)
 {
-    // done (optional, pinned host memory): seq once everything this launch
-    // writes for the host (status already, scale, trk) is final -- the host
-    // polls it instead of waiting for an event (an event between two
-    // kernels costs a dispatch gap)
-    auto signal_done = [&]() {
-        if (done && threadIdx.x == 0) {
-            __threadfence_system();
-            __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    };
-    if (status && *status != 0) { // the device plan found no bucket path
-        signal_done();
-        return;
-    }
+    if (status && *status != 0) return; // the device plan found no bucket path
     __shared__ uint32_t sHist[2][RADIX];
     __shared__ unsigned long long sW[16];
     __shared__ unsigned long long sMn[2][16], sMx[2][16];
@@ -1397,7 +1382,6 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
                     trk[6] = ok ? 0 : 1;
                 }
             }
-            signal_done();
             return;
         }
     }
@@ -1518,7 +1502,6 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
             trk[6] = err ? 1 : 0;
         }
     }
-    signal_done();
 }
 
 // One radix-select step: for each active selection find the digit holding
@@ -4019,11 +4002,10 @@ hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, 
 
 hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
                                int navg, int src_lo, int src_hi, double logn, double *scal,
-                               const int *status, hipStream_t stream, uint64_t *trk,
-                               unsigned int *done, unsigned int seq)
+                               const int *status, hipStream_t stream, uint64_t *trk)
 {
     hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg, seg_cap,
-                       navg, src_lo, src_hi, logn, scal, status, trk, done, seq);
+                       navg, src_lo, src_hi, logn, scal, status, trk);
     return hipGetLastError();
 }
 
