@@ -1659,10 +1659,17 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
         ncclUniqueId id;
         std::memcpy(&id, unique_id128, sizeof(id));
         NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
-        // the G all-gather's communicator and stream (upload_g_finish)
-        NCCLCHK(c, ncclCommSplit(c->comm, 0, rank, &c->gcomm, nullptr));
-        HIPCHK(c, hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_gg, hipEventDisableTiming));
+        // the G all-gather's communicator and stream (upload_g_finish); if
+        // the split is refused the G all-gather stays on the compute stream
+        // (SVGD_G_COMM=0 forces that: collective, so set it on every rank)
+        bool want_g = true;
+        if (const char *e = std::getenv("SVGD_G_COMM")) want_g = std::atoi(e) != 0;
+        if (want_g && ncclCommSplit(c->comm, 0, rank, &c->gcomm, nullptr) != ncclSuccess)
+            c->gcomm = nullptr;
+        if (c->gcomm) {
+            HIPCHK(c, hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+            HIPCHK(c, hipEventCreateWithFlags(&c->ev_gg, hipEventDisableTiming));
+        }
     }
     return SVGD_OK;
 }
