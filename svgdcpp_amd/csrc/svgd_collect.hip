@@ -309,13 +309,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                     for (int q = 0; q < RW; q += 4)
                         *reinterpret_cast<f4 *>(&Bg[g][q]) =
                             *reinterpret_cast<const f4 *>(sRow + ((g0 + g) * 64 + lane) * RW + q);
+                // k-step outer, row block inner: the MC_NG chains interleave,
+                // so no MFMA waits for the one before it (dependent-accumulator
+                // latency 40 cycles); each chain still runs k ascending
 #pragma unroll
-                for (int g = 0; g < MC_NG; ++g) {
-                    acc[g] = hq;
+                for (int g = 0; g < MC_NG; ++g) acc[g] = hq;
 #pragma unroll
-                    for (int kk = 0; kk < KK; ++kk)
+                for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+                    for (int g = 0; g < MC_NG; ++g)
                         acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(A[kk], Bg[g][kk], acc[g], 0, 0, 0);
-                }
             };
             // Per 16-column block: the groups' MFMAs run one group ahead of the
             // classification (phase 2: two compares per value straight into
