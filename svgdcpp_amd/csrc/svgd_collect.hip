@@ -38,6 +38,11 @@ typedef f4_t f4;
 // every pair is then finished exactly (correct, slow).
 constexpr int MC_STG = 512; // staged band pairs per wave
 constexpr int MC_NG = 4;    // 16-row blocks per classification group
+// Timing ablations of k_pair_mcol (tools/gpu_mcol_abl.sh; WRONG results, never
+// a shipped build): 1 = no band staging, 2 = MFMAs only (no classification)
+#ifndef SVGD_MCOL_ABL
+#define SVGD_MCOL_ABL 0
+#endif
 
 __device__ __forceinline__ float f32_up(double x)
 {
@@ -344,7 +349,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
 #pragma unroll
                         for (int g = 0; g < MC_NG; ++g) {
                             unsigned long long h[4], any = 0;
-                            if constexpr (DIAG) {
+                            if constexpr (SVGD_MCOL_ABL == 2) {
+                                asm volatile("" ::"v"(acc[g][0]), "v"(acc[g][1]), "v"(acc[g][2]),
+                                             "v"(acc[g][3]), "v"(Bg[g][KK]), "v"(Bg[g][KK + 1]));
+                                continue;
+                            } else if constexpr (DIAG) {
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
                                     h[r] = mcol_classify_diag(acc[g][r], Bg[g][KK], Bg[g][KK + 1], xl,
@@ -355,7 +364,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                 any = mcol_classify4(acc[g], Bg[g][KK], Bg[g][KK + 1], nbelow, h);
                             }
                             // rare (~0.4 of the blocks, ~1 band pair each): stage the band pairs
-                            if (__builtin_expect(any != 0, 0)) {
+                            if (SVGD_MCOL_ABL == 0 && __builtin_expect(any != 0, 0)) {
                                 const uint32_t il = 16 * (g0 + g) + ql;
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
