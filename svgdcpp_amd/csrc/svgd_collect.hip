@@ -124,6 +124,20 @@ __device__ __forceinline__ unsigned long long mcol_classify_diag(float v, float 
     return mh;
 }
 
+// The lane's bits of the 4 band masks of one 16 x 16 block (bit r: value r
+// is a band value), straight from the scalar masks.
+__device__ __forceinline__ uint32_t mcol_code4(const unsigned long long (&h)[4])
+{
+    uint32_t c0, c1, c2, c3;
+    asm volatile("v_cndmask_b32_e64 %[c0], 0, 1, %[h0]\n\t"
+                 "v_cndmask_b32_e64 %[c1], 0, 2, %[h1]\n\t"
+                 "v_cndmask_b32_e64 %[c2], 0, 4, %[h2]\n\t"
+                 "v_cndmask_b32_e64 %[c3], 0, 8, %[h3]"
+                 : [c0] "=&v"(c0), [c1] "=&v"(c1), [c2] "=&v"(c2), [c3] "=&v"(c3)
+                 : [h0] "s"(h[0]), [h1] "s"(h[1]), [h2] "s"(h[2]), [h3] "s"(h[3]));
+    return c0 | c1 | c2 | c3;
+}
+
 // Row operands of one 16-row block for one lane: B (KK fp32) | TLf | THf | pad.
 template <int D> struct McolRow {
     static constexpr int KK = (D + 3) / 4;
@@ -170,32 +184,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     int scnt = 0;                 // staged band pairs
     bool ovf = false;             // a group outgrew the staging area
 
-    // Staged pairs (row offset | column offset << 16 of the tile at rows ib,
-    // columns jbase) -> the exact fp64 key with k_pair_rows' arithmetic (e =
-    // h_j + fma chain over k ascending, s = max(fl(-2 h_i - 2 e), 0)), then
-    // below lo (counted) / in [lo, hi) (appended to the region, bucketed) /
-    // dropped.
+    // Staged entries: one per (lane, 16 x 16 block) holding band values --
+    // row offset (bits 0..15) | column offset of the lane's 4 columns (16..27)
+    // | which of the 4 are band pairs (28..31), all of the tile at rows ib,
+    // columns jbase.  Each marked pair -> the exact fp64 key with
+    // k_pair_rows' arithmetic (e = h_j + fma chain over k ascending,
+    // s = max(fl(-2 h_i - 2 e), 0)), then below lo (counted) / in [lo, hi)
+    // (appended to the region, bucketed) / dropped.
     auto flush = [&](int64_t ib, int64_t jbase) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // other lanes' staging stores
         for (int q0 = 0; q0 < scnt; q0 += 64) {
             const bool valid = q0 + lane < scnt;
             const uint32_t e = valid ? stage[q0 + lane] : 0u;
+            uint32_t code = e >> 28; // 0 on invalid lanes
             const double *ri = xc + (valid ? ib + (e & 0xffffu) : 0) * KP;
-            const double *rj = xc + (valid ? jbase + (e >> 16) : 0) * KP;
-            double ev = rj[D];
+            double xi[D + 1];
 #pragma unroll
-            for (int k = 0; k < D; ++k) ev = fma(ri[k], rj[k], ev);
-            const double ni = -2.0 * ri[D];
-            const uint64_t key = key_of(fmax(fma(-2.0, ev, ni), 0.0));
-            below += __popcll(__ballot(valid && key < lo_key));
-            const bool keep = valid && key >= lo_key && key < hi_key;
-            const unsigned long long mk = __ballot(keep);
-            if (keep) {
-                const int64_t pos = wcnt + __popcll(mk & ((1ull << lane) - 1ull));
-                if (pos < sc.cap) wregion[pos] = key;
-                if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
+            for (int k = 0; k <= D; ++k) xi[k] = ri[k];
+            const double ni = -2.0 * xi[D];
+            const int64_t jl = jbase + ((e >> 16) & 0xfffu);
+            // the lane's marked columns, lowest first (usually one)
+            while (__any(code != 0)) {
+                const bool act = code != 0;
+                const int r = act ? __builtin_ctz(code) : 0;
+                code &= code - 1u;
+                const double *rj = xc + (act ? jl + r : 0) * KP;
+                double ev = rj[D];
+#pragma unroll
+                for (int k = 0; k < D; ++k) ev = fma(xi[k], rj[k], ev);
+                const uint64_t key = key_of(fmax(fma(-2.0, ev, ni), 0.0));
+                below += __popcll(__ballot(act && key < lo_key));
+                const bool keep = act && key >= lo_key && key < hi_key;
+                const unsigned long long mk = __ballot(keep);
+                if (keep) {
+                    const int64_t pos = wcnt + __popcll(mk & ((1ull << lane) - 1ull));
+                    if (pos < sc.cap) wregion[pos] = key;
+                    if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
+                }
+                wcnt += __popcll(mk);
             }
-            wcnt += __popcll(mk);
         }
         scnt = 0;
     };
@@ -363,21 +390,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                             } else {
                                 any = mcol_classify4(acc[g], Bg[g][KK], Bg[g][KK + 1], nbelow, h);
                             }
-                            // rare (~0.4 of the blocks, ~1 band pair each): stage the band pairs
+                            // ~0.4 of the blocks, ~1 band pair each: ONE entry per
+                            // lane holding band values (its 4 values' band bits),
+                            // branch-free (the flush expands the bits)
                             if (SVGD_MCOL_ABL == 0 && __builtin_expect(any != 0, 0)) {
-                                const uint32_t il = 16 * (g0 + g) + ql;
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) {
-                                    const unsigned long long m = h[r];
-                                    if (!m) continue;
-                                    const int c = __popcll(m);
-                                    if (scnt + c > MC_STG) { // pathological band: give up
-                                        ovf = true;      // (region overflow -> exact fallback)
-                                        continue;
-                                    }
-                                    if ((m >> lane) & 1ull)
-                                        stage[scnt + __popcll(m & ((1ull << lane) - 1ull))] =
-                                            il | ((uint32_t)(jl0 + 4 * kq + r) << 16);
+                                const int c = __popcll(any);
+                                if (scnt + c > MC_STG) { // pathological band: give up
+                                    ovf = true;          // (region overflow -> exact fallback)
+                                } else {
+                                    const uint32_t code = mcol_code4(h);
+                                    const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
+                                        (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
+                                    if (code)
+                                        stage[scnt + pre] = (16u * (g0 + g) + ql) |
+                                                            ((uint32_t)(jl0 + 4 * kq) << 16) | (code << 28);
                                     scnt += c;
                                 }
                             }
