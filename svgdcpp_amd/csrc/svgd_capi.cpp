@@ -333,6 +333,29 @@ struct svgd_ctx {
 
 namespace {
 
+// CPUs the cgroup (v2 cpu.max "quota period", v1 cfs files) allows this
+// process, rounded down; 0 = no quota or unreadable
+int cgroup_cpus()
+{
+    long long quota = -1, period = 0;
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0)
+            quota = std::atoll(q);
+        std::fclose(f);
+    } else {
+        if (FILE *f1 = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+            if (std::fscanf(f1, "%lld", &quota) != 1) quota = -1;
+            std::fclose(f1);
+        }
+        if (FILE *f2 = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+            if (std::fscanf(f2, "%lld", &period) != 1) period = 0;
+            std::fclose(f2);
+        }
+    }
+    return (quota > 0 && period > 0) ? (int)(quota / period) : 0;
+}
+
 int fail(svgd_ctx *c, int code, const std::string &msg)
 {
     if (c) c->err = "SVGDCpp: " + msg;
@@ -1603,7 +1626,16 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     if (const char *e = std::getenv("SVGD_TRACK_BRACKET")) c->trk_allowed = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_TRACK_MIN_WIDTH")) c->trk_min_w = std::atof(e);
     if (const char *e = std::getenv("SVGD_TRACK_ERR_MULT")) c->trk_err_mult = std::atof(e);
-    c->host_threads = std::max(1, omp_get_max_threads() / 2);
+    // half the OpenMP threads, but no more than this rank's share of the
+    // cgroup CPU quota (ranks of one node share it; OpenMP sees the affinity
+    // mask, not the quota) and at most 32 (the gradient of a 65536-row share
+    // takes 0.4 ms on 8 threads, hidden behind the device median)
+    {
+        int t = std::max(1, omp_get_max_threads() / 2);
+        const int q = cgroup_cpus();
+        if (q > 0) t = std::min(t, std::max(1, q / std::max(1, c->world)));
+        c->host_threads = std::min(t, 32);
+    }
     if (const char *e = std::getenv("SVGD_HOST_THREADS")) c->host_threads = std::max(1, std::atoi(e));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SVGD_OK;
