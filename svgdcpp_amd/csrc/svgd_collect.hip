@@ -33,15 +33,24 @@ typedef f4_t f4;
 // TH_i of k_pair_rows (e > TL => key < lo, e <= TH => key >= hi):
 //   ef >  TLf_i = up(TL_i + delta)    => below (counted)
 //   ef <= THf_i = down(TH_i - delta)  => above (dropped)
-// otherwise the pair is staged as (row, column) in LDS and finished exactly
+// otherwise the pair is staged in LDS (one entry per lane and 16 x 16 block)
+// and finished exactly
 // in a batch (mcol_flush).  Data outside |x|^2 <= 2^40 sets delta = inf:
 // every pair is then finished exactly (correct, slow).
 constexpr int MC_STG = 512; // staged band pairs per wave
 constexpr int MC_NG = 4;    // 16-row blocks per classification group
 // Timing ablations of k_pair_mcol (tools/gpu_mcol_abl.sh; WRONG results, never
-// a shipped build): 1 = no band staging, 2 = MFMAs only (no classification)
+// a shipped build): 1 = no band staging, 2 = MFMAs only (no classification),
+// 3 = staging without the exact flush
 #ifndef SVGD_MCOL_ABL
 #define SVGD_MCOL_ABL 0
+#endif
+// Band staging form: 0 = exec-masked store under a branch on "any band
+// value", 1 = the same branch, every lane stores (lanes without band values,
+// and entries past the area, into a 64-slot spill zone: no exec change, no
+// second branch), 2 = as 1 without the branch (every block)
+#ifndef SVGD_MCOL_STAGE
+#define SVGD_MCOL_STAGE 1
 #endif
 
 __device__ __forceinline__ float f32_up(double x)
@@ -160,7 +169,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     constexpr int RW = McolRow<D>::RW;
     constexpr int NI = PBLK / 16;          // 16-row blocks of a tile
     __shared__ __attribute__((aligned(16))) float sRow[NI * 64 * RW];
-    __shared__ uint32_t sStage[4][MC_STG];
+    __shared__ uint32_t sStage[4][MC_STG + 64]; // + the spill zone (SVGD_MCOL_STAGE)
     __shared__ uint32_t sBk[NBK];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -193,7 +202,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     // (appended to the region, bucketed) / dropped.
     auto flush = [&](int64_t ib, int64_t jbase) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // other lanes' staging stores
-        for (int q0 = 0; q0 < scnt; q0 += 64) {
+        if (scnt > MC_STG) { // entries went to the spill zone (SVGD_MCOL_STAGE >= 1)
+            ovf = true;
+            scnt = MC_STG;
+        }
+        for (int q0 = 0; q0 < (SVGD_MCOL_ABL == 3 ? 0 : scnt); q0 += 64) {
             const bool valid = q0 + lane < scnt;
             const uint32_t e = valid ? stage[q0 + lane] : 0u;
             uint32_t code = e >> 28; // 0 on invalid lanes
@@ -390,10 +403,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                             } else {
                                 any = mcol_classify4(acc[g], Bg[g][KK], Bg[g][KK + 1], nbelow, h);
                             }
-                            // ~0.4 of the blocks, ~1 band pair each: ONE entry per
-                            // lane holding band values (its 4 values' band bits),
-                            // branch-free (the flush expands the bits)
-                            if (SVGD_MCOL_ABL == 0 && __builtin_expect(any != 0, 0)) {
+                            // ~0.4 of the blocks hold band values (~1 pair each):
+                            // ONE entry per lane with its 4 values' band bits (the
+                            // flush expands the bits)
+                            if constexpr (SVGD_MCOL_STAGE >= 1 && (SVGD_MCOL_ABL == 0 || SVGD_MCOL_ABL == 3)) {
+                                if (SVGD_MCOL_STAGE == 2 || __builtin_expect(any != 0, 0)) {
+                                    // every lane stores: a lane without band values, or an
+                                    // entry past the area, lands in the spill zone; the
+                                    // flush reports an overflowed area (scnt > MC_STG)
+                                    const uint32_t code = mcol_code4(h);
+                                    const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
+                                        (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
+                                    uint32_t idx = code ? (uint32_t)scnt + pre : (uint32_t)(MC_STG + lane);
+                                    idx = min(idx, (uint32_t)(MC_STG + lane));
+                                    stage[idx] = (16u * (g0 + g) + ql) | ((uint32_t)(jl0 + 4 * kq) << 16) |
+                                                 (code << 28);
+                                    scnt += __popcll(any);
+                                }
+                            } else if ((SVGD_MCOL_ABL == 0 || SVGD_MCOL_ABL == 3) && __builtin_expect(any != 0, 0)) {
+                                // ~0.4 of the blocks, ~1 band pair each: ONE entry per
+                                // lane holding band values (its 4 values' band bits)
                                 const int c = __popcll(any);
                                 if (scnt + c > MC_STG) { // pathological band: give up
                                     ovf = true;          // (region overflow -> exact fallback)
