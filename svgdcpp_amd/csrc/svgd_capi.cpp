@@ -187,6 +187,7 @@ struct svgd_ctx {
     bool shard_sample = false;
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
     bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol / _tcol)
+    bool mcol_bf16 = true;         // k_pair_mcol's Gram as split bf16 (d <= 8; SVGD_MCOL_BF16=0: f32)
     double band_est = 1.0;         // this step's bracket: expected share of the pairs
     bool samp_shard = false;    // this step's sample is sharded
     int64_t samp_local = 0;     // sample keys held by this rank
@@ -880,7 +881,7 @@ int collect_counts(svgd_ctx *c)
         // (a thin band only: each band pair is staged and finished one by one)
         HIPCHK(c, launch_pair_mcol(c->dim, c->collect_grid, c->xc, c->xf, c->nmax, c->n, c->pnb,
                                    c->tile0, c->tile0 + c->own_tiles, c->regions, c->reg_cap,
-                                   c->counts, c->below, c->st, c->bpart, c->stream));
+                                   c->counts, c->below, c->st, c->bpart, c->mcol_bf16, c->stream));
     else if (!c->rowpath && c->dtype == SVGD_F32 && c->mcol)
         // fp32 tile path: k_pair_tiles' keys, rows held in VGPRs, no LDS
         HIPCHK(c, launch_pair_tcol(c->KP, c->collect_grid, c->xcf, c->nrmf, c->n, c->pnb, c->tile0,
@@ -1597,6 +1598,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     // A/B and test knob: the reference collect passes (k_pair_rows / k_pair_tiles
     // MODE 0) instead of the matrix-core ones (k_pair_mcol / k_pair_tcol)
     if (const char *e = std::getenv("SVGD_COLLECT_FP64")) c->mcol = std::atoi(e) == 0;
+    if (const char *e = std::getenv("SVGD_MCOL_BF16")) c->mcol_bf16 = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));

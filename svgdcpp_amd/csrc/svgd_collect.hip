@@ -2,6 +2,7 @@
 // (gfx950).  Built with VGPR-form MFMA operands (Makefile), which the other
 // kernels are not.
 #include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
 #include <stdint.h>
 #include <type_traits>
 
@@ -153,11 +154,39 @@ template <int D> struct McolRow {
     static constexpr int RW = ((KK + 2 + 3) / 4) * 4; // floats per lane slot (16-byte units)
 };
 
+// BF (d <= 8): the Gram on ONE v_mfma_f32_16x16x32_bf16 per 16 x 16 block
+// instead of KK = 2 f32 16x16x4 steps (16 instead of 64 cycles).  Each fp32
+// coordinate is split x = hi + lo + r, hi = bf16(x), lo = bf16(x - hi)
+// (x - hi exact in fp32), |r| <= 2^-16 |x|, and the k = 32 slots hold all four
+// products: A (columns) k-groups [hi | lo | hi | lo], B (rows) [hi | hi | lo |
+// lo].  Error of the fp32 value against h_j + xc_i.xc_j (S = sum_k |x_ik x_jk|
+// <= nmax by Cauchy-Schwarz, |h_j| <= nmax / 2): h_j rounding 2^-25 nmax,
+// fp32 inputs 2^-23 S, the split (|r_i||x_j| + |x_i||r_j| + |r_i r_j|) <=
+// 2^-15 S, the bf16 products exact in fp32 and at most 33 fp32 roundings of
+// the sum over |h_j| + 1.02 S: in all <= 3.4e-5 nmax.  MCOL_DELTA_BF =
+// 2^-14 nmax (1.8x that) plus 2^-100 for flushed denormals.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint4 mcol_split_bf16(const float (&x)[8], bool lo_part)
+{
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const __hip_bfloat162 h = __float22bfloat162_rn(make_float2(x[2 * q], x[2 * q + 1]));
+        const uint32_t hb = *reinterpret_cast<const uint32_t *>(&h);
+        const float r0 = x[2 * q] - __uint_as_float(hb << 16);
+        const float r1 = x[2 * q + 1] - __uint_as_float(hb & 0xffff0000u);
+        const __hip_bfloat162 l = __float22bfloat162_rn(make_float2(r0, r1));
+        const uint32_t lb = *reinterpret_cast<const uint32_t *>(&l);
+        o[q] = lo_part ? lb : hb;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // A block's 4 waves share one tile at a time: the tile's 256 rows live in LDS
 // (B operands and thresholds, written when the row block changes), and wave w
 // takes the 16-column blocks w, w + 4, ...  Each wave stages its own band
 // pairs and owns region blockIdx * 4 + w, as k_pair_rows.
-template <int D>
+template <int D, bool BF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 : 2, 8))) void k_pair_mcol(const double *__restrict__ xc,
                                                   const float *__restrict__ xf, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
@@ -168,7 +197,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     constexpr int KK = McolRow<D>::KK;     // MFMA k-steps
     constexpr int RW = McolRow<D>::RW;
     constexpr int NI = PBLK / 16;          // 16-row blocks of a tile
-    __shared__ __attribute__((aligned(16))) float sRow[NI * 64 * RW];
+    static_assert(!BF || (D <= 8 && RW == 4), "the bf16 split form takes d <= 8");
+    __shared__ __attribute__((aligned(16))) float sRow[NI * 64 * RW]; // BF: the B fragments
+    __shared__ float2 sThr[BF ? PBLK : 1];                            // BF: (TLf, THf) per row
     __shared__ uint32_t sStage[4][MC_STG + 64]; // + the spill zone (SVGD_MCOL_STAGE)
     __shared__ uint32_t sBk[NBK];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -182,7 +213,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     const double lo_d = __longlong_as_double((long long)lo_key);
     const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
                                                         : __longlong_as_double((long long)hi_key);
-    const double delta = nmax <= 0x1p40 ? 4.0 * (D + 4) * 0x1p-24 * nmax + 0x1p-100 : __builtin_inf();
+    const double delta = nmax > 0x1p40 ? __builtin_inf()
+                         : BF     ? 0x1p-14 * nmax + 0x1p-100 // MCOL_DELTA_BF (above)
+                                  : 4.0 * (D + 4) * 0x1p-24 * nmax + 0x1p-100;
+    constexpr int AK = BF ? 4 : KK; // A operand dwords per lane (BF: 8 bf16)
+    constexpr int BW = BF ? 2 : RW; // per-group row values kept in registers
+    constexpr int TI = BF ? 0 : KK; // their (TLf, THf) slots
     if (sc.bpart)
         for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
 
@@ -315,6 +351,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                     const bool iv = i < n;
                     const int64_t ic = iv ? i : n - 1;
                     float *o = sRow + e * RW;
+                    if constexpr (BF) {
+                        // B fragment: k-groups [hi | hi | lo | lo] of row i
+                        float x[8];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) x[k] = k < D ? xf[ic * KF + k] : 0.0f;
+                        *reinterpret_cast<uint4 *>(o) = mcol_split_bf16(x, (l >> 4) >= 2);
+                        if (e < PBLK) { // thresholds once per row: row ib + e
+                            const int64_t it = ib + e;
+                            const bool tv = it < n;
+                            const int64_t tc = tv ? it : n - 1;
+                            const double ni = -2.0 * xc[tc * KP + D];
+                            const double m = 0x1p-48 * (ni + nmax);
+                            const double TL = lo_key == 0 ? __builtin_inf() : 0.5 * (ni - lo_d + m);
+                            const double TH = 0.5 * (ni - hi_d - m);
+                            sThr[e] = make_float2(tv ? f32_up(TL + delta) : __builtin_inff(),
+                                                  tv ? f32_down(TH - delta) : __builtin_inff());
+                        }
+                        continue;
+                    }
 #pragma unroll
                     for (int kk = 0; kk < KK; ++kk) {
                         const int k = 4 * kk + (l >> 4);
@@ -335,8 +390,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
             // this wave's 16-column blocks; the next one's operands load during
             // the current one's MFMAs (xf rows [n, np) hold h = -inf: padding
             // columns are never below or in the band; blocks end before np)
-            auto load_cols = [&](int jb, float (&A)[KK], f4 &hq) {
+            auto load_cols = [&](int jb, float (&A)[AK], f4 &hq) {
                 const float *xcol = xf + (jbase + 16 * jb) * KF;
+                if constexpr (BF) {
+                    // A fragment: k-groups [hi | lo | hi | lo] of column j
+                    float x[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) x[k] = k < D ? xcol[ql * KF + k] : 0.0f;
+                    *reinterpret_cast<uint4 *>(A) = mcol_split_bf16(x, (kq & 1) != 0);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
+                    return;
+                }
 #pragma unroll
                 for (int kk = 0; kk < KK; ++kk) {
                     const float x = xcol[ql * KF + 4 * kk + kq];
@@ -346,8 +411,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                 for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
             };
             // one group of MC_NG row blocks: its row operands from LDS, its MFMAs
-            auto group_mfma = [&](int g0, const f4 &hq, const float (&A)[KK],
-                                  float (&Bg)[MC_NG][RW], f4 (&acc)[MC_NG]) {
+            auto group_mfma = [&](int g0, const f4 &hq, const float (&A)[AK],
+                                  float (&Bg)[MC_NG][BW], f4 (&acc)[MC_NG]) {
+                if constexpr (BF) {
+                    const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(A));
+#pragma unroll
+                    for (int g = 0; g < MC_NG; ++g) {
+                        const uint4 b = *reinterpret_cast<const uint4 *>(sRow + ((g0 + g) * 64 + lane) * RW);
+                        const float2 t = sThr[16 * (g0 + g) + ql];
+                        Bg[g][0] = t.x;
+                        Bg[g][1] = t.y;
+                        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, b), hq,
+                                                                         0, 0, 0);
+                    }
+                    return;
+                }
 #pragma unroll
                 for (int g = 0; g < MC_NG; ++g)
 #pragma unroll
@@ -371,7 +449,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
             // > THf but not below) OR-ed; phase 3, rare: stage the band pairs).
             auto jloop = [&](auto diag_tag) {
                 constexpr bool DIAG = decltype(diag_tag)::value;
-                float A[KK], An[KK];
+                float A[AK], An[AK];
                 f4 hq, hqn;
                 if (w < njb) load_cols(w, A, hq);
                 for (int jb = w; jb < njb; jb += 4) {
@@ -380,7 +458,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                     if (scnt > MC_STG / 2) flush(ib, jbase);
                     if (jb + 4 < njb) load_cols(jb + 4, An, hqn);
                     const int jl0 = 16 * jb;
-                    float Bg[MC_NG][RW], Bn[MC_NG][RW];
+                    float Bg[MC_NG][BW], Bn[MC_NG][BW];
                     f4 acc[MC_NG], accn[MC_NG];
                     group_mfma(0, hq, A, Bg, acc);
                     for (int g0 = 0; g0 < NI; g0 += MC_NG) {
@@ -391,17 +469,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                             unsigned long long h[4], any = 0;
                             if constexpr (SVGD_MCOL_ABL == 2) {
                                 asm volatile("" ::"v"(acc[g][0]), "v"(acc[g][1]), "v"(acc[g][2]),
-                                             "v"(acc[g][3]), "v"(Bg[g][KK]), "v"(Bg[g][KK + 1]));
+                                             "v"(acc[g][3]), "v"(Bg[g][TI]), "v"(Bg[g][TI + 1]));
                                 continue;
                             } else if constexpr (DIAG) {
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
-                                    h[r] = mcol_classify_diag(acc[g][r], Bg[g][KK], Bg[g][KK + 1], xl,
+                                    h[r] = mcol_classify_diag(acc[g][r], Bg[g][TI], Bg[g][TI + 1], xl,
                                                               16 * (g0 + g) - jl0 - r, nbelow);
                                     any |= h[r];
                                 }
                             } else {
-                                any = mcol_classify4(acc[g], Bg[g][KK], Bg[g][KK + 1], nbelow, h);
+                                any = mcol_classify4(acc[g], Bg[g][TI], Bg[g][TI + 1], nbelow, h);
                             }
                             // ~0.4 of the blocks hold band values (~1 pair each):
                             // ONE entry per lane with its 4 values' band bits (the
@@ -442,11 +520,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                         for (int g = 0; g < MC_NG; ++g) {
                             acc[g] = accn[g];
 #pragma unroll
-                            for (int q = 0; q < RW; ++q) Bg[g][q] = Bn[g][q];
+                            for (int q = 0; q < BW; ++q) Bg[g][q] = Bn[g][q];
                         }
                     }
 #pragma unroll
-                    for (int kk = 0; kk < KK; ++kk) A[kk] = An[kk];
+                    for (int kk = 0; kk < AK; ++kk) A[kk] = An[kk];
                     hq = hqn;
                 }
             };
@@ -801,16 +879,36 @@ hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm,
         hipLaunchKernelGGL((k_pair_mcol<Dv>), dim3(grid), dim3(256), 0, stream, xc, xf, n, nb, t0, \
                            t1, sc);                                                          \
         break;
+#define SVGD_MCOLB_CASE(Dv)                                                                  \
+    case Dv:                                                                                 \
+        hipLaunchKernelGGL((k_pair_mcol<Dv, true>), dim3(grid), dim3(256), 0, stream, xc, xf, n, nb, \
+                           t0, t1, sc);                                                      \
+        return hipGetLastError();
+
 
 hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
                             const unsigned long long *nmax_bits, int64_t n, int64_t nb, int64_t t0,
                             int64_t t1, uint64_t *regions, int64_t cap, uint32_t *counts,
                             unsigned long long *below, const SelState *st, uint32_t *bpart,
-                            hipStream_t stream)
+                            bool bf16, hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
     if (!nmax_bits || !xf) return hipErrorInvalidValue;
     SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, bpart};
+    if (d <= 8 && bf16) { // the bf16-split Gram (k_pair_mcol<D, true>)
+        switch (d) {
+            SVGD_MCOLB_CASE(1)
+            SVGD_MCOLB_CASE(2)
+            SVGD_MCOLB_CASE(3)
+            SVGD_MCOLB_CASE(4)
+            SVGD_MCOLB_CASE(5)
+            SVGD_MCOLB_CASE(6)
+            SVGD_MCOLB_CASE(7)
+            SVGD_MCOLB_CASE(8)
+        default:
+            break;
+        }
+    }
     switch (d) {
         SVGD_MCOL_CASE(1)
         SVGD_MCOL_CASE(2)

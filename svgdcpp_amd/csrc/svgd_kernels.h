@@ -249,7 +249,7 @@ hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
                             const unsigned long long *nmax_bits, int64_t n, int64_t nb, int64_t t0,
                             int64_t t1, uint64_t *regions, int64_t cap, uint32_t *counts,
                             unsigned long long *below, const SelState *st, uint32_t *bpart,
-                            hipStream_t stream);
+                            bool bf16, hipStream_t stream);
 // fp32 tile-path collect (k_pair_tiles<float> MODE 0 on the matrix cores,
 // same keys): one region per block; KP in {4, 8, 12, 16, 32, 64}
 hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, int64_t n,

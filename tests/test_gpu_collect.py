@@ -12,6 +12,10 @@ the exact streamed fallback selects).  GaussianRBFKernel.hpp:164-188, 222-254.
 
 The sample (2^16 pairs, 3 sigma) keeps the bracket under the 2 % band share
 above which the library takes k_pair_rows' collect instead.
+
+For d <= 8 the Gram is split bf16 by default (one v_mfma_f32_16x16x32_bf16 per
+16 x 16 block, a wider proven margin); SVGD_MCOL_BF16=0 selects the f32 Gram.
+Both are checked against the same fp64 collect and exact statistics.
 """
 import numpy as np
 import pytest
@@ -22,8 +26,9 @@ from svgdcpp_amd import _capi as C
 pytestmark = pytest.mark.gpu
 
 
-def _median(X, monkeypatch, fp64, sample=1 << 16):
+def _median(X, monkeypatch, fp64, sample=1 << 16, bf16=True):
     monkeypatch.setenv("SVGD_COLLECT_FP64", "1" if fp64 else "0")
+    monkeypatch.setenv("SVGD_MCOL_BF16", "1" if bf16 else "0")
     n, d = X.shape
     c = S.Context(d, n)
     c.set_particles(X)
@@ -45,11 +50,14 @@ def _exact_median(c, n):
     return (at(tot // 2 - 1) + at(tot // 2)) / 2 if tot % 2 == 0 else at(tot // 2)
 
 
+@pytest.mark.parametrize("bf16", [True, False], ids=["bf16", "f32"])
 @pytest.mark.parametrize("d", [1, 2, 3, 4, 5, 8, 12, 16])
 @pytest.mark.parametrize("n", [300, 1000, 2049, 4097])
-def test_mcol_matches_fp64_collect_and_exact(oracle, monkeypatch, n, d):
+def test_mcol_matches_fp64_collect_and_exact(oracle, monkeypatch, n, d, bf16):
+    if not bf16 and d > 8:
+        pytest.skip("d > 8 always takes the f32 Gram")
     X = oracle.splitmix((n, d), 3.0, 7 * n + d)
-    c, got = _median(X, monkeypatch, fp64=False)
+    c, got = _median(X, monkeypatch, fp64=False, bf16=bf16)
     assert got[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET), got
     exp = _exact_median(c, n)
     c.close()
@@ -59,8 +67,9 @@ def test_mcol_matches_fp64_collect_and_exact(oracle, monkeypatch, n, d):
     assert got[1] == exp
 
 
+@pytest.mark.parametrize("bf16", [True, False], ids=["bf16", "f32"])
 @pytest.mark.parametrize("kind", ["ties", "huge", "tiny", "outlier"])
-def test_mcol_pathological_inputs_exact(oracle, monkeypatch, kind):
+def test_mcol_pathological_inputs_exact(oracle, monkeypatch, kind, bf16):
     """Bands the fp32 classification cannot narrow: the result is still exact."""
     n, d = 1500, 8
     X = oracle.splitmix((n, d), 1.0, 99)
@@ -73,7 +82,7 @@ def test_mcol_pathological_inputs_exact(oracle, monkeypatch, kind):
     else:
         X[17] = 1e6  # one far particle widens every threshold
     n = X.shape[0]
-    c, got = _median(X, monkeypatch, fp64=False)
+    c, got = _median(X, monkeypatch, fp64=False, bf16=bf16)
     exp = _exact_median(c, n)
     c.close()
     f, ref = _median(X, monkeypatch, fp64=True)
@@ -87,15 +96,16 @@ def test_mcol_large_matches_fp64_collect(oracle, monkeypatch, n, d):
     """Default sample sizes (no tuning) at sizes where the bracket path is the default."""
     X = oracle.splitmix((n, d), 3.0, n + d)
     res = []
-    for fp64 in (False, True):
+    for fp64, bf16 in ((False, True), (False, False), (True, True)):
         monkeypatch.setenv("SVGD_COLLECT_FP64", "1" if fp64 else "0")
+        monkeypatch.setenv("SVGD_MCOL_BF16", "1" if bf16 else "0")
         c = S.Context(d, n)
         c.set_particles(X)
         a, med = c.median_scale()
         res.append((a, med, c.last_median_keys()))
         assert c.last_scale()[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
         c.close()
-    assert res[0] == res[1]
+    assert res[0] == res[2] and res[1] == res[2]
 
 
 # ---------------------------------------------------------------- fp32 tiles --
@@ -168,4 +178,4 @@ def test_tcol_full_size_matches_tile_collect(oracle, monkeypatch):
         res.append(c.median_scale() + (c.last_median_keys(),))
         assert c.last_scale()[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
         c.close()
-    assert res[0] == res[1]
+    assert res[0] == res[2] and res[1] == res[2]
