@@ -1,0 +1,82 @@
+"""The error bound behind k_pair_mcol's split-bf16 Gram (svgd_collect.hip,
+MCOL_DELTA_BF).  CPU only (numpy emulation of the arithmetic).
+
+Each fp32 coordinate is split x = hi + lo + r with hi = bf16_rn(x) and
+lo = bf16_rn(x - hi); the MFMA sums the four bf16 products hi.hi, lo.hi,
+hi.lo, lo.lo (exact in fp32) and h_j in fp32.  The classification margin
+2^-14 max|xc|^2 must cover |ef - e| for e = h_j + xc_i.xc_j: checked here on
+random, clustered and cancelling data, with every fp32 addition rounded (the
+worst order the hardware could use is not known, so sequential rounding in
+two orders is emulated) and with truncation instead of rounding.
+"""
+import numpy as np
+import pytest
+
+
+def bf16_rn(x32):
+    """fp32 -> bf16 (round to nearest even), returned as fp32 values."""
+    u = x32.astype(np.float32).view(np.uint32).astype(np.uint64)
+    r = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return r.astype(np.uint32).view(np.float32)
+
+
+def split(x32):
+    hi = bf16_rn(x32)
+    lo = bf16_rn((x32 - hi).astype(np.float32))
+    return hi, lo
+
+
+def f32_sum(terms, trunc=False):
+    """Sequential fp32 sum (each addition rounded, or truncated toward 0)."""
+    acc = np.zeros(terms.shape[1:], dtype=np.float32)
+    for t in terms:
+        exact = acc.astype(np.float64) + t.astype(np.float64)
+        s = exact.astype(np.float32)
+        if trunc:
+            over = np.abs(s.astype(np.float64)) > np.abs(exact)
+            s = np.where(over, np.nextafter(s, np.float32(0)), s)
+        acc = s
+    return acc
+
+
+@pytest.mark.parametrize("kind", ["gauss", "cluster", "cancel", "wide"])
+@pytest.mark.parametrize("d", [1, 2, 5, 8])
+def test_split_bf16_gram_within_margin(kind, d):
+    rng = np.random.default_rng(1000 * d + len(kind))
+    n = 4000
+    if kind == "gauss":
+        X = rng.normal(size=(n, d))
+    elif kind == "cluster":
+        X = rng.normal(size=(n, d)) * 1e-3 + 5.0
+    elif kind == "cancel":
+        X = rng.normal(size=(n, d))
+        X[n // 2:] = -X[: n // 2] + rng.normal(size=(n // 2, d)) * 1e-6
+    else:
+        X = rng.normal(size=(n, d)) * np.exp(rng.uniform(-8, 8, size=(n, 1)))
+    X -= X.mean(axis=0)
+    nmax = float(np.max(np.sum(X * X, axis=1)))
+    delta = 2.0 ** -14 * nmax
+
+    i = rng.integers(0, n, 20000)
+    j = rng.integers(0, n, 20000)
+    xi, xj = X[i], X[j]
+    e = -0.5 * np.sum(xj * xj, axis=1) + np.sum(xi * xj, axis=1)  # fp64 reference
+
+    xi32, xj32 = xi.astype(np.float32), xj.astype(np.float32)
+    hj = (-0.5 * np.sum(xj * xj, axis=1)).astype(np.float32)
+    hi_i, lo_i = split(xi32)
+    hi_j, lo_j = split(xj32)
+    # the split itself: |x - hi - lo| <= 2^-16 |x|
+    for x, h, l in ((xi32, hi_i, lo_i), (xj32, hi_j, lo_j)):
+        r = x.astype(np.float64) - h.astype(np.float64) - l.astype(np.float64)
+        assert np.all(np.abs(r) <= 2.0 ** -16 * np.abs(x.astype(np.float64)) + 1e-300)
+    prods = np.concatenate([hi_i * hi_j, lo_i * hi_j, hi_i * lo_j, lo_i * lo_j], axis=1).astype(np.float64)
+    # bf16 x bf16 products are exact in fp32
+    assert np.all(prods.astype(np.float32).astype(np.float64) == prods)
+    for order in (1, -1):
+        for trunc in (False, True):
+            terms = np.concatenate([hj[None, :], prods.T[::order].astype(np.float32)], axis=0)
+            ef = f32_sum(terms, trunc=trunc).astype(np.float64)
+            err = np.max(np.abs(ef - e))
+            assert err <= 3.4e-5 * nmax + 1e-300, (kind, d, err / nmax)
+            assert err < delta
