@@ -73,11 +73,13 @@ def workload(n, d, k):
 
 # SURVEY §8(d) configurations (the default cfg3 is the headline metric; the
 # others are reported on request: --config cfg2 / cfg5)
+# cpu_rows: the cpu_baseline's row sample (its median work is rows x N/2
+# distances, ~10-30 s of the port's work on the box's 16 threads)
 CONFIGS = {
-    "cfg2": dict(n=16384, d=2, desc="N=16384 d=2 multivariate normal (mvn_example parameters)"),
-    "cfg3": dict(n=65536, d=8, desc="N=65536 d=8 GMM(k=4)"),
-    "cfg4": dict(n=262144, d=8, desc="N=262144 d=8 GMM(k=4)"),
-    "cfg5": dict(n=65536, d=64, dtype="f32", desc="N=65536 d=64 multivariate normal, fp32 compute"),
+    "cfg2": dict(n=16384, d=2, cpu_rows=16384, desc="N=16384 d=2 multivariate normal (mvn_example parameters)"),
+    "cfg3": dict(n=65536, d=8, cpu_rows=32768, desc="N=65536 d=8 GMM(k=4)"),
+    "cfg4": dict(n=262144, d=8, cpu_rows=8192, desc="N=262144 d=8 GMM(k=4)"),
+    "cfg5": dict(n=65536, d=64, dtype="f32", cpu_rows=8192, desc="N=65536 d=64 multivariate normal, fp32 compute"),
 }
 
 
@@ -268,10 +270,11 @@ def _cpu_sample(o, X0, mus, covs, rows):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(X0, mus, covs, rows, rows_1t):
+def cpu_baseline(X0, mus, covs, rows, rows_1t, repeats=3):
     """Oracle (CPU port of the reference arithmetic) on a row sample of one step:
     median work of `rows` rows, their log-gradients, phi_hat and Adam -- with
-    the OpenMP threads of this box (OMP_NUM_THREADS) and with one thread."""
+    the OpenMP threads of this box (OMP_NUM_THREADS) and with one thread;
+    `repeats` timings each, the median reported."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as o
 
@@ -284,12 +287,15 @@ def cpu_baseline(X0, mus, covs, rows, rows_1t):
     threads = max(1, min(affinity, int(quota)) if quota else affinity)
     keep = int(o.num_threads())
     o.set_threads(threads)
-    dt = _cpu_sample(o, X0, mus, covs, rows)
+    dts = sorted(_cpu_sample(o, X0, mus, covs, rows) for _ in range(repeats))
     o.set_threads(1)
-    dt1 = _cpu_sample(o, X0, mus, covs, rows_1t)
+    dt1s = sorted(_cpu_sample(o, X0, mus, covs, rows_1t) for _ in range(repeats))
     o.set_threads(keep)
+    dt, dt1 = dts[len(dts) // 2], dt1s[len(dt1s) // 2]
     return {
         "value": rows / dt,
+        "repeats": {"n": repeats, "rule": "median", "value_runs": [rows / t for t in dts],
+                    "value_1thread_runs": [rows_1t / t for t in dt1s]},
         "unit": "particle-updates/s",
         "cores": threads,
         "kind": "port",
@@ -301,7 +307,25 @@ def cpu_baseline(X0, mus, covs, rows, rows_1t):
         "sample": f"one step of the N={n} d={d} Gaussian-sum(k={len(mus)}) workload restricted to {rows} particle rows "
                   f"(their median pair share, grad log p of all N, phi_hat of {rows} rows against all N, "
                   f"Adam); {dt:.2f} s on {threads} OpenMP threads; 1 thread: {rows_1t} rows in {dt1:.2f} s",
+        # why the thread scaling is far below `cores`: the reference's median
+        # is std::nth_element + max_element over the N^2 distance list
+        # (GaussianRBFKernel.hpp:222-254), serial in the reference, and the
+        # port keeps it serial (the sample's rows x N/2 distances)
+        "dominant_cost": f"the serial nth_element of the reference's ComputeMedian over the sample's "
+                         f"{rows} x {n // 2} pair distances (serial in the reference as well)",
     }
+
+
+def _kernel_src_sha():
+    """First 16 hex digits of sha256 over the device sources (the key of the
+    committed PMC profiles: a kernel edit leaves them unmatched)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("svgd_kernels.hip", "svgd_collect.hip", "svgd_kernels.h"):
+        with open(os.path.join(ROOT, "svgdcpp_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def spawn_ranks(nproc):
@@ -333,7 +357,7 @@ def main():
     ap.add_argument("--n", type=int, default=None)
     ap.add_argument("--d", type=int, default=None)
     ap.add_argument("--k", type=int, default=4)
-    ap.add_argument("--cpu-rows", type=int, default=32768)
+    ap.add_argument("--cpu-rows", type=int, default=None, help="cpu_baseline row sample (default: the config's)")
     ap.add_argument("--cpu-rows-1t", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--repeats", type=int, default=5, help="timed runs of K steps; the median is reported")
@@ -350,8 +374,6 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
 
-    if args.sim_world > 1:
-        os.environ["SVGD_SIM_WORLD"] = str(args.sim_world)
     import torch
     import svgdcpp_amd as S
     from svgdcpp_amd import _capi as C
@@ -384,7 +406,8 @@ def main():
         dist.broadcast_object_list(box, src=0)
         uid = box[0]
     ctx = S.Context(d, n, device=local_rank, world=world, rank=rank, unique_id=uid,
-                    dtype=C.SVGD_F32 if dtype == "f32" else C.SVGD_F64)
+                    dtype=C.SVGD_F32 if dtype == "f32" else C.SVGD_F64,
+                    sim_world=args.sim_world if args.sim_world > 1 else None)
     ctx.set_particles(X0)
     ctx.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
     model = S.GaussianSum(list(mus), list(covs))
@@ -468,7 +491,10 @@ def main():
                              "xwait": per_step(host_timed["host_xwait_ms"], host_timed["steps"]),
                              "job": per_step(host_timed["host_job_ms"], host_timed["steps"]),
                              "caller_wait": per_step(host_timed["host_wait_ms"], host_timed["steps"]),
-                             "threads": host_timed["host_threads"]},
+                             "threads": host_timed["host_threads"],
+                             # the gradient's threads: min(OMP threads / 2, cgroup quota / ranks)
+                             "cpu_quota": host_timed["cpu_quota"],
+                             "ranks_sharing_quota": int(host_timed["sim_world"]) if args.sim_world > 1 else world},
         # speculative steps whose median bracket was predicted from the last
         # medians (no sample), and of those the ones redone after a miss
         "tracked_brackets": {"steps": int(host_timed["steps"]), "predicted": int(host_timed["trk_steps"]),
@@ -493,21 +519,26 @@ def main():
         flops_launch = float(rows) * n * (5 * d + 4)
         achieved = flops_launch / (phi_kernel_ms / 1e3) / 1e12 if phi_kernel_ms else None
         peak = FP32_PEAK_TFLOPS if dtype == "f32" else FP64_PEAK_TFLOPS
-        traffic = None
+        # committed PMC passes (not this run) count only for the same kernel
+        # (name + template arguments, svgd_phi_kernel_name), the same kernel
+        # source (hash of svgd_kernels.hip) and the same workload (N, d, P)
         wkey = args.sim_world if args.sim_world > 1 else world  # the profiles' world
-        pmc_path = os.path.join(ROOT, "profiles", "phi_pmc_traffic.json")
-        if os.path.exists(pmc_path):
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            if pmc.get("n") == n and pmc.get("d") == d and pmc.get("world") == wkey:
-                traffic = pmc.get("bytes_per_launch")
-        issue = None  # SQ counters of the same kernel (committed profile, not this run)
-        issue_path = os.path.join(ROOT, "profiles", "phi_pmc_issue.json")
-        if os.path.exists(issue_path):
-            with open(issue_path) as f:
-                iss = json.load(f)
-            if iss.get("n") == n and iss.get("d") == d and iss.get("world") == wkey and dtype == "f64":
-                issue = iss
+        kname = ctx.phi_kernel_name()
+        src_sha = _kernel_src_sha()
+
+        def committed(name):
+            path = os.path.join(ROOT, "profiles", name)
+            if not os.path.exists(path):
+                return None
+            with open(path) as f:
+                p = json.load(f)
+            ok = (p.get("n") == n and p.get("d") == d and p.get("world") == wkey and kname in p.get("kernel", "")
+                  and p.get("src_sha16") == src_sha)
+            return p if ok else None
+
+        pmc = committed("phi_pmc_traffic.json")
+        traffic = pmc.get("bytes_per_launch") if pmc else None
+        issue = committed("phi_pmc_issue.json")
         row_kernel = dtype == "f64" and d <= 16
         out = {
             "metric": METRIC,
@@ -548,6 +579,9 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": (achieved / peak) if achieved else None,
                 "traffic": traffic,
+                "traffic_source": (pmc or {}).get("source") if traffic else
+                                  f"none committed for {kname} at this source hash / workload",
+                "kernel_launched": kname,
                 "avg_launch_ms": phi_kernel_ms,
                 "flop_per_launch": flops_launch,
             },
@@ -584,7 +618,7 @@ def main():
             out["metric"] = (f"particle-updates/s, {desc}"
                              f"{', device grad log p' if args.device_model else ''} (not the headline config)")
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows, args.cpu_rows_1t)
+            out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows or cfg["cpu_rows"], args.cpu_rows_1t)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

@@ -91,6 +91,15 @@ int svgd_create(svgd_ctx **out, int dim, int64_t n, int dtype, int device);
 int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device,
                      int world, int rank, const void *unique_id128);
 int svgd_get_unique_id(void *unique_id128);
+/* Measurement only (not a drop-in call): a one-GPU context that runs rank 0's
+ * share of a `sim_world`-rank step -- its rows of phi and the update, its
+ * share of the median's pair tiles (order statistics re-anchored inside its
+ * own candidates), the host gradient on the threads one rank of sim_world
+ * would get -- with no collectives, to time the per-rank work of a P-GPU run
+ * on one GPU.  Its results are not the step's: svgd_get_particles,
+ * svgd_get_shard, svgd_median_scale and svgd_phi return SVGD_ERR_RUNTIME, and
+ * svgd_get_diagnostics reports SIM_WORLD. */
+int svgd_create_sim(svgd_ctx **out, int dim, int64_t n, int dtype, int device, int sim_world);
 int svgd_destroy(svgd_ctx *ctx);
 const char *svgd_last_error(const svgd_ctx *ctx);
 
@@ -200,7 +209,10 @@ int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *c
  *   HOST_THREADS     OpenMP threads of the host gradient
  *   TRK_STEPS        speculative steps whose median bracket was predicted from
  *                    the previous steps' medians (no sample, no bracket passes)
- *   TRK_MISS         of those, steps redone because the bracket missed */
+ *   TRK_MISS         of those, steps redone because the bracket missed
+ *   SIM_WORLD        simulated world of a measurement context (svgd_create_sim), else 1
+ *   CPU_QUOTA        CPUs of the cgroup quota (0: none); a rank's gradient
+ *                    threads are at most CPU_QUOTA / world (or / SIM_WORLD) */
 #define SVGD_DIAG_STEPS 0
 #define SVGD_DIAG_PHI_KERNEL_MS 1
 #define SVGD_DIAG_PHI_KERNEL_N 2
@@ -218,8 +230,14 @@ int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *c
 #define SVGD_DIAG_HOST_THREADS 14
 #define SVGD_DIAG_TRK_STEPS 15
 #define SVGD_DIAG_TRK_MISS 16
-#define SVGD_DIAG_LEN 17
+#define SVGD_DIAG_SIM_WORLD 17
+#define SVGD_DIAG_CPU_QUOTA 18
+#define SVGD_DIAG_LEN 19
 int svgd_get_diagnostics(svgd_ctx *ctx, double *out, int cap);
+/* Name and template arguments of the phi kernel this context launches, as
+ * rocprofv3 prints them (e.g. "k_phi_rows<8, 4, 8, 8192, 8>"): the key under
+ * which committed PMC profiles of that kernel are matched (bench.py). */
+int svgd_phi_kernel_name(const svgd_ctx *ctx, char *buf, int cap);
 /* Median tuning knobs (tests force each path): pair count at or below which
  * all keys are stored (direct path), sample size, candidate capacity.
  * Values <= 0 keep the current setting. */

@@ -37,7 +37,8 @@ SVGD_MEDIAN_REBRACKET = 3
 # svgd_get_diagnostics slots (svgd_capi.h SVGD_DIAG_*)
 DIAG_NAMES = ("steps", "phi_kernel_ms", "phi_kernel_n", "phi_wait_ms", "phi_wait_n", "coll_ms",
               "coll_n", "gather_g_ms", "gather_g_n", "host_grad_ms", "host_xwait_ms",
-              "host_job_ms", "host_wait_ms", "ranks", "host_threads", "trk_steps", "trk_miss")
+              "host_job_ms", "host_wait_ms", "ranks", "host_threads", "trk_steps", "trk_miss",
+              "sim_world", "cpu_quota")
 SVGD_DIAG_LEN = len(DIAG_NAMES)
 
 _D = ctypes.POINTER(ctypes.c_double)
@@ -49,6 +50,8 @@ SIGNATURES = {
     "svgd_create": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int]),
     "svgd_create_dist": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _I64, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+    "svgd_create_sim": (ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _I64, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int]),
     "svgd_get_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "svgd_destroy": (ctypes.c_int, [_P]),
     "svgd_last_error": (ctypes.c_char_p, [_P]),
@@ -75,6 +78,7 @@ SIGNATURES = {
     "svgd_get_timing": (ctypes.c_int, [_P, _D, _D, ctypes.POINTER(_I64)]),
     "svgd_get_diagnostics": (ctypes.c_int, [_P, _D, ctypes.c_int]),
     "svgd_set_median_tuning": (ctypes.c_int, [_P, _I64, _I64, _I64]),
+    "svgd_phi_kernel_name": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
     "svgd_debug_pair_keys": (ctypes.c_int, [_P, _D, _I64]),
     "svgd_set_scale_matrix": (ctypes.c_int, [_P, _D]),
     "svgd_set_step_hessian_sum": (ctypes.c_int, [_P, _D]),

@@ -510,11 +510,17 @@ class SVGDOptions:
 class Context:
     """Owns one svgd_ctx (one GPU).  Thin RAII wrapper used by SVGD and the bench."""
 
-    def __init__(self, dim, n, device=0, world=1, rank=0, unique_id=None, dtype=None):
+    def __init__(self, dim, n, device=0, world=1, rank=0, unique_id=None, dtype=None, sim_world=None):
+        """sim_world=P (measurement only): svgd_create_sim -- rank 0's share of
+        a P-rank step on one GPU; result calls on it raise."""
         self.lib = C.lib()
         h = ctypes.c_void_p()
         dt = C.SVGD_F64 if dtype is None else int(dtype)
-        if world == 1 and unique_id is None:
+        if sim_world is not None and sim_world > 1:
+            if world != 1:
+                raise ValueError("sim_world is a one-rank measurement context")
+            rc = self.lib.svgd_create_sim(ctypes.byref(h), int(dim), int(n), dt, int(device), int(sim_world))
+        elif world == 1 and unique_id is None:
             rc = self.lib.svgd_create(ctypes.byref(h), int(dim), int(n), dt, int(device))
         else:
             rc = self.lib.svgd_create_dist(ctypes.byref(h), int(dim), int(n), dt,
@@ -665,6 +671,12 @@ class Context:
 
     def sync(self):
         self.check(self.lib.svgd_sync(self.h))
+
+    def phi_kernel_name(self):
+        """The phi kernel (name<template args>) this context launches."""
+        buf = ctypes.create_string_buffer(128)
+        self.check(self.lib.svgd_phi_kernel_name(self.h, buf, 128))
+        return buf.value.decode()
 
     def diagnostics(self):
         """svgd_get_diagnostics as a dict (accumulated since the last call, then reset)."""

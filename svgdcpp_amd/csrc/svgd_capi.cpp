@@ -121,13 +121,34 @@ struct svgd_ctx {
     int dtype = SVGD_F64;
     int device = 0;
     int world = 1, rank = 0;
-    int sim_world = 1; // SVGD_SIM_WORLD (measurement only): rank 0's share of a P-rank step
+    // svgd_create_sim (measurement only): rank 0's share of a P-rank step on
+    // one GPU; every result-returning call refuses such a context
+    int sim_world = 1;
     int64_t sim_pairs = 0; // the unordered pairs in that share's tiles
+    int plan_world = 1;    // ranks the rows and pair tiles are planned for (world or sim_world)
+    int cpu_quota = 0;     // the cgroup's CPUs (0: no quota), shared by plan_world ranks
     ncclComm_t comm = nullptr;
     // a second communicator (ncclCommSplit of comm) for the G all-gather on
     // its own stream: it overlaps the median chain's kernels and collectives
-    // (one communicator's operations would run in issue order behind them)
+    // (one communicator's operations would run in issue order behind them).
+    // Opt-in (SVGD_G_COMM=1, the same on every rank) until a P >= 2 RCCL run
+    // has exercised it; the split's outcome is agreed across ranks.
+    //
+    // Cross-communicator issue order (the invariant both communicators rely
+    // on): within a step every rank issues
+    //   comm:  the counts all-reduce [+ the keys all-gather when speculative]
+    //          (scale_begin, all of it before returning)
+    //   gcomm: the G all-gather                   (upload_g_finish)
+    //   comm:  [the keys all-gather when synchronous] + the X all-gather
+    // -- the same sequence on every rank because every branch in it depends on
+    // all-reduced state only.  upload_g_finish checks that scale_begin has
+    // issued its comm calls (coll_phase); SVGD_DEBUG_COLL=1 also all-gathers a
+    // hash of each step's collective sequence and fails on any mismatch.
     ncclComm_t gcomm = nullptr;
+    int coll_phase = 0;      // 0 step not begun, 1 scale_begin's comm calls issued, 2 G gathered
+    uint64_t coll_sig = 0;   // FNV hash of this step's collectives (communicator, op, count)
+    bool dbg_coll = false;   // SVGD_DEBUG_COLL
+    uint64_t *sig_buf = nullptr; // world u64 (the debug all-gather)
     hipStream_t gstream = nullptr;
     hipEvent_t ev_gg = nullptr;   // G all-gathered (gstream)
     bool gg_pending = false;      // phi must wait for ev_gg
@@ -329,6 +350,9 @@ struct svgd_ctx {
     uint64_t trk_lo = 0, trk_hi = 0;
     double trk_band = 0;        // its expected share of the pairs
     bool trk_keys = false;      // this step's k_select_small writes h_trk
+    // a synchronous step's selection to add to the history (resolve_pending):
+    // 1 its keys are in h_trk / h_cnt, 2 it took another path (history restarts)
+    int trk_sync = 0;
     int64_t trk_steps = 0, trk_miss = 0;
 };
 
@@ -462,11 +486,25 @@ void diag_end(svgd_ctx *c, hipStream_t s, hipEvent_t a, int kind, bool own_a = t
 
 // ---------------------------------------------------------- collectives --
 
+// Every collective this rank issues goes into the step's sequence hash (the
+// SVGD_DEBUG_COLL cross-rank check of the issue-order invariant, svgd_ctx).
+enum { CO_GATHER_ROWS = 1, CO_REDUCE_U64 = 2, CO_GATHER_U64 = 3, CO_REDUCE_F64 = 4, CO_GCOMM = 16 };
+void coll_note(svgd_ctx *c, int op, size_t cnt)
+{
+    uint64_t h = c->coll_sig ? c->coll_sig : 0xcbf29ce484222325ull;
+    for (uint64_t v : {(uint64_t)op, (uint64_t)cnt}) {
+        h ^= v;
+        h *= 0x100000001b3ull;
+    }
+    c->coll_sig = h;
+}
+
 int allgather_rows_on(svgd_ctx *c, double *buf, ncclComm_t comm, hipStream_t s, int kind)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
     c->mark = c->phi_end = nullptr; // work queued after the median's / phi's end event
     const size_t cnt = (size_t)c->chunk * c->dim;
+    coll_note(c, CO_GATHER_ROWS | (comm && comm == c->gcomm ? CO_GCOMM : 0), cnt);
     hipEvent_t d0 = diag_begin(c, s);
     if (c->hcomm) {
         if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(double), s))
@@ -486,6 +524,7 @@ int allgather_rows(svgd_ctx *c, double *buf)
 int allreduce_u64(svgd_ctx *c, unsigned long long *buf, size_t cnt)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
+    coll_note(c, CO_REDUCE_U64, cnt);
     hipEvent_t d0 = diag_begin(c, c->stream);
     if (c->hcomm) {
         if (hostcomm_allreduce_u64(c->hcomm, buf, cnt, c->stream))
@@ -508,6 +547,7 @@ int allreduce_cnt3(svgd_ctx *c)
 int allgather_u64(svgd_ctx *c, uint64_t *buf, size_t cnt)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
+    coll_note(c, CO_GATHER_U64, cnt);
     hipEvent_t d0 = diag_begin(c, c->stream);
     if (c->hcomm) {
         if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(buf), cnt * sizeof(uint64_t),
@@ -526,6 +566,7 @@ bool matrix_scale(const svgd_ctx *c);
 int allreduce_f64(svgd_ctx *c, double *buf, size_t cnt)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank, no communicator
+    coll_note(c, CO_REDUCE_F64, cnt);
     if (c->hcomm) {
         if (hostcomm_allreduce_f64(c->hcomm, buf, cnt, c->stream))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
@@ -542,6 +583,19 @@ SelState make_state(int nsel, const uint64_t *ranks, uint64_t lo_key, uint64_t h
 
 // st_init (optional): the predicted bracket's select state, written by the
 // centring launch itself (no launch of its own)
+// Level 2: the start of the phi-wait span (run_phi) -- a pooled event of its
+// own, recorded where the median ends (the phase events go back to the pool
+// in svgd_get_timing; a diagnostic span must not share one of them)
+int mark_median_end(svgd_ctx *c)
+{
+    if (c->tlevel < 2) return SVGD_OK;
+    if (c->med_end_ev) c->ev_single.push_back(c->med_end_ev); // (never consumed)
+    c->med_end_ev = take_ev(c);
+    HIPCHK(c, hipEventRecord(c->med_end_ev, c->stream));
+    c->mark = nullptr; // work (an event) queued after the median's end
+    return SVGD_OK;
+}
+
 int center(svgd_ctx *c, const SelState *st_init = nullptr)
 {
     HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
@@ -927,13 +981,13 @@ int median_finish_spec(svgd_ctx *c, double logn)
     // complete, by median_finish: resolve_pending never redoes half a step)
     if (c->timing && !c->ev_med.empty()) {
         c->ev_status_use = c->ev_med.back().b; // also the median phase's end
-        c->med_end_ev = c->ev_status_use;
         c->med_ev_done = true;
         c->mark = c->ev_status_use;
     } else {
         c->ev_status_use = c->ev_status;
     }
     HIPCHK(c, hipEventRecord(c->ev_status_use, c->stream));
+    CHK(mark_median_end(c));
     return SVGD_OK;
 }
 
@@ -1081,6 +1135,19 @@ int check_ready(svgd_ctx *c)
     return SVGD_OK;
 }
 
+// Calls that hand results back refuse a measurement context (svgd_create_sim):
+// its particles, phi and scale are one rank's share computed without the
+// other ranks' data, not the step's.
+int check_results(svgd_ctx *c)
+{
+    CHK(check_ready(c));
+    if (c->sim_world > 1)
+        return fail(c, SVGD_ERR_RUNTIME,
+                    "[Runtime Error] measurement context (svgd_create_sim, world " +
+                        std::to_string(c->sim_world) + "): its results are not the step's.");
+    return SVGD_OK;
+}
+
 // G shard -> device on the copy stream (ready at ev_g) ...
 int upload_g_begin(svgd_ctx *c, const double *G_shard)
 {
@@ -1105,6 +1172,13 @@ int upload_g_begin(svgd_ctx *c, const double *G_shard)
 int upload_g_finish(svgd_ctx *c)
 {
     if (c->gcomm) {
+        // the issue-order invariant (svgd_ctx): with a median pending, every
+        // comm call of scale_begin precedes this gcomm call on every rank
+        if (c->median_pending && c->coll_phase != 1)
+            return fail(c, SVGD_ERR_RUNTIME,
+                        "[Runtime Error] G all-gather issued before the median's collectives "
+                        "(cross-communicator issue order).");
+        c->coll_phase = 2;
         if (hipEventQuery(c->ev_g) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(c->gstream, c->ev_g, 0));
         CHK(allgather_rows_on(c, c->G, c->gcomm, c->gstream, DG_GATHER_G));
         HIPCHK(c, hipEventRecord(c->ev_gg, c->gstream));
@@ -1161,7 +1235,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         if (hipEventQuery(c->ev_gg) != hipSuccess) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_gg, 0));
         c->gg_pending = false;
     }
-    if (med_end) diag_end(c, c->stream, med_end, DG_PHI_WAIT, false);
+    if (med_end) diag_end(c, c->stream, med_end, DG_PHI_WAIT, true);
     const bool mat = matrix_scale(c);
     if (mat) {
         // M = factor * src, L = chol(M), a_eff = 1 (GaussianRBFKernel.hpp:189-210)
@@ -1254,6 +1328,41 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     return SVGD_OK;
 }
 
+// End of a step's collectives: SVGD_DEBUG_COLL=1 all-gathers every rank's
+// hash of the step's collective sequence (communicator, op, count, in issue
+// order) and fails unless all are equal -- the cross-rank check of the issue
+// order both communicators rely on (svgd_ctx).  Off by default (a blocking
+// all-gather per step).
+int coll_check_step(svgd_ctx *c)
+{
+    const uint64_t mine = c->coll_sig;
+    c->coll_sig = 0;
+    c->coll_phase = 0;
+    if (!c->dbg_coll || (!c->comm && !c->hcomm)) return SVGD_OK;
+    if (!c->sig_buf) {
+        HIPCHK(c, hipMalloc((void **)&c->sig_buf, sizeof(uint64_t) * (size_t)c->world));
+    }
+    HIPCHK(c, hipMemcpyAsync(c->sig_buf + c->rank, &mine, sizeof(uint64_t), hipMemcpyHostToDevice,
+                             c->stream));
+    if (c->hcomm) {
+        if (hostcomm_allgather(c->hcomm, reinterpret_cast<char *>(c->sig_buf), sizeof(uint64_t),
+                               c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-gather failed.");
+    } else {
+        NCCLCHK(c, ncclAllGather(c->sig_buf + c->rank, c->sig_buf, 1, ncclUint64, c->comm, c->stream));
+    }
+    std::vector<uint64_t> all((size_t)c->world);
+    HIPCHK(c, hipMemcpyAsync(all.data(), c->sig_buf, sizeof(uint64_t) * all.size(),
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->mark = c->phi_end = nullptr;
+    for (uint64_t s : all)
+        if (s != mine)
+            return fail(c, SVGD_ERR_RCCL,
+                        "[RCCL Error] ranks issued different collective sequences this step.");
+    return SVGD_OK;
+}
+
 // This step's optimizer arguments (advances t: call once per step).
 int opt_args(svgd_ctx *c, OptArgs *o)
 {
@@ -1300,7 +1409,7 @@ int run_phi_opt(svgd_ctx *c)
     }
     CHK(allgather_rows(c, c->X));
     c->phi_end = nullptr;
-    return SVGD_OK;
+    return coll_check_step(c);
 }
 
 int scale_begin(svgd_ctx *c)
@@ -1332,8 +1441,9 @@ int scale_begin(svgd_ctx *c)
     } else {
         CHK(center(c));
     }
-    if (!med) return SVGD_OK;
-    return median_begin(c);
+    if (med) CHK(median_begin(c));
+    c->coll_phase = 1; // every comm call of this phase is issued (upload_g_finish)
+    return SVGD_OK;
 }
 
 int scale_finish(svgd_ctx *c)
@@ -1354,19 +1464,20 @@ int scale_finish(svgd_ctx *c)
         return SVGD_OK;
     }
     CHK(median_finish(c));
+    // a synchronous selection joins the tracking history when resolved
+    // (the speculative ones in resolve_pending)
+    if (!c->spec_step) c->trk_sync = c->trk_keys ? 1 : 2;
     // [a, med] reach the host only when asked (fetch_scale): no copy on the
     // step's path; the event marks where this step's scale is final (on the
     // speculative path the status event, recorded right after the selection)
     if (c->med_ev_done) {
         c->ev_fin_use = c->ev_status_use;
     } else {
-        if (c->timing && !c->ev_med.empty()) {
-            HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
-            c->med_end_ev = c->ev_med.back().b;
-        }
+        if (c->timing && !c->ev_med.empty()) HIPCHK(c, hipEventRecord(c->ev_med.back().b, c->stream));
         HIPCHK(c, hipEventRecord(c->ev_fin, c->stream));
         c->ev_fin_use = c->ev_fin;
         c->mark = nullptr;
+        CHK(mark_median_end(c));
     }
     c->med_ev_done = false;
     c->scal_fresh = false;
@@ -1390,8 +1501,26 @@ int fetch_scale(svgd_ctx *c)
 // m_t, v_t, t and redo the step on the synchronous path (G_t is still on the
 // device).  Every rank sees the same status (it derives from all-reduced
 // counts), so the redo's collectives match across ranks.
+// A synchronous step's selection into the tracking history (its keys are in
+// h_trk once the step's scale is final; its bracket counts in h_cnt), or a
+// restart of the history when that step selected another way.
+int trk_resolve_sync(svgd_ctx *c)
+{
+    const int s = c->trk_sync;
+    c->trk_sync = 0;
+    if (s == 0) return SVGD_OK;
+    if (s == 2 || !c->trk_allowed) {
+        c->trk_n = 0;
+        return SVGD_OK;
+    }
+    HIPCHK(c, hipEventSynchronize(c->ev_fin_use ? c->ev_fin_use : c->ev_fin));
+    trk_record(c, c->h_cnt[CNT_LO], c->h_cnt[CNT_HI], c->h_cnt[1]);
+    return SVGD_OK;
+}
+
 int resolve_pending(svgd_ctx *c)
 {
+    CHK(trk_resolve_sync(c));
     if (!c->pending) return SVGD_OK;
     c->pending = false;
     HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
@@ -1419,13 +1548,7 @@ int resolve_pending(svgd_ctx *c)
     CHK(scale_finish(c));
     CHK(run_phi_opt(c));
     // the redo's selection (synchronous path) continues the tracking history
-    if (c->trk_allowed && c->trk_keys) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        trk_record(c, c->h_cnt[CNT_LO], c->h_cnt[CNT_HI], c->h_cnt[1]);
-    } else {
-        c->trk_n = 0;
-    }
-    return SVGD_OK;
+    return trk_resolve_sync(c);
 }
 
 // Speculate this step's median when the last one would have allowed it.
@@ -1437,7 +1560,7 @@ int plan_step(svgd_ctx *c)
     return SVGD_OK;
 }
 
-int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
+int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_world = 1)
 {
     if (dim <= 0 || n <= 0)
         return fail(c, SVGD_ERR_DIM, "[Dimension Error] Particle count and dimension must be positive.");
@@ -1456,15 +1579,15 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     c->nb = (n + TB - 1) / TB;
     c->np = c->nb * TB + TB;
     c->chunk = (n + c->world - 1) / c->world;
-    // SVGD_SIM_WORLD=P (measurement only, one rank): run rank 0's share of a
+    // svgd_create_sim (measurement only, one rank): run rank 0's share of a
     // P-rank step -- its rows of phi and the optimizer, 1/P of the median's
-    // pair tiles with the order statistics' ranks scaled to that share -- on
-    // one GPU without collectives, to time the per-rank kernels of a P-GPU
-    // run.  The results are NOT the step's (no data from the other ranks).
-    const int plan_world = c->world == 1 && std::getenv("SVGD_SIM_WORLD")
-                               ? std::max(1, std::atoi(std::getenv("SVGD_SIM_WORLD")))
-                               : c->world;
+    // pair tiles with the order statistics' ranks scaled to that share, the
+    // host gradient on the threads a rank of P gets -- on one GPU without
+    // collectives, to time the per-rank work of a P-GPU run.  The results are
+    // NOT the step's (no data from the other ranks): result calls refuse it.
+    const int plan_world = c->world == 1 && sim_world > 1 ? sim_world : c->world;
     c->sim_world = plan_world != c->world ? plan_world : 1;
+    c->plan_world = plan_world;
     svgd_plan_rows(n, plan_world, c->rank, &c->row0, &c->row1);
     c->nrows = c->row1 - c->row0;
     c->pblock = SVGD_PAIR_BLOCK_DT(dim, dtype);
@@ -1631,14 +1754,18 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device)
     // half the OpenMP threads, but no more than this rank's share of the
     // cgroup CPU quota (ranks of one node share it; OpenMP sees the affinity
     // mask, not the quota) and at most 32 (the gradient of a 65536-row share
-    // takes 0.4 ms on 8 threads, hidden behind the device median)
+    // takes 0.4 ms on 8 threads, hidden behind the device median).  A
+    // measurement context (svgd_create_sim) takes the share of a rank of its
+    // simulated world, as that rank would.
     {
         int t = std::max(1, omp_get_max_threads() / 2);
         const int q = cgroup_cpus();
-        if (q > 0) t = std::min(t, std::max(1, q / std::max(1, c->world)));
+        c->cpu_quota = q;
+        if (q > 0) t = std::min(t, std::max(1, q / std::max(1, c->plan_world)));
         c->host_threads = std::min(t, 32);
     }
     if (const char *e = std::getenv("SVGD_HOST_THREADS")) c->host_threads = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("SVGD_DEBUG_COLL")) c->dbg_coll = std::atoi(e) != 0;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SVGD_OK;
 }
@@ -1662,6 +1789,15 @@ int svgd_create(svgd_ctx **out, int dim, int64_t n, int dtype, int device)
     svgd_ctx *c = new svgd_ctx();
     *out = c;
     return init_ctx(c, dim, n, dtype, device);
+}
+
+int svgd_create_sim(svgd_ctx **out, int dim, int64_t n, int dtype, int device, int sim_world)
+{
+    if (!out) return SVGD_ERR_ARG;
+    svgd_ctx *c = new svgd_ctx();
+    *out = c;
+    if (sim_world < 1) return fail(c, SVGD_ERR_ARG, "[Argument Error] Invalid simulated world size.");
+    return init_ctx(c, dim, n, dtype, device, sim_world);
 }
 
 int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, int world,
@@ -1693,16 +1829,29 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
         ncclUniqueId id;
         std::memcpy(&id, unique_id128, sizeof(id));
         NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
-        // the G all-gather's communicator and stream (upload_g_finish); if
-        // the split is refused the G all-gather stays on the compute stream
-        // (SVGD_G_COMM=0 forces that: collective, so set it on every rank)
-        bool want_g = true;
+        // the G all-gather's own communicator and stream (upload_g_finish),
+        // opt-in: SVGD_G_COMM=1 on every rank (the split is collective).
+        // Every rank learns whether every split succeeded (a min all-reduce
+        // over comm): one rank gathering G on gcomm while another gathers it
+        // on comm would hang both, so any failure drops gcomm everywhere and
+        // the G all-gather stays on the compute stream.
+        bool want_g = false;
         if (const char *e = std::getenv("SVGD_G_COMM")) want_g = std::atoi(e) != 0;
-        if (want_g && ncclCommSplit(c->comm, 0, rank, &c->gcomm, nullptr) != ncclSuccess)
-            c->gcomm = nullptr;
-        if (c->gcomm) {
-            HIPCHK(c, hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
-            HIPCHK(c, hipEventCreateWithFlags(&c->ev_gg, hipEventDisableTiming));
+        if (want_g) {
+            int ok = ncclCommSplit(c->comm, 0, rank, &c->gcomm, nullptr) == ncclSuccess && c->gcomm;
+            if (ok && hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking) != hipSuccess) ok = 0;
+            if (ok && hipEventCreateWithFlags(&c->ev_gg, hipEventDisableTiming) != hipSuccess) ok = 0;
+            int *d_ok = nullptr;
+            HIPCHK(c, hipMalloc((void **)&d_ok, sizeof(int)));
+            HIPCHK(c, hipMemcpy(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice));
+            NCCLCHK(c, ncclAllReduce(d_ok, d_ok, 1, ncclInt32, ncclMin, c->comm, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, hipMemcpy(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost));
+            (void)hipFree(d_ok);
+            if (!ok) {
+                if (c->gcomm) (void)ncclCommDestroy(c->gcomm);
+                c->gcomm = nullptr;
+            }
         }
     }
     return SVGD_OK;
@@ -1922,7 +2071,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
 
 int svgd_get_particles(svgd_ctx *c, double *X)
 {
-    CHK(check_ready(c));
+    CHK(check_results(c));
     CHK(resolve_pending(c));
     if (!X) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null output buffer.");
     HIPCHK(c, hipMemcpyAsync(X, c->X, sizeof(double) * (size_t)c->n * c->dim,
@@ -1933,7 +2082,7 @@ int svgd_get_particles(svgd_ctx *c, double *X)
 
 int svgd_get_shard(svgd_ctx *c, double *X_shard)
 {
-    CHK(check_ready(c));
+    CHK(check_results(c));
     CHK(resolve_pending(c));
     if (c->nrows == 0) return SVGD_OK;
     HIPCHK(c, hipMemcpyAsync(X_shard, c->X + (size_t)c->row0 * c->dim,
@@ -1945,7 +2094,7 @@ int svgd_get_shard(svgd_ctx *c, double *X_shard)
 
 int svgd_median_scale(svgd_ctx *c, double *a_out, double *med_out)
 {
-    CHK(check_ready(c));
+    CHK(check_results(c));
     CHK(resolve_pending(c));
     c->spec_step = false;
     const int keep = c->scale_method;
@@ -1953,6 +2102,8 @@ int svgd_median_scale(svgd_ctx *c, double *a_out, double *med_out)
     int rc = scale_begin(c);
     if (rc == SVGD_OK) rc = scale_finish(c);
     c->scale_method = keep;
+    c->trk_sync = 0; // not a step: X_t's median would enter the history twice
+    c->coll_phase = 0;
     CHK(rc);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     CHK(fetch_scale(c));
@@ -1963,7 +2114,7 @@ int svgd_median_scale(svgd_ctx *c, double *a_out, double *med_out)
 
 int svgd_phi(svgd_ctx *c, const double *G_shard, double a, double *phi_out)
 {
-    CHK(check_ready(c));
+    CHK(check_results(c));
     CHK(resolve_pending(c));
     c->spec_step = false;
     if (hipEventQuery(c->ev_scal) != hipSuccess) // the last [a, med] copy has read scal
@@ -2011,6 +2162,8 @@ int svgd_begin_step(svgd_ctx *c, double *X_shard_out)
 int svgd_finish_step(svgd_ctx *c, const double *G_shard)
 {
     CHK(check_ready(c));
+    if (c->coll_phase != 1) // (also keeps the collectives in their order, svgd_ctx)
+        return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] svgd_finish_step without svgd_begin_step.");
     CHK(upload_g_begin(c, G_shard));
     // the G all-gather is queued before the host waits for the median counts
     // (scale_finish), so the device runs it during that round trip
@@ -2275,7 +2428,9 @@ int svgd_get_diagnostics(svgd_ctx *c, double *out, int cap)
                                      (double)ranks,
                                      (double)c->host_threads,
                                      (double)c->trk_steps,
-                                     (double)c->trk_miss};
+                                     (double)c->trk_miss,
+                                     (double)c->sim_world,
+                                     (double)c->cpu_quota};
     for (int i = 0; i < cap && i < SVGD_DIAG_LEN; ++i) out[i] = v[i];
     for (int k = 0; k < 4; ++k) c->dg_ms[k] = 0, c->dg_cnt[k] = 0;
     c->h_grad_ms = c->h_xwait_ms = c->h_job_ms = c->h_wait_ms = 0;
@@ -2313,6 +2468,28 @@ int svgd_get_timing(svgd_ctx *c, double *phi_ms, double *median_ms, int64_t *cou
     if (count) *count = c->tcount;
     c->phi_ms = c->med_ms = 0;
     c->tcount = 0;
+    return SVGD_OK;
+}
+
+int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
+{
+    if (!c || !buf || cap <= 0) return SVGD_ERR_ARG;
+    char s[96];
+    const int d = c->dim;
+    if (c->rowpath) {
+        if (c->phi_kind == 2)
+            std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 8, 8192, 8>", d, c->R);
+        else if (c->phi_kind == 1)
+            std::snprintf(s, sizeof s, "k_phi_rows_s<%d, %d>", d, c->R);
+        else
+            std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 4, 4096, 1>", d, c->R);
+    } else if (c->dtype == SVGD_F32 && c->XS) {
+        std::snprintf(s, sizeof s, "k_phi_f32s<%d, %d>", c->KP, c->NCB);
+    } else {
+        std::snprintf(s, sizeof s, "k_phi<%s, %d, %d>", c->dtype == SVGD_F32 ? "float" : "double", c->KP,
+                      c->NCB);
+    }
+    std::snprintf(buf, (size_t)cap, "%s", s);
     return SVGD_OK;
 }
 

@@ -43,7 +43,9 @@ def _run_ranks(world, n, d, steps, env=None, trk=None):
 @pytest.mark.parametrize("world,n", [(2, 3001), (3, 6007), (8, 20011)])
 def test_sharded_step_matches_single_rank(world, n):
     d, steps = 5, 4
-    multi = _run_ranks(world, n, d, steps)
+    # SVGD_DEBUG_COLL: every step all-gathers each rank's hash of its
+    # collective sequence and fails on a mismatch (svgd_ctx issue order)
+    multi = _run_ranks(world, n, d, steps, {"SVGD_DEBUG_COLL": "1"})
     single = _run_ranks(1, n, d, steps)[0]
     X1, s1, _ = single
     shards = sorted(v[2] for v in multi.values())
@@ -75,3 +77,44 @@ def test_sharded_tracked_brackets_bit_identical(world, n):
         Xb, sb, _ = sampled[rank]
         assert np.array_equal(Xa, Xb), rank
         assert sa == sb, rank
+
+
+def test_measurement_context_refuses_results():
+    """svgd_create_sim (bench.py --sim-world): rank 0's share of a P-rank step,
+    measurement only -- it steps, but every call that hands results back
+    raises, and the diagnostics name the simulated world and the quota share."""
+    import svgdcpp_amd as S
+    from svgdcpp_amd import _capi as C
+
+    n, d = 4096, 4
+    X0 = np.random.default_rng(3).standard_normal((n, d))
+    ctx = S.Context(d, n, sim_world=4)
+    ctx.set_particles(X0)
+    ctx.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+    assert (ctx.row0, ctx.row1) == (0, n // 4)
+    model = S.GaussianSum([np.zeros(d)], [np.eye(d)])
+    ctx.step_with_model(model)
+    ctx.sync()
+    for call in (ctx.get_particles, ctx.median_scale, lambda: ctx.phi(np.zeros((n // 4, d)), 1.0)):
+        with pytest.raises(Exception, match="measurement context"):
+            call()
+    dg = ctx.diagnostics()
+    assert dg["sim_world"] == 4
+    if dg["cpu_quota"] > 0:
+        assert dg["host_threads"] <= max(1, dg["cpu_quota"] // 4)
+    ctx.close()
+
+
+def test_finish_step_needs_begin_step():
+    """svgd_finish_step without svgd_begin_step fails before any collective."""
+    import svgdcpp_amd as S
+    from svgdcpp_amd import _capi as C
+
+    n, d = 512, 3
+    ctx = S.Context(d, n)
+    ctx.set_particles(np.random.default_rng(4).standard_normal((n, d)))
+    ctx.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
+    G = np.zeros((n, d))
+    with pytest.raises(Exception, match="without svgd_begin_step"):
+        ctx.check(ctx.lib.svgd_finish_step(ctx.h, C.dptr(G)))
+    ctx.close()

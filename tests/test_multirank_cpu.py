@@ -1,13 +1,18 @@
-"""World-size-2 (and 3) gloo rehearsal of the sharded SVGD step on CPU.
+"""World-size 2/3/4 gloo rehearsal of the sharded SVGD step on CPU.
 
-The library's multi-GPU step shards rows with svgd_plan_rows,
-splits median pair tiles with svgd_plan_pair_tiles, brackets the median from
-a sharded sample (two histogram all-reduces), all-reduces the counts + bucket
-histogram once, all-gathers the selected buckets' keys once (or, after a
-bracket miss, runs the per-digit radix fallback) and all-gathers X and G.
-tests/_multirank_worker.py runs that protocol with gloo in place of RCCL and
-numpy/the oracle as the arithmetic; the result must equal the single-process
-oracle step.
+The library's multi-GPU step (svgd_capi.cpp) shards rows with
+svgd_plan_rows and median pair tiles with svgd_plan_pair_tiles; per step it
+takes the median bracket tracked from the last medians (speculative steps) or
+from a sample EVERY rank draws whole (no histogram all-reduces), all-reduces
+the counts + bucket histogram once, all-gathers the selected buckets' keys
+once, all-gathers G (on a second communicator when SVGD_G_COMM=1, issued
+after every comm call of the median's first phase) and X.
+tests/_multirank_worker.py runs that protocol for several steps with gloo in
+place of RCCL (a second gloo group for the G communicator) and numpy / the
+oracle as the arithmetic; every step must equal the single-process oracle
+step, and every rank must issue the same collective sequence, the one the
+library issues.  Round 2's sharded-sample protocol (SVGD_SAMPLE_SHARD=1) and
+the radix fallback after a (forced) bracket miss are kept as scenarios.
 """
 import multiprocessing as mp
 import socket
@@ -24,23 +29,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,n,d,block,sample,sigma,shift,path", [
-    (2, 301, 3, 64, 4096, 3.0, 0.0, "bracket"),
-    (2, 64, 2, 64, 512, 3.0, 0.0, "bracket"),
-    (3, 700, 5, 256, 4096, 3.0, 0.0, "bracket"),
-    (4, 900, 8, 256, 8192, 3.0, 0.0, "bracket"),
-    (3, 700, 5, 256, 4096, 3.0, 20.0, "fallback"),
-])
-def test_sharded_step_matches_single_process(oracle, world, n, d, block, sample, sigma, shift, path):
+def _run(world, n, d, block, steps, protocol="shipped", gcomm=True, shift=0.0, lr=0.1, bound=2.0):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=W.run, args=(r, world, port, n, d, block, q, sample, sigma, shift))
+    procs = [ctx.Process(target=W.run, args=(r, world, port, n, d, block, q, 3.0, shift, steps, protocol, gcomm,
+                                             lr, bound))
              for r in range(world)]
     for p in procs:
         p.start()
     try:
-        status, res = q.get(timeout=240)
+        status, res = q.get(timeout=300)
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -49,23 +48,82 @@ def test_sharded_step_matches_single_process(oracle, world, n, d, block, sample,
     assert status == "ok", res
     for p in procs:
         assert p.exitcode == 0
+    return res
 
-    X, mus, covs = res["X"], res["mus"], res["covs"]
-    # every unordered pair was keyed by exactly one rank
-    assert res["total"] == n * (n - 1) // 2
-    # G all-gather reassembles the full matrix bit-for-bit
-    np.testing.assert_array_equal(res["G_all"], oracle.logp_grad_gmm(X, mus, covs))
-    assert res["path"] == path
-    # bracket path: 2 sample-histogram all-reduces + 1 counts all-reduce + 1 key all-gather
-    if path == "bracket":
-        assert res["collectives"] == 4
-    # distributed exact median == single-process median (difference form vs Gram form)
-    a_ref, med_ref = oracle.median_scale(X)
-    assert res["med"] == pytest.approx(med_ref, rel=1e-13)
-    # the sharded step == the single-process step (same a, same rows)
-    G = oracle.logp_grad_gmm(X, mus, covs)
-    ph = oracle.phi(X, G, res["a"])
-    opt = oracle.Adam((n, d), 0.1, 0.9, 0.999)
-    X_ref = X.copy()
-    oracle.apply_update(X_ref, opt.step(ph), -np.full(d, 2.0), np.full(d, 2.0))
-    np.testing.assert_array_equal(res["X_new"], X_ref)
+
+def _check_steps(oracle, res, n, d):
+    """Every step == the single-process oracle step from the same X_t."""
+    mus, covs, b = res["mus"], res["covs"], res["bound"]
+    opt = oracle.Adam((n, d), res["lr"], 0.9, 0.999)
+    for st in res["steps"]:
+        X = st["X"]
+        assert st["total"] == n * (n - 1) // 2  # every unordered pair keyed by exactly one rank
+        G = oracle.logp_grad_gmm(X, mus, covs)
+        np.testing.assert_array_equal(st["G_all"], G)  # the G all-gather reassembles G bit for bit
+        _, med_ref = oracle.median_scale(X)
+        assert st["med"] == pytest.approx(med_ref, rel=1e-13)  # difference form vs Gram form
+        X_ref = X.copy()
+        oracle.apply_update(X_ref, opt.step(oracle.phi(X, G, st["a"])), -np.full(d, b), np.full(d, b))
+        np.testing.assert_array_equal(st["X_new"], X_ref)
+
+
+def _expected(st, g):
+    """The library's collective sequence for one step (svgd_ctx issue order)."""
+    head = [("comm", "allreduce")] * (2 if st["bracket"] == "sampled" and st.get("shard") else 0)
+    if st["redo"]:
+        failed = [("comm", "allreduce"), ("comm", "keys"), (g, "G"), ("comm", "X"), ("comm", "X_restore")]
+        return failed + head + [("comm", "allreduce"), ("comm", "keys"), ("comm", "X")]
+    if st["path"] == "fallback":
+        return head + [("comm", "allreduce"), (g, "G")] + [("comm", "allreduce")] * 6 + [("comm", "X")]
+    if st["spec"]:
+        return head + [("comm", "allreduce"), ("comm", "keys"), (g, "G"), ("comm", "X")]
+    return head + [("comm", "allreduce"), (g, "G"), ("comm", "keys"), ("comm", "X")]
+
+
+# The tracked bracket is taken only when its band holds fewer pairs than the
+# sampled one's; at these N a rank's sample is a large share of the pairs
+# (2^18 of ~4e5), so it wins only on a slowly moving median: the tracked
+# scenarios take lr 0.01 and bounds the particles never reach (the ±2 clamp
+# of X0 = 3 U[-1,1] moves the median ~30 % on step 1 and ~4 % per step after).
+@pytest.mark.parametrize("world,n,d,block,steps,gcomm,lr,bound,tracked", [
+    (2, 900, 3, 64, 7, True, 0.01, 10.0, True),
+    (3, 700, 5, 256, 4, True, 0.1, 2.0, False),
+    (4, 1000, 8, 256, 7, True, 0.01, 10.0, True),
+    (2, 800, 2, 64, 4, False, 0.1, 2.0, False),
+])
+def test_shipped_protocol_matches_single_process(oracle, world, n, d, block, steps, gcomm, lr, bound, tracked):
+    res = _run(world, n, d, block, steps, "shipped", gcomm, lr=lr, bound=bound)
+    _check_steps(oracle, res, n, d)
+    g = "gcomm" if gcomm else "comm"
+    for st in res["steps"]:
+        assert st["path"] == "bracket"
+        assert st["colls"] == _expected(st, g), st["colls"]
+    kinds = [st["bracket"] for st in res["steps"]]
+    # step 1 synchronous + sampled (no history), step 2 speculative + sampled
+    # (one median recorded), then the tracked bracket whenever the medians'
+    # drift allows it -- no sample and no histogram collective on those steps
+    assert [st["spec"] for st in res["steps"][:2]] == [False, True]
+    assert kinds[:2] == ["sampled", "sampled"]
+    if tracked:
+        assert "tracked" in kinds, kinds
+
+
+def test_sharded_sample_protocol(oracle):
+    """SVGD_SAMPLE_SHARD=1 (round 2's protocol): disjoint sample shards and one
+    histogram all-reduce per radix pass."""
+    res = _run(2, 301, 3, 64, 1, "shard", True)
+    _check_steps(oracle, res, 301, 3)
+    st = res["steps"][0]
+    st["shard"] = True
+    assert st["path"] == "bracket"
+    assert st["colls"] == _expected(st, "gcomm"), st["colls"]
+
+
+def test_bracket_miss_fallback(oracle):
+    """A (forced) bracket miss on a sampled step: the streamed radix select,
+    one all-reduce per 11-bit digit, still the exact median."""
+    res = _run(3, 700, 5, 256, 1, "shipped", True, shift=20.0)
+    _check_steps(oracle, res, 700, 5)
+    st = res["steps"][0]
+    assert st["path"] == "fallback"
+    assert st["colls"] == _expected(st, "gcomm"), st["colls"]

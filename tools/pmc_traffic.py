@@ -44,7 +44,10 @@ def main():
         sys.exit(f"kernel '{kname}' matched {match}")
     k = match[0]
     rd, wr = 2 * fetch[k] * 1024, write[k] * 1024
-    rec = {"kernel": k, "n": n, "d": d, "world": world,
+    sys.path.insert(0, ROOT)
+    from bench import _kernel_src_sha
+
+    rec = {"kernel": k, "n": n, "d": d, "world": world, "src_sha16": _kernel_src_sha(),
            "fetch_size_kib": fetch[k], "write_size_kib": write[k],
            "read_bytes": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
            "correction": "FETCH_SIZE x2 (gfx950 16B/lane reads), WRITE_SIZE as is",
