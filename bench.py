@@ -500,9 +500,13 @@ def main():
         "tracked_brackets": {"steps": int(host_timed["steps"]), "predicted": int(host_timed["trk_steps"]),
                              "missed": int(host_timed["trk_miss"])},
     }
+    # phi launches per step: 2 when the context runs phi in row halves
+    # (P > 1 with few gradient threads per rank)
+    parts = max(1, round(diag["phi_kernel_n"] / args.steps)) if diag is not None and diag["phi_kernel_n"] else 1
     if diag is not None:
         mine["diag_ms_per_step"] = {
-            "phi_kernel": per_step(diag["phi_kernel_ms"], diag["phi_kernel_n"]),
+            "phi_kernel": per_step(diag["phi_kernel_ms"], diag["phi_kernel_n"] / parts),
+            "phi_launches_per_step": parts,
             "phi_wait_for_g": per_step(diag["phi_wait_ms"], diag["phi_wait_n"]),
             "collectives": per_step(diag["coll_ms"], args.steps),
             "g_allgather": per_step(diag["gather_g_ms"], args.steps),
@@ -515,8 +519,9 @@ def main():
         dist.all_gather_object(per_rank, mine)
 
     if rank == 0:
-        phi_kernel_ms = mine.get("diag_ms_per_step", {}).get("phi_kernel")
-        flops_launch = float(rows) * n * (5 * d + 4)
+        phi_step_ms = (mine.get("diag_ms_per_step") or {}).get("phi_kernel")
+        phi_kernel_ms = phi_step_ms / parts if phi_step_ms else None  # one launch
+        flops_launch = float(rows) * n * (5 * d + 4) / parts
         achieved = flops_launch / (phi_kernel_ms / 1e3) / 1e12 if phi_kernel_ms else None
         peak = FP32_PEAK_TFLOPS if dtype == "f32" else FP64_PEAK_TFLOPS
         # committed PMC passes (not this run) count only for the same kernel

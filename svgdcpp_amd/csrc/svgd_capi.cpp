@@ -186,6 +186,14 @@ struct svgd_ctx {
     float *xf = nullptr;    // np x med_f32_stride(d) fp32 median records
     unsigned long long *nmax = nullptr; // max |xc|^2 (double bits)
     int S = 1;
+    // phi in two row halves (svgd_step_host_model when split_rows): rows
+    // [0, split_h) then [split_h, nrows) of this rank, S2 column splits each
+    bool split_rows = false;      // policy (init_ctx)
+    bool in_host_step = false;    // run_phi_opt called by svgd_step_host_model
+    bool xhalf_ready = false;     // the last step's ev_xhalf marks its first half's X_{t+1}
+    int64_t split_h = 0, ldp2 = 0;
+    int S2 = 0;
+    hipEvent_t ev_xhalf = nullptr;
     int R = 2; // rows per lane of k_phi_rows
     int phi_kind = 0; // 0 k_phi_rows (4 waves), 1 k_phi_rows_s (scalar columns), 2 k_phi_rows (8 waves, column-split)
     // symmetric phi pass (k_phi_sym, one rank, d <= 8): geometry and buffers
@@ -224,6 +232,8 @@ struct svgd_ctx {
     uint32_t *bpart = nullptr;         // collect blocks' key-range bucket histograms (max blocks x NBK)
     uint64_t *gseg = nullptr;          // world x (CAPG + 1): compacted selected-bucket keys
     int64_t bucket_cap = CAPG;         // bucket select path if the selected buckets hold <= this
+    int64_t last_tot = 0;              // the last selection's selected-bucket keys (all ranks)
+    int64_t spec_cap = CAPR_MIN;       // this speculative step's segment capacity (plan_step)
     uint32_t *counts = nullptr;
     unsigned long long *below = nullptr;
     int collect_grid = 0;
@@ -945,7 +955,7 @@ int collect_counts(svgd_ctx *c)
         HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
                                    c->collect_grid, c->cnt3, c->stream,
-                                   c->spec_step ? c->gseg + (size_t)c->rank * (CAPR + 1) : nullptr));
+                                   c->spec_step ? c->gseg + (size_t)c->rank * (c->spec_cap + 1) : nullptr));
     CHK(allreduce_cnt3(c));
     // speculative: the device plan and the selection are queued right behind
     // the counts (while the device still runs the collect pass), not when the
@@ -961,18 +971,19 @@ int collect_counts(svgd_ctx *c)
 // plan's status goes to the host on the copy stream (resolve_pending).
 int median_finish_spec(svgd_ctx *c, double logn)
 {
-    uint64_t *seg = c->gseg + (size_t)c->rank * (CAPR + 1);
+    const int64_t cap = c->spec_cap;
+    uint64_t *seg = c->gseg + (size_t)c->rank * (cap + 1);
     // the plan also stores its status straight into pinned host memory: no
     // copy on the copy stream (a small copy there turned the X shard copies
     // into blit kernels competing with the median kernels)
     // (the compaction's blocks derive the bucket plan themselves: no plan launch)
     const PlanArgs pa{c->cnt3, c->nsel, (uint64_t)c->sel_rank[0], (uint64_t)c->sel_rank[c->nsel - 1],
-                      std::min<int64_t>(c->bucket_cap, CAPR), c->d_status, c->h_status_dev,
+                      cap, c->d_status, c->h_status_dev,
                       c->sim_world > 1 ? 1 : 0, c->h_trk_dev};
-    HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, CAPR,
+    HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, cap,
                                      c->d_status, c->stream, &pa));
-    CHK(allgather_u64(c, c->gseg, (size_t)CAPR + 1));
-    HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, CAPR, c->navg, c->src_lo, c->src_hi, logn,
+    CHK(allgather_u64(c, c->gseg, (size_t)cap + 1));
+    HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, cap, c->navg, c->src_lo, c->src_hi, logn,
                                   c->scal, c->d_status, c->stream, c->h_trk_dev));
     c->trk_keys = true;
     // the plan's status is final once this completes (recorded after the
@@ -1076,7 +1087,8 @@ int median_finish(svgd_ctx *c)
             c->last_path = path;
             // the next step may take the device plan if this one would have
             c->last_fast = (path == SVGD_MEDIAN_BRACKET || path == SVGD_MEDIAN_DIRECT) &&
-                           tot <= std::min<int64_t>(c->bucket_cap, CAPR);
+                           tot <= std::min<int64_t>(c->bucket_cap, CAPG);
+            c->last_tot = tot;
             return SVGD_OK;
         }
     }
@@ -1283,6 +1295,8 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     // level 2: the phi kernel alone (k_phi_rows before its reduce, k_phi_sym,
     // or the tile kernel)
     const bool sym = c->sym && !mat;
+    const bool split = c->split_rows && c->in_host_step && c->rowpath && !mat && !sym && opt;
+    c->xhalf_ready = split;
     hipEvent_t k0 = sym ? (c->tlevel >= 2 ? take_ev(c) : nullptr) : diag_begin(c, c->stream);
     hipEvent_t k1 = k0 ? take_ev(c) : nullptr;
     if (sym) {
@@ -1297,6 +1311,26 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, opt,
                                   c->stream, nullptr, c->phi_kind, c->symok));
+    } else if (c->rowpath && split) {
+        // two row halves: the first half's X_{t+1} is final at ev_xhalf, while
+        // the second half's phi runs (svgd_step_host_model copies it down and
+        // starts its gradient there)
+        const int64_t h = c->split_h, d = c->dim;
+        OptArgs o2 = *opt;
+        o2.X += h * d;
+        o2.m += h * d;
+        o2.v += h * d;
+        if (o2.bak) o2.bak += h * d;
+        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, h, c->n, c->S2, c->part, c->ldp2,
+                                  1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, opt, c->stream, k1,
+                                  c->phi_kind));
+        HIPCHK(c, hipEventRecord(c->ev_xhalf, c->stream));
+        hipEvent_t k2 = diag_begin(c, c->stream);
+        hipEvent_t k3 = k2 ? take_ev(c) : nullptr;
+        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0 + h, c->nrows - h, c->n, c->S2,
+                                  c->part, c->ldp2, 1.0 / (double)c->n, nullptr, nullptr, c->nmax,
+                                  c->phi + h * d, &o2, c->stream, k3, c->phi_kind));
+        if (k2) c->ev_diag.push_back({k2, k3, DG_PHI_KERNEL, true});
     } else if (c->rowpath)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
@@ -1525,6 +1559,7 @@ int resolve_pending(svgd_ctx *c)
     c->pending = false;
     HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
     if (*c->h_status == 0) {
+        c->last_tot = (int64_t)c->h_trk[7];
         if (c->trk_allowed) trk_record(c, c->h_trk[0], c->h_trk[1], c->h_trk[3]);
         return SVGD_OK;
     }
@@ -1554,8 +1589,14 @@ int resolve_pending(svgd_ctx *c)
 // Speculate this step's median when the last one would have allowed it.
 int plan_step(svgd_ctx *c)
 {
+    // the segment capacity: twice the last selection's keys, a power of two
+    // in [CAPR_MIN, CAPG] (a step whose buckets outgrow it fails its plan
+    // and is redone synchronously)
+    int64_t cap = CAPR_MIN;
+    while (cap < 2 * c->last_tot && cap < CAPG) cap <<= 1;
+    c->spec_cap = std::min<int64_t>(cap, CAPG);
     c->spec_step = c->spec_allowed && c->last_fast && c->scale_method == SVGD_SCALE_MEDIAN &&
-                   c->bucket_cap >= CAPR;
+                   c->bucket_cap >= c->spec_cap;
     if (c->spec_step && !c->bak) CHK(dalloc(c, &c->bak, 3 * std::max<int64_t>(1, c->nrows) * c->dim));
     return SVGD_OK;
 }
@@ -1658,10 +1699,20 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         c->S = (int)S;
         c->RS = phi_rec_stride(dim);
         c->ldp = std::max<int64_t>(1, c->nrows);
+        // row halves (svgd_step_host_model at P > 1, split_rows policy below):
+        // the first half's rows get their X_{t+1} while the second half's phi
+        // still runs; each half's launch takes twice the column splits
+        c->split_h = (c->nrows / 2) / rows_wg * rows_wg;
+        if (c->split_h > 0) {
+            const int64_t ib2 = std::max<int64_t>(1, (c->nrows - c->split_h + rows_wg - 1) / rows_wg);
+            int64_t S2 = std::max<int64_t>(1, (resident + ib2 - 1) / ib2) * split_mult;
+            c->S2 = (int)std::min<int64_t>(S2, std::max<int64_t>(1, n / 256));
+            c->ldp2 = c->nrows - c->split_h;
+        }
         CHK(dalloc(c, &c->rec, c->np * c->RS));
         CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
         CHK(dalloc(c, &c->nmax, 1));
-        CHK(dalloc(c, &c->part, (int64_t)c->S * c->ldp * (dim + 1)));
+        CHK(dalloc(c, &c->part, std::max<int64_t>((int64_t)c->S * c->ldp, (int64_t)c->S2 * c->ldp2) * (dim + 1)));
         // symmetric phi pass: one rank (a pair feeds two particles, which
         // ranks would have to exchange), isotropic scales, d <= 8
         bool want_sym = c->world == 1 && phi_sym_supported(dim);
@@ -1766,6 +1817,16 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     }
     if (const char *e = std::getenv("SVGD_HOST_THREADS")) c->host_threads = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SVGD_DEBUG_COLL")) c->dbg_coll = std::atoi(e) != 0;
+    // phi in row halves when a rank of several has more than 2048 rows per
+    // gradient thread: then the host gradient (~18 us per 1000 rows and
+    // thread at cfg3's GMM) outlasts the device's median phase of a P-GPU
+    // step and phi waited for G (8-rank share at 2 threads: 0.14 ms); with
+    // halves the first half's gradient runs beside the second half's phi
+    // (cost: one launch pair and one event more per step)
+    c->split_rows = c->rowpath && c->split_h > 0 && c->plan_world >= 2 &&
+                    c->nrows > 2048 * (int64_t)std::max(1, c->host_threads);
+    if (const char *e = std::getenv("SVGD_PHI_SPLIT")) c->split_rows = c->rowpath && c->split_h > 0 && std::atoi(e) != 0;
+    HIPCHK(c, hipEventCreateWithFlags(&c->ev_xhalf, hipEventDisableTiming));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return SVGD_OK;
 }
@@ -1902,6 +1963,7 @@ int svgd_destroy(svgd_ctx *c)
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->gstream) (void)hipStreamDestroy(c->gstream);
     if (c->ev_gg) (void)hipEventDestroy(c->ev_gg);
+    if (c->ev_xhalf) (void)hipEventDestroy(c->ev_xhalf);
     for (auto &e : c->ev_diag) {
         if (e.own_a) (void)hipEventDestroy(e.a);
         (void)hipEventDestroy(e.b);
@@ -2065,6 +2127,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     c->ev_xready_use = c->ev_xready;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_particles = true;
+    c->xhalf_ready = false;
     c->trk_n = c->trk_nerr = 0; // new particles: the median history restarts
     return SVGD_OK;
 }
@@ -2192,18 +2255,33 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     // row chunks of >= 1 MiB (a chunk's copy, event and OpenMP region cost
     // ~10 us: smaller chunks lose more than they overlap), at most XCH
     const int64_t min_rows = std::max<int64_t>(1, (int64_t(1) << 20) / (8 * d));
-    const int nch = (int)std::max<int64_t>(1, std::min<int64_t>(XCH, rows / min_rows));
-    auto chunk = [&](int q, int64_t *r0, int64_t *r1) {
+    // the last step ran phi in row halves: the first half's chunks wait for
+    // its X_{t+1} only (ev_xhalf), so their gradient starts while the second
+    // half's phi still runs; chunks never straddle the halves
+    const int64_t hsplit = c->xhalf_ready ? c->split_h : 0;
+    const int nh = hsplit > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(XCH / 2, hsplit / min_rows)) : 0;
+    const int nch = hsplit > 0 ? 2 * nh
+                               : (int)std::max<int64_t>(1, std::min<int64_t>(XCH, rows / min_rows));
+    auto chunk = [hsplit, nh, nch, rows](int q, int64_t *r0, int64_t *r1) {
+        if (hsplit > 0) {
+            const int64_t b = q < nh ? 0 : hsplit, len = q < nh ? hsplit : rows - hsplit;
+            const int qq = q < nh ? q : q - nh;
+            *r0 = b + len * qq / nh;
+            *r1 = b + len * (qq + 1) / nh;
+            return;
+        }
         *r0 = rows * q / nch;
         *r1 = rows * (q + 1) / nch;
     };
     HIPCHK(c, hipEventSynchronize(c->ev_g)); // the previous step's upload has left h_g
     if (rows > 0) {
         // X_t is final once the previous step's update (and all-gather) ran
-        HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_xready_use ? c->ev_xready_use : c->ev_xready, 0));
+        hipEvent_t xev = c->ev_xready_use ? c->ev_xready_use : c->ev_xready;
+        HIPCHK(c, hipStreamWaitEvent(c->cstream, hsplit > 0 ? c->ev_xhalf : xev, 0));
         for (int q = 0; q < nch; ++q) {
             int64_t r0, r1;
             chunk(q, &r0, &r1);
+            if (hsplit > 0 && q == nh) HIPCHK(c, hipStreamWaitEvent(c->cstream, xev, 0));
             HIPCHK(c, hipMemcpyAsync(c->h_x + r0 * d, c->X + (size_t)(c->row0 + r0) * d,
                                      sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyDeviceToHost,
                                      c->cstream));
@@ -2271,8 +2349,10 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     }
     CHK(upload_g_finish(c));
     CHK(scale_finish(c));
-    CHK(run_phi_opt(c));
-    return SVGD_OK;
+    c->in_host_step = true;
+    rc = run_phi_opt(c);
+    c->in_host_step = false;
+    return rc;
 }
 
 int svgd_step(svgd_ctx *c, const double *G_shard)

@@ -31,8 +31,13 @@ struct SelState {
 // contiguous key ranges.  The collect pass histograms them, so one all-reduce
 // (counts + buckets) tells every rank which bucket holds each order statistic.
 constexpr int NBK = 2048;
-// per-rank capacity of the compacted selected-bucket keys (gathered over ranks)
-constexpr int CAPG = 16384;
+// per-rank capacity of the compacted selected-bucket keys (gathered over
+// ranks).  At cfg4 (N = 262144, 3.4e10 pairs) a sampled bracket's bucket
+// holds ~25k keys on one rank (2^22-pair sample) and ~100k at P > 1 (2^20):
+// 16384 sent every cfg4 step down the radix path, so it never speculated
+// and never tracked its bracket.  The synchronous path's all-gather moves
+// the step's own total, the speculative one the adaptive spec cap.
+constexpr int CAPG = 262144;
 
 // xc = X - mean (stride KP, zero padded), nrm = |xc|^2; nrm_in_slot also
 // stores |xc|^2 at xc[j*KP + d] (the row-stream median record).
@@ -163,11 +168,13 @@ hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int
 hipError_t launch_plan_select(const unsigned long long *cnt, SelState *st, int nsel, uint64_t r0,
                               uint64_t r1, int64_t capr, uint64_t *seg, int *status,
                               int *host_status, hipStream_t stream);
-// per-rank segment capacity of the speculative bucket select.  At cfg3 a
-// bucket holds ~3k keys: 4096 made ~1 in 5 early steps fail the plan (each
-// failure redoes the step); the selection reads only the keys present, and
-// the all-gather (P > 1) moves 128 KiB per rank
-constexpr int CAPR = 16384;
+// per-rank segment capacity of the speculative bucket select: adaptive
+// (svgd_capi.cpp plan_step: twice the last step's selected-bucket total,
+// rounded up to a power of two, within [CAPR_MIN, CAPG]); the all-gather
+// (P > 1) moves cap + 1 keys per rank.  At cfg3 a bucket holds ~3k keys:
+// a fixed 4096 made ~1 in 5 early steps fail the plan (each failure redoes
+// the step); the selection reads only the keys present.
+constexpr int CAPR_MIN = 4096;
 
 // Row-stream path (d <= 16): particle records rec_j = [xc_j | G_j - 2a xc_j | c_j | 0..],
 // stride phi_rec_stride(d).  phi partials over S column splits -> part[S][ldp][d+1].

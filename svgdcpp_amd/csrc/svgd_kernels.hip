@@ -1032,7 +1032,7 @@ __global__ __launch_bounds__(1024) void k_select_tail(SelState *st, const uint64
 // 3 (selected buckets above capr).  Block-uniform results.
 struct PlanOut {
     int status, b0, b1, ns;
-    unsigned long long in0, in1;
+    unsigned long long in0, in1, tot;
 };
 __device__ PlanOut plan_block(const unsigned long long *__restrict__ cnt, int nsel, uint64_t r0,
                               uint64_t r1, int64_t capr, int sim = 0)
@@ -1041,7 +1041,7 @@ __device__ PlanOut plan_block(const unsigned long long *__restrict__ cnt, int ns
     __shared__ int sB[2];
     __shared__ unsigned long long sIn[2];
     const int tid = threadIdx.x;
-    PlanOut o{0, -1, -1, 1, 0, 0};
+    PlanOut o{0, -1, -1, 1, 0, 0, 0};
     const unsigned long long below = cnt[0], cand = cnt[1], ovf = cnt[2];
     if (sim) { // measurement mode (PlanArgs::sim)
         const uint64_t dr = r1 - r0;
@@ -1091,6 +1091,7 @@ __device__ PlanOut plan_block(const unsigned long long *__restrict__ cnt, int ns
     o.in0 = sIn[0];
     o.in1 = ns > 1 ? sIn[1] : sIn[0];
     const unsigned long long tot = cnt[3 + o.b0] + (o.b1 != o.b0 ? cnt[3 + o.b1] : 0ull);
+    o.tot = tot;
     if (tot > (unsigned long long)capr) o.status = 3;
     return o;
 }
@@ -1169,6 +1170,7 @@ __global__ __launch_bounds__(256) void k_compact_buckets(const uint64_t *__restr
                 pa.trk[1] = st->hi_key;
                 pa.trk[2] = pa.cnt[0];
                 pa.trk[3] = pa.cnt[1];
+                pa.trk[7] = o.tot; // the selected buckets' keys (the next step's segment size)
             }
             plan_publish(o, st, pa.nsel, pa.status, pa.host_status);
         }

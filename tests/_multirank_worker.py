@@ -52,7 +52,16 @@ for p in (ROOT, os.path.join(ROOT, "oracle")):
 
 RADIX = 11
 NBK = 2048  # svgd_kernels.h
-CAPR = 16384  # svgd_kernels.h: speculative steps' selected-bucket cap
+CAPG = 262144  # svgd_kernels.h: the selected buckets' key cap of the bucket path
+CAPR_MIN = 4096  # svgd_kernels.h: the speculative cap's floor (plan_step: adaptive)
+
+
+def spec_cap(last_tot):
+    """svgd_capi.cpp plan_step: twice the last total, a power of two in [CAPR_MIN, CAPG]."""
+    cap = CAPR_MIN
+    while cap < 2 * last_tot and cap < CAPG:
+        cap <<= 1
+    return min(cap, CAPG)
 M64 = (1 << 64) - 1
 # svgd_capi.cpp tracked-bracket constants (trk_min_w, trk_err_mult)
 TRK_MIN_W = 2e-5
@@ -214,7 +223,7 @@ def _bucket_of(keys, lo, binv):
     return np.where(t < NBK - 1, np.where(t > 0, t, 0).astype(np.int64), NBK - 1)
 
 
-def _median(cm, lib, X, keys, protocol, sigma, shift, trk, spec, on_g):
+def _median(cm, lib, X, keys, protocol, sigma, shift, trk, spec, on_g, cap=CAPG):
     """One step's exact median; on_g() issues the G all-gather where
     upload_g_finish would.  Returns (med, path, bracket kind, selected D^2
     of the lower order statistic, fast, bracket record for the tracker)."""
@@ -266,12 +275,12 @@ def _median(cm, lib, X, keys, protocol, sigma, shift, trk, spec, on_g):
         bc = (ctypes.c_ulonglong * NBK)(*[int(x) for x in buckets])
         ns = 2 if r1 != r0 else 1
         assert lib.svgd_plan_bucket_select(bc, NBK, ns, ranks, bsel, rin, ctypes.byref(tot)) == 0
-        if spec and tot.value > CAPR:
+        if spec and tot.value > cap:
             hit = False  # the device plan fails on oversized buckets (redo)
     if spec and not hit:
         # failed device plan: the speculative chain still ran (its keys
         # all-gather, the G all-gather); the caller redoes the step
-        cm.allgather(np.zeros(CAPR + 1, dtype=np.int64), what="keys")
+        cm.allgather(np.zeros(cap + 1, dtype=np.int64), what="keys")
         on_g()
         return None
     if hit:
@@ -286,7 +295,7 @@ def _median(cm, lib, X, keys, protocol, sigma, shift, trk, spec, on_g):
         pool = {s: np.sort(gathered[gb == bsel[s]])[rin[s]] for s in range(ns)}
         vals = {r0: pool[0], r1: pool[ns - 1]}
         path = "bracket"
-        fast = tot.value <= CAPR
+        fast = tot.value <= CAPG
     else:
         # fallback: streamed radix select over every key, all 64 bits
         (k0, k1), _ = _radix_select(cm.allreduce, keys, (r0, r1), 6)
@@ -299,7 +308,7 @@ def _median(cm, lib, X, keys, protocol, sigma, shift, trk, spec, on_g):
            for kr in [lo_r.value, hi_r.value][:navg]]
     m_sel = float(np.uint64(vals[r0]).view(np.float64))
     rec = (lo, hi, cand_all) if path == "bracket" else None
-    return sum(out) / len(out), path, kind, m_sel, fast, rec
+    return sum(out) / len(out), path, kind, m_sel, fast, rec, (tot.value if hit else 0)
 
 
 def run(rank, world, port, n, d, block, q, sigma=3.0, shift=0.0, steps=1, protocol="shipped",
@@ -338,6 +347,7 @@ def run(rank, world, port, n, d, block, q, sigma=3.0, shift=0.0, steps=1, protoc
         lower, upper = -np.full(d, bound), np.full(d, bound)
         trk = Tracker()
         last_fast = False
+        last_tot = 0
         hist = []
         for _ in range(steps):
             Xt = X.copy()
@@ -356,7 +366,7 @@ def run(rank, world, port, n, d, block, q, sigma=3.0, shift=0.0, steps=1, protoc
 
             # 2. the median: speculative when the last selection allowed it
             spec = last_fast
-            res = _median(cm, lib, X, keys, protocol, sigma, shift, trk, spec, on_g)
+            res = _median(cm, lib, X, keys, protocol, sigma, shift, trk, spec, on_g, spec_cap(last_tot))
             redo = res is None
             if redo:
                 # a failed device plan (resolve_pending): the speculative
@@ -367,7 +377,7 @@ def run(rank, world, port, n, d, block, q, sigma=3.0, shift=0.0, steps=1, protoc
                 gather_rows(X[row0:row1], what="X_restore")
                 trk.pred = -1.0
                 res = _median(cm, lib, X, keys, protocol, sigma, shift, trk, False, on_g)
-            med, path, kind, m_sel, fast, rec = res
+            med, path, kind, m_sel, fast, rec, last_tot = res
             if rec is not None:
                 trk.record(m_sel, *rec)
             else:

@@ -66,3 +66,36 @@ def test_pipelined_step_rejects_bad_model():
     with pytest.raises(ValueError):
         c.step_with_model(other)
     c.close()
+
+
+@pytest.mark.parametrize("n,d,k", [(9000, 8, 4), (13001, 5, 2)])
+def test_row_halves_step_matches_oracle(oracle, monkeypatch, n, d, k):
+    """phi in two row halves (SVGD_PHI_SPLIT=1; by default a rank of several
+    with > 2048 rows per gradient thread): the first half's X_{t+1} goes to
+    the host gradient while the second half's phi runs.  Each half sums its
+    own column splits, so the trajectory matches the whole-rows one to fp64
+    rounding, and every step matches the oracle's."""
+    X = oracle.splitmix((n, d), 3.0, 31 + d)
+    mus = oracle.splitmix((k, d), 3.0, 32)
+    covs = np.stack([np.eye(d) * (1.0 + 0.25 * c) for c in range(k)])
+    model = S.GaussianSum(list(mus), list(covs))
+    monkeypatch.setenv("SVGD_PHI_SPLIT", "1")
+    a = _ctx(X)
+    monkeypatch.setenv("SVGD_PHI_SPLIT", "0")
+    b = _ctx(X)
+    opt = oracle.Adam((n, d), 0.1, 0.9, 0.999)
+    Xr = X.copy()
+    for step in range(4):
+        a_ref, _ = oracle.median_scale(Xr)
+        G = oracle.logp_grad_gmm(Xr, mus, covs)
+        a.step_with_model(model)
+        b.step_with_model(model)
+        a_dev = a.last_scale()[0]
+        assert a_dev == pytest.approx(a_ref, rel=1e-12), step
+        oracle.apply_update(Xr, opt.step(oracle.phi(Xr, G, a_dev)))
+        Xa = a.get_particles()
+        assert np.max(np.abs(Xa - Xr)) <= 1e-9, step
+        assert np.max(np.abs(Xa - b.get_particles())) <= 1e-10, step
+    a.diagnostics()
+    a.close()
+    b.close()
