@@ -1817,13 +1817,16 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     }
     if (const char *e = std::getenv("SVGD_HOST_THREADS")) c->host_threads = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SVGD_DEBUG_COLL")) c->dbg_coll = std::atoi(e) != 0;
-    // phi in row halves when a rank of several has more than 2048 rows per
+    // phi in row halves when a rank of 4 or more has more than 2048 rows per
     // gradient thread: then the host gradient (~18 us per 1000 rows and
     // thread at cfg3's GMM) outlasts the device's median phase of a P-GPU
-    // step and phi waited for G (8-rank share at 2 threads: 0.14 ms); with
-    // halves the first half's gradient runs beside the second half's phi
-    // (cost: one launch pair and one event more per step)
-    c->split_rows = c->rowpath && c->split_h > 0 && c->plan_world >= 2 &&
+    // step and phi waited for G; with halves the first half's gradient runs
+    // beside the second half's phi (cost: one launch pair and one event more
+    // per step).  Measured per-rank share of cfg3 (profiles/r04_sim_world):
+    // P = 8 at 2 threads 0.714 -> 0.656 ms, P = 4 at 4 threads 1.135 ->
+    // 1.098; P = 2 at 8 threads 2.020 -> 2.052 (its phi is long enough to hide
+    // the gradient whole: not split)
+    c->split_rows = c->rowpath && c->split_h > 0 && c->plan_world >= 4 &&
                     c->nrows > 2048 * (int64_t)std::max(1, c->host_threads);
     if (const char *e = std::getenv("SVGD_PHI_SPLIT")) c->split_rows = c->rowpath && c->split_h > 0 && std::atoi(e) != 0;
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_xhalf, hipEventDisableTiming));
@@ -2556,7 +2559,9 @@ int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
     if (!c || !buf || cap <= 0) return SVGD_ERR_ARG;
     char s[96];
     const int d = c->dim;
-    if (c->rowpath) {
+    if (c->rowpath && c->sym) {
+        std::snprintf(s, sizeof s, "k_phi_sym<%d>", d);
+    } else if (c->rowpath) {
         if (c->phi_kind == 2)
             std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 8, 8192, 8>", d, c->R);
         else if (c->phi_kind == 1)

@@ -2231,42 +2231,52 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
 //
 // K_ij = K_ji: each unordered pair's kernel value feeds both particles.  With
 // w_j = 2^(c_j/4096) = exp(-a |xc_j|^2) and E_ij = 2^(u_ij/4096),
-// u_ij = 8192 a log2e xc_i.xc_j (= E_ji), K_ij = w_i w_j E_ij, so
+// u_ij = 8192 a log2e xc_i.xc_j (= u_ji), K_ij = w_i w_j E_ij, so
 //   S_i = sum_j E_ij W_j,   W_j = w_j [V_j, 1]   (V_j = G_j - 2a xc_j)
 //   phi_i = (1/N) w_i (S_i[0..d) + 2a xc_i S_i[d])        (SVGD.hpp:453)
 // and the pair (i, j) adds E_ij W_j to S_i and E_ij W_i to S_j: per
-// unordered pair one Gram (d FMA), one exp and 2(d+1) FMA -- instead of twice
-// the Gram and the exp.  Valid while y = a log2e max|xc|^2 <= 300 (the row
-// stream's fold condition): then |u| <= 600 x 4096 and w >= 2^-300, far from
-// overflow; otherwise (flag symok = 0) the row stream runs instead.
+// unordered pair ONE Gram (d FMA) and ONE exp (7 VALU: the row stream's
+// biased exponent and 8192-entry table, the bias riding in the Gram's first
+// FMA) and 2(d+1) FMA -- instead of twice the Gram and the exp.  Valid while
+// y = a log2e max|xc|^2 <= 300: then |u| <= 600 x 4096, w >= 2^-300 and
+// E <= 2^600, far from over- and underflow; otherwise (symok = 0, set by
+// k_prep_sym) the row stream runs instead.
 //
-// Work: the row-stream median's block-pair plan (tile_coords) over blocks of
-// B = 256 R particles, each tile cut into B / 64 sub-tiles of 64 columns; a
-// work-group takes a contiguous range of (tile, sub-tile) units, holds the
-// tile's B rows in registers (R per lane, 4 waves) and streams the sub-tiles
-// through two LDS buffers (global_load_lds DMA).  Inside a sub-tile each
-// 16-lane group walks a 16-column set in 16 steps on a skewed schedule --
-// lane t meets column (t + s) mod 16 at step s, reading that record from LDS
-// (a conflict-free 16-lane pattern) -- and the column accumulators rotate one
-// lane per step (DPP row_ror:15), so BOTH sums stay in registers; after the
-// 16 steps lane t holds its column's sum over the group's rows.  4 phases
-// give every group every set.  Diagonal tiles take the ordered form (row
-// sums only).  Row sums go to rowpart when the work-group's row block
-// changes; a sub-tile's column sums (4 waves added in fixed order) to
-// colpart.  k_sym_finish adds every partial of a particle in a fixed order
-// (deterministic), forms phi and applies the optimizer (opt_elem).
+// Work-group: SYM_NW = 8 waves (2 per SIMD); wave w holds rows
+// I B + (w R + r) 64 + lane, r < R, of row block I (B = 512 R rows).  The
+// column block J streams through two LDS buffers in sub-tiles of 64 records
+// (global_load_lds DMA).  A sub-tile is 4 sets of 16 columns; in phase ph
+// the 16-lane group g of every wave takes set (g + ph) & 3 on a skewed
+// schedule: at step s lane t meets column (t + s) & 15 of the set -- its
+// record is a per-lane LDS read (16 distinct records per group, an odd
+// 16-byte record stride: conflict-free) -- and the set's column sums (one
+// column per lane) rotate one lane per step with DPP row_ror, so BOTH sums
+// stay in registers.  Per step and lane that is R unordered pairs for
+// R (3d + 9) VALU, 2(d+1) + 1 DPP moves (the packet and the record address),
+// R table reads and (2d+1)/2 b128 record reads -- d = 8, R = 3: 19.5 VALU
+// per ordered pair-row against the row stream's 24.3.  (Round 3's version
+// held R = 2 rows per lane, the unbiased exp and a 4096 table: 4.8 vs 4.7 ms.)
+// After 16 steps lane t holds column (t - 1) & 15's sum over its group's
+// 16 R rows; a wave's 64 column sums of a sub-tile go to LDS (sCol) and the
+// 8 waves' are added in wave order (deterministic) into colpart.  Row sums
+// go to rowpart when the work-group's row block changes.  Diagonal tiles
+// (I == J) run the row side only over the whole square (every ordered pair
+// once).  k_sym_finish adds every partial of a particle in a fixed order,
+// forms phi and applies the optimizer (opt_elem).
 constexpr int SYM_SUB = 64; // columns per sub-tile (4 sets of 16)
+constexpr int SYM_NW = 8;   // waves per work-group (2 per SIMD)
 template <int D> struct SymGeom {
-    // rows per lane: as many as fit 256 VGPRs (2 waves/SIMD) without spilling
-    static constexpr int R = D == 1 ? 8 : D == 2 ? 6 : D == 3 ? 5 : D == 4 ? 4 : D <= 6 ? 3 : 2;
-    static constexpr int B = 4 * 64 * R;                 // block: a work-group's rows
+    // rows per lane: as many as 256 VGPRs hold at 2 waves/SIMD
+    static constexpr int R = D <= 2 ? 8 : D == 3 ? 6 : D == 4 ? 5 : D == 5 ? 4 : 3;
+    static constexpr int B = SYM_NW * 64 * R;            // block: a work-group's rows
     static constexpr int NSUB = B / SYM_SUB;
     static constexpr int DP = D + 1;
-    // record [xc (D) | W (D+1) | pad], stride 2H doubles, H odd: the 16
-    // per-lane 16-byte reads of a set hit 16 distinct 4-bank groups
+    // record [xc (D) | W (D+1) | pad], stride 2H doubles with H odd: a
+    // group's 16 per-lane 16-byte reads hit 16 distinct 4-bank groups
     static constexpr int H = (DP % 2 == 1) ? DP : DP + 1;
     static constexpr int SRS = 2 * H;
-    static constexpr int SUBB = SYM_SUB * SRS * 8; // bytes per sub-tile (whole KiB)
+    static constexpr int SUBB = SYM_SUB * SRS * 8;       // bytes per sub-tile (whole KiB)
+    static constexpr int LDS = 2 * SUBB + 8192 * 8 + SYM_NW * SYM_SUB * DP * 8;
 };
 
 __device__ __forceinline__ int64_t sym_cnt(int64_t nb, int64_t I)
@@ -2284,14 +2294,14 @@ __device__ __forceinline__ int64_t sym_base(int64_t nb, int64_t I)
     return I * (H + 1);
 }
 
+// lane t <- lane t + 1 (mod 16) within each row of 16 lanes (DPP row_ror:15)
+__device__ __forceinline__ int dpp_ror15_i(int v)
+{
+    return __builtin_amdgcn_update_dpp(v, v, 0x12F, 0xF, 0xF, false);
+}
 __device__ __forceinline__ double dpp_ror15(double v)
 {
-    // lane t <- lane t + 1 (mod 16) within each row of 16 lanes; old = src
-    // (every lane has a source in a full-row rotation)
-    const int l = __double2loint(v), h = __double2hiint(v);
-    const int lo = __builtin_amdgcn_update_dpp(l, l, 0x12F, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(h, h, 0x12F, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
+    return __hiloint2double(dpp_ror15_i(__double2hiint(v)), dpp_ror15_i(__double2loint(v)));
 }
 
 // vmcnt wait with a wave-uniform count (0..3)
@@ -2343,80 +2353,132 @@ __global__ void k_prep_sym(const double *__restrict__ xc, int KP, const double *
     }
 }
 
-template <int D, int R, bool SYMM>
-__device__ __forceinline__ void sym_step(const double *__restrict__ rj, const double (&xs)[R][D],
-                                         const double (&wi)[R][D + 1], double (&acc)[R][D + 1],
+// One skew step: the lane's R rows against the column record at rj (LDS).
+// SYMM: also the column side into cacc; ROT: then rotate cacc one lane.
+template <int D, int R, bool SYMM, bool ROT>
+__device__ __forceinline__ void sym_step(const double *rj, const double (&xs)[R][D],
+                                         const double (&wr)[R][D + 1], double (&acc)[R][D + 1],
                                          double (&cacc)[D + 1], const double *tab)
 {
-    // the column's coordinates first, its weights only once the Gram is done
-    // (sched_barrier: the two never hold registers at the same time)
-    double u[R], f[R], T[R], E[R];
-    int ki[R];
+    constexpr int DP = D + 1;
+    // (no scheduling across steps: a step's loads hoisted into the previous
+    // step would hold a second column record -- the registers are all taken)
+    __builtin_amdgcn_sched_barrier(0);
+    double u[R];
     {
+        // the column's coordinates first, its weights only once the Gram is
+        // issued (the two never hold registers at the same time)
         double xj[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) xj[k] = rj[k];
 #pragma unroll
-        for (int r = 0; r < R; ++r) u[r] = xs[r][0] * xj[0];
+        for (int r = 0; r < R; ++r) u[r] = fma(xs[r][0], xj[0], EXP_UB); // biased: u >= 0
 #pragma unroll
         for (int k = 1; k < D; ++k)
 #pragma unroll
             for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], xj[k], u[r]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    double wj[D + 1];
+    double wj[DP];
 #pragma unroll
-    for (int k = 0; k <= D; ++k) wj[k] = rj[D + k];
+    for (int k = 0; k < DP; ++k) wj[k] = rj[D + k];
+    double f[R], T[R], E[R];
+    int ki[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const double kk = __builtin_rint(u[r]);
-        f[r] = u[r] - kk;
-        ki[r] = (int)kk;
-        T[r] = tab[ki[r] & (EXP_TB - 1)];
+        f[r] = __builtin_amdgcn_fract(u[r]); // u >= 0: u - floor(u)
+        ki[r] = (int)u[r];                    // = floor(u)
+        T[r] = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(tab) + tab8k_offset(ki[r]));
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int r = 0; r < R; ++r) E[r] = exp2_4096_poly(f[r]) * tab_scale(T[r], ki[r]);
+    for (int r = 0; r < R; ++r) E[r] = exp2_4096_poly01(f[r]);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int k = 0; k <= D; ++k)
+    for (int r = 0; r < R; ++r) E[r] = E[r] * tab_scale(T[r], ki[r]);
+#pragma unroll
+    for (int k = 0; k < DP; ++k)
 #pragma unroll
         for (int r = 0; r < R; ++r) acc[r][k] = fma(E[r], wj[k], acc[r][k]);
     if constexpr (SYMM) {
 #pragma unroll
-        for (int k = 0; k <= D; ++k)
+        for (int k = 0; k < DP; ++k) {
+            double c = cacc[k];
 #pragma unroll
-            for (int r = 0; r < R; ++r) cacc[k] = fma(E[r], wi[r][k], cacc[k]);
+            for (int r = 0; r < R; ++r) c = fma(E[r], wr[r][k], c);
+            cacc[k] = ROT ? dpp_ror15(c) : c;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// The 4 phases of one sub-tile (buffer cb) for this wave: group grp takes
+// set (grp + ph) & 3 in phase ph, 16 skew steps each; SYMM: the set's column
+// sums go to this wave's sCol slots.
+template <int D, bool SYMM>
+__device__ __forceinline__ void sym_phases(const char *cb, int grp, int tl, int w,
+                                           const double (&xs)[SymGeom<D>::R][D],
+                                           const double (&wr)[SymGeom<D>::R][D + 1],
+                                           double (&acc)[SymGeom<D>::R][D + 1], double *sCol,
+                                           const double *tab)
+{
+    using Gm = SymGeom<D>;
+    constexpr int R = Gm::R, SRS = Gm::SRS, DP = Gm::DP;
+#pragma unroll 1
+    for (int ph = 0; ph < 4; ++ph) {
+        const int set = (grp + ph) & 3;
+        // this lane's record at step s: column (tl + s) & 15 of the set; the
+        // byte offset rotates with the column packet
+        int roff = (set * 16 + tl) * SRS * 8;
+        double cacc[DP];
 #pragma unroll
-        for (int k = 0; k <= D; ++k) cacc[k] = dpp_ror15(cacc[k]);
+        for (int k = 0; k < DP; ++k) cacc[k] = 0.0;
+        // 16 steps straight-line: the last one leaves the packet in place
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            if (s < 15) {
+                sym_step<D, R, SYMM, true>(reinterpret_cast<const double *>(cb + roff), xs, wr, acc, cacc, tab);
+                roff = dpp_ror15_i(roff);
+            } else {
+                sym_step<D, R, SYMM, false>(reinterpret_cast<const double *>(cb + roff), xs, wr, acc, cacc, tab);
+            }
+        }
+        if constexpr (SYMM) {
+            // lane t holds column (t - 1) & 15's sum over this group's rows
+            double *sc = sCol + (w * SYM_SUB + set * 16 + ((tl + 15) & 15)) * DP;
+#pragma unroll
+            for (int k = 0; k < DP; ++k) sc[k] = cacc[k];
+        }
     }
 }
 
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_phi_sym(const double *__restrict__ srec,
-                                                 const double *__restrict__ a_ptr, int64_t nb,
-                                                 int64_t U, const int *__restrict__ symok,
-                                                 double *__restrict__ rowpart, int rslots,
-                                                 double *__restrict__ colpart)
+__global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_phi_sym(
+    const double *__restrict__ srec, const double *__restrict__ a_ptr, int64_t nb, int64_t U,
+    const int *__restrict__ symok, double *__restrict__ rowpart, int rslots, double *__restrict__ colpart)
 {
     using Gm = SymGeom<D>;
     constexpr int R = Gm::R, B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP,
-                  SUBB = Gm::SUBB, NP = SUBB / 1024;
-    __shared__ __attribute__((aligned(16))) char smem[2 * SUBB + 4 * SYM_SUB * DP * 8 + EXP_TB * 8];
+                  SUBB = Gm::SUBB, NP = SUBB / 1024, NT = SYM_NW * 64;
+    __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
     if (!*symok) return; // uniform: the row stream runs instead
-    double *sCol = reinterpret_cast<double *>(smem + 2 * SUBB);
-    double *tab = sCol + 4 * SYM_SUB * DP;
+    double *tab = reinterpret_cast<double *>(smem + 2 * SUBB);
+    double *sCol = tab + 8192;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = lane >> 4, tl = lane & 15;
-#pragma unroll
-    for (int e = 0; e < EXP_TB / 256; ++e)
-        tab[e * 256 + tid] = tab_biased(EXP2_TAB4096[e * 256 + tid], e * 256 + tid);
-    for (int e = tid; e < 4 * SYM_SUB * DP; e += 256) sCol[e] = 0.0;
+    // the biased 8192-entry table of the row stream (k_phi_rows, TABN 8192)
+    for (int m = tid; m < 8192; m += NT) {
+        const double t = EXP2_TAB4096[m & (EXP_TB - 1)];
+        const double tb = tab_biased(m >= EXP_TB ? 2.0 * t : t, m);
+        tab[m] = __hiloint2double(__double2hiint(tb) - (EXP_QB << 20), __double2loint(tb));
+    }
     __syncthreads();
 
     const double alpha = 8192.0 * LOG2E * (*a_ptr);
     const int64_t Gn = gridDim.x;
     const int64_t u0 = U * (int64_t)blockIdx.x / Gn, u1 = U * ((int64_t)blockIdx.x + 1) / Gn;
-    const int npw = (NP - w + 3) / 4; // this wave's DMA pieces per sub-tile
+    const int npw = (NP - w + SYM_NW - 1) / SYM_NW; // this wave's DMA pieces per sub-tile
     // (tile, sub-tile) cursor: the plan's tile t = (I, J), J = I + slot mod nb
     // (plan.cpp); advanced incrementally (no 64-bit divisions per sub-tile)
     struct Cur {
@@ -2447,23 +2509,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const char *src =
             reinterpret_cast<const char *>(srec + (c.J * B + (int64_t)c.q * SYM_SUB) * SRS);
         char *dst = smem + buf * SUBB;
-        for (int p = w; p < NP; p += 4)
+        for (int p = w; p < NP; p += SYM_NW)
             __builtin_amdgcn_global_load_lds((gbl_void *)(src + p * 1024 + lane * 16),
                                              (lds_void *)(dst + p * 1024), 16, 0, 0);
     };
 
-    double xs[R][D], wi[R][DP], acc[R][DP];
+    double xs[R][D], wr[R][DP], acc[R][DP];
     int64_t curI = -1, firstI = 0;
-    auto flush_rows = [&]() {
-        const int slot = (int)(curI - firstI);
-        double *o = rowpart + ((int64_t)blockIdx.x * rslots + slot) * B * DP;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int lr = w * 64 * R + r * 64 + lane;
-#pragma unroll
-            for (int k = 0; k < DP; ++k) o[lr * DP + k] = acc[r][k];
-        }
-    };
+    // row sums of block curI -> rowpart slot curI - firstI
+#define SYM_FLUSH_ROWS()                                                                        \
+    do {                                                                                        \
+        double *o_ = rowpart + ((int64_t)blockIdx.x * rslots + (curI - firstI)) * B * DP;        \
+        _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
+            const int lr = (w * R + r) * 64 + lane;                                             \
+            _Pragma("unroll") for (int k = 0; k < DP; ++k) o_[lr * DP + k] = acc[r][k];         \
+        }                                                                                       \
+    } while (0)
 
     if (u0 >= u1) return;
     Cur cu = cur_at(u0), cn = cu;
@@ -2477,65 +2538,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         } else {
             wait_vmcnt<0>();
         }
-        sym_lds_barrier(); // every wave's pieces of sub-tile u are in LDS
+        sym_lds_barrier(); // every wave's pieces of sub-tile u are in LDS; sCol free
         const int64_t t = cu.t, I = cu.I, J = cu.J;
         const int q = cu.q;
         cur_next(cu);
         if (I != curI) {
-            if (curI >= 0) flush_rows();
+            if (curI >= 0) SYM_FLUSH_ROWS();
             else firstI = I;
             curI = I;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const double *ri = srec + (I * B + w * 64 * R + r * 64 + lane) * SRS;
+                const double *ri = srec + (I * B + (w * R + r) * 64 + lane) * SRS;
 #pragma unroll
                 for (int k = 0; k < D; ++k) xs[r][k] = alpha * ri[k];
 #pragma unroll
                 for (int k = 0; k < DP; ++k) {
-                    wi[r][k] = ri[D + k];
+                    wr[r][k] = ri[D + k];
                     acc[r][k] = 0.0;
                 }
             }
             wait_vmcnt<0>(); // (rare: once per row block) also drains the next sub-tile's DMA
         }
-        const double *cb = reinterpret_cast<const double *>(smem + buf * SUBB);
-        auto phases = [&](auto symm_tag) {
-            constexpr bool SYMM = decltype(symm_tag)::value;
-#pragma unroll 1
-            for (int ph = 0; ph < 4; ++ph) {
-                const int set = (grp + ph) & 3;
-                const double *cset = cb + set * 16 * SRS;
-                double cacc[DP];
-#pragma unroll
-                for (int k = 0; k < DP; ++k) cacc[k] = 0.0;
-#pragma unroll 1
-                for (int s = 0; s < 16; ++s)
-                    sym_step<D, R, SYMM>(cset + ((tl + s) & 15) * SRS, xs, wi, acc, cacc, tab);
-                if constexpr (SYMM) {
-                    // lane tl holds column set*16 + tl; the 4 phases of a set
-                    // come from different groups of this wave, in phase order
-                    double *sc = sCol + (w * SYM_SUB + set * 16 + tl) * DP;
-#pragma unroll
-                    for (int k = 0; k < DP; ++k) sc[k] += cacc[k];
-                }
-            }
-        };
-        if (I == J) phases(std::false_type{});
-        else phases(std::true_type{});
-        sym_lds_barrier(); // every wave is done with buffer buf and its column slots
+        const char *cb = smem + buf * SUBB;
+        // one code path for both tile kinds (two would double the live
+        // register ranges: the allocator spilled); a diagonal tile's column
+        // sums are computed and dropped -- its row side already holds every
+        // ordered pair of the square (~2 % of the tiles)
+        sym_phases<D, true>(cb, grp, tl, w, xs, wr, acc, sCol, tab);
+        // every wave is done with buffer buf (the next iteration's DMA
+        // refills it) and its column sums of this sub-tile are in sCol
+        sym_lds_barrier();
         if (I != J) {
             double *o = colpart + (t * B + (int64_t)q * SYM_SUB) * DP;
-            for (int e = tid; e < SYM_SUB * DP; e += 256) {
+            for (int e = tid; e < SYM_SUB * DP; e += NT) {
                 double v = sCol[e];
 #pragma unroll
-                for (int ww = 1; ww < 4; ++ww) v += sCol[ww * SYM_SUB * DP + e];
+                for (int ww = 1; ww < SYM_NW; ++ww) v += sCol[ww * SYM_SUB * DP + e];
                 o[e] = v;
-#pragma unroll
-                for (int ww = 0; ww < 4; ++ww) sCol[ww * SYM_SUB * DP + e] = 0.0;
             }
         }
     }
-    if (curI >= 0) flush_rows();
+    if (curI >= 0) SYM_FLUSH_ROWS();
+#undef SYM_FLUSH_ROWS
 }
 
 // phi_p = (1/N) w_p (S_p[0..d) + 2a xc_p S_p[d]) for this rank's rows, S_p =
@@ -4108,14 +4152,14 @@ int phi_sym_blocks_per_cu(int d)
     int nb = 0;
     hipError_t e = hipErrorInvalidValue;
     switch (d) {
-    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<1>, 256, 0); break;
-    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<2>, 256, 0); break;
-    case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<3>, 256, 0); break;
-    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<4>, 256, 0); break;
-    case 5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<5>, 256, 0); break;
-    case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<6>, 256, 0); break;
-    case 7: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<7>, 256, 0); break;
-    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<8>, 256, 0); break;
+    case 1: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<1>, SYM_NW * 64, 0); break;
+    case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<2>, SYM_NW * 64, 0); break;
+    case 3: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<3>, SYM_NW * 64, 0); break;
+    case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<4>, SYM_NW * 64, 0); break;
+    case 5: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<5>, SYM_NW * 64, 0); break;
+    case 6: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<6>, SYM_NW * 64, 0); break;
+    case 7: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<7>, SYM_NW * 64, 0); break;
+    case 8: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_sym<8>, SYM_NW * 64, 0); break;
     default: break;
     }
     return (e == hipSuccess && nb > 0) ? nb : 1;
@@ -4131,7 +4175,7 @@ int phi_sym_blocks_per_cu(int d)
                            a.nrm, a.a_ptr, a.nmax, a.n, npad, a.srec, a.symok);               \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k0 && (e = hipEventRecord(ev_k0, stream)) != hipSuccess) return e;             \
-        hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(256), 0, stream, a.srec, a.a_ptr, \
+        hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(SYM_NW * 64), 0, stream, a.srec, a.a_ptr, \
                            a.nbs, a.units, a.symok, a.rowpart, a.rslots, a.colpart);          \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k1 && (e = hipEventRecord(ev_k1, stream)) != hipSuccess) return e;             \

@@ -35,12 +35,15 @@ def _ctx(X, **kw):
     return c
 
 
-# n around the work-group block B = 256 R (R = 8, 6, 5, 4, 3, 3, 2, 2 rows per
-# lane for d = 1..8): a single partial block, exact multiples, ragged tails,
-# and several blocks (odd and even block counts of the tile plan)
-@pytest.mark.parametrize("n,d", [(1, 2), (2, 1), (5, 8), (64, 3), (300, 8), (512, 8), (513, 8),
-                                 (1000, 8), (1536, 8), (2100, 8), (700, 2), (1536, 2), (4000, 2),
-                                 (3000, 1), (1500, 3), (1100, 4), (900, 5), (800, 6), (700, 7)])
+# n around the work-group block B = 512 R (R = 8, 8, 6, 5, 4, 3, 3, 3 rows per
+# lane for d = 1..8: B = 4096, 4096, 3072, 2560, 2048, 1536, 1536, 1536): a
+# single partial block, exact multiples, ragged tails, and several blocks
+# (odd and even block counts of the tile plan)
+@pytest.mark.parametrize("n,d", [(1, 2), (2, 1), (5, 8), (64, 3), (300, 8), (1536, 8), (1537, 8),
+                                 (3072, 8), (3100, 8), (4700, 8), (6200, 8), (700, 2), (4096, 2),
+                                 (5000, 2), (9000, 2), (13000, 2), (3000, 1), (9000, 1), (1500, 3),
+                                 (7000, 3), (1100, 4), (6000, 4), (900, 5), (5000, 5), (800, 6),
+                                 (3500, 6), (700, 7), (3500, 7)])
 def test_sym_phi_matches_oracle(oracle, sym_env, n, d):
     X = oracle.splitmix((n, d), 2.0, 300 + n + d)
     G = oracle.splitmix((n, d), 1.0, 400 + n + d)
