@@ -2257,8 +2257,9 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
 // per ordered pair-row against the row stream's 24.3.  (Round 3's version
 // held R = 2 rows per lane, the unbiased exp and a 4096 table: 4.8 vs 4.7 ms.)
 // After 16 steps lane t holds column (t - 1) & 15's sum over its group's
-// 16 R rows; a wave's 64 column sums of a sub-tile go to LDS (sCol) and the
-// 8 waves' are added in wave order (deterministic) into colpart.  Row sums
+// 16 R rows; the wave's 4 groups add theirs into the wave's LDS slots
+// (sCol) in phase order, and the 8 waves' are added in wave order into
+// colpart (deterministic).  Row sums
 // go to rowpart when the work-group's row block changes.  Diagonal tiles
 // (I == J) run the row side only over the whole square (every ordered pair
 // once).  k_sym_finish adds every partial of a particle in a fixed order,
@@ -2444,10 +2445,14 @@ __device__ __forceinline__ void sym_phases(const char *cb, int grp, int tl, int 
             }
         }
         if constexpr (SYMM) {
-            // lane t holds column (t - 1) & 15's sum over this group's rows
+            // lane t holds column (t - 1) & 15's sum over this group's rows;
+            // the wave's 4 groups (different rows) visit every set once, in
+            // phase order, and add into the wave's zeroed slots (in order
+            // within the wave: deterministic; a branch on the phase here
+            // would let the compiler peel the 16-step body and spill)
             double *sc = sCol + (w * SYM_SUB + set * 16 + ((tl + 15) & 15)) * DP;
 #pragma unroll
-            for (int k = 0; k < DP; ++k) sc[k] = cacc[k];
+            for (int k = 0; k < DP; ++k) sc[k] += cacc[k];
         }
     }
 }
@@ -2465,6 +2470,7 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     double *tab = reinterpret_cast<double *>(smem + 2 * SUBB);
     double *sCol = tab + 8192;
     const int tid = threadIdx.x, lane = tid & 63;
+    for (int e = tid; e < SYM_NW * SYM_SUB * DP; e += NT) sCol[e] = 0.0;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = lane >> 4, tl = lane & 15;
     // the biased 8192-entry table of the row stream (k_phi_rows, TABN 8192)
@@ -2568,14 +2574,18 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
         // every wave is done with buffer buf (the next iteration's DMA
         // refills it) and its column sums of this sub-tile are in sCol
         sym_lds_barrier();
-        if (I != J) {
-            double *o = colpart + (t * B + (int64_t)q * SYM_SUB) * DP;
-            for (int e = tid; e < SYM_SUB * DP; e += NT) {
-                double v = sCol[e];
+        // the 8 waves' column sums added in wave order into colpart (off the
+        // diagonal), and the slots zeroed for the next sub-tile
+        double *o = colpart + (t * B + (int64_t)q * SYM_SUB) * DP;
+        for (int e = tid; e < SYM_SUB * DP; e += NT) {
+            double v = sCol[e];
+            sCol[e] = 0.0;
 #pragma unroll
-                for (int ww = 1; ww < SYM_NW; ++ww) v += sCol[ww * SYM_SUB * DP + e];
-                o[e] = v;
+            for (int ww = 1; ww < SYM_NW; ++ww) {
+                v += sCol[ww * SYM_SUB * DP + e];
+                sCol[ww * SYM_SUB * DP + e] = 0.0;
             }
+            if (I != J) o[e] = v;
         }
     }
     if (curI >= 0) SYM_FLUSH_ROWS();

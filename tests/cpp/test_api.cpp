@@ -502,6 +502,255 @@ static void TestGenericKernelHostPath()
     }
 }
 
+// Model composition over closed forms (reference tests/test_model.cpp:186-315:
+// the same functions, compositions and hand-derived values; gradients and
+// Hessians also against central differences).
+static const Eigen::VectorXd &LowX()
+{
+    static Eigen::VectorXd x = Eigen::Vector2d(0.7, -1.3);
+    return x;
+}
+
+static std::vector<Eigen::MatrixXd> CompParams()
+{
+    Eigen::Matrix2d P;
+    P << 2.0, 0.3, -0.1, 1.5; // not symmetric: grad x^T P x = (P + P^T) x
+    return {Eigen::MatrixXd(Eigen::Vector2d(1.5, -0.4)), Eigen::MatrixXd(P)};
+}
+
+static Model LinearModel() // test_model.cpp:60-67: sum(p .* x)
+{
+    Model m(2);
+    m.UpdateModel([](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &p)
+                  { return p[0](0) * x(0) + p[0](1) * x(1); },
+                  [](const Eigen::VectorXd &, const std::vector<Eigen::MatrixXd> &p)
+                  { return Eigen::VectorXd(p[0]); },
+                  [](const Eigen::VectorXd &, const std::vector<Eigen::MatrixXd> &)
+                  { return Eigen::MatrixXd(Eigen::MatrixXd::Zero(2, 2)); });
+    m.UpdateParameters(CompParams());
+    return m;
+}
+
+static Model SquaredModel() // test_model.cpp:69-76: x^T P x
+{
+    Model m(2);
+    m.UpdateModel([](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &p)
+                  { return (x.transpose() * p[1] * x)(0, 0); },
+                  [](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &p)
+                  { return Eigen::VectorXd((p[1] + p[1].transpose()) * x); },
+                  [](const Eigen::VectorXd &, const std::vector<Eigen::MatrixXd> &p)
+                  { return Eigen::MatrixXd(p[1] + p[1].transpose()); });
+    m.UpdateParameters(CompParams());
+    return m;
+}
+
+static Model SumModel(double scale) // test_model.cpp:78-85 (scale 1) and :203-209 (scale 2): scale * sum(x)
+{
+    Model m(5);
+    m.UpdateModel([scale](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &)
+                  {
+                      double s = 0.0;
+                      for (long k = 0; k < x.rows(); ++k)
+                          s += x(k);
+                      return scale * s;
+                  },
+                  [scale](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &)
+                  { return Eigen::VectorXd(Eigen::VectorXd::Constant(x.rows(), scale)); },
+                  [](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &)
+                  { return Eigen::MatrixXd(Eigen::MatrixXd::Zero(x.rows(), x.rows())); });
+    return m;
+}
+
+// "Method 3" (doc/instructions.md:234-301): a derived model with its own
+// closed forms, p(x) = 1 + (x0 - 0.5)^2 + x0 x1^2, that composes through
+// CloneSharedPointer.
+class ShiftedQuad : public Model
+{
+public:
+    ShiftedQuad() : Model(2) {}
+    std::shared_ptr<Model> CloneSharedPointer() const override { return std::make_shared<ShiftedQuad>(*this); }
+    double EvaluateModel(const Eigen::VectorXd &x) override
+    {
+        return 1.0 + (x(0) - 0.5) * (x(0) - 0.5) + x(0) * x(1) * x(1);
+    }
+    Eigen::VectorXd EvaluateModelGrad(const Eigen::VectorXd &x) override
+    {
+        return Eigen::Vector2d(2.0 * (x(0) - 0.5) + x(1) * x(1), 2.0 * x(0) * x(1));
+    }
+    Eigen::MatrixXd EvaluateModelHessian(const Eigen::VectorXd &x) override
+    {
+        Eigen::Matrix2d H;
+        H << 2.0, 2.0 * x(1), 2.0 * x(1), 2.0 * x(0);
+        return H;
+    }
+};
+
+// grad (and Hessian) of m at x against central differences of the level below
+static void CheckDerivatives(Model &m, const Eigen::VectorXd &x, bool hess)
+{
+    const double h = 1e-5;
+    const Eigen::VectorXd g = m.EvaluateModelGrad(x), lg = m.EvaluateLogModelGrad(x);
+    const Eigen::MatrixXd H = m.EvaluateModelHessian(x), LH = m.EvaluateLogModelHessian(x);
+    for (long c = 0; c < x.rows(); ++c)
+    {
+        Eigen::VectorXd xp = x, xm = x;
+        xp(c) += h;
+        xm(c) -= h;
+        const double fd = (m.EvaluateModel(xp) - m.EvaluateModel(xm)) / (2 * h);
+        CHECK(std::fabs(g(c) - fd) <= 1e-7 * std::max(1.0, std::fabs(fd)));
+        const double lfd = (m.EvaluateLogModel(xp) - m.EvaluateLogModel(xm)) / (2 * h);
+        CHECK(std::fabs(lg(c) - lfd) <= 1e-7 * std::max(1.0, std::fabs(lfd)));
+        if (!hess)
+            continue;
+        const Eigen::VectorXd gp = m.EvaluateModelGrad(xp), gm = m.EvaluateModelGrad(xm);
+        const Eigen::VectorXd lgp = m.EvaluateLogModelGrad(xp), lgm = m.EvaluateLogModelGrad(xm);
+        for (long r = 0; r < x.rows(); ++r)
+        {
+            const double hfd = (gp(r) - gm(r)) / (2 * h), lhfd = (lgp(r) - lgm(r)) / (2 * h);
+            CHECK(std::fabs(H(r, c) - hfd) <= 1e-6 * std::max(1.0, std::fabs(hfd)));
+            CHECK(std::fabs(LH(r, c) - lhfd) <= 1e-6 * std::max(1.0, std::fabs(lhfd)));
+        }
+    }
+}
+
+static void TestModelComposition()
+{
+    const Eigen::VectorXd xl = LowX();
+    Eigen::VectorXd xh(5);
+    xh << 0.3, -0.2, 1.1, 0.4, 0.25;
+    const std::vector<Eigen::MatrixXd> p = CompParams();
+    const Eigen::VectorXd pv = Eigen::VectorXd(p[0]);
+    const Eigen::MatrixXd P = p[1], Ps = P + P.transpose();
+    Model lin = LinearModel(), sq = SquaredModel(), hi = SumModel(1.0), hi2 = SumModel(2.0);
+
+    // test_model.cpp:190-193: dimension mismatch
+    CHECK(Throws<DimensionMismatchException>([&] { Model s = lin + hi; }));
+    CHECK(Throws<DimensionMismatchException>([&] { Model s = lin * hi; }));
+    CHECK(Throws<DimensionMismatchException>([&] { Model s = lin - hi; }));
+    CHECK(Throws<DimensionMismatchException>([&] { Model s = lin / hi; }));
+    Model unset(2);
+    CHECK(Throws<UnsetException>([&] { Model s = lin + unset; }));
+    CHECK(Throws<UnsetException>([&] { unset.EvaluateModel(xl); }));
+
+    // test_model.cpp:206-233: the compositions and their values
+    Model sum1 = lin + lin, sum2 = lin + sq, diff = sq - lin, prod = hi * hi, quot = hi / hi2;
+    for (Model *m : {&sum1, &sum2, &diff, &prod, &quot})
+        m->Initialize();
+    const double lv = pv(0) * xl(0) + pv(1) * xl(1), qv = (xl.transpose() * P * xl)(0, 0);
+    double sx = 0.0;
+    for (long k = 0; k < 5; ++k)
+        sx += xh(k);
+    CHECK(std::fabs(sum1.EvaluateModel(xl) - 2 * lv) < 1e-14);
+    CHECK(std::fabs(sum2.EvaluateModel(xl) - (lv + qv)) < 1e-14);
+    CHECK(std::fabs(diff.EvaluateModel(xl) - (qv - lv)) < 1e-14);
+    CHECK(std::fabs(prod.EvaluateModel(xh) - sx * sx) < 1e-14);
+    CHECK(std::fabs(quot.EvaluateModel(xh) - 0.5) < 1e-15);
+
+    // hand-derived gradients and Hessians (test_model.cpp:246-315's closed forms, composed)
+    CHECK(MaxAbsDiff(sum1.EvaluateModelGrad(xl), 2.0 * pv) < 1e-14);
+    CHECK(MaxAbsDiff(sum2.EvaluateModelGrad(xl), Eigen::VectorXd(pv + Ps * xl)) < 1e-14);
+    CHECK(MaxAbsDiff(diff.EvaluateModelGrad(xl), Eigen::VectorXd(Ps * xl - pv)) < 1e-14);
+    CHECK(MaxAbsDiff(prod.EvaluateModelGrad(xh), Eigen::VectorXd(Eigen::VectorXd::Constant(5, 2.0 * sx))) < 1e-14);
+    CHECK(MaxAbsDiff(quot.EvaluateModelGrad(xh), Eigen::VectorXd(Eigen::VectorXd::Zero(5))) < 1e-15);
+    CHECK(MaxAbsDiff(sum2.EvaluateModelHessian(xl), Ps) < 1e-14);
+    CHECK(MaxAbsDiff(prod.EvaluateModelHessian(xh), Eigen::MatrixXd(Eigen::MatrixXd::Constant(5, 5, 2.0))) < 1e-14);
+    CHECK(MaxAbsDiff(quot.EvaluateModelHessian(xh), Eigen::MatrixXd(Eigen::MatrixXd::Zero(5, 5))) < 1e-15);
+    // grad log p = grad p / p, hess log p = hess p / p - grad p grad p^T / p^2
+    const Eigen::VectorXd g2 = pv + Ps * xl;
+    CHECK(MaxAbsDiff(sum2.EvaluateLogModelGrad(xl), Eigen::VectorXd(g2 / (lv + qv))) < 1e-14);
+    CHECK(MaxAbsDiff(sum2.EvaluateLogModelHessian(xl),
+                     Eigen::MatrixXd(Ps / (lv + qv) - (g2 * g2.transpose()) / ((lv + qv) * (lv + qv)))) < 1e-13);
+    CHECK(std::fabs(sum2.EvaluateLogModel(xl) - std::log(lv + qv)) < 1e-14);
+
+    // parameters concatenate (test_model.cpp:70-74) and update the operands
+    CHECK(sum2.GetParameters().size() == 4);
+    std::vector<Eigen::MatrixXd> q = sum2.GetParameters();
+    q[0] = Eigen::MatrixXd(Eigen::Vector2d(3.0, 1.0));
+    sum2.UpdateParameters(q);
+    CHECK(std::fabs(sum2.EvaluateModel(xl) - (3.0 * xl(0) + xl(1) + qv)) < 1e-14);
+    CHECK(std::fabs(lin.EvaluateModel(xl) - lv) < 1e-15); // the operand itself is untouched
+    CHECK(Throws<DimensionMismatchException>([&] { sum2.UpdateParameters({p[0]}); }));
+
+    // method-3 derived models compose (through CloneSharedPointer), also
+    // with Gaussian forms and inside deeper compositions
+    ShiftedQuad sqd;
+    Eigen::Matrix2d cov;
+    cov << 1.2, 0.3, 0.3, 0.8;
+    MultivariateNormal mvn(Eigen::Vector2d(0.2, -0.1), cov);
+    Model mix1 = sqd * mvn, mix2 = (sqd + lin) / sqd, mix3 = sqd * sq - mvn, mix4 = sqd + mvn;
+    CHECK(!mix1.IsGaussianForm() && !mix4.IsGaussianForm() && mvn.IsGaussianForm());
+    for (Model *m : {&mix1, &mix2, &mix3, &mix4, &sum1, &sum2, &diff})
+        CheckDerivatives(*m, xl, true);
+    CheckDerivatives(prod, xh, true);
+    CheckDerivatives(quot, xh, true);
+    CHECK(std::fabs(mix1.EvaluateModel(xl) - sqd.EvaluateModel(xl) * mvn.EvaluateModel(xl)) < 1e-15);
+
+    // the Gaussian fast path is unchanged: MVN + MVN stays a Gaussian form
+    // (the batched host kernel) and equals the same sum composed in closed
+    // form from function models of the two densities
+    Eigen::Matrix2d cov2;
+    cov2 << 0.5, -0.1, -0.1, 0.9;
+    MultivariateNormal mvn2(Eigen::Vector2d(-0.6, 0.4), cov2);
+    Model gsum = mvn + mvn2;
+    CHECK(gsum.IsGaussianForm());
+    auto wrap = [](const MultivariateNormal &g) {
+        auto gp = std::make_shared<MultivariateNormal>(g);
+        Model w(2);
+        w.UpdateModel([gp](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &)
+                      { return gp->EvaluateModel(x); },
+                      [gp](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &)
+                      { return gp->EvaluateModelGrad(x); },
+                      [gp](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &)
+                      { return gp->EvaluateModelHessian(x); });
+        return w;
+    };
+    Model fsum = wrap(mvn) + wrap(mvn2);
+    CHECK(!fsum.IsGaussianForm());
+    for (const Eigen::VectorXd &x : {LowX(), Eigen::VectorXd(Eigen::Vector2d(-0.4, 0.9))})
+    {
+        CHECK(MaxAbsDiff(gsum.EvaluateLogModelGrad(x), fsum.EvaluateLogModelGrad(x)) < 1e-12);
+        CHECK(MaxAbsDiff(gsum.EvaluateLogModelHessian(x), fsum.EvaluateLogModelHessian(x)) < 1e-11);
+        CHECK(std::fabs(gsum.EvaluateModel(x) - fsum.EvaluateModel(x)) < 1e-15);
+    }
+}
+
+// A composed (closed-form) model on the host-gradient path of the device
+// step: the same density as a Gaussian form (the batched fast path) gives
+// the same trajectory.
+static void TestComposedModelSVGD()
+{
+    const size_t d = 2, n = 300;
+    Eigen::Matrix2d c1, c2;
+    c1 << 0.5, 0.1, 0.1, 0.7;
+    c2 << 0.9, -0.2, -0.2, 0.4;
+    auto g1 = std::make_shared<MultivariateNormal>(Eigen::Vector2d(-1.0, 0.5), c1);
+    auto g2 = std::make_shared<MultivariateNormal>(Eigen::Vector2d(0.8, -0.3), c2);
+    auto fast = std::make_shared<Model>(*g1 + *g2);
+    auto wrap = [](const std::shared_ptr<MultivariateNormal> &g) {
+        Model w(2);
+        w.UpdateModel([g](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &) { return g->EvaluateModel(x); },
+                      [g](const Eigen::VectorXd &x, const std::vector<Eigen::MatrixXd> &) { return g->EvaluateModelGrad(x); });
+        return w;
+    };
+    auto composed = std::make_shared<Model>(wrap(g1) + wrap(g2));
+    std::srand(5);
+    const Eigen::MatrixXd x0 = 2.0 * Eigen::MatrixXd::Random(d, n);
+    Eigen::MatrixXd out[2];
+    for (int w = 0; w < 2; ++w)
+    {
+        auto x = std::make_shared<Eigen::MatrixXd>(x0);
+        std::shared_ptr<Model> model = w ? std::static_pointer_cast<Model>(composed) : fast;
+        auto kernel = std::make_shared<GaussianRBFKernel>(x, GaussianRBFKernel::ScaleMethod::Median, model);
+        auto opt = std::make_shared<Adam>(d, n, 5.0e-2, 0.9, 0.999);
+        SVGD svgd(d, 10, x, kernel, model, opt);
+        svgd.Initialize();
+        svgd.Run();
+        out[w] = *x;
+    }
+    CHECK(MaxAbsDiff(out[0], out[1]) < 1e-10);
+    CHECK(MaxAbsDiff(out[0], x0) > 1e-3);
+}
+
 // Logged-matrix runs for tests/test_cpp_api.py (value parity of the
 // intermediate-matrix log, SVGD.hpp:345-365, against the oracle):
 //   host   generic closed-form unit RBF (host path), test_svgd.cpp scenario
@@ -562,8 +811,10 @@ int main(int argc, char **argv)
     const bool cpu_only = argc > 1 && std::strcmp(argv[1], "cpu") == 0;
     TestArgumentChecks();
     TestGenericKernelHostPath();
+    TestModelComposition();
     if (!cpu_only)
     {
+        TestComposedModelSVGD();
         TestSVGDClassConstantScale();
         for (int w = 0; w < 3; ++w)
             TestSVGDMedianGMM(w);
