@@ -74,11 +74,24 @@ def _raise(ctx, rc):
 class Model:
     """Model base (Model.hpp:20-494): host-side target density.
 
-    Subclasses override EvaluateLogModelGrad(x) (one particle, d-vector) or the
-    batched log_model_grad(X) (X: (n, d) particle rows -> (n, d))."""
+    CppAD is not part of this build, so a model is given in closed form (the
+    reference's "Method 3", doc/instructions.md:234-301): a subclass overrides
+    EvaluateLogModelGrad(x) (one particle, d-vector) or the batched
+    log_model_grad(X) ((n, d) rows -> (n, d)), or -- to compose --
+    EvaluateModel / EvaluateModelGrad [/ EvaluateModelHessian]; or the
+    function is set with its derivatives, UpdateModel(f, grad_f[, hess_f]),
+    each taking (x, params) like the reference's ModelFun (:434-443).
+    Composition (+ - * /, :55-227) applies the sum, product and quotient rules
+    to the operands' closed forms; log p and its derivatives follow from p
+    (grad log p = grad p / p, hess log p = hess p / p - grad p grad p^T / p^2,
+    the reference's LogModelFun :451-454).  Two Gaussian forms add into a
+    Gaussian form (GaussianSum: the batched C++ host gradient)."""
 
     def __init__(self, dim: int = -1):
         self.dimension_ = int(dim)
+        self.model_parameters_ = []
+        self._fun = self._grad = self._hess = None
+        self._op, self._lhs, self._rhs = None, None, None
 
     def Initialize(self):
         if self.dimension_ <= 0:  # Model.hpp:271-274
@@ -87,15 +100,82 @@ class Model:
     def Step(self):  # Model.hpp:413
         pass
 
-    def EvaluateLogModelGrad(self, x):
+    # ---- closed forms (Model.hpp:290-370) ----
+    def UpdateModel(self, fun, grad, hess=None):  # Model.hpp:421-424, derivatives in closed form
+        self._fun, self._grad, self._hess = fun, grad, hess
+        self._op, self._lhs, self._rhs = None, None, None
+
+    def UpdateParameters(self, params):  # Model.hpp:377-388
+        if self._lhs is not None:  # the operands' parameters, concatenated (:70-74)
+            n1 = len(self._lhs.GetParameters())
+            if len(params) != n1 + len(self._rhs.GetParameters()):
+                raise DimensionMismatchException("Number of parameters does not match the model.")
+            self._lhs.UpdateParameters(list(params[:n1]))
+            self._rhs.UpdateParameters(list(params[n1:]))
+            return
+        self.model_parameters_ = [np.asarray(q, dtype=np.float64) for q in params]
+
+    def GetParameters(self):  # Model.hpp:395-406
+        if self._lhs is not None:
+            return self._lhs.GetParameters() + self._rhs.GetParameters()
+        return list(self.model_parameters_)
+
+    def EvaluateModel(self, x):
+        x = np.asarray(x, dtype=np.float64).reshape(-1)
+        if self._fun is not None:
+            return float(self._fun(x, self.model_parameters_))
+        if self._lhs is not None:
+            a, b = self._lhs.EvaluateModel(x), self._rhs.EvaluateModel(x)
+            return {"+": a + b, "-": a - b, "*": a * b}.get(self._op, a / b if self._op == "/" else None)
         raise UnsetException("Model function is unset.")
+
+    def EvaluateLogModel(self, x):
+        return math.log(self.EvaluateModel(x))
+
+    def EvaluateModelGrad(self, x):
+        x = np.asarray(x, dtype=np.float64).reshape(-1)
+        if self._grad is not None:
+            return np.asarray(self._grad(x, self.model_parameters_), dtype=np.float64).reshape(-1)
+        if self._lhs is not None:
+            a, b = self._lhs.EvaluateModel(x), self._rhs.EvaluateModel(x)
+            ga, gb = self._lhs.EvaluateModelGrad(x), self._rhs.EvaluateModelGrad(x)
+            if self._op == "+":
+                return ga + gb
+            if self._op == "-":
+                return ga - gb
+            if self._op == "*":
+                return b * ga + a * gb
+            return (b * ga - a * gb) / (b * b)
+        raise UnsetException("Model function is unset.")
+
+    def EvaluateModelHessian(self, x):
+        x = np.asarray(x, dtype=np.float64).reshape(-1)
+        if self._hess is not None:
+            return np.asarray(self._hess(x, self.model_parameters_), dtype=np.float64)
+        if self._lhs is not None:
+            a, b = self._lhs.EvaluateModel(x), self._rhs.EvaluateModel(x)
+            ga, gb = self._lhs.EvaluateModelGrad(x), self._rhs.EvaluateModelGrad(x)
+            Ha, Hb = self._lhs.EvaluateModelHessian(x), self._rhs.EvaluateModelHessian(x)
+            cross = np.outer(ga, gb) + np.outer(gb, ga)
+            if self._op == "+":
+                return Ha + Hb
+            if self._op == "-":
+                return Ha - Hb
+            if self._op == "*":
+                return b * Ha + cross + a * Hb
+            return Ha / b - cross / (b * b) + (2.0 * a / b ** 3) * np.outer(gb, gb) - (a / (b * b)) * Hb
+        raise UnsetException("Model function is unset.")
+
+    def EvaluateLogModelGrad(self, x):
+        return self.EvaluateModelGrad(x) / self.EvaluateModel(x)
+
+    def EvaluateLogModelHessian(self, x):  # Model.hpp:366-370
+        p, g = self.EvaluateModel(x), self.EvaluateModelGrad(x)
+        return self.EvaluateModelHessian(x) / p - np.outer(g, g) / (p * p)
 
     def log_model_grad(self, X):
         X = np.asarray(X, dtype=np.float64)
         return np.stack([np.asarray(self.EvaluateLogModelGrad(x), dtype=np.float64) for x in X])
-
-    def EvaluateLogModelHessian(self, x):  # Model.hpp:366-370
-        raise UnsetException("Model function is unset.")
 
     def neg_hess_sum(self, X):
         """sum_i -hess log p(x_i): the sum inside the Hessian kernel scale."""
@@ -105,14 +185,37 @@ class Model:
             H -= np.asarray(self.EvaluateLogModelHessian(x), dtype=np.float64)
         return H
 
-    def __add__(self, other):  # Model.hpp:55-92
+    # ---- composition (Model.hpp:55-227) ----
+    def _has_function(self):
+        t = type(self)
+        return (self._fun is not None or self._lhs is not None or t.EvaluateModel is not Model.EvaluateModel
+                or t.EvaluateLogModelGrad is not Model.EvaluateLogModelGrad)
+
+    def _compose(self, other, op, verb):
         if not isinstance(other, Model) or self.dimension_ != other.dimension_:
-            raise DimensionMismatchException("Only models with the same variable dimensions can be added.")
-        comps = _gaussian_components(self), _gaussian_components(other)
-        if comps[0] is None or comps[1] is None:
+            raise DimensionMismatchException(f"Only models with the same variable dimensions can be {verb}.")
+        if not self._has_function() or not other._has_function():
             raise UnsetException("One of the model functions is unset; functional composition "
                                  "requires both model functions to be set.")
-        return GaussianSum(comps[0][0] + comps[1][0], comps[0][1] + comps[1][1])
+        out = Model(self.dimension_)
+        out._op, out._lhs, out._rhs = op, self, other
+        return out
+
+    def __add__(self, other):  # Model.hpp:55-92
+        comps = _gaussian_components(self), _gaussian_components(other)
+        if (comps[0] is not None and comps[1] is not None and self.dimension_ == other.dimension_
+                and all(_builtin_grad(m) and _builtin_hess(m) for m in (self, other))):
+            return GaussianSum(comps[0][0] + comps[1][0], comps[0][1] + comps[1][1])
+        return self._compose(other, "+", "added")
+
+    def __sub__(self, other):  # Model.hpp:100-137
+        return self._compose(other, "-", "added")
+
+    def __mul__(self, other):  # Model.hpp:145-182
+        return self._compose(other, "*", "multiplied")
+
+    def __truediv__(self, other):  # Model.hpp:190-227
+        return self._compose(other, "/", "multiplied")
 
 
 class GaussianSum(Model):
@@ -189,6 +292,30 @@ class GaussianSum(Model):
 
     def EvaluateModel(self, x):
         return math.exp(self.EvaluateLogModel(x))
+
+    def EvaluateModelGrad(self, x):  # p grad log p (an operand of a composition)
+        return self.EvaluateModel(x) * self.EvaluateLogModelGrad(x)
+
+    def EvaluateModelHessian(self, x):  # p (hess log p + grad log p grad log p^T)
+        g = self.EvaluateLogModelGrad(x)
+        return self.EvaluateModel(x) * (self.EvaluateLogModelHessian(x) + np.outer(g, g))
+
+    def UpdateParameters(self, params):  # (mean, covariance) per component, in order
+        if len(params) != 2 * len(self.means_):
+            raise DimensionMismatchException("Number of parameters does not match the model.")
+        means = [np.asarray(m, dtype=np.float64).reshape(-1) for m in params[0::2]]
+        covs = [np.asarray(c, dtype=np.float64) for c in params[1::2]]
+        for m, c in zip(means, covs):
+            if m.shape[0] != self.dimension_ or c.shape != (self.dimension_, self.dimension_):
+                raise DimensionMismatchException("Dimensions of parameter vectors/matrices do not match original dimension.")
+        self.means_, self.covs_ = means, covs
+        self._build()
+
+    def GetParameters(self):  # Model.hpp:395-406: mean0, cov0, mean1, cov1, ...
+        out = []
+        for m, c in zip(self.means_, self.covs_):
+            out += [m.copy(), c.copy()]
+        return out
 
 
 class MultivariateNormal(GaussianSum):

@@ -1342,12 +1342,12 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
                                   mat ? c->wv : nullptr, c->xc, c->KP, c->phi, opt, c->stream));
     else if (c->dtype == SVGD_F32)
         HIPCHK(c, launch_phi_f32(c->KP, c->NCB, mat ? c->zcf : c->xcf, c->cvf, c->Vf, c->scal,
-                                 c->row0, c->nrows, (c->n + TB - 1) / TB, c->dim,
+                                 c->row0, c->nrows, (c->n + TB - 1) / TB, c->n, c->dim,
                                  1.0 / (double)c->n, mat ? c->wv : nullptr, c->xc, c->phi,
                                  c->stream));
     else
         HIPCHK(c, launch_phi(c->KP, c->NCB, mat ? c->zc : c->xc, c->cvec, c->V, c->scal, c->row0,
-                             c->nrows, (c->n + TB - 1) / TB, c->dim, 1.0 / (double)c->n,
+                             c->nrows, (c->n + TB - 1) / TB, c->n, c->dim, 1.0 / (double)c->n,
                              mat ? c->wv : nullptr, c->phi, c->stream));
     if (k0) {
         if (!c->rowpath) HIPCHK(c, hipEventRecord(k1, c->stream));
@@ -1612,6 +1612,12 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         return fail(c, SVGD_ERR_DIM, "[Dimension Error] Device path supports dimension <= 64.");
     // row-stream path (fp64, d <= 16): xc rows are the median records [xc | |xc|^2 | 0..]
     if (dim <= ROWS_MAX_D && !f32) c->KP = med_rec_stride(dim);
+    // fp64 tiles with d = 16 NCB: no V column of ones (row sums on the VALU);
+    // SVGD_PHI_S1V=0 keeps the ones column (A/B knob)
+    if (!f32 && phi_tile_s1v(dim)) {
+        const char *e = std::getenv("SVGD_PHI_S1V");
+        if (!e || std::atoi(e) != 0) c->NCB = dim / 16;
+    }
     c->dim = dim;
     c->n = n;
     c->dtype = dtype;
@@ -2571,8 +2577,11 @@ int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
     } else if (c->dtype == SVGD_F32 && c->XS) {
         std::snprintf(s, sizeof s, "k_phi_f32s<%d, %d>", c->KP, c->NCB);
     } else {
-        std::snprintf(s, sizeof s, "k_phi<%s, %d, %d>", c->dtype == SVGD_F32 ? "float" : "double", c->KP,
-                      c->NCB);
+        const bool f64 = c->dtype != SVGD_F32;
+        int nw = 4, pre = 0;
+        phi_tile_cfg(f64, &nw, &pre);
+        std::snprintf(s, sizeof s, "k_phi<%s, %d, %d, %d, %s, %s>", f64 ? "double" : "float", c->KP,
+                      c->NCB, nw, pre ? "true" : "false", f64 && c->dim == 16 * c->NCB ? "true" : "false");
     }
     std::snprintf(buf, (size_t)cap, "%s", s);
     return SVGD_OK;

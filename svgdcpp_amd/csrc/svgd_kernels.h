@@ -53,14 +53,18 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);
+// n: particles (columns j >= n are padding); an fp64 tile with d = 16 NCB
+// (phi_tile_s1v) sums P's rows on the VALU instead of a V column of ones
 hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
-                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
-                      double inv_n, const double *wv, double *phi, hipStream_t stream);
+                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int64_t n,
+                      int d, double inv_n, const double *wv, double *phi, hipStream_t stream);
+bool phi_tile_s1v(int d);
+void phi_tile_cfg(bool f64, int *nw, int *pre); // k_phi's waves per block and prefetch flag
 // fp32 variants of the tile kernels (SVGD_F32); phi and the epilogue stay fp64
 hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, const float *V,
                           const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j,
-                          int d, double inv_n, const double *wv, const double *xc, double *phi,
-                          hipStream_t stream);
+                          int64_t n, int d, double inv_n, const double *wv, const double *xc,
+                          double *phi, hipStream_t stream);
 hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, const float *nrm,
                                  int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                                  int64_t cap, uint32_t *counts, unsigned long long *below,

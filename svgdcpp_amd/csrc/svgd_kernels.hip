@@ -358,7 +358,7 @@ __global__ void k_prep_v(const double *__restrict__ xc, const double *__restrict
 
 // ------------------------------------------------------------------ phi --
 //
-// One workgroup = 4 waves = 64 rows i (wave w: rows 16w..16w+15).  The
+// One workgroup = NW waves = 16 NW rows i (wave w: rows 16w..16w+15).  The
 // workgroup sweeps all column tiles of 64 particles j staged through LDS.
 // Per 16(j) x 16(i) sub-tile:
 //   Gram   dot[j][i] = xc_j . xc_i     KP/4 MFMAs (A = X_J from LDS, B = X_I regs)
@@ -368,87 +368,126 @@ __global__ void k_prep_v(const double *__restrict__ xc, const double *__restrict
 // Epilogue: phi_i = (acc[i][0:d] + 2a xc_i acc[i][d]) / N (fp64).
 // T = double (default) or float (SVGD_F32: Gram, exp and contraction on
 // v_mfma_f32_16x16x4f32 / v_exp_f32 from fp32 copies xg, cvec, V).
-template <class T, int KP, int NCB>
-__global__ __launch_bounds__(256) void k_phi(const T *__restrict__ xg, const T *__restrict__ cvec,
-                                            const T *__restrict__ V,
-                                            const double *__restrict__ a_ptr, int64_t row0,
-                                            int64_t nrows, int64_t ntiles_j, int d,
-                                            double inv_n, const double *__restrict__ wv,
-                                            const double *__restrict__ xc,
-                                            double *__restrict__ phi)
+//
+// LDS layout (bank-conflict-free for the MFMA operand reads, whose lanes
+// (lo, hi) touch rows lo / hi + 4r): X_J is j-major with row stride LDK, an
+// odd multiple of 4 elements (the 16 lo rows x 4 hi columns of a Gram
+// A-operand land in distinct banks; the fill is a straight 16-byte copy), and
+// V_J rows are padded to VWP.  fp64 d = 64 thus needs 76 KB (was 124 KB with a
+// k-major X_J and a separate epilogue buffer, 1 block of 4 waves per CU): the
+// epilogue's per-wave accumulator tiles now reuse the staging buffers, in as
+// many phases as needed, and an 8-wave block keeps 2 blocks = 4 waves/SIMD.
+template <class T, int KP> struct PhiTile {
+    static constexpr int LDK = ((KP / 4) & 1) ? KP : KP + 4;
+};
+template <class T, int VW> struct PhiVPad;
+template <int VW> struct PhiVPad<double, VW> {
+    static constexpr int VWP = ((VW / 16) & 1) ? VW : VW + 16;
+};
+template <int VW> struct PhiVPad<float, VW> {
+    static constexpr int VWP = VW + 4;
+};
+template <class T, int KP, int NCB> struct PhiLds {
+    static constexpr int VW = 16 * NCB, LDK = PhiTile<T, KP>::LDK, VWP = PhiVPad<T, VW>::VWP;
+    static constexpr int XB = TB * LDK * (int)sizeof(T), VB = TB * VWP * (int)sizeof(T);
+    static constexpr int MAIN = XB + VB + TB * (int)sizeof(T);
+    static constexpr int ACCW = 16 * (VW + 1) * (int)sizeof(T); // one wave's epilogue tile
+};
+
+#ifndef SVGD_PHI_WPE
+#define SVGD_PHI_WPE 1
+#endif
+// S1V (d = 16 NCB, fp64 d = 32/48/64): V holds no column of ones; the row
+// sums s1_i = sum_j P_ij are added on the VALU (16 adds per tile and lane
+// instead of a whole 16-column MFMA block: d = 64 runs 4 blocks, not 5), the
+// padded columns j >= n masked through c_j = -huge (P = 0).
+template <class T, int KP, int NCB, int NW, bool PRE, bool S1V>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(SVGD_PHI_WPE))) void k_phi(const T *__restrict__ xg, const T *__restrict__ cvec,
+                                                 const T *__restrict__ V,
+                                                 const double *__restrict__ a_ptr, int64_t row0,
+                                                 int64_t nrows, int64_t ntiles_j, int64_t n, int d,
+                                                 double inv_n, const double *__restrict__ wv,
+                                                 const double *__restrict__ xc,
+                                                 double *__restrict__ phi)
 {
     typedef typename Acc4<T>::type A4;
-    constexpr int VW = 16 * NCB;
-    __shared__ T sX[KP * LDP];
-    __shared__ __attribute__((aligned(16))) T sV[TB * VW];
-    __shared__ T sC[TB];
-    __shared__ T sAcc[4][16][VW + 1];
+    typedef PhiLds<T, KP, NCB> L;
+    constexpr int VW = L::VW, LDK = L::LDK, VWP = L::VWP, NT = 64 * NW;
+    constexpr int NWE = L::MAIN / L::ACCW < NW ? L::MAIN / L::ACCW : NW; // waves per epilogue phase
+    static_assert(NWE >= 1, "phi epilogue tile exceeds the staging buffers");
+    __shared__ __attribute__((aligned(16))) char smem[L::MAIN];
+    T *sX = reinterpret_cast<T *>(smem);
+    T *sV = reinterpret_cast<T *>(smem + L::XB);
+    T *sC = reinterpret_cast<T *>(smem + L::XB + L::VB);
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int lo = lane & 15, hi = lane >> 4;
     const double a = *a_ptr;
     const T alpha = (T)(2.0 * a * LOG2E);
 
-    const int64_t ibase = row0 + (int64_t)blockIdx.x * TB + w * 16;
+    const int64_t ibase = row0 + (int64_t)blockIdx.x * (16 * NW) + w * 16;
+    // rows past the slice read its last row (valid memory; never stored)
+    const int64_t il_ld = ibase + lo < row0 + nrows ? ibase + lo : row0 + nrows - 1;
     // B operand of the Gram MFMA: X_I^T, lane holds xg[i = lo][k = 4kk + hi]
     T bI[KP / 4];
 #pragma unroll
-    for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = xg[(ibase + lo) * KP + 4 * kk + hi];
-    const T ci = cvec[ibase + lo];
+    for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = xg[il_ld * KP + 4 * kk + hi];
+    const T ci = cvec[il_ld];
 
     A4 acc[NCB];
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) acc[cb] = A4{0, 0, 0, 0};
+    T ps = (T)0; // S1V: this lane's share of s1_i (i = lo)
+    const T CPAD = S1V ? (T)-1.0e300 : (T)0;
 
-    // the next column tile (X_J, V_J, c_J) is loaded into registers while the
-    // current one is computed, and stored to LDS between the two barriers
-    constexpr int PU = TB * KP / 256;
-    constexpr int NV = TB * VW * (int)sizeof(T) / 16; // 16-byte pieces of V_J
-    constexpr int PV = (NV + 255) / 256;
-    T preX[PU];
-    uint4 preV[PV];
+    // 16-byte pieces: X_J row jl holds KP/EP of them, V_J row VW/EP
+    constexpr int EP = 16 / (int)sizeof(T);
+    constexpr int NXP = TB * KP / EP, NVP = TB * VW / EP;
+    constexpr int PX = (NXP + NT - 1) / NT, PV = (NVP + NT - 1) / NT;
+    uint4 preX[PRE ? PX : 1], preV[PRE ? PV : 1];
     T preC = (T)0;
+    auto put = [&](int e, uint4 vx, bool isv) {
+        if (!isv) {
+            const int jl = e / (KP / EP), q = e - jl * (KP / EP);
+            *reinterpret_cast<uint4 *>(sX + jl * LDK + q * EP) = vx;
+        } else {
+            const int jl = e / (VW / EP), q = e - jl * (VW / EP);
+            *reinterpret_cast<uint4 *>(sV + jl * VWP + q * EP) = vx;
+        }
+    };
     auto fetch = [&](int64_t j0) {
 #pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
-            preX[u] = xg[(j0 + jl) * KP + k];
+        for (int u = 0; u < PX; ++u) {
+            const int e = tid + NT * u;
+            if (NXP % NT == 0 || e < NXP) preX[u] = reinterpret_cast<const uint4 *>(xg + j0 * KP)[e];
         }
 #pragma unroll
         for (int u = 0; u < PV; ++u) {
-            const int e = tid + 256 * u;
-            if (e < NV) preV[u] = reinterpret_cast<const uint4 *>(V + j0 * VW)[e];
+            const int e = tid + NT * u;
+            if (NVP % NT == 0 || e < NVP) preV[u] = reinterpret_cast<const uint4 *>(V + j0 * VW)[e];
         }
         if (tid < TB) preC = cvec[j0 + tid];
     };
-    // (fp64 only: measured 49.5 -> 40.2 ms at d = 64; the fp32 kernel, which
-    // keeps 2 waves/SIMD, is no faster with it and stages synchronously)
-    constexpr bool PRE = std::is_same<T, double>::value;
     if (PRE && ntiles_j > 0) fetch(0);
     for (int64_t jt = 0; jt < ntiles_j; ++jt) {
         __syncthreads();
-        // stage X_J (k-major, padded rows) and V_J, c_J
         if constexpr (PRE) {
 #pragma unroll
-            for (int u = 0; u < PU; ++u) {
-                const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
-                sX[k * LDP + jl] = preX[u];
+            for (int u = 0; u < PX; ++u) {
+                const int e = tid + NT * u;
+                if (NXP % NT == 0 || e < NXP) put(e, preX[u], false);
             }
 #pragma unroll
             for (int u = 0; u < PV; ++u) {
-                const int e = tid + 256 * u;
-                if (e < NV) reinterpret_cast<uint4 *>(sV)[e] = preV[u];
+                const int e = tid + NT * u;
+                if (NVP % NT == 0 || e < NVP) put(e, preV[u], true);
             }
-            if (tid < TB) sC[tid] = preC;
+            if (tid < TB) sC[tid] = !S1V || jt * TB + tid < n ? preC : CPAD;
         } else {
             const int64_t j0 = jt * TB;
-            for (int e = tid; e < TB * KP; e += 256) {
-                const int jl = e / KP, k = e - jl * KP;
-                sX[k * LDP + jl] = xg[(j0 + jl) * KP + k];
-            }
-            for (int e = tid; e < NV; e += 256)
-                reinterpret_cast<uint4 *>(sV)[e] = reinterpret_cast<const uint4 *>(V + j0 * VW)[e];
-            if (tid < TB) sC[tid] = cvec[j0 + tid];
+            for (int e = tid; e < NXP; e += NT) put(e, reinterpret_cast<const uint4 *>(xg + j0 * KP)[e], false);
+            for (int e = tid; e < NVP; e += NT) put(e, reinterpret_cast<const uint4 *>(V + j0 * VW)[e], true);
+            if (tid < TB) sC[tid] = !S1V || j0 + tid < n ? cvec[j0 + tid] : CPAD;
         }
         __syncthreads();
         if (PRE && jt + 1 < ntiles_j) fetch((jt + 1) * TB);
@@ -458,32 +497,49 @@ __global__ __launch_bounds__(256) void k_phi(const T *__restrict__ xg, const T *
             A4 dot = {0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < KP / 4; ++kk)
-                dot = mfma16(sX[(4 * kk + hi) * LDP + js * 16 + lo], bI[kk], dot);
+                dot = mfma16(sX[(js * 16 + lo) * LDK + 4 * kk + hi], bI[kk], dot);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int jl = js * 16 + acc_row<T>(hi, r);
                 const T p = exp2_nonpos(fma(alpha, dot[r], ci + sC[jl]));
+                if (S1V) ps += p;
 #pragma unroll
                 for (int cb = 0; cb < NCB; ++cb)
-                    acc[cb] = mfma16(p, sV[jl * VW + cb * 16 + lo], acc[cb]);
+                    acc[cb] = mfma16(p, sV[jl * VWP + cb * 16 + lo], acc[cb]);
             }
         }
     }
 
-    // epilogue (fp64): acc lane map row i = acc_row(hi, q), col c = lo (+16cb)
-#pragma unroll
-    for (int cb = 0; cb < NCB; ++cb)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) sAcc[w][acc_row<T>(hi, q)][cb * 16 + lo] = acc[cb][q];
-    __syncthreads();
+    // epilogue (fp64): acc lane map row i = acc_row(hi, q), col c = lo (+16cb);
+    // waves w with w / NWE == ph use slot w % NWE of the staging buffers
     const double two_a = 2.0 * a;
-    for (int e = lane; e < 16 * d; e += 64) {
-        const int il = e / d, c = e - il * d;
-        const int64_t i = ibase + il;
-        if (i - row0 < nrows) {
-            const double s1 = (double)sAcc[w][il][d];
-            const double wgt = wv ? wv[i * d + c] : two_a * xc[i * KP + c];
-            phi[(i - row0) * d + c] = inv_n * ((double)sAcc[w][il][c] + wgt * s1);
+    T *sAcc = reinterpret_cast<T *>(smem) + (w % NWE) * 16 * (VW + 1);
+    if (S1V) { // the 4 lane groups' shares of row lo, in fixed order
+        ps += __shfl_xor(ps, 16);
+        ps += __shfl_xor(ps, 32);
+    }
+    const int s1c = S1V ? VW : d;
+#pragma unroll 1
+    for (int ph = 0; ph < (NW + NWE - 1) / NWE; ++ph) {
+        __syncthreads();
+        if (w / NWE == ph) {
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) sAcc[acc_row<T>(hi, q) * (VW + 1) + cb * 16 + lo] = acc[cb][q];
+            if (S1V && hi == 0) sAcc[lo * (VW + 1) + VW] = ps;
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int e = lane; e < 16 * d; e += 64) {
+                const int il = e / d, c = e - il * d;
+                const int64_t i = ibase + il;
+                if (i - row0 < nrows) {
+                    const double s1 = (double)sAcc[il * (VW + 1) + s1c];
+                    const double wgt = wv ? wv[i * d + c] : two_a * xc[i * KP + c];
+                    phi[(i - row0) * d + c] = inv_n * ((double)sAcc[il * (VW + 1) + c] + wgt * s1);
+                }
+            }
         }
     }
 }
@@ -3718,21 +3774,65 @@ hipError_t launch_pair_rows(int d, int KP, int mode, int grid, const double *xc,
                               KP, nrm, nb, t0, t1, sc, sh, sd, stream);
 }
 
+// fp64: 8-wave blocks, 2 per CU (76 KB LDS at d = 64), column tile prefetched
+// into registers; fp32 (small-N fallback of SVGD_F32): 4 waves, synchronous
+// staging.  SVGD_PHI_NW / _PRE / _WPE override at build time for measurements.
+#ifndef SVGD_PHI_NW
+#define SVGD_PHI_NW 8
+#endif
+#ifndef SVGD_PHI_PRE
+#define SVGD_PHI_PRE 1
+#endif
+template <class T> struct PhiCfg {
+    static constexpr int NW = 4;
+    static constexpr bool PRE = false;
+};
+template <> struct PhiCfg<double> {
+    static constexpr int NW = SVGD_PHI_NW;
+    static constexpr bool PRE = SVGD_PHI_PRE;
+};
+
+template <class T, int KPv, int NCBv, bool S1V>
+static hipError_t launch_phi_tile(const T *xg, const T *cvec, const T *V, const double *a_ptr,
+                                  int64_t row0, int64_t nrows, int64_t ntiles_j, int64_t n, int d,
+                                  double inv_n, const double *wv, const double *xc, double *phi,
+                                  hipStream_t stream)
+{
+    constexpr int NW = PhiCfg<T>::NW;
+    const int64_t grid = (nrows + 16 * NW - 1) / (16 * NW);
+    hipLaunchKernelGGL((k_phi<T, KPv, NCBv, NW, PhiCfg<T>::PRE, S1V>), dim3(grid), dim3(64 * NW), 0,
+                       stream, xg, cvec, V, a_ptr, row0, nrows, ntiles_j, n, d, inv_n, wv, xc, phi);
+    return hipGetLastError();
+}
 #define SVGD_PHI_CASE(KPv, NCBv)                                                             \
-    if (KP == KPv && NCB == NCBv) {                                                          \
-        hipLaunchKernelGGL((k_phi<T, KPv, NCBv>), dim3(grid), dim3(256), 0, stream, xg, cvec,  \
-                           V, a_ptr, row0, nrows, ntiles_j, d, inv_n, wv, xc, phi);          \
-        return hipGetLastError();                                                            \
-    }
+    if (KP == KPv && NCB == NCBv)                                                            \
+        return launch_phi_tile<T, KPv, NCBv, false>(xg, cvec, V, a_ptr, row0, nrows, ntiles_j, \
+                                                    n, d, inv_n, wv, xc, phi, stream);
+#define SVGD_PHI_CASE_S1V(KPv, NCBv)                                                         \
+    if (KP == KPv && NCB == NCBv && d == 16 * NCBv)                                          \
+        return launch_phi_tile<T, KPv, NCBv, true>(xg, cvec, V, a_ptr, row0, nrows, ntiles_j,  \
+                                                   n, d, inv_n, wv, xc, phi, stream);
+
+// S1V tiles (fp64, d = 16 NCB > 16): pick_tiles_s1v in the C ABI
+bool phi_tile_s1v(int d) { return d > 16 && d <= 64 && d % 16 == 0; }
+void phi_tile_cfg(bool f64, int *nw, int *pre)
+{
+    *nw = f64 ? PhiCfg<double>::NW : PhiCfg<float>::NW;
+    *pre = f64 ? PhiCfg<double>::PRE : PhiCfg<float>::PRE;
+}
 
 template <class T>
 static hipError_t launch_phi_t(int KP, int NCB, const T *xg, const T *cvec, const T *V,
                                const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j,
-                               int d, double inv_n, const double *wv, const double *xc,
+                               int64_t n, int d, double inv_n, const double *wv, const double *xc,
                                double *phi, hipStream_t stream)
 {
-    const int64_t grid = (nrows + TB - 1) / TB;
-    if (grid == 0) return hipSuccess;
+    if (nrows <= 0) return hipSuccess;
+    if constexpr (std::is_same<T, double>::value) {
+        SVGD_PHI_CASE_S1V(32, 2)
+        SVGD_PHI_CASE_S1V(64, 3)
+        SVGD_PHI_CASE_S1V(64, 4)
+    }
     SVGD_PHI_CASE(4, 1)
     SVGD_PHI_CASE(8, 1)
     SVGD_PHI_CASE(12, 1)
@@ -3745,21 +3845,22 @@ static hipError_t launch_phi_t(int KP, int NCB, const T *xg, const T *cvec, cons
     return hipErrorInvalidValue;
 }
 #undef SVGD_PHI_CASE
+#undef SVGD_PHI_CASE_S1V
 
 hipError_t launch_phi(int KP, int NCB, const double *xc, const double *cvec, const double *V,
-                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int d,
-                      double inv_n, const double *wv, double *phi, hipStream_t stream)
+                      const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j, int64_t n,
+                      int d, double inv_n, const double *wv, double *phi, hipStream_t stream)
 {
-    return launch_phi_t<double>(KP, NCB, xc, cvec, V, a_ptr, row0, nrows, ntiles_j, d, inv_n, wv,
-                                xc, phi, stream);
+    return launch_phi_t<double>(KP, NCB, xc, cvec, V, a_ptr, row0, nrows, ntiles_j, n, d, inv_n,
+                                wv, xc, phi, stream);
 }
 
 hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, const float *V,
                           const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles_j,
-                          int d, double inv_n, const double *wv, const double *xc, double *phi,
-                          hipStream_t stream)
+                          int64_t n, int d, double inv_n, const double *wv, const double *xc,
+                          double *phi, hipStream_t stream)
 {
-    return launch_phi_t<float>(KP, NCB, xg, cvec, V, a_ptr, row0, nrows, ntiles_j, d, inv_n, wv,
+    return launch_phi_t<float>(KP, NCB, xg, cvec, V, a_ptr, row0, nrows, ntiles_j, n, d, inv_n, wv,
                                xc, phi, stream);
 }
 

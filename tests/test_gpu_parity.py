@@ -82,6 +82,32 @@ def test_phi_row_kernel_variants(oracle, monkeypatch, n, d):
     assert np.max(np.abs(out["1"] - out["0"])) <= 1e-12
 
 
+@pytest.mark.parametrize("n,d", [(300, 32), (1111, 32), (1111, 48), (300, 64), (1111, 64), (1111, 17),
+                                 (1111, 33), (1111, 63), (129, 64)])
+def test_phi_tile_kernel_variants(oracle, monkeypatch, n, d):
+    """The fp64 tile kernel (d > 16, k_phi<double>: 8-wave blocks of 128 rows,
+    j-major X_J in LDS): with d = 16 NCB its row sums run on the VALU
+    (SVGD_PHI_S1V, default) or through a V column of ones (=0).  Ragged n
+    leaves a partial last row block and padded columns j >= n, which the VALU
+    sums must mask.  Both against the oracle; against each other only the
+    summation order of s1 differs."""
+    X = oracle.splitmix((n, d), 2.0, 700 + n + d)
+    G = oracle.splitmix((n, d), 1.0, 800 + n + d)
+    a = 0.05
+    ref = oracle.phi(X, G, a)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SVGD_PHI_S1V", v)
+        c = _ctx(X)
+        out[v] = c.phi(G, a)
+        name = c.phi_kernel_name()
+        c.close()
+        assert name.startswith("k_phi<double"), name
+        assert name.endswith("true>") == (v == "1" and d % 16 == 0), name
+        assert np.max(np.abs(out[v] - ref)) <= PHI_TOL, (v, name)
+    assert np.max(np.abs(out["1"] - out["0"])) <= 1e-12
+
+
 def test_phi_far_from_origin(oracle):
     """Translation: particles around 1e3 (mean-centring keeps the x_i*sum K -
     sum K x_j assembly accurate)."""
