@@ -17,6 +17,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -114,6 +115,7 @@ class HostWorker {
 } // namespace
 
 constexpr int64_t MAX_COLLECT_BLOCKS = 2048; // collect-pass grid limit (buffer sizes)
+constexpr size_t XMIRROR_MAX = size_t(1) << 20; // shard bytes for the host mirror / G host read
 
 struct svgd_ctx {
     int dim = 0;
@@ -186,13 +188,13 @@ struct svgd_ctx {
     float *xf = nullptr;    // np x med_f32_stride(d) fp32 median records
     unsigned long long *nmax = nullptr; // max |xc|^2 (double bits)
     int S = 1;
-    // phi in two row halves (svgd_step_host_model when split_rows): rows
-    // [0, split_h) then [split_h, nrows) of this rank, S2 column splits each
+    // phi in two row parts (svgd_step_host_model when split_rows): rows
+    // [0, split_h) with S2 column splits, then [split_h, nrows) with S2b
     bool split_rows = false;      // policy (init_ctx)
     bool in_host_step = false;    // run_phi_opt called by svgd_step_host_model
     bool xhalf_ready = false;     // the last step's ev_xhalf marks its first half's X_{t+1}
-    int64_t split_h = 0, ldp2 = 0;
-    int S2 = 0;
+    int64_t split_h = 0;
+    int S2 = 0, S2b = 0;
     hipEvent_t ev_xhalf = nullptr;
     int R = 2; // rows per lane of k_phi_rows
     int phi_kind = 0; // 0 k_phi_rows (4 waves), 1 k_phi_rows_s (scalar columns), 2 k_phi_rows (8 waves, column-split)
@@ -255,6 +257,14 @@ struct svgd_ctx {
 
     // pinned host
     double *h_x = nullptr, *h_g = nullptr;
+    double *h_x_dev = nullptr, *h_g_dev = nullptr; // their device addresses (coherent memory)
+    // svgd_step_host_model on a small shard (<= XMIRROR_MAX bytes): the update
+    // epilogue also stores X_{t+1} into h_x (xmirror; xh_valid while X has not
+    // changed otherwise since), and a single rank's record prep reads G_t
+    // straight from h_g (ghost, ghost_step for the step that does) -- no D2H /
+    // H2D copy-engine round trips and cross-queue waits on the host
+    // gradient's path (cfg2: phi waited ~70 us for G behind them)
+    bool xmirror = false, xh_valid = false, ghost = false, ghost_step = false;
     unsigned long long *h_cnt = nullptr;
     double *h_scal = nullptr;
     hipEvent_t ev_x = nullptr, ev_cnt = nullptr, ev_scal = nullptr, ev_fin = nullptr;
@@ -1163,6 +1173,7 @@ int check_results(svgd_ctx *c)
 // G shard -> device on the copy stream (ready at ev_g) ...
 int upload_g_begin(svgd_ctx *c, const double *G_shard)
 {
+    c->ghost_step = false;
     const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
     if (!G_shard) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null log-gradient buffer.");
     if (c->nrows > 0) {
@@ -1183,6 +1194,7 @@ int upload_g_begin(svgd_ctx *c, const double *G_shard)
 // compute stream once it needs G.
 int upload_g_finish(svgd_ctx *c)
 {
+    if (c->ghost_step) return SVGD_OK; // one rank, G read from h_g by the record prep
     if (c->gcomm) {
         // the issue-order invariant (svgd_ctx): with a median pending, every
         // comm call of scale_begin precedes this gcomm call on every rank
@@ -1210,6 +1222,9 @@ int upload_g(svgd_ctx *c, const double *G_shard)
     CHK(upload_g_begin(c, G_shard));
     return upload_g_finish(c);
 }
+
+// G_t as the phi chain reads it (all n rows)
+const double *gin(const svgd_ctx *c) { return c->ghost_step ? c->h_g_dev : c->G; }
 
 bool matrix_scale(const svgd_ctx *c)
 {
@@ -1268,16 +1283,16 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         if (*c->h_err == 1 && !c->rowpath)
             return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] The kernel scale matrix is not finite.");
         if (c->rowpath)
-            HIPCHK(c, launch_prep_rec_mat(c->xc, c->G, c->sc_M, c->sc_L, c->sc_sgn, c->n, c->np,
+            HIPCHK(c, launch_prep_rec_mat(c->xc, gin(c), c->sc_M, c->sc_L, c->sc_sgn, c->n, c->np,
                                           c->dim, c->KP, c->RS, c->rec, c->wv, c->stream));
         else
-            HIPCHK(c, launch_prep_v_mat(c->xc, c->G, c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
+            HIPCHK(c, launch_prep_v_mat(c->xc, gin(c), c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
                                         c->VW, c->zc, c->V, c->cvec, c->wv, c->stream));
     } else if (c->rowpath)
-        HIPCHK(c, launch_prep_rec(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->RS,
+        HIPCHK(c, launch_prep_rec(c->xc, gin(c), c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->RS,
                                   c->rec, c->stream));
     else
-        HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
+        HIPCHK(c, launch_prep_v(c->xc, gin(c), c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
                                 c->V, c->cvec, c->stream));
     // F32: the streamed kernel's operand-ordered column copies (k_swz_f32), or
     // the row-major fp32 copies of the generic tile kernel
@@ -1301,7 +1316,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     hipEvent_t k1 = k0 ? take_ev(c) : nullptr;
     if (sym) {
         c->mark = c->phi_end = nullptr;
-        SymArgs sa{c->dim,    c->xc,        c->KP,          c->G,        c->nrm,       c->scal,
+        SymArgs sa{c->dim,    c->xc,        c->KP,          gin(c),        c->nrm,       c->scal,
                    c->nmax,   c->n,         c->sym_nb,      c->sym_units, c->srec,     c->symok,
                    c->rowpart, c->sym_rslots, c->colpart,   c->sym_grid, c->row0,      c->nrows,
                    1.0 / (double)c->n, c->phi};
@@ -1321,14 +1336,15 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         o2.m += h * d;
         o2.v += h * d;
         if (o2.bak) o2.bak += h * d;
-        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, h, c->n, c->S2, c->part, c->ldp2,
+        if (o2.xh) o2.xh += h * d;
+        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, h, c->n, c->S2, c->part, h,
                                   1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, opt, c->stream, k1,
                                   c->phi_kind));
         HIPCHK(c, hipEventRecord(c->ev_xhalf, c->stream));
         hipEvent_t k2 = diag_begin(c, c->stream);
         hipEvent_t k3 = k2 ? take_ev(c) : nullptr;
-        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0 + h, c->nrows - h, c->n, c->S2,
-                                  c->part, c->ldp2, 1.0 / (double)c->n, nullptr, nullptr, c->nmax,
+        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0 + h, c->nrows - h, c->n, c->S2b,
+                                  c->part, c->nrows - h, 1.0 / (double)c->n, nullptr, nullptr, c->nmax,
                                   c->phi + h * d, &o2, c->stream, k3, c->phi_kind));
         if (k2) c->ev_diag.push_back({k2, k3, DG_PHI_KERNEL, true});
     } else if (c->rowpath)
@@ -1413,7 +1429,9 @@ int opt_args(svgd_ctx *c, OptArgs *o)
                  c->b2, c->eps, c1, c2, c->bounded ? c->lower : nullptr,
                  c->bounded ? c->upper : nullptr,
                  // X_t, m_t, v_t of this rank's rows for a redo if the device plan failed
-                 c->spec_step ? c->bak : nullptr};
+                 c->spec_step ? c->bak : nullptr,
+                 // the next host gradient's X_{t+1}
+                 c->in_host_step && c->xmirror ? c->h_x_dev : nullptr};
     return SVGD_OK;
 }
 
@@ -1428,11 +1446,13 @@ int run_phi_opt(svgd_ctx *c)
     CHK(opt_args(c, &o));
     const bool fused = c->rowpath || phi_streamed(c);
     c->phi_end = nullptr;
+    c->xh_valid = false;
     CHK(run_phi(c, fused ? &o : nullptr));
     if (!fused) {
         HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
         c->phi_end = nullptr;
     }
+    c->xh_valid = o.xh != nullptr;
     // this rank's rows of X_{t+1} are final here: the next step's X_t copy
     // down (host gradient) need not wait for the X all-gather (P > 1)
     if (c->phi_end) {
@@ -1705,20 +1725,30 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         c->S = (int)S;
         c->RS = phi_rec_stride(dim);
         c->ldp = std::max<int64_t>(1, c->nrows);
-        // row halves (svgd_step_host_model at P > 1, split_rows policy below):
-        // the first half's rows get their X_{t+1} while the second half's phi
-        // still runs; each half's launch takes twice the column splits
-        c->split_h = (c->nrows / 2) / rows_wg * rows_wg;
+        // two row parts (svgd_step_host_model at P > 1, split_rows policy
+        // below): the first part's rows get their X_{t+1} while the second
+        // part's phi still runs.  The first part is the larger (SVGD_PHI_SPLIT_FRAC
+        // percent, default 62): its gradient overlaps the second part's phi,
+        // and the second part's gradient -- the one left exposed -- must fit
+        // in the next step's median phase.  Each launch takes its own splits.
+        int frac = 62;
+        if (const char *e = std::getenv("SVGD_PHI_SPLIT_FRAC")) frac = std::min(90, std::max(10, std::atoi(e)));
+        c->split_h = (c->nrows * frac / 100) / rows_wg * rows_wg;
+        if (c->split_h >= c->nrows) c->split_h = 0;
+        auto splits = [&](int64_t rows) {
+            const int64_t ib = std::max<int64_t>(1, (rows + rows_wg - 1) / rows_wg);
+            const int64_t s = std::max<int64_t>(1, (resident + ib - 1) / ib) * split_mult;
+            return (int)std::min<int64_t>(s, std::max<int64_t>(1, n / 256));
+        };
         if (c->split_h > 0) {
-            const int64_t ib2 = std::max<int64_t>(1, (c->nrows - c->split_h + rows_wg - 1) / rows_wg);
-            int64_t S2 = std::max<int64_t>(1, (resident + ib2 - 1) / ib2) * split_mult;
-            c->S2 = (int)std::min<int64_t>(S2, std::max<int64_t>(1, n / 256));
-            c->ldp2 = c->nrows - c->split_h;
+            c->S2 = splits(c->split_h);
+            c->S2b = splits(c->nrows - c->split_h);
         }
         CHK(dalloc(c, &c->rec, c->np * c->RS));
         CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
         CHK(dalloc(c, &c->nmax, 1));
-        CHK(dalloc(c, &c->part, std::max<int64_t>((int64_t)c->S * c->ldp, (int64_t)c->S2 * c->ldp2) * (dim + 1)));
+        CHK(dalloc(c, &c->part, std::max({(int64_t)c->S * c->ldp, (int64_t)c->S2 * c->split_h,
+                                          (int64_t)c->S2b * (c->nrows - c->split_h)}) * (dim + 1)));
         // symmetric phi pass: one rank (a pair feeds two particles, which
         // ranks would have to exchange), isotropic scales, d <= 8
         bool want_sym = c->world == 1 && phi_sym_supported(dim);
@@ -1784,8 +1814,18 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
     CHK(dalloc(c, &c->ccount, 1));
     const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
-    HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocDefault));
+    // coherent: the device writes h_x (mirror) and reads h_g (ghost) uncached
+    HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocCoherent));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocCoherent));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_x_dev, c->h_x, 0));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_g_dev, c->h_g, 0));
+    {
+        const bool small = hb <= XMIRROR_MAX;
+        c->xmirror = small;
+        c->ghost = small && c->plan_world == 1;
+        if (const char *e = std::getenv("SVGD_X_MIRROR")) c->xmirror = std::atoi(e) != 0;
+        if (const char *e = std::getenv("SVGD_G_HOSTREAD")) c->ghost = c->plan_world == 1 && std::atoi(e) != 0;
+    }
     HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, (CNT_LEN + 3) * sizeof(unsigned long long),
                             hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_scal, 2 * sizeof(double), hipHostMallocDefault));
@@ -2137,6 +2177,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->have_particles = true;
     c->xhalf_ready = false;
+    c->xh_valid = false;
     c->trk_n = c->trk_nerr = 0; // new particles: the median history restarts
     return SVGD_OK;
 }
@@ -2283,20 +2324,31 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
         *r1 = rows * (q + 1) / nch;
     };
     HIPCHK(c, hipEventSynchronize(c->ev_g)); // the previous step's upload has left h_g
+    // the event chunk q's X_t waits for: its copy's, or -- when the last
+    // update stored X_t into h_x (xh_valid) -- that update's own end
+    hipEvent_t xwait[XCH];
     if (rows > 0) {
         // X_t is final once the previous step's update (and all-gather) ran
         hipEvent_t xev = c->ev_xready_use ? c->ev_xready_use : c->ev_xready;
-        HIPCHK(c, hipStreamWaitEvent(c->cstream, hsplit > 0 ? c->ev_xhalf : xev, 0));
-        for (int q = 0; q < nch; ++q) {
-            int64_t r0, r1;
-            chunk(q, &r0, &r1);
-            if (hsplit > 0 && q == nh) HIPCHK(c, hipStreamWaitEvent(c->cstream, xev, 0));
-            HIPCHK(c, hipMemcpyAsync(c->h_x + r0 * d, c->X + (size_t)(c->row0 + r0) * d,
-                                     sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyDeviceToHost,
-                                     c->cstream));
-            HIPCHK(c, hipEventRecord(c->ev_xch[q], c->cstream));
+        if (c->xh_valid) {
+            for (int q = 0; q < nch; ++q) xwait[q] = hsplit > 0 && q < nh ? c->ev_xhalf : xev;
+        } else {
+            HIPCHK(c, hipStreamWaitEvent(c->cstream, hsplit > 0 ? c->ev_xhalf : xev, 0));
+            for (int q = 0; q < nch; ++q) {
+                int64_t r0, r1;
+                chunk(q, &r0, &r1);
+                if (hsplit > 0 && q == nh) HIPCHK(c, hipStreamWaitEvent(c->cstream, xev, 0));
+                HIPCHK(c, hipMemcpyAsync(c->h_x + r0 * d, c->X + (size_t)(c->row0 + r0) * d,
+                                         sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyDeviceToHost,
+                                         c->cstream));
+                HIPCHK(c, hipEventRecord(c->ev_xch[q], c->cstream));
+                xwait[q] = c->ev_xch[q];
+            }
         }
     }
+    // one rank and a small G: the record prep reads h_g (no G copies)
+    const bool ghost = c->ghost;
+    c->ghost_step = ghost;
     // the gradient thread: each chunk waits for its X_t copy, evaluates the
     // model and queues its G copy on the copy stream (the calling thread only
     // touches `stream` until it waits for this job)
@@ -2306,12 +2358,14 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
         return std::chrono::duration<double, std::milli>(t1 - t0).count();
     };
     const clk::time_point t_post = clk::now();
-    c->worker->post([c, m, d, rows, nch, chunk, ms_since, t_post](std::string &msg) -> int {
+    std::array<hipEvent_t, XCH> xw;
+    std::copy(xwait, xwait + (rows > 0 ? nch : 0), xw.begin());
+    c->worker->post([c, m, d, rows, nch, chunk, ms_since, t_post, xw, ghost](std::string &msg) -> int {
         for (int q = 0; q < nch && rows > 0; ++q) {
             int64_t r0, r1;
             chunk(q, &r0, &r1);
             const clk::time_point tw = clk::now();
-            hipError_t e = hipEventSynchronize(c->ev_xch[q]);
+            hipError_t e = hipEventSynchronize(xw[q]);
             if (e != hipSuccess) {
                 msg = std::string("SVGDCpp: [HIP Error] X_t chunk copy: ") + hipGetErrorString(e);
                 return SVGD_ERR_HIP;
@@ -2324,6 +2378,7 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
             }
             c->h_xwait_ms += ms_since(tw, tg);
             c->h_grad_ms += ms_since(tg, clk::now());
+            if (ghost) continue;
             e = hipMemcpyAsync(c->G + (size_t)(c->row0 + r0) * d, c->h_g + r0 * d,
                                sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyHostToDevice,
                                c->cstream);
@@ -2331,6 +2386,11 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
                 msg = std::string("SVGDCpp: [HIP Error] G chunk copy: ") + hipGetErrorString(e);
                 return SVGD_ERR_HIP;
             }
+        }
+        if (ghost) { // h_g complete before the prep that reads it is queued
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            c->h_job_ms += ms_since(t_post, clk::now());
+            return SVGD_OK;
         }
         hipError_t e = hipEventRecord(c->ev_g, c->cstream);
         // the gradient thread waits for its copies to land (the device is
@@ -2376,6 +2436,7 @@ int svgd_step(svgd_ctx *c, const double *G_shard)
         return fail(c, SVGD_ERR_ARG,
                     "[Argument Error] Null log-gradient buffer and no device model set.");
     CHK(svgd_begin_step(c, nullptr));
+    c->ghost_step = false;
     HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
                                 c->dm_mu, c->dm_prec, c->G + (size_t)c->row0 * c->dim, c->stream));
     c->mark = nullptr; // (the gradient kernel runs after the median's end event)
@@ -2415,6 +2476,7 @@ int svgd_device_logp_grad(svgd_ctx *c, double *G_shard_out)
     CHK(resolve_pending(c));
     if (c->dm_k == 0) return fail(c, SVGD_ERR_UNSET, "[Unset Error] No device model set.");
     if (!G_shard_out) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null output buffer.");
+    c->ghost_step = false;
     HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
                                 c->dm_mu, c->dm_prec, c->phi, c->stream));
     HIPCHK(c, hipMemcpyAsync(G_shard_out, c->phi, sizeof(double) * (size_t)c->nrows * c->dim,

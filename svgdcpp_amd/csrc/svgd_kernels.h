@@ -86,6 +86,7 @@ struct OptArgs {
     double lr, b1, b2, eps, c1, c2;
     const double *lower, *upper; // clamp bounds (both or neither)
     double *bak;                 // X_t, m_t, v_t saved here when set (speculative step)
+    double *xh = nullptr;        // X_{t+1} also stored here when set (pinned host mirror)
 };
 hipError_t launch_opt_update(const OptArgs &o, const double *g, hipStream_t stream);
 // mode 0: collect keys in [st->lo_key, st->hi_key) into per-block regions and count

@@ -581,6 +581,7 @@ __device__ __forceinline__ void opt_elem(const OptArgs &o, int64_t e, double ge)
         x = x > o.lower[k] ? x : o.lower[k];
     }
     X[e] = x;
+    if (o.xh) o.xh[e] = x; // the host gradient's copy of X_{t+1} (no D2H copy)
 }
 
 __global__ void k_opt_update(OptArgs o, const double *__restrict__ g)

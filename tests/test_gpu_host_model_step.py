@@ -68,13 +68,16 @@ def test_pipelined_step_rejects_bad_model():
     c.close()
 
 
-@pytest.mark.parametrize("n,d,k", [(9000, 8, 4), (13001, 5, 2)])
-def test_row_halves_step_matches_oracle(oracle, monkeypatch, n, d, k):
-    """phi in two row halves (SVGD_PHI_SPLIT=1; by default a rank of several
-    with > 2048 rows per gradient thread): the first half's X_{t+1} goes to
-    the host gradient while the second half's phi runs.  Each half sums its
-    own column splits, so the trajectory matches the whole-rows one to fp64
-    rounding, and every step matches the oracle's."""
+@pytest.mark.parametrize("n,d,k,frac", [(9000, 8, 4, "62"), (13001, 5, 2, "62"), (9000, 8, 4, "50"),
+                                        (13001, 5, 2, "80")])
+def test_row_halves_step_matches_oracle(oracle, monkeypatch, n, d, k, frac):
+    """phi in two row parts (SVGD_PHI_SPLIT=1; by default a rank of several
+    with > 2048 rows per gradient thread; the first part SVGD_PHI_SPLIT_FRAC
+    percent of the rows): the first part's X_{t+1} goes to the host gradient
+    while the second part's phi runs.  Each part sums its own column splits,
+    so the trajectory matches the whole-rows one to fp64 rounding, and every
+    step matches the oracle's."""
+    monkeypatch.setenv("SVGD_PHI_SPLIT_FRAC", frac)
     X = oracle.splitmix((n, d), 3.0, 31 + d)
     mus = oracle.splitmix((k, d), 3.0, 32)
     covs = np.stack([np.eye(d) * (1.0 + 0.25 * c) for c in range(k)])
@@ -99,3 +102,33 @@ def test_row_halves_step_matches_oracle(oracle, monkeypatch, n, d, k):
     a.diagnostics()
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("n,d,k,split", [(3000, 8, 4, "0"), (9000, 3, 2, "1"), (700, 2, 1, "0"),
+                                         (2000, 20, 1, "0")])
+def test_host_mirror_and_g_hostread_bit_exact(oracle, monkeypatch, n, d, k, split):
+    """Small shards (<= 1 MiB): the update epilogue stores X_{t+1} into the
+    pinned host buffer the gradient reads (SVGD_X_MIRROR) and one rank's
+    record prep reads G_t from pinned host memory (SVGD_G_HOSTREAD), instead
+    of the copy-engine round trips.  Same kernels, same values: the
+    trajectory is bit-identical to the copying path, row split included, and
+    a set_particles in between invalidates the mirror."""
+    X = oracle.splitmix((n, d), 3.0, 40 + n + d)
+    mus = oracle.splitmix((k, d), 2.0, 41)
+    model = S.GaussianSum(list(mus), [np.eye(d) * (1.0 + 0.25 * c) for c in range(k)])
+    monkeypatch.setenv("SVGD_PHI_SPLIT", split)
+    ctxs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SVGD_X_MIRROR", v)
+        monkeypatch.setenv("SVGD_G_HOSTREAD", v)
+        ctxs[v] = _ctx(X)
+    X2 = oracle.splitmix((n, d), 2.0, 42 + n)
+    for step in range(6):
+        if step == 3:
+            for c in ctxs.values():
+                c.set_particles(X2)
+        for c in ctxs.values():
+            c.step_with_model(model)
+        assert np.array_equal(ctxs["1"].get_particles(), ctxs["0"].get_particles()), step
+    for c in ctxs.values():
+        c.close()
