@@ -1727,11 +1727,12 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         c->ldp = std::max<int64_t>(1, c->nrows);
         // two row parts (svgd_step_host_model at P > 1, split_rows policy
         // below): the first part's rows get their X_{t+1} while the second
-        // part's phi still runs.  The first part is the larger (SVGD_PHI_SPLIT_FRAC
-        // percent, default 62): its gradient overlaps the second part's phi,
-        // and the second part's gradient -- the one left exposed -- must fit
-        // in the next step's median phase.  Each launch takes its own splits.
-        int frac = 62;
+        // part's phi still runs; the second part's gradient has to fit in the
+        // next step's median phase.  Each launch takes its own column splits.
+        // First part SVGD_PHI_SPLIT_FRAC percent of the rows, default 50
+        // (cfg3 8-rank share, profiles/r04_sim_world.jsonl: 50 % 0.632 ms,
+        // 62 % 0.783, 72 % 0.765 -- uneven parts made phi itself 40 % slower)
+        int frac = 50;
         if (const char *e = std::getenv("SVGD_PHI_SPLIT_FRAC")) frac = std::min(90, std::max(10, std::atoi(e)));
         c->split_h = (c->nrows * frac / 100) / rows_wg * rows_wg;
         if (c->split_h >= c->nrows) c->split_h = 0;

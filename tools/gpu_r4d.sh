@@ -44,7 +44,7 @@ export SVGD_PHI_SYM=1
 STEPS=20 WARMUP=3 TAG=_sym bash tools/profile.sh > /dev/null || exit 1
 python3 tools/ktimed.py gpurun_out/prof_sym/run_kernel_trace.csv 3 > $O/rocprof_sym_kernel_timed.txt
 head -6 $O/rocprof_sym_kernel_timed.txt
-TAG=_sym BENCH_ARGS="--repeats 1 --no-diag" bash tools/pmc_sq.sh "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE" || exit 1
+TAG=_sym BENCH_ARGS="--repeats 1 --no-diag" bash tools/pmc_sq.sh "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE" || exit 1
 python3 tools/pmc_summary.py $O/pmc_sq_sym.csv gpurun_out/pmc_sq_sym/p1 > $O/pmc_sq_sym.txt
 python3 tools/pmc_summary.py $O/pmc_lds_sym.csv gpurun_out/pmc_sq_sym/p2 > $O/pmc_lds_sym.txt
 head -3 $O/pmc_sq_sym.txt
