@@ -750,7 +750,8 @@ class Context:
         device median via begin/finish).  hessian=True: the Hessian kernel
         scale, with this shard's sum of -hess log p supplied from `model`.
         A built-in GaussianSum runs through svgd_step_host_model (the X_t copy,
-        the gradient and the G upload pipelined in row chunks, all in C);
+        the gradient and the G upload pipelined in row chunks, all in C; the
+        host buffers x_host / g_host are then not guaranteed to hold X_t);
         pipelined=False takes the split begin / gradient / finish calls."""
         if pipelined and not hessian and _builtin_grad(model):
             self.check(self.lib.svgd_step_host_model(self.h, model._handle))
@@ -933,7 +934,10 @@ class SVGD:
                     c.g_host[:nr] = self.model_.log_model_grad(c.x_host[:nr])
                 c.check(c.lib.svgd_finish_step(c.h, c.g_host_ptr))
             else:
-                c.step_with_model(self.model_, hessian=hess)
+                # logging re-evaluates K at X_t from the host buffers, which
+                # only the split begin / finish calls fill (the pipelined step
+                # may take X_t from its own mirror)
+                c.step_with_model(self.model_, hessian=hess, pipelined=not self.log_)
             if self.log_:
                 self._log_device_step(len(self.logs_))
         X = c.get_particles()

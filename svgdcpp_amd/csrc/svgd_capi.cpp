@@ -257,14 +257,16 @@ struct svgd_ctx {
 
     // pinned host
     double *h_x = nullptr, *h_g = nullptr;
-    double *h_x_dev = nullptr, *h_g_dev = nullptr; // their device addresses (coherent memory)
+    double *h_g_dev = nullptr; // its device address (coherent memory)
     // svgd_step_host_model on a small shard (<= XMIRROR_MAX bytes): the update
-    // epilogue also stores X_{t+1} into h_x (xmirror; xh_valid while X has not
-    // changed otherwise since), and a single rank's record prep reads G_t
+    // epilogue also stores X_{t+1} into h_xm (xmirror; xh_valid while X has not
+    // changed otherwise since; a buffer of its own: h_x, the caller's, is
+    // never written by the device behind its back), and a single rank's record prep reads G_t
     // straight from h_g (ghost, ghost_step for the step that does) -- no D2H /
     // H2D copy-engine round trips and cross-queue waits on the host
     // gradient's path (cfg2: phi waited ~70 us for G behind them)
     bool xmirror = false, xh_valid = false, ghost = false, ghost_step = false;
+    double *h_xm = nullptr, *h_xm_dev = nullptr;
     unsigned long long *h_cnt = nullptr;
     double *h_scal = nullptr;
     hipEvent_t ev_x = nullptr, ev_cnt = nullptr, ev_scal = nullptr, ev_fin = nullptr;
@@ -1431,7 +1433,7 @@ int opt_args(svgd_ctx *c, OptArgs *o)
                  // X_t, m_t, v_t of this rank's rows for a redo if the device plan failed
                  c->spec_step ? c->bak : nullptr,
                  // the next host gradient's X_{t+1}
-                 c->in_host_step && c->xmirror ? c->h_x_dev : nullptr};
+                 c->in_host_step && c->xmirror ? c->h_xm_dev : nullptr};
     return SVGD_OK;
 }
 
@@ -1816,9 +1818,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     CHK(dalloc(c, &c->ccount, 1));
     const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
     // coherent: the device writes h_x (mirror) and reads h_g (ghost) uncached
-    HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocCoherent));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
     HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocCoherent));
-    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_x_dev, c->h_x, 0));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_xm, hb, hipHostMallocCoherent));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_xm_dev, c->h_xm, 0));
     HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_g_dev, c->h_g, 0));
     {
         const bool small = hb <= XMIRROR_MAX;
@@ -1992,7 +1995,7 @@ int svgd_destroy(svgd_ctx *c)
                      c->bpart,       c->gseg, c->symok};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
-    void *hbufs[] = {c->h_x, c->h_g, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk};
+    void *hbufs[] = {c->h_x, c->h_g, c->h_xm, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk};
     for (void *p : hbufs)
         if (p) (void)hipHostFree(p);
     for (auto *v : {&c->ev_phi, &c->ev_med, &c->ev_pool})
@@ -2350,6 +2353,8 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     // one rank and a small G: the record prep reads h_g (no G copies)
     const bool ghost = c->ghost;
     c->ghost_step = ghost;
+    // the gradient's input: X_t from the last update's mirror, or its copy
+    const double *hx = c->xh_valid ? c->h_xm : c->h_x;
     // the gradient thread: each chunk waits for its X_t copy, evaluates the
     // model and queues its G copy on the copy stream (the calling thread only
     // touches `stream` until it waits for this job)
@@ -2361,7 +2366,7 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     const clk::time_point t_post = clk::now();
     std::array<hipEvent_t, XCH> xw;
     std::copy(xwait, xwait + (rows > 0 ? nch : 0), xw.begin());
-    c->worker->post([c, m, d, rows, nch, chunk, ms_since, t_post, xw, ghost](std::string &msg) -> int {
+    c->worker->post([c, m, d, rows, nch, chunk, ms_since, t_post, xw, ghost, hx](std::string &msg) -> int {
         for (int q = 0; q < nch && rows > 0; ++q) {
             int64_t r0, r1;
             chunk(q, &r0, &r1);
@@ -2372,7 +2377,7 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
                 return SVGD_ERR_HIP;
             }
             const clk::time_point tg = clk::now();
-            if (model_logp_grad_threads(m, c->h_x + r0 * d, r1 - r0, c->h_g + r0 * d,
+            if (model_logp_grad_threads(m, hx + r0 * d, r1 - r0, c->h_g + r0 * d,
                                         c->host_threads)) {
                 msg = "SVGDCpp: [Argument Error] Host model evaluation failed.";
                 return SVGD_ERR_ARG;
