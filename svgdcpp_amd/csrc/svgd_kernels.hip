@@ -619,8 +619,16 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
                                                    SinkCollect sc, SinkHist sh, SinkDebug sd)
 {
     typedef typename Acc4<T>::type A4;
-    __shared__ T sXI[KP * LDP];
-    __shared__ T sXJ[KP * LDP];
+    // fp64: the X tiles j-major with row stride LDK (an odd multiple of 4
+    // doubles: the MFMA operand reads of 16 rows x 4 columns hit distinct
+    // banks, the fill is a straight 16-byte copy) -- 70 KB instead of 80 KB
+    // of tiles, so two work-groups fit a CU (round 3: one, 1 wave/SIMD);
+    // fp32 keeps the k-major tiles (its kslot order would conflict j-major)
+    constexpr bool JM = sizeof(T) == 8 && (KP / 4) % 2 == 0;
+    constexpr int LDK = PhiTile<T, KP>::LDK;
+    constexpr int XT = JM ? TB * LDK : KP * LDP;
+    __shared__ __attribute__((aligned(16))) T sXI[XT];
+    __shared__ __attribute__((aligned(16))) T sXJ[XT];
     __shared__ T sNI[TB], sNJ[TB];
     __shared__ uint32_t sHist[(MODE == 1) ? 2 * RADIX : 1];
     __shared__ uint32_t sCnt;
@@ -685,15 +693,29 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     // the next tile's column block is loaded into registers while the current
     // tile is computed, then stored to LDS between the two barriers
     constexpr int PU = TB * KP / 256;
-    T preX[PU];
+    constexpr int EP = 16 / (int)sizeof(T), PQ = JM ? PU / EP : 1; // 16-byte pieces
+    static_assert(!JM || PU % EP == 0, "tile pieces");
+    T preX[JM ? 1 : PU];
+    uint4 preQ[PQ];
     T preN = (T)0;
     auto fetch = [&](int64_t Jn) {
+        if constexpr (JM) {
 #pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
-            preX[u] = xc[(Jn * TB + jl) * KP + k];
+            for (int u = 0; u < PQ; ++u)
+                preQ[u] = reinterpret_cast<const uint4 *>(xc + Jn * TB * KP)[tid + 256 * u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
+                preX[u] = xc[(Jn * TB + jl) * KP + k];
+            }
         }
         if (tid < TB) preN = nrm[Jn * TB + tid];
+    };
+    // piece e of a 64-particle block (row jl = e / (KP/EP)) into a j-major tile
+    auto put = [&](T *dst, int e, uint4 v) {
+        const int jl = e / (KP / EP), q = e - jl * (KP / EP);
+        *reinterpret_cast<uint4 *>(dst + jl * LDK + q * EP) = v;
     };
     int64_t curI = -1, I = 0, J = 0;
     if (tb < te) {
@@ -703,16 +725,26 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     for (int64_t t = tb; t < te; ++t) {
         __syncthreads();
         if (I != curI) {
-            for (int e = tid; e < TB * KP; e += 256) {
-                const int il = e / KP, k = e - il * KP;
-                sXI[k * LDP + il] = xc[(I * TB + il) * KP + k];
+            if constexpr (JM) {
+                for (int e = tid; e < TB * KP / EP; e += 256)
+                    put(sXI, e, reinterpret_cast<const uint4 *>(xc + I * TB * KP)[e]);
+            } else {
+                for (int e = tid; e < TB * KP; e += 256) {
+                    const int il = e / KP, k = e - il * KP;
+                    sXI[k * LDP + il] = xc[(I * TB + il) * KP + k];
+                }
             }
             if (tid < TB) sNI[tid] = nrm[I * TB + tid];
         }
+        if constexpr (JM) {
 #pragma unroll
-        for (int u = 0; u < PU; ++u) {
-            const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
-            sXJ[k * LDP + jl] = preX[u];
+            for (int u = 0; u < PQ; ++u) put(sXJ, tid + 256 * u, preQ[u]);
+        } else {
+#pragma unroll
+            for (int u = 0; u < PU; ++u) {
+                const int e = tid + 256 * u, jl = e / KP, k = e - jl * KP;
+                sXJ[k * LDP + jl] = preX[u];
+            }
         }
         if (tid < TB) sNJ[tid] = preN;
         __syncthreads();
@@ -726,7 +758,9 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
         const bool full = Ic != Jc && (Ic + 1) * TB <= n && (Jc + 1) * TB <= n;
         T bI[KP / 4];
 #pragma unroll
-        for (int kk = 0; kk < KP / 4; ++kk) bI[kk] = sXI[kslot<T, KP>(kk, hi) * LDP + w * 16 + lo];
+        for (int kk = 0; kk < KP / 4; ++kk)
+            bI[kk] = JM ? sXI[(w * 16 + lo) * LDK + kslot<T, KP>(kk, hi)]
+                        : sXI[kslot<T, KP>(kk, hi) * LDP + w * 16 + lo];
         const int il = w * 16 + lo;
         const int64_t i = Ic * TB + il;
         const T ni = sNI[il];
@@ -736,7 +770,9 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
             A4 dot = {0, 0, 0, 0};
 #pragma unroll
             for (int kk = 0; kk < KP / 4; ++kk)
-                dot = mfma16(sXJ[kslot<T, KP>(kk, hi) * LDP + js * 16 + lo], bI[kk], dot);
+                dot = mfma16(JM ? sXJ[(js * 16 + lo) * LDK + kslot<T, KP>(kk, hi)]
+                                : sXJ[kslot<T, KP>(kk, hi) * LDP + js * 16 + lo],
+                             bI[kk], dot);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int jl = js * 16 + acc_row<T>(hi, r);
