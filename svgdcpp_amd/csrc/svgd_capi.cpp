@@ -179,6 +179,7 @@ struct svgd_ctx {
     // SVGD_F32: fp32 copies feeding the tile kernels
     float *xcf = nullptr, *nrmf = nullptr, *cvf = nullptr, *Vf = nullptr, *zcf = nullptr;
     float *XS = nullptr, *VS = nullptr; // operand-ordered column copies (k_phi_f32s)
+    uint32_t *B3 = nullptr;             // operand-ordered bf16 parts (k_phi_b3), replaces XS / VS
 
     // row-stream path (d <= ROWS_MAX_D)
     bool rowpath = false;
@@ -1236,7 +1237,7 @@ bool matrix_scale(const svgd_ctx *c)
 // F32 with the streamed tile phi (operand-ordered copies allocated, 16-aligned rows)
 bool phi_streamed(const svgd_ctx *c)
 {
-    return c->dtype == SVGD_F32 && c->XS && c->row0 % 16 == 0;
+    return c->dtype == SVGD_F32 && (c->XS || c->B3) && c->row0 % 16 == 0;
 }
 
 int run_phi(svgd_ctx *c, const OptArgs *opt)
@@ -1301,7 +1302,10 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     const bool phis = phi_streamed(c);
     const int64_t ntl = (c->n + TBJ_COLS - 1) / TBJ_COLS;
     if (c->dtype == SVGD_F32) {
-        if (phis)
+        if (phis && c->B3)
+            HIPCHK(c, launch_swz_b3(mat ? c->zc : c->xc, c->KP, c->V, c->VW, c->cvec, ntl, c->B3,
+                                    c->stream));
+        else if (phis)
             HIPCHK(c, launch_swz_f32(mat ? c->zc : c->xc, c->KP, c->V, c->VW, c->cvec, ntl, c->XS,
                                      c->VS, c->stream));
         else
@@ -1355,7 +1359,10 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
                                   mat ? c->sc_sgn : nullptr, mat ? nullptr : c->nmax, c->phi, opt,
                                   c->stream, k1, mat ? 0 : c->phi_kind));
     else if (phis)
-        HIPCHK(c, launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
+        HIPCHK(c, c->B3 ? launch_phi_b3(c->KP, c->NCB, c->B3, c->cvf, c->scal, c->row0, c->nrows, ntl,
+                                        c->dim, 1.0 / (double)c->n, mat ? c->wv : nullptr, c->xc, c->KP,
+                                        c->phi, opt, c->stream)
+                        : launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
                                   c->row0, c->nrows, ntl, c->dim, 1.0 / (double)c->n,
                                   mat ? c->wv : nullptr, c->xc, c->KP, c->phi, opt, c->stream));
     else if (c->dtype == SVGD_F32)
@@ -1787,8 +1794,14 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
         if (f32 && phi_f32s_supported(c->KP, c->NCB) && !std::getenv("SVGD_PHI_TILE_GENERIC")) {
             // np is a multiple of 2 TBJ_COLS: ceil(n / TBJ_COLS) tiles fit
-            CHK(dalloc(c, &c->XS, c->np * c->KP));
-            CHK(dalloc(c, &c->VS, c->np * 16 * (c->NCB + 1)));
+            // SVGD_PHI_B3=1: the bf16 matrix-core form (k_phi_b3) where it applies
+            const char *eb = std::getenv("SVGD_PHI_B3");
+            if (eb && std::atoi(eb) != 0 && phi_b3_supported(c->KP, c->NCB)) {
+                CHK(dalloc(c, &c->B3, (c->np / TBJ_COLS) * phi_b3_tile_words(c->KP, c->NCB)));
+            } else {
+                CHK(dalloc(c, &c->XS, c->np * c->KP));
+                CHK(dalloc(c, &c->VS, c->np * 16 * (c->NCB + 1)));
+            }
         }
     }
     CHK(dalloc(c, &c->phi, std::max<int64_t>(1, c->nrows) * dim));
@@ -1988,6 +2001,7 @@ int svgd_destroy(svgd_ctx *c)
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf, c->XS, c->VS};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
+    if (c->B3) (void)hipFree(c->B3);
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
@@ -2642,6 +2656,8 @@ int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
             std::snprintf(s, sizeof s, "k_phi_rows_s<%d, %d>", d, c->R);
         else
             std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 4, 4096, 1>", d, c->R);
+    } else if (c->dtype == SVGD_F32 && c->B3) {
+        std::snprintf(s, sizeof s, "k_phi_b3<%d, %d, 8>", c->KP, c->NCB);
     } else if (c->dtype == SVGD_F32 && c->XS) {
         std::snprintf(s, sizeof s, "k_phi_f32s<%d, %d>", c->KP, c->NCB);
     } else {

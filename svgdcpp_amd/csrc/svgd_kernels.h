@@ -277,6 +277,19 @@ hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm,
 hipError_t launch_swz_f32(const double *x, int KP, const double *V, int VW, const double *cvec,
                           int64_t ntiles, float *XS, float *VS, hipStream_t stream);
 bool phi_f32s_supported(int KP, int NCB);
+// F32 tile phi on the bf16 matrix cores (k_phi_b3: each fp32 operand as three
+// bf16 parts, six part products per fp32 product): per 32-column tile
+// phi_b3_tile_words(KP, NCB) dwords of operand-ordered parts made by
+// launch_swz_b3 from x (stride KP), V (stride VW = 16 NCB) and cvec.
+// KP = 32 or 64; row0 % 16 == 0.
+bool phi_b3_supported(int KP, int NCB);
+int64_t phi_b3_tile_words(int KP, int NCB);
+hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const double *cvec,
+                         int64_t ntiles, uint32_t *B3, hipStream_t stream);
+hipError_t launch_phi_b3(int KP, int NCB, const uint32_t *B3, const float *crow,
+                         const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles, int d,
+                         double inv_n, const double *wv, const double *xc, int xc_stride,
+                         double *phi, const OptArgs *opt, hipStream_t stream);
 hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, const float *xrow,
                            const float *crow, const double *a_ptr, int64_t row0, int64_t nrows,
                            int64_t ntiles, int d, double inv_n, const double *wv, const double *xc,

@@ -3040,6 +3040,220 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
 }
 
+// ------------------------- fp32 tile phi on the bf16 matrix cores (F32, B3) --
+//
+// The F32 path's arithmetic at the bf16 MFMA rate (16x the f32 MFMA's on
+// gfx950): every fp32 operand is split exactly into three bf16 parts,
+// x = h + m + l (8 + 8 + 8 significant bits), and each fp32 product a.b is
+// formed from the six part products that reach 2^-24 of it -- hh, hm, mh,
+// hl, lh, mm (the dropped ml, lm, ll are < 2^-23 |a b|): the Gram and the
+// P.V contraction keep fp32-level accuracy, both on v_mfma_f32_16x16x32_bf16
+// (products exact, fp32 accumulation).  Per 16 x 16 pair block: 6 KP/32
+// Gram MFMAs and (per 32 columns) 6 NCB P.V MFMAs of 16 cycles instead of
+// KP/4 + 4 NCB f32 MFMAs of 32.  P = 2^t by v_exp_f32 as k_phi_f32s; P's three
+// parts are formed in registers, P already being the P.V A operand in the
+// 16x16x32 lane map (lane l: row l%16, k = 8(l/16) + e).
+// Operand-ordered parts, once per step (k_swz_b3), per 32-column tile t, in
+// 1 KiB pieces of 64 lanes x 16 bytes:
+//   XB[t][js][db][part][lane][e] = part of x[32t + 16js + lane%16][32db + 8(lane/16) + e]
+//   VB[t][cb][part][lane][e]     = part of V[32t + 16(e/4) + 4(lane/16) + e%4][16cb + lane%16]
+//   CB[t][js][lane][r]           = c_j (fp32), j = 32t + 16js + 4(lane/16) + r
+// Rows (the Gram's B operand) come from XB of the row's own tile: the same
+// lane map.
+__device__ __forceinline__ uint32_t b3_split_pair(float &x0, float &x1)
+{
+    // bf16(x0) | bf16(x1) << 16 (round to nearest even), and the residuals
+    // x - bf16(x) back in x0, x1 (exact in fp32)
+    uint32_t w;
+    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(w) : "v"(x0), "v"(x1));
+    x0 -= __uint_as_float(w << 16);
+    x1 -= __uint_as_float(w & 0xffff0000u);
+    return w;
+}
+
+template <int KP>
+__global__ void k_swz_b3(const double *__restrict__ x, const double *__restrict__ V, int VW,
+                         const double *__restrict__ cvec, int64_t ntiles, uint32_t *__restrict__ B3)
+{
+    // one thread per (piece, lane) pair of elements: 4 dwords (8 bf16) of one
+    // part, the three parts of one (row, 8-k) slice formed together
+    constexpr int NDB = KP / 32;
+    const int NCB = VW / 16;
+    const int PT = 6 * NDB + 3 * NCB + 2; // pieces per tile
+    const int64_t nslices = ntiles * (2 * NDB + NCB) * 64; // (lane, slice) items of XB and VB
+    const int64_t ncb = ntiles * 2 * 64;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nslices + ncb;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        if (e < nslices) {
+            const int lane = (int)(e & 63);
+            int64_t r = e >> 6;
+            const int sl = (int)(r % (2 * NDB + NCB));
+            const int64_t t = r / (2 * NDB + NCB);
+            const int lo = lane & 15, hi = lane >> 4;
+            float v[8];
+            int piece0;
+            if (sl < 2 * NDB) { // XB slice (js, db)
+                const int js = sl / NDB, db = sl - js * NDB;
+                const int64_t j = t * 32 + 16 * js + lo;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) v[q] = (float)x[j * KP + 32 * db + 8 * hi + q];
+                piece0 = (js * NDB + db) * 3;
+            } else { // VB slice cb
+                const int cb = sl - 2 * NDB;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int64_t j = t * 32 + 16 * (q >> 2) + 4 * hi + (q & 3);
+                    v[q] = (float)V[j * VW + 16 * cb + lo];
+                }
+                piece0 = 6 * NDB + 3 * cb;
+            }
+            uint32_t *o = B3 + (t * PT + piece0) * 256 + lane * 4;
+#pragma unroll
+            for (int part = 0; part < 3; ++part)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[part * 256 + q] = b3_split_pair(v[2 * q], v[2 * q + 1]);
+        } else {
+            const int64_t f = e - nslices;
+            const int lane = (int)(f & 63);
+            const int64_t r = f >> 6;
+            const int js = (int)(r & 1);
+            const int64_t t = r >> 1;
+            float *o = reinterpret_cast<float *>(B3 + (t * PT + 6 * NDB + 3 * NCB + js) * 256) + lane * 4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = (float)cvec[t * 32 + 16 * js + 4 * (lane >> 4) + q];
+        }
+    }
+}
+
+typedef __bf16 b16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f4_t mfma_b3(uint4 a, uint4 b, f4_t c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b16x8_t, a),
+                                                   __builtin_bit_cast(b16x8_t, b), c, 0, 0, 0);
+}
+// a.b from the parts (smallest products first)
+__device__ __forceinline__ f4_t mfma_b3x6(const uint4 (&a)[3], const uint4 (&b)[3], f4_t c)
+{
+    c = mfma_b3(a[1], b[1], c); // mm
+    c = mfma_b3(a[0], b[2], c); // hl
+    c = mfma_b3(a[2], b[0], c); // lh
+    c = mfma_b3(a[0], b[1], c); // hm
+    c = mfma_b3(a[1], b[0], c); // mh
+    return mfma_b3(a[0], b[0], c); // hh
+}
+
+template <int KP, int NCB, int NW>
+__global__ __launch_bounds__(64 * NW) void k_phi_b3(
+    const uint32_t *__restrict__ B3, const float *__restrict__ crow, const double *__restrict__ a_ptr,
+    int64_t row0, int64_t nrows, int64_t ntiles, int d, double inv_n, const double *__restrict__ wv,
+    const double *__restrict__ xc, int xc_stride, double *__restrict__ phi, OptArgs opt, int do_opt)
+{
+    constexpr int NDB = KP / 32, VW = 16 * NCB;
+    constexpr int PT = 6 * NDB + 3 * NCB + 2, BUF = PT * 256; // dwords per tile / LDS buffer
+    constexpr int NT = 64 * NW;
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[2 * BUF];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lo = lane & 15, hi = lane >> 4;
+    const double a = *a_ptr;
+    const float alpha = (float)(2.0 * a * LOG2E);
+
+    const int64_t ibase = row0 + (int64_t)blockIdx.x * (16 * NW) + w * 16;
+    // a wave past the slice (the last block of a rank's rows) loads the
+    // slice's first rows instead: valid memory, nothing stored
+    const int64_t ild = ibase < row0 + nrows ? ibase : row0;
+    // the Gram's B operand: this wave's 16 rows, from their tile's XB slices
+    uint4 bR[NDB][3];
+    {
+        const int64_t tr = ild / 32;
+        const int jsr = (int)((ild / 16) & 1);
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int part = 0; part < 3; ++part)
+                bR[db][part] = *reinterpret_cast<const uint4 *>(
+                    B3 + (tr * PT + (jsr * NDB + db) * 3 + part) * 256 + lane * 4);
+    }
+    const float ci = crow[ild + lo];
+
+    f4_t acc[NCB];
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
+
+    auto issue = [&](int64_t t, int b) {
+        const char *g = reinterpret_cast<const char *>(B3 + t * BUF);
+        char *lb = reinterpret_cast<char *>(sbuf + b * BUF);
+        for (int p = w; p < PT; p += NW)
+            __builtin_amdgcn_global_load_lds((gbl_void *)(g + p * 1024 + lane * 16), (lds_void *)(lb + p * 1024), 16, 0, 0);
+    };
+    if (ntiles > 0) issue(0, 0);
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int b = (int)(t & 1);
+        wait_vmcnt<0>();
+        __syncthreads();
+        if (t + 1 < ntiles) issue(t + 1, b ^ 1);
+        const uint32_t *lb = sbuf + b * BUF;
+        float pv[8]; // P[i = lo][j = 16js + 4hi + r] at k-slot 4js + r
+#pragma unroll
+        for (int js = 0; js < 2; ++js) {
+            f4_t dot = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) {
+                uint4 aX[3];
+#pragma unroll
+                for (int part = 0; part < 3; ++part)
+                    aX[part] = *reinterpret_cast<const uint4 *>(lb + ((js * NDB + db) * 3 + part) * 256 + lane * 4);
+                dot = mfma_b3x6(aX, bR[db], dot);
+            }
+            const f4_t cj = *reinterpret_cast<const f4_t *>(lb + (6 * NDB + 3 * NCB + js) * 256 + lane * 4);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) pv[4 * js + r] = exp2_nonpos(fmaf(alpha, dot[r], ci + cj[r]));
+        }
+        uint4 aP[3];
+        {
+            uint32_t wd[3][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float x0 = pv[2 * q], x1 = pv[2 * q + 1];
+#pragma unroll
+                for (int part = 0; part < 3; ++part) wd[part][q] = b3_split_pair(x0, x1);
+            }
+#pragma unroll
+            for (int part = 0; part < 3; ++part) aP[part] = make_uint4(wd[part][0], wd[part][1], wd[part][2], wd[part][3]);
+        }
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) {
+            uint4 bV[3];
+#pragma unroll
+            for (int part = 0; part < 3; ++part)
+                bV[part] = *reinterpret_cast<const uint4 *>(lb + (6 * NDB + 3 * cb + part) * 256 + lane * 4);
+            acc[cb] = mfma_b3x6(aP, bV, acc[cb]);
+        }
+    }
+
+    // epilogue (fp64): acc lane map row i = 4 hi + q, column c = lo (+16 cb)
+    __syncthreads();
+    float *sAcc = reinterpret_cast<float *>(sbuf) + w * 16 * (VW + 1);
+    static_assert(NW * 16 * (VW + 1) <= 2 * BUF, "epilogue tiles exceed the buffers");
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) sAcc[(4 * hi + q) * (VW + 1) + cb * 16 + lo] = acc[cb][q];
+    __syncthreads();
+    const double two_a = 2.0 * a;
+    for (int e = lane; e < 16 * d; e += 64) {
+        const int il = e / d, c = e - il * d;
+        const int64_t i = ibase + il;
+        if (i - row0 < nrows) {
+            const double s1 = (double)sAcc[il * (VW + 1) + d];
+            const double wgt = wv ? wv[i * d + c] : two_a * xc[i * xc_stride + c];
+            const double ph = inv_n * ((double)sAcc[il * (VW + 1) + c] + wgt * s1);
+            phi[(i - row0) * d + c] = ph;
+            if (do_opt) opt_elem(opt, (i - row0) * d + c, ph);
+        }
+    }
+}
+
 // phi_i = (sum_s acc_s + 2a xc_i sum_s acc1_s) / N, partials summed in s order.
 // wv (full-matrix scale): 2 M xc_i per particle, in place of 2 a xc_i.
 // A block owns phi_red_rows(d) = 256 / (d+1) rows: their (d+1)-element
@@ -4010,6 +4224,48 @@ hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, co
     return hipErrorInvalidValue;
 }
 #undef SVGD_PHIS_CASE
+
+bool phi_b3_supported(int KP, int NCB) { return (KP == 32 || KP == 64) && NCB >= 1 && NCB <= 5; }
+int64_t phi_b3_tile_words(int KP, int NCB) { return (int64_t)(6 * (KP / 32) + 3 * NCB + 2) * 256; }
+
+hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const double *cvec,
+                         int64_t ntiles, uint32_t *B3, hipStream_t stream)
+{
+    if (!phi_b3_supported(KP, VW / 16) || VW % 16 || ntiles <= 0) return hipErrorInvalidValue;
+    const int64_t tot = ntiles * (2 * (KP / 32) + VW / 16) * 64 + ntiles * 128;
+    int64_t g = (tot + 255) / 256;
+    if (g > 8192) g = 8192;
+    if (KP == 32)
+        hipLaunchKernelGGL(k_swz_b3<32>, dim3(g), dim3(256), 0, stream, x, V, VW, cvec, ntiles, B3);
+    else
+        hipLaunchKernelGGL(k_swz_b3<64>, dim3(g), dim3(256), 0, stream, x, V, VW, cvec, ntiles, B3);
+    return hipGetLastError();
+}
+
+#ifndef SVGD_B3_NW
+#define SVGD_B3_NW 8
+#endif
+#define SVGD_PHIB3_CASE(KPv, NCBv)                                                           \
+    if (KP == KPv && NCB == NCBv) {                                                          \
+        hipLaunchKernelGGL((k_phi_b3<KPv, NCBv, SVGD_B3_NW>), dim3(grid), dim3(64 * SVGD_B3_NW), 0, \
+                           stream, B3, crow, a_ptr, row0, nrows, ntiles, d, inv_n, wv, xc,     \
+                           xc_stride, phi, opt ? *opt : OptArgs{}, opt ? 1 : 0);             \
+        return hipGetLastError();                                                            \
+    }
+hipError_t launch_phi_b3(int KP, int NCB, const uint32_t *B3, const float *crow,
+                         const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles, int d,
+                         double inv_n, const double *wv, const double *xc, int xc_stride,
+                         double *phi, const OptArgs *opt, hipStream_t stream)
+{
+    if (nrows <= 0) return hipSuccess;
+    if (row0 % 16) return hipErrorInvalidValue; // (waves own 16-row groups of the padded rows)
+    const int64_t grid = (nrows + 16 * SVGD_B3_NW - 1) / (16 * SVGD_B3_NW);
+    SVGD_PHIB3_CASE(32, 1) SVGD_PHIB3_CASE(32, 2) SVGD_PHIB3_CASE(32, 3)
+    SVGD_PHIB3_CASE(64, 1) SVGD_PHIB3_CASE(64, 2) SVGD_PHIB3_CASE(64, 3) SVGD_PHIB3_CASE(64, 4)
+    SVGD_PHIB3_CASE(64, 5)
+    return hipErrorInvalidValue;
+}
+#undef SVGD_PHIB3_CASE
 
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream)
 {

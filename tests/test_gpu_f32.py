@@ -136,3 +136,57 @@ def test_streamed_tile_phi_matches_generic(oracle, monkeypatch, n, d):
     scale = np.max(np.abs(ref))
     assert np.max(np.abs(out[0] - ref)) <= 1e-4 * scale
     assert np.max(np.abs(out[0] - out[1])) <= 1e-4 * scale
+
+
+@pytest.mark.parametrize("n,d", [(300, 64), (1000, 64), (2049, 33), (4096, 64), (777, 32), (129, 17),
+                                 (640, 40), (3001, 48)])
+def test_b3_tile_phi_matches_oracle(oracle, monkeypatch, n, d):
+    """k_phi_b3 (SVGD_PHI_B3=1: the F32 tile phi on the bf16 matrix cores,
+    each fp32 operand as three bf16 parts and six part products per fp32
+    product) against the fp64 oracle and the fp32-MFMA kernel k_phi_f32s, at
+    the F32 tolerance; ragged N leaves a partial last row block and padded
+    columns."""
+    X = oracle.splitmix((n, d), 2.0, 3 * n + d)
+    G = oracle.splitmix((n, d), 1.0, 3 * n + d + 1)
+    a = 0.7 / d
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("SVGD_PHI_B3", v)
+        c = S.Context(d, n, dtype=C.SVGD_F32)
+        c.set_particles(X)
+        out[v] = c.phi(G, a)
+        name = c.phi_kernel_name()
+        c.close()
+        assert name.startswith("k_phi_b3" if v == "1" else "k_phi_f32s"), name
+    ref = oracle.phi(X, G, a)
+    scale = np.max(np.abs(ref))
+    assert np.all(np.isfinite(out["1"]))
+    assert np.max(np.abs(out["1"] - ref)) <= REL * scale
+    assert np.max(np.abs(out["1"] - out["0"])) <= REL * scale
+
+
+def test_b3_matrix_scale_and_step(oracle, monkeypatch):
+    """k_phi_b3 under a full-matrix scale (whitened coordinates) and inside
+    the fused step (optimizer epilogue) against the fp64 oracle."""
+    monkeypatch.setenv("SVGD_PHI_B3", "1")
+    n, d = 600, 32
+    X = oracle.splitmix((n, d), 2.0, 41)
+    G = oracle.splitmix((n, d), 1.0, 42)
+    B = oracle.splitmix((d, d), 0.2, 43)
+    M = (B @ B.T + 0.5 * np.eye(d)) / d
+    c = _ctx(X)
+    c.set_scale_matrix(M)
+    ph = c.phi(G, 0.0)
+    ref = oracle.phi_matrix(X, G, M)
+    assert np.max(np.abs(ph - ref)) <= REL * np.max(np.abs(ref))
+    c.close()
+    mu = oracle.splitmix((1, d), 0.5, 44)
+    model = S.GaussianSum(mu, np.eye(d)[None])
+    c32 = S.Context(d, n, dtype=C.SVGD_F32)
+    c32.set_particles(X)
+    c32.set_optimizer(C.SVGD_OPT_ADAM, 0.01, 0.9, 0.999, 1e-8)
+    assert c32.phi_kernel_name().startswith("k_phi_b3")
+    for _ in range(3):
+        c32.step_with_model(model)
+    assert np.all(np.isfinite(c32.get_particles()))
+    c32.close()
