@@ -48,6 +48,7 @@ sys.path.insert(0, ROOT)
 METRIC = "particle-updates/sec (N×iters/s) + per-step ms, N=65536 d=8, 1/2/4/8 GPU"
 FP64_PEAK_TFLOPS = 78.6  # MI355X spec (not in MI355X_MICROARCH.md; vector = matrix for fp64)
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 matrix = vector (v_mfma_f32_16x16x4_f32)
+BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA ~2.5 PF dense
 
 
 def splitmix(shape, scale, seed):
@@ -524,6 +525,21 @@ def main():
         flops_launch = float(rows) * n * (5 * d + 4) / parts
         achieved = flops_launch / (phi_kernel_ms / 1e3) / 1e12 if phi_kernel_ms else None
         peak = FP32_PEAK_TFLOPS if dtype == "f32" else FP64_PEAK_TFLOPS
+        b3 = None
+        if ctx.phi_kernel_name().startswith("k_phi_b3"):
+            # fp32 products as six bf16 part products on the bf16 matrix cores:
+            # the MFMA work per ordered pair is 6 x 2 x (KP + 16 NCB) flops
+            # (Gram over KP padded dims, P.V over the padded V width), so the
+            # ceiling for the algorithmic flops is the bf16 dense peak scaled
+            # by algorithmic / MFMA flops
+            kp = 32 if d <= 32 else 64
+            ncb = d // 16 if d % 16 == 0 else (d + 16) // 16
+            mfma_pair = 6.0 * 2.0 * (kp + 16 * ncb)
+            peak = BF16_PEAK_TFLOPS * (5 * d + 4) / mfma_pair
+            b3 = {"peak_basis": f"bf16 dense MFMA peak {BF16_PEAK_TFLOPS:.0f} TF/s x algorithmic / MFMA flops "
+                                f"per pair ({5 * d + 4} / {mfma_pair:.0f}: six bf16 part products per fp32 product)",
+                  "fp32_mfma_peak_frac": (achieved / FP32_PEAK_TFLOPS) if achieved else None,
+                  "bf16_mfma_tflops": (achieved * mfma_pair / (5 * d + 4)) if achieved else None}
         # committed PMC passes (not this run) count only for the same kernel
         # (name + template arguments, svgd_phi_kernel_name), the same kernel
         # source (hash of svgd_kernels.hip) and the same workload (N, d, P)
@@ -574,6 +590,9 @@ def main():
                 # its reduce), so it is comparable with rocprof's kernel mean
                 "kernel": ("k_phi_rows (fused RBF + grad + phi contraction, fp64 VALU row stream)"
                            if row_kernel else
+                           "k_phi_b3 (fused RBF + grad + phi contraction, fp32-accurate on the bf16 "
+                           "matrix cores: three-part operands, six part products)"
+                           if b3 else
                            "k_phi_f32s (fused RBF + grad + phi contraction, streamed fp32 MFMA tiles)"
                            if dtype == "f32" and d > 12 else
                            "k_phi (fused RBF + grad + phi contraction, MFMA tiles)"),
@@ -599,6 +618,8 @@ def main():
             "median_path": ["direct", "bracket", "fallback", "rebracket"][path],
             "scale_a": a,
         }
+        if b3:
+            out["roofline"].update(b3)
         if world > 1:
             out["per_rank"] = per_rank
         clk = (gpu_diag or {}).get("gfxclk_mhz_median")

@@ -180,6 +180,7 @@ struct svgd_ctx {
     float *xcf = nullptr, *nrmf = nullptr, *cvf = nullptr, *Vf = nullptr, *zcf = nullptr;
     float *XS = nullptr, *VS = nullptr; // operand-ordered column copies (k_phi_f32s)
     uint32_t *B3 = nullptr;             // operand-ordered bf16 parts (k_phi_b3), replaces XS / VS
+    bool want_b3 = false;               // F32 phi on the bf16 matrix cores (init)
 
     // row-stream path (d <= ROWS_MAX_D)
     bool rowpath = false;
@@ -1303,7 +1304,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     const int64_t ntl = (c->n + TBJ_COLS - 1) / TBJ_COLS;
     if (c->dtype == SVGD_F32) {
         if (phis && c->B3)
-            HIPCHK(c, launch_swz_b3(mat ? c->zc : c->xc, c->KP, c->V, c->VW, c->cvec, ntl, c->B3,
+            HIPCHK(c, launch_swz_b3(mat ? c->zc : c->xc, c->KP, c->V, c->VW, c->cvec, c->n, ntl, c->B3,
                                     c->stream));
         else if (phis)
             HIPCHK(c, launch_swz_f32(mat ? c->zc : c->xc, c->KP, c->V, c->VW, c->cvec, ntl, c->XS,
@@ -1641,9 +1642,16 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         return fail(c, SVGD_ERR_DIM, "[Dimension Error] Device path supports dimension <= 64.");
     // row-stream path (fp64, d <= 16): xc rows are the median records [xc | |xc|^2 | 0..]
     if (dim <= ROWS_MAX_D && !f32) c->KP = med_rec_stride(dim);
-    // fp64 tiles with d = 16 NCB: no V column of ones (row sums on the VALU);
-    // SVGD_PHI_S1V=0 keeps the ones column (A/B knob)
-    if (!f32 && phi_tile_s1v(dim)) {
+    // F32: the phi on the bf16 matrix cores (k_phi_b3) where it applies
+    // (SVGD_PHI_B3=0: the fp32-MFMA kernel k_phi_f32s)
+    c->want_b3 = false;
+    if (f32 && phi_b3_supported(c->KP, c->NCB) && !std::getenv("SVGD_PHI_TILE_GENERIC")) {
+        const char *e = std::getenv("SVGD_PHI_B3");
+        c->want_b3 = !e || std::atoi(e) != 0;
+    }
+    // fp64 tiles and the bf16 F32 phi with d = 16 NCB: no V column of ones
+    // (row sums on the VALU); SVGD_PHI_S1V=0 keeps the ones column (A/B knob)
+    if ((!f32 || c->want_b3) && phi_tile_s1v(dim)) {
         const char *e = std::getenv("SVGD_PHI_S1V");
         if (!e || std::atoi(e) != 0) c->NCB = dim / 16;
     }
@@ -1794,9 +1802,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
         if (f32 && phi_f32s_supported(c->KP, c->NCB) && !std::getenv("SVGD_PHI_TILE_GENERIC")) {
             // np is a multiple of 2 TBJ_COLS: ceil(n / TBJ_COLS) tiles fit
-            // SVGD_PHI_B3=1: the bf16 matrix-core form (k_phi_b3) where it applies
-            const char *eb = std::getenv("SVGD_PHI_B3");
-            if (eb && std::atoi(eb) != 0 && phi_b3_supported(c->KP, c->NCB)) {
+            if (c->want_b3) {
                 CHK(dalloc(c, &c->B3, (c->np / TBJ_COLS) * phi_b3_tile_words(c->KP, c->NCB)));
             } else {
                 CHK(dalloc(c, &c->XS, c->np * c->KP));
@@ -2657,7 +2663,8 @@ int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
         else
             std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 4, 4096, 1>", d, c->R);
     } else if (c->dtype == SVGD_F32 && c->B3) {
-        std::snprintf(s, sizeof s, "k_phi_b3<%d, %d, 8>", c->KP, c->NCB);
+        std::snprintf(s, sizeof s, "k_phi_b3<%d, %d, 8, %s>", c->KP, c->NCB,
+                      c->dim == 16 * c->NCB ? "true" : "false");
     } else if (c->dtype == SVGD_F32 && c->XS) {
         std::snprintf(s, sizeof s, "k_phi_f32s<%d, %d>", c->KP, c->NCB);
     } else {
@@ -2665,7 +2672,7 @@ int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
         int nw = 4, pre = 0;
         phi_tile_cfg(f64, &nw, &pre);
         std::snprintf(s, sizeof s, "k_phi<%s, %d, %d, %d, %s, %s>", f64 ? "double" : "float", c->KP,
-                      c->NCB, nw, pre ? "true" : "false", f64 && c->dim == 16 * c->NCB ? "true" : "false");
+                      c->NCB, nw, pre ? "true" : "false", c->dim == 16 * c->NCB ? "true" : "false");
     }
     std::snprintf(buf, (size_t)cap, "%s", s);
     return SVGD_OK;

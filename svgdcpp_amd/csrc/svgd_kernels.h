@@ -285,7 +285,7 @@ bool phi_f32s_supported(int KP, int NCB);
 bool phi_b3_supported(int KP, int NCB);
 int64_t phi_b3_tile_words(int KP, int NCB);
 hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const double *cvec,
-                         int64_t ntiles, uint32_t *B3, hipStream_t stream);
+                         int64_t n, int64_t ntiles, uint32_t *B3, hipStream_t stream);
 hipError_t launch_phi_b3(int KP, int NCB, const uint32_t *B3, const float *crow,
                          const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles, int d,
                          double inv_n, const double *wv, const double *xc, int xc_stride,

@@ -438,7 +438,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(SVGD_PH
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) acc[cb] = A4{0, 0, 0, 0};
     T ps = (T)0; // S1V: this lane's share of s1_i (i = lo)
-    const T CPAD = S1V ? (T)-1.0e300 : (T)0;
+    const T CPAD = S1V ? (T)-1.0e300 : (T)0; // (fp32: -inf)
 
     // 16-byte pieces: X_J row jl holds KP/EP of them, V_J row VW/EP
     constexpr int EP = 16 / (int)sizeof(T);
@@ -3060,6 +3060,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 //   CB[t][js][lane][r]           = c_j (fp32), j = 32t + 16js + 4(lane/16) + r
 // Rows (the Gram's B operand) come from XB of the row's own tile: the same
 // lane map.
+// Truncating form (exact as well: h = the top 16 bits of x, x - h exact with
+// at most 16 significant bits, and so on; |m| < 2^-7 |x|, |l| < 2^-15 |x|):
+// the high halves of two floats packed by one v_perm, the residual by a mask
+// and a packed subtract -- no conversion instructions
+__device__ __forceinline__ uint32_t b3_trunc_pair(float &x0, float &x1)
+{
+    const uint32_t u0 = __float_as_uint(x0), u1 = __float_as_uint(x1);
+    const uint32_t w = __builtin_amdgcn_perm(u1, u0, 0x07060302u); // hi16(x1) << 16 | hi16(x0)
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v r = f2v{x0, x1} - f2v{__uint_as_float(u0 & 0xffff0000u), __uint_as_float(u1 & 0xffff0000u)};
+    x0 = r[0];
+    x1 = r[1];
+    return w;
+}
+#ifndef SVGD_B3_TRUNC
+#define SVGD_B3_TRUNC 1
+#endif
 __device__ __forceinline__ uint32_t b3_split_pair(float &x0, float &x1)
 {
     // bf16(x0) | bf16(x1) << 16 (round to nearest even), and the residuals
@@ -3073,7 +3090,8 @@ __device__ __forceinline__ uint32_t b3_split_pair(float &x0, float &x1)
 
 template <int KP>
 __global__ void k_swz_b3(const double *__restrict__ x, const double *__restrict__ V, int VW,
-                         const double *__restrict__ cvec, int64_t ntiles, uint32_t *__restrict__ B3)
+                         const double *__restrict__ cvec, int64_t n, int64_t ntiles,
+                         uint32_t *__restrict__ B3)
 {
     // one thread per (piece, lane) pair of elements: 4 dwords (8 bf16) of one
     // part, the three parts of one (row, 8-k) slice formed together
@@ -3120,7 +3138,10 @@ __global__ void k_swz_b3(const double *__restrict__ x, const double *__restrict_
             const int64_t t = r >> 1;
             float *o = reinterpret_cast<float *>(B3 + (t * PT + 6 * NDB + 3 * NCB + js) * 256) + lane * 4;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = (float)cvec[t * 32 + 16 * js + 4 * (lane >> 4) + q];
+            for (int q = 0; q < 4; ++q) {
+                const int64_t j = t * 32 + 16 * js + 4 * (lane >> 4) + q;
+                o[q] = j < n ? (float)cvec[j] : -__builtin_inff(); // padding: P = 0
+            }
         }
     }
 }
@@ -3131,18 +3152,12 @@ __device__ __forceinline__ f4_t mfma_b3(uint4 a, uint4 b, f4_t c)
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b16x8_t, a),
                                                    __builtin_bit_cast(b16x8_t, b), c, 0, 0, 0);
 }
-// a.b from the parts (smallest products first)
-__device__ __forceinline__ f4_t mfma_b3x6(const uint4 (&a)[3], const uint4 (&b)[3], f4_t c)
-{
-    c = mfma_b3(a[1], b[1], c); // mm
-    c = mfma_b3(a[0], b[2], c); // hl
-    c = mfma_b3(a[2], b[0], c); // lh
-    c = mfma_b3(a[0], b[1], c); // hm
-    c = mfma_b3(a[1], b[0], c); // mh
-    return mfma_b3(a[0], b[0], c); // hh
-}
-
-template <int KP, int NCB, int NW>
+// S1V (d = 16 NCB): V holds no column of ones; the row sums sum_j P_ij are
+// added on the VALU (padded columns carry c_j = -inf: P = 0).  The part
+// products are issued term by term across independent accumulators (the
+// four Gram chains js x db, the NCB P.V blocks), so no MFMA waits for the
+// one before it.
+template <int KP, int NCB, int NW, bool S1V>
 __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     const uint32_t *__restrict__ B3, const float *__restrict__ crow, const double *__restrict__ a_ptr,
     int64_t row0, int64_t nrows, int64_t ntiles, int d, double inv_n, const double *__restrict__ wv,
@@ -3150,8 +3165,7 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
 {
     constexpr int NDB = KP / 32, VW = 16 * NCB;
     constexpr int PT = 6 * NDB + 3 * NCB + 2, BUF = PT * 256; // dwords per tile / LDS buffer
-    constexpr int NT = 64 * NW;
-    __shared__ __attribute__((aligned(16))) uint32_t sbuf[2 * BUF];
+    __shared__ __attribute__((aligned(16))) uint32_t sbuf[3 * BUF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lo = lane & 15, hi = lane >> 4;
@@ -3179,6 +3193,7 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     f4_t acc[NCB];
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    float ps = 0.0f; // S1V: this lane's share of sum_j P_ij, i = lo
 
     auto issue = [&](int64_t t, int b) {
         const char *g = reinterpret_cast<const char *>(B3 + t * BUF);
@@ -3186,66 +3201,118 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
         for (int p = w; p < PT; p += NW)
             __builtin_amdgcn_global_load_lds((gbl_void *)(g + p * 1024 + lane * 16), (lds_void *)(lb + p * 1024), 16, 0, 0);
     };
+    // part products (A part, B part), smallest first
+    constexpr int TA[6] = {1, 0, 2, 0, 1, 0}, TB_[6] = {1, 2, 0, 1, 0, 0};
+    // P.V of a tile whose P parts are in aP, its V parts in LDS buffer lv:
+    // by V part (l, m, h), each part's terms across the NCB blocks
+    auto pv_mfma = [&](const uint32_t *lv, const uint4 (&aP)[3]) {
+#pragma unroll
+        for (int vp = 2; vp >= 0; --vp) {
+            uint4 bV[NCB];
+#pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+                bV[cb] = *reinterpret_cast<const uint4 *>(lv + (6 * NDB + 3 * cb + vp) * 256 + lane * 4);
+            // P parts paired with V part vp: l -> h; m -> m, h; h -> l, m, h
+#pragma unroll
+            for (int pp = 2; pp >= 0; --pp) {
+                if (pp + vp > 2) continue;
+#pragma unroll
+                for (int cb = 0; cb < NCB; ++cb) acc[cb] = mfma_b3(aP[pp], bV[cb], acc[cb]);
+            }
+        }
+    };
+    // Software pipeline over three LDS buffers: iteration t issues tile t's
+    // Gram MFMAs, then tile t-1's P.V MFMAs (its P parts from the last
+    // iteration, its V parts still in buffer (t-1) % 3), and forms tile t's P
+    // on the VALU while those are in the matrix pipe.  The DMA of tile t+1
+    // goes to buffer (t+1) % 3, whose tile (t-2) every wave finished before
+    // this iteration's barrier.
+    uint4 aP[3] = {};
     if (ntiles > 0) issue(0, 0);
     for (int64_t t = 0; t < ntiles; ++t) {
-        const int b = (int)(t & 1);
+        const int b = (int)(t % 3);
         wait_vmcnt<0>();
         __syncthreads();
-        if (t + 1 < ntiles) issue(t + 1, b ^ 1);
+        if (t + 1 < ntiles) issue(t + 1, b == 2 ? 0 : b + 1);
         const uint32_t *lb = sbuf + b * BUF;
+        // Gram: dot[js][db] (4 independent chains at KP = 64), term by term
+        f4_t dot[2][NDB];
+#pragma unroll
+        for (int js = 0; js < 2; ++js)
+#pragma unroll
+            for (int db = 0; db < NDB; ++db) dot[js][db] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        {
+            uint4 aX[2][NDB][3];
+#pragma unroll
+            for (int js = 0; js < 2; ++js)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                    for (int part = 0; part < 3; ++part)
+                        aX[js][db][part] =
+                            *reinterpret_cast<const uint4 *>(lb + ((js * NDB + db) * 3 + part) * 256 + lane * 4);
+#pragma unroll
+            for (int tm = 0; tm < 6; ++tm)
+#pragma unroll
+                for (int js = 0; js < 2; ++js)
+#pragma unroll
+                    for (int db = 0; db < NDB; ++db)
+                        dot[js][db] = mfma_b3(aX[js][db][TA[tm]], bR[db][TB_[tm]], dot[js][db]);
+        }
+        if (t > 0) pv_mfma(sbuf + (b == 0 ? 2 : b - 1) * BUF, aP);
         float pv[8]; // P[i = lo][j = 16js + 4hi + r] at k-slot 4js + r
 #pragma unroll
         for (int js = 0; js < 2; ++js) {
-            f4_t dot = {0.0f, 0.0f, 0.0f, 0.0f};
+            f4_t dd = dot[js][0];
 #pragma unroll
-            for (int db = 0; db < NDB; ++db) {
-                uint4 aX[3];
-#pragma unroll
-                for (int part = 0; part < 3; ++part)
-                    aX[part] = *reinterpret_cast<const uint4 *>(lb + ((js * NDB + db) * 3 + part) * 256 + lane * 4);
-                dot = mfma_b3x6(aX, bR[db], dot);
-            }
+            for (int db = 1; db < NDB; ++db) dd += dot[js][db];
             const f4_t cj = *reinterpret_cast<const f4_t *>(lb + (6 * NDB + 3 * NCB + js) * 256 + lane * 4);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pv[4 * js + r] = exp2_nonpos(fmaf(alpha, dot[r], ci + cj[r]));
+            for (int r = 0; r < 4; ++r) pv[4 * js + r] = exp2_nonpos(fmaf(alpha, dd[r], ci + cj[r]));
         }
-        uint4 aP[3];
+        if (S1V) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) ps += pv[q];
+        }
         {
             uint32_t wd[3][4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float x0 = pv[2 * q], x1 = pv[2 * q + 1];
 #pragma unroll
-                for (int part = 0; part < 3; ++part) wd[part][q] = b3_split_pair(x0, x1);
+                for (int part = 0; part < 3; ++part)
+                    wd[part][q] = SVGD_B3_TRUNC ? b3_trunc_pair(x0, x1) : b3_split_pair(x0, x1);
             }
 #pragma unroll
             for (int part = 0; part < 3; ++part) aP[part] = make_uint4(wd[part][0], wd[part][1], wd[part][2], wd[part][3]);
         }
-#pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) {
-            uint4 bV[3];
-#pragma unroll
-            for (int part = 0; part < 3; ++part)
-                bV[part] = *reinterpret_cast<const uint4 *>(lb + (6 * NDB + 3 * cb + part) * 256 + lane * 4);
-            acc[cb] = mfma_b3x6(aP, bV, acc[cb]);
-        }
+    }
+    if (ntiles > 0) { // the last tile's P.V (its buffer is intact: no DMA after it)
+        const int b = (int)((ntiles - 1) % 3);
+        pv_mfma(sbuf + b * BUF, aP);
     }
 
     // epilogue (fp64): acc lane map row i = 4 hi + q, column c = lo (+16 cb)
+    if (S1V) { // the 4 lane groups' shares of row lo, in a fixed tree
+        ps += __shfl_xor(ps, 16);
+        ps += __shfl_xor(ps, 32);
+    }
     __syncthreads();
     float *sAcc = reinterpret_cast<float *>(sbuf) + w * 16 * (VW + 1);
-    static_assert(NW * 16 * (VW + 1) <= 2 * BUF, "epilogue tiles exceed the buffers");
+    static_assert(NW * 16 * (VW + 1) <= 3 * BUF, "epilogue tiles exceed the buffers");
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb)
 #pragma unroll
         for (int q = 0; q < 4; ++q) sAcc[(4 * hi + q) * (VW + 1) + cb * 16 + lo] = acc[cb][q];
+    if (S1V && hi == 0) sAcc[lo * (VW + 1) + VW] = ps;
     __syncthreads();
     const double two_a = 2.0 * a;
+    const int s1c = S1V ? VW : d;
     for (int e = lane; e < 16 * d; e += 64) {
         const int il = e / d, c = e - il * d;
         const int64_t i = ibase + il;
         if (i - row0 < nrows) {
-            const double s1 = (double)sAcc[il * (VW + 1) + d];
+            const double s1 = (double)sAcc[il * (VW + 1) + s1c];
             const double wgt = wv ? wv[i * d + c] : two_a * xc[i * xc_stride + c];
             const double ph = inv_n * ((double)sAcc[il * (VW + 1) + c] + wgt * s1);
             phi[(i - row0) * d + c] = ph;
@@ -4064,7 +4131,7 @@ static hipError_t launch_phi_tile(const T *xg, const T *cvec, const T *V, const 
         return launch_phi_tile<T, KPv, NCBv, true>(xg, cvec, V, a_ptr, row0, nrows, ntiles_j,  \
                                                    n, d, inv_n, wv, xc, phi, stream);
 
-// S1V tiles (fp64, d = 16 NCB > 16): pick_tiles_s1v in the C ABI
+// S1V tiles (d = 16 NCB > 16: fp64, and F32 under the bf16 matrix-core phi)
 bool phi_tile_s1v(int d) { return d > 16 && d <= 64 && d % 16 == 0; }
 void phi_tile_cfg(bool f64, int *nw, int *pre)
 {
@@ -4079,11 +4146,9 @@ static hipError_t launch_phi_t(int KP, int NCB, const T *xg, const T *cvec, cons
                                double *phi, hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
-    if constexpr (std::is_same<T, double>::value) {
-        SVGD_PHI_CASE_S1V(32, 2)
-        SVGD_PHI_CASE_S1V(64, 3)
-        SVGD_PHI_CASE_S1V(64, 4)
-    }
+    SVGD_PHI_CASE_S1V(32, 2)
+    SVGD_PHI_CASE_S1V(64, 3)
+    SVGD_PHI_CASE_S1V(64, 4)
     SVGD_PHI_CASE(4, 1)
     SVGD_PHI_CASE(8, 1)
     SVGD_PHI_CASE(12, 1)
@@ -4229,16 +4294,16 @@ bool phi_b3_supported(int KP, int NCB) { return (KP == 32 || KP == 64) && NCB >=
 int64_t phi_b3_tile_words(int KP, int NCB) { return (int64_t)(6 * (KP / 32) + 3 * NCB + 2) * 256; }
 
 hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const double *cvec,
-                         int64_t ntiles, uint32_t *B3, hipStream_t stream)
+                         int64_t n, int64_t ntiles, uint32_t *B3, hipStream_t stream)
 {
     if (!phi_b3_supported(KP, VW / 16) || VW % 16 || ntiles <= 0) return hipErrorInvalidValue;
     const int64_t tot = ntiles * (2 * (KP / 32) + VW / 16) * 64 + ntiles * 128;
     int64_t g = (tot + 255) / 256;
     if (g > 8192) g = 8192;
     if (KP == 32)
-        hipLaunchKernelGGL(k_swz_b3<32>, dim3(g), dim3(256), 0, stream, x, V, VW, cvec, ntiles, B3);
+        hipLaunchKernelGGL(k_swz_b3<32>, dim3(g), dim3(256), 0, stream, x, V, VW, cvec, n, ntiles, B3);
     else
-        hipLaunchKernelGGL(k_swz_b3<64>, dim3(g), dim3(256), 0, stream, x, V, VW, cvec, ntiles, B3);
+        hipLaunchKernelGGL(k_swz_b3<64>, dim3(g), dim3(256), 0, stream, x, V, VW, cvec, n, ntiles, B3);
     return hipGetLastError();
 }
 
@@ -4247,9 +4312,16 @@ hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const
 #endif
 #define SVGD_PHIB3_CASE(KPv, NCBv)                                                           \
     if (KP == KPv && NCB == NCBv) {                                                          \
-        hipLaunchKernelGGL((k_phi_b3<KPv, NCBv, SVGD_B3_NW>), dim3(grid), dim3(64 * SVGD_B3_NW), 0, \
-                           stream, B3, crow, a_ptr, row0, nrows, ntiles, d, inv_n, wv, xc,     \
-                           xc_stride, phi, opt ? *opt : OptArgs{}, opt ? 1 : 0);             \
+        if (d == 16 * NCBv)                                                                   \
+            hipLaunchKernelGGL((k_phi_b3<KPv, NCBv, SVGD_B3_NW, true>), dim3(grid),           \
+                               dim3(64 * SVGD_B3_NW), 0, stream, B3, crow, a_ptr, row0, nrows, \
+                               ntiles, d, inv_n, wv, xc, xc_stride, phi,                      \
+                               opt ? *opt : OptArgs{}, opt ? 1 : 0);                          \
+        else                                                                                  \
+            hipLaunchKernelGGL((k_phi_b3<KPv, NCBv, SVGD_B3_NW, false>), dim3(grid),          \
+                               dim3(64 * SVGD_B3_NW), 0, stream, B3, crow, a_ptr, row0, nrows, \
+                               ntiles, d, inv_n, wv, xc, xc_stride, phi,                      \
+                               opt ? *opt : OptArgs{}, opt ? 1 : 0);                          \
         return hipGetLastError();                                                            \
     }
 hipError_t launch_phi_b3(int KP, int NCB, const uint32_t *B3, const float *crow,

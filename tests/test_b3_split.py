@@ -55,3 +55,36 @@ def test_six_products_bound():
         exact = (a.astype(np.float64) * b.astype(np.float64)).sum(-1)
         mag = np.abs(a.astype(np.float64) * b.astype(np.float64)).sum(-1)
         assert np.all(np.abs(six - exact) <= 2.0 ** -22 * mag)
+
+
+def split3_trunc(x):
+    """The kernel's split of P (b3_trunc_pair): each part the top 16 bits of
+    the remaining residual (truncation), residuals exact in fp32."""
+    x = np.asarray(x, dtype=np.float32)
+    mask = np.uint32(0xFFFF0000)
+    h = (x.view(np.uint32) & mask).view(np.float32)
+    r1 = (x - h).astype(np.float32)
+    m = (r1.view(np.uint32) & mask).view(np.float32)
+    r2 = (r1 - m).astype(np.float32)
+    low = (r2.view(np.uint32) & mask).view(np.float32)
+    return h, m, low
+
+
+def test_truncating_split_is_exact_and_mixed_bound():
+    rng = np.random.default_rng(3)
+    for scale in (1e-20, 1e-3, 1.0, 1e4):
+        x = (rng.random(200000) * scale).astype(np.float32)  # P in (0, scale)
+        x = x[x >= 2.0 ** -100]
+        h, m, low = split3_trunc(x)
+        assert np.array_equal(h.astype(np.float64) + m + low, x.astype(np.float64))
+        ax = x.astype(np.float64)
+        assert np.all(np.abs(m) < 2.0 ** -7 * ax) and np.all(np.abs(low) < 2.0 ** -15 * ax)
+    # P (truncated parts) against V (round-to-nearest parts): six products
+    p = rng.random((2000, 32)).astype(np.float32)
+    v = (rng.standard_normal((2000, 32)) * 5).astype(np.float32)
+    ph, pm, pl = (q.astype(np.float64) for q in split3_trunc(p))
+    vh, vm, vl = (q.astype(np.float64) for q in split3(v))
+    six = (ph * vh + ph * vm + pm * vh + ph * vl + pl * vh + pm * vm).sum(-1)
+    exact = (p.astype(np.float64) * v.astype(np.float64)).sum(-1)
+    mag = np.abs(p.astype(np.float64) * v.astype(np.float64)).sum(-1)
+    assert np.all(np.abs(six - exact) <= 2.0 ** -22 * mag)

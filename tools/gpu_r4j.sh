@@ -7,7 +7,7 @@ O=gpurun_out/r4j
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_f32.py -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -1 $O/pytest.log; fault_guard $O/pytest.log; [ $rc -ne 0 ] && { grep -E "^FAILED|Error|assert" $O/pytest.log | head -20; exit $rc; }
-SVGD_PHI_B3=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_f32.py -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_b3.log 2>&1; rc=$?
+SVGD_PHI_B3=0 timeout -k 10 400 python -u -m pytest tests/test_gpu_f32.py -q -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest_b3.log 2>&1; rc=$?
 echo "pytest b3 rc=$rc"; tail -1 $O/pytest_b3.log; fault_guard $O/pytest_b3.log; [ $rc -ne 0 ] && { grep -E "^FAILED|Error|assert" $O/pytest_b3.log | head -20; exit $rc; }
 b() { # name timeout args...
   local name=$1 t=$2; shift 2
@@ -18,9 +18,9 @@ b() { # name timeout args...
 }
 for i in 1 2; do
   SVGD_PHI_B3=0 b cfg5_f32s_$i 400 --config cfg5 --steps 20 --warmup 3 --no-cpu
-  SVGD_PHI_B3=1 b cfg5_b3_$i 400 --config cfg5 --steps 20 --warmup 3 --no-cpu
+  b cfg5_b3_$i 400 --config cfg5 --steps 20 --warmup 3 --no-cpu
 done
-export SVGD_PHI_B3=1
+unset SVGD_PHI_B3
 STEPS=10 WARMUP=3 TAG=_b3 BENCH_ARGS="--config cfg5 --repeats 1" bash tools/profile.sh > /dev/null || exit 1
 python3 tools/ktimed.py gpurun_out/prof_b3/run_kernel_trace.csv 3 > $O/rocprof_cfg5_b3_kernel_timed.txt
 head -6 $O/rocprof_cfg5_b3_kernel_timed.txt
