@@ -181,7 +181,6 @@ struct svgd_ctx {
     float *XS = nullptr, *VS = nullptr; // operand-ordered column copies (k_phi_f32s)
     uint32_t *B3 = nullptr;             // operand-ordered bf16 parts (k_phi_b3), replaces XS / VS
     bool want_b3 = false;               // F32 phi on the bf16 matrix cores (init)
-    bool tcolb = false;                 // F32 collect classified on the bf16 matrix cores
 
     // row-stream path (d <= ROWS_MAX_D)
     bool rowpath = false;
@@ -965,8 +964,7 @@ int collect_counts(svgd_ctx *c)
         // fp32 tile path: k_pair_tiles' keys, rows held in VGPRs, no LDS
         HIPCHK(c, launch_pair_tcol(c->KP, c->collect_grid, c->xcf, c->nrmf, c->n, c->pnb, c->tile0,
                                    c->tile0 + c->own_tiles, c->regions, c->reg_cap, c->counts,
-                                   c->below, c->st, c->bpart, c->tcolb ? c->nmax : nullptr,
-                                   c->stream));
+                                   c->below, c->st, c->bpart, c->stream));
     else
         HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
@@ -1647,10 +1645,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     // F32: the phi on the bf16 matrix cores (k_phi_b3) where it applies
     // (SVGD_PHI_B3=0: the fp32-MFMA kernel k_phi_f32s)
     c->want_b3 = false;
-    // F32 tile collect with the bf16 classification (k_pair_tcolb, KP 32 / 64;
-    // SVGD_TCOL_BF16=0: the fp32 MFMA classification k_pair_tcol)
-    c->tcolb = f32 && (c->KP == 32 || c->KP == 64);
-    if (const char *e = std::getenv("SVGD_TCOL_BF16")) c->tcolb = c->tcolb && std::atoi(e) != 0;
     if (f32 && phi_b3_supported(c->KP, c->NCB) && !std::getenv("SVGD_PHI_TILE_GENERIC")) {
         const char *e = std::getenv("SVGD_PHI_B3");
         c->want_b3 = !e || std::atoi(e) != 0;
@@ -1702,7 +1696,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     const int64_t rows_all = c->chunk * c->world;
     CHK(dalloc(c, &c->X, rows_all * dim));
     CHK(dalloc(c, &c->G, rows_all * dim));
-    CHK(dalloc(c, &c->nmax, 1)); // max |xc|^2 of the step (centring): classification margins
     CHK(dalloc(c, &c->xc, c->np * c->KP));
     CHK(dalloc(c, &c->nrm, c->np));
     CHK(dalloc(c, &c->cvec, c->np));
@@ -1771,6 +1764,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         }
         CHK(dalloc(c, &c->rec, c->np * c->RS));
         CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
+        CHK(dalloc(c, &c->nmax, 1));
         CHK(dalloc(c, &c->part, std::max({(int64_t)c->S * c->ldp, (int64_t)c->S2 * c->split_h,
                                           (int64_t)c->S2b * (c->nrows - c->split_h)}) * (dim + 1)));
         // symmetric phi pass: one rank (a pair feeds two particles, which

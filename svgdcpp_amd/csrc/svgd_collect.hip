@@ -846,334 +846,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
 }
 
-// ====================== fp32 tile-path collect, bf16 classification (F32) ==
-//
-// k_pair_tcol's keys at the bf16 MFMA rate (KP = 32, 64): every pair is
-// CLASSIFIED from a Gram on v_mfma_f32_16x16x32_bf16 with each fp32
-// coordinate split x = h + l + r (h, l bf16, |r| <= 2^-16 |x|) and the part
-// products hh, hl, lh (3 KP/32 MFMAs of 16 cycles per 16 x 16 block instead
-// of KP/4 f32 MFMAs of 32); only the pairs the classification cannot decide
-// form their key, with k_pair_tiles<float>'s exact arithmetic (the fp32 fmaf
-// chain in kslot order, then fmaf(2, dot, (-n_i) + (-n_j))), so every pass
-// still agrees bit for bit.
-// Margin, per tile: with m = the largest |x|^2 of the tile's 64 rows and the
-// wave's 16 columns, S = sum_k |x_ik x_jk| <= |x_i| |x_j| <= m.  The split
-// costs <= (2 2^-16 + 2^-32) S, the bf16 products are exact, the fp32
-// accumulation of 3 KP products <= 3 KP 2^-24 S and the exact chain's own
-// KP roundings <= KP 2^-24 S; v = fmaf(2, dot, t) doubles that and adds one
-// rounding of |v| <= 4 m on each side: |v_approx - v_exact| <= 2^-13.3 m at
-// KP = 64.  delta = 2^-12 m (2.5x that); the thresholds widen by it (rounded
-// outward to fp32): v > tl + delta => below (counted), v <= th - delta =>
-// above (dropped), else the pair is staged (one LDS entry per lane and
-// 16 x 16 block) and finished exactly at the end of its tile.  (A per-tile m:
-// one far particle widens only its own tiles' bands.)
-constexpr int TB_STG = 256; // staged entries per wave and tile (4 row blocks x 64 lanes)
-
-template <int KP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_tcolb(
-    const float *__restrict__ xc, const float *__restrict__ nrm, int64_t n, int64_t nb, int64_t t0,
-    int64_t t1, SinkCollect sc)
-{
-    static_assert(KP % 32 == 0, "bf16 classification takes KP = 32, 64");
-    constexpr int KK = KP / 4, NDB = KP / 32;
-    __shared__ uint32_t sBk[NBK];
-    __shared__ uint32_t sCnt;
-    __shared__ unsigned long long sBelow[4];
-    __shared__ __attribute__((aligned(16))) uint4 sB[4 * NDB * 2 * 64]; // [rb][db][part][lane]
-    __shared__ uint32_t sStage[4][TB_STG];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int kq = lane >> 4, ql = lane & 15;
-    uint32_t *stage = sStage[w];
-
-    const uint64_t lo_key = sc.st->lo_key, hi_key = sc.st->hi_key;
-    const double binv = sc.st->binv;
-    const double lo_d = __longlong_as_double((long long)lo_key);
-    const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
-                                                        : __longlong_as_double((long long)hi_key);
-    float loT = (float)lo_d, hiT = (float)hi_d;
-    if ((double)loT < lo_d) loT = __int_as_float(__float_as_int(loT) + 1);
-    if ((double)hiT < hi_d) hiT = __int_as_float(__float_as_int(hiT) + 1);
-    const float tl = loT > 0.0f ? -loT : __builtin_inff();
-    const float th = hiT > 0.0f ? -hiT : __builtin_inff();
-    // widened thresholds, rounded outward (an infinite one stays infinite)
-    auto up = [](double x) {
-        float f = (float)x;
-        if ((double)f < x) f = __int_as_float(__float_as_int(f) + (f >= 0.0f ? 1 : -1));
-        return f;
-    };
-    auto down = [](double x) {
-        float f = (float)x;
-        if ((double)f > x) f = __int_as_float(__float_as_int(f) + (f > 0.0f ? -1 : 1));
-        return f;
-    };
-    auto widen = [&](float rm, float cm, float &tlw, float &thw) {
-        const float m = fmaxf(rm, cm);
-        const double delta = !(m <= 0x1p100f) ? __builtin_inf() : 0x1p-12 * (double)m + 0x1p-120;
-        tlw = tl == __builtin_inff() ? tl : up((double)tl + delta);
-        thw = th == __builtin_inff() ? th : down((double)th - delta);
-    };
-    auto wave_max = [](float x) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
-        return x;
-    };
-    if (tid == 0) sCnt = 0;
-    if (sc.bpart)
-        for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
-    __syncthreads();
-
-    uint64_t *region = sc.region + (int64_t)blockIdx.x * sc.cap;
-    uint32_t below = 0;
-    const int xl = 4 * kq - ql;
-    const float ninf = -__builtin_inff();
-
-    struct Cols {
-        uint4 A[NDB][2]; // bf16 parts h, l of x_j[32 db + 8 kq + e], j = j0 + ql
-        f4 nv;
-    };
-    auto load_cols = [&](int J, Cols &c) {
-        const int64_t j0 = (int64_t)J * TB + 16 * w;
-        const float *xcol = xc + (j0 + ql) * KP + 8 * kq;
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-            const f4 t0 = *reinterpret_cast<const f4 *>(xcol + 32 * db);
-            const f4 t1 = *reinterpret_cast<const f4 *>(xcol + 32 * db + 4);
-            const float x[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-            c.A[db][0] = mcol_split_bf16(x, false);
-            c.A[db][1] = mcol_split_bf16(x, true);
-        }
-        c.nv = *reinterpret_cast<const f4 *>(nrm + j0 + 4 * kq);
-    };
-
-    const int G = gridDim.x;
-    const int nG = (G % 8 == 0) ? 8 : 1;
-    const int P = G / nG, g = blockIdx.x % nG, q = blockIdx.x / nG;
-    int R = 32;
-    while (P % R) R >>= 1;
-    const int S = P / R, rr = q % R, ph = q / R;
-    const int nb32 = (int)nb, n32 = (int)min<int64_t>(n, 0x7fffffff);
-    const int64_t H = (nb - 1) / 2;
-    const int64_t half = (nb & 1) == 0 ? nb / 2 : 0, c1 = H + 2, c2 = H + 1;
-    int Ia = 0, Ib = -1;
-    if (t1 > t0) {
-        int64_t I64, Jd;
-        tile_coords(nb, t0, &I64, &Jd);
-        Ia = (int)I64;
-        tile_coords(nb, t1 - 1, &I64, &Jd);
-        Ib = (int)I64;
-    }
-    const int nbands = (Ib - Ia + 1 + R - 1) / R;
-    struct Pos {
-        int k, I, s, J, hi;
-    };
-    auto enter_row = [&](Pos &p) {
-        for (; p.k < nbands; p.k += nG) {
-            const int I = Ia + p.k * R + rr;
-            if (I > Ib) continue;
-            const int64_t rs = I < half ? I * c1 : half * c1 + (I - half) * c2;
-            const int lo = (int)max<int64_t>(0, t0 - rs);
-            const int hi = (int)min<int64_t>(I < half ? c1 : c2, t1 - rs);
-            const int s = lo <= ph ? ph : ph + (lo - ph + S - 1) / S * S;
-            if (s < hi) {
-                p.I = I;
-                p.s = s;
-                p.hi = hi;
-                p.J = I + s >= nb32 ? I + s - nb32 : I + s;
-                return true;
-            }
-        }
-        return false;
-    };
-    auto advance = [&](Pos &p) {
-        p.s += S;
-        if (p.s < p.hi) {
-            p.J = p.I + p.s >= nb32 ? p.I + p.s - nb32 : p.I + p.s;
-            return true;
-        }
-        p.k += nG;
-        return enter_row(p);
-    };
-
-    // staged entries of tile (I, J): bits 0..5 the lane (ql | kq << 4), 6..7
-    // the row block, 8..11 which of the lane's 4 values are band pairs
-    int scnt = 0;
-    auto flush = [&](int I, int J) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // other lanes' staging stores
-        for (int q0 = 0; q0 < scnt; q0 += 64) {
-            const bool valid = q0 + lane < scnt;
-            const uint32_t e = valid ? stage[q0 + lane] : 0u;
-            uint32_t code = (e >> 8) & 15u;
-            const int sl = (int)(e & 63u), rb = (int)((e >> 6) & 3u);
-            const int64_t i = (int64_t)I * TB + 16 * rb + (sl & 15);
-            const int64_t jb = (int64_t)J * TB + 16 * w + 4 * (sl >> 4);
-            const float *xi = xc + (valid ? i : 0) * KP;
-            const float hi_ = valid ? -nrm[i] : 0.0f;
-            while (__any(code != 0)) {
-                const bool act = code != 0;
-                const int r = act ? __builtin_ctz(code) : 0;
-                code &= code - 1u;
-                const int64_t j = act ? jb + r : 0;
-                const float *xj = xc + j * KP;
-                float dot = 0.0f; // the MFMA chain: instruction kk, lane groups q in order
-#pragma unroll
-                for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-                    for (int qq = 0; qq < 4; ++qq) {
-                        const int k = kslot<float, KP>(kk, qq);
-                        dot = fmaf(xj[k], xi[k], dot);
-                    }
-                const float v = fmaf(2.0f, dot, hi_ + (-nrm[j]));
-                const uint64_t key = key_of((double)(v >= 0.0f ? 0.0f : -v));
-                below += (uint32_t)__popcll(__ballot(act && key < lo_key));
-                const bool keep = act && key >= lo_key && key < hi_key;
-                const unsigned long long mk = __ballot(keep);
-                if (mk) {
-                    uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mk));
-                    base = __shfl(base, 0);
-                    if (keep) {
-                        const int64_t pos = (int64_t)base + __popcll(mk & ((1ull << lane) - 1ull));
-                        if (pos < sc.cap) region[pos] = key;
-                        if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
-                    }
-                }
-            }
-        }
-        scnt = 0;
-    };
-
-    float hr[4];
-    float rmax = 0.0f; // the tile row's largest |x_i|^2
-    auto tile = [&](const Pos &p, const Cols &c) {
-        const int j0 = p.J * TB + 16 * w + 4 * kq;
-        float hc[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hc[r] = j0 + r < n32 ? -c.nv[r] : ninf;
-        float tlw, thw;
-        float cm = 0.0f; // (padding columns, norm -inf, do not count)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cm = j0 + r < n32 ? fmaxf(cm, c.nv[r]) : cm;
-        widen(rmax, wave_max(cm), tlw, thw);
-        f4 acc[4];
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) acc[rb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-        // part products hl, lh, then hh, across the 4 row blocks
-#pragma unroll
-        for (int tm = 0; tm < 3; ++tm)
-#pragma unroll
-            for (int db = 0; db < NDB; ++db)
-#pragma unroll
-                for (int rb = 0; rb < 4; ++rb) {
-                    const int pa = tm == 1 ? 1 : 0, pb = tm == 0 ? 1 : 0;
-                    const uint4 bq = sB[((rb * NDB + db) * 2 + pb) * 64 + lane];
-                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        __builtin_bit_cast(bf16x8_t, c.A[db][pa]), __builtin_bit_cast(bf16x8_t, bq), acc[rb], 0, 0, 0);
-                }
-        const bool diag = p.s == 0;
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            const f2 hh = {hr[rb], hr[rb]}, two = {2.0f, 2.0f};
-            const f2 t01 = hh + f2{hc[0], hc[1]}, t23 = hh + f2{hc[2], hc[3]};
-            const f2 v01 = __builtin_elementwise_fma(two, f2{acc[rb][0], acc[rb][1]}, t01);
-            const f2 v23 = __builtin_elementwise_fma(two, f2{acc[rb][2], acc[rb][3]}, t23);
-            const f4 v = {v01[0], v01[1], v23[0], v23[1]};
-            unsigned long long h[4], any = 0;
-            uint32_t nbl = 0;
-            if (diag) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    h[r] = mcol_classify_diag(v[r], tlw, thw, xl, 16 * rb - 16 * w - r, nbl);
-                    any |= h[r];
-                }
-            } else {
-                any = mcol_classify4(v, tlw, thw, nbl, h);
-            }
-            below += nbl;
-            if (__builtin_expect(any != 0, 0)) {
-                const uint32_t code = mcol_code4(h);
-                const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
-                if (code) stage[scnt + pre] = (uint32_t)lane | ((uint32_t)rb << 6) | (code << 8);
-                scnt += __popcll(any);
-            }
-        }
-        if (scnt) flush(p.I, p.J);
-    };
-    auto rows = [&](int I) {
-        const int ib = I * TB;
-        __syncthreads(); // every wave is done with the previous row
-        for (int e = tid; e < 4 * NDB * 64; e += 256) {
-            const int l = e & 63, db = (e >> 6) % NDB, rb = (e >> 6) / NDB;
-            const int64_t i = ib + 16 * rb + (l & 15);
-            const float *xr = xc + i * KP + 32 * db + 8 * (l >> 4);
-            const f4 t0 = *reinterpret_cast<const f4 *>(xr), t1 = *reinterpret_cast<const f4 *>(xr + 4);
-            const float x[8] = {t0[0], t0[1], t0[2], t0[3], t1[0], t1[1], t1[2], t1[3]};
-            sB[((rb * NDB + db) * 2 + 0) * 64 + l] = mcol_split_bf16(x, false);
-            sB[((rb * NDB + db) * 2 + 1) * 64 + l] = mcol_split_bf16(x, true);
-        }
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-            const int i = ib + 16 * rb + ql;
-            const float nv = nrm[i];
-            hr[rb] = i < n32 ? -nv : ninf;
-        }
-        float rm = 0.0f; // (padding rows do not count)
-#pragma unroll
-        for (int rb = 0; rb < 4; ++rb) rm = ib + 16 * rb + ql < n32 ? fmaxf(rm, -hr[rb]) : rm;
-        rmax = wave_max(rm);
-        __syncthreads();
-        __builtin_amdgcn_s_waitcnt(0x0F70);
-    };
-
-    Pos p0{g, 0, 0, 0, 0};
-    if (enter_row(p0)) {
-        Cols c0, c1;
-        load_cols(p0.J, c0);
-        for (bool live = true; live;) {
-            rows(p0.I);
-            for (;;) {
-                Pos p1 = p0;
-                const bool m1 = advance(p1);
-                load_cols(m1 ? p1.J : 0, c1);
-                __builtin_amdgcn_sched_barrier(0);
-                tile(p0, c0);
-                if (!m1) {
-                    live = false;
-                    break;
-                }
-                if (p1.I != p0.I) {
-                    p0 = p1;
-                    c0 = c1;
-                    break;
-                }
-                Pos p2 = p1;
-                const bool m2 = advance(p2);
-                load_cols(m2 ? p2.J : 0, c0);
-                __builtin_amdgcn_sched_barrier(0);
-                tile(p1, c1);
-                if (!m2) {
-                    live = false;
-                    break;
-                }
-                const bool row_end = p2.I != p1.I;
-                p0 = p2;
-                if (row_end) break;
-            }
-        }
-    }
-
-    if (lane == 0) sBelow[w] = below;
-    __syncthreads();
-    if (tid == 0) {
-        sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
-        sc.count_out[blockIdx.x] = sCnt;
-    }
-    if (sc.bpart)
-        for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
-}
-
 // ============================================================ launcher ==
 
 #define SVGD_TCOL_CASE(KPv)                                                                  \
@@ -1185,18 +857,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, int64_t n,
                             int64_t nb, int64_t t0, int64_t t1, uint64_t *regions, int64_t cap,
                             uint32_t *counts, unsigned long long *below, const SelState *st,
-                            uint32_t *bpart, const unsigned long long *nmax_bits, hipStream_t stream)
+                            uint32_t *bpart, hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
-    SinkCollect sc{st, regions, cap, counts, below, nullptr, nmax_bits, bpart};
-    if (nmax_bits && (KP == 32 || KP == 64)) { // bf16 classification (k_pair_tcolb; its
-        // margins come from each tile's own norms: nmax_bits only selects it)
-        if (KP == 32)
-            hipLaunchKernelGGL((k_pair_tcolb<32>), dim3(grid), dim3(256), 0, stream, xc, nrm, n, nb, t0, t1, sc);
-        else
-            hipLaunchKernelGGL((k_pair_tcolb<64>), dim3(grid), dim3(256), 0, stream, xc, nrm, n, nb, t0, t1, sc);
-        return hipGetLastError();
-    }
+    SinkCollect sc{st, regions, cap, counts, below, nullptr, nullptr, bpart};
     switch (KP) {
         SVGD_TCOL_CASE(4)
         SVGD_TCOL_CASE(8)

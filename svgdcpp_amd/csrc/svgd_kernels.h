@@ -267,7 +267,7 @@ hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
 hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, int64_t n,
                             int64_t nb, int64_t t0, int64_t t1, uint64_t *regions, int64_t cap,
                             uint32_t *counts, unsigned long long *below, const SelState *st,
-                            uint32_t *bpart, const unsigned long long *nmax_bits, hipStream_t stream);
+                            uint32_t *bpart, hipStream_t stream);
 // F32 tile phi, streamed (k_phi_f32s): operand-ordered fp32 copies of the
 // columns (XS, VS: ntiles = ceil(n / 32) tiles of 32 particles; XS holds
 // ntiles * 32 * KP floats, VS ntiles * 2 * (VW/16 + 1) * 256) made by

@@ -199,8 +199,6 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
             for (int k = 0; k < KF; ++k)
                 xf[j * KF + k] = k < d ? (float)xc[j * KP + k]
                                        : (k == d ? (j < n ? (float)(-0.5 * s) : -__builtin_inff()) : 0.0f);
-        }
-        if (nmax_bits) {
             unsigned long long m = (unsigned long long)__double_as_longlong(s);
             for (int o = 32; o > 0; o >>= 1) {
                 const unsigned long long t = __shfl_xor(m, o);
@@ -209,7 +207,7 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
             bmax = m > bmax ? m : bmax;
         }
     }
-    if (nmax_bits) {
+    if (xf) {
         // one atomic per block (per-wave atomics on one address serialise)
         __shared__ unsigned long long wmax[4];
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bmax;
@@ -4359,7 +4357,7 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
     const SelState sinit = st_init ? *st_init : SelState{};
     if (!st_init) st_out = nullptr;
     hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial,
-                       nmax_bits);
+                       xf ? nmax_bits : nullptr);
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
 #define SVGD_CENTER_CASE(Dv)                                                                  \

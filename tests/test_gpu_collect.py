@@ -179,22 +179,3 @@ def test_tcol_full_size_matches_tile_collect(oracle, monkeypatch):
         assert c.last_scale()[2] in (C.SVGD_MEDIAN_BRACKET, C.SVGD_MEDIAN_REBRACKET)
         c.close()
     assert res[0] == res[1]
-
-
-@pytest.mark.parametrize("n,d", [(1000, 20), (4097, 33), (4097, 64), (3001, 48), (777, 32)])
-def test_tcolb_matches_f32_classification(oracle, monkeypatch, n, d):
-    """k_pair_tcolb (KP = 32, 64: classification on the bf16 matrix cores,
-    the exact fp32 keys for the undecided band) against k_pair_tcol's fp32
-    MFMA classification (SVGD_TCOL_BF16=0) and the exact order statistics:
-    the same keys and counts bit for bit."""
-    X = oracle.splitmix((n, d), 3.0, 13 * n + d)
-    res = []
-    for v in ("1", "0"):
-        monkeypatch.setenv("SVGD_TCOL_BF16", v)
-        c, got = _median32(X, monkeypatch, ref=False)
-        if v == "1":
-            exp = _exact_median(c, n)
-        c.close()
-        res.append(got)
-    assert res[0] == res[1]
-    assert res[0][1] == exp
