@@ -180,6 +180,7 @@ struct svgd_ctx {
     float *xcf = nullptr, *nrmf = nullptr, *cvf = nullptr, *Vf = nullptr, *zcf = nullptr;
     float *XS = nullptr, *VS = nullptr; // operand-ordered column copies (k_phi_f32s)
     uint32_t *B3 = nullptr;             // operand-ordered bf16 parts (k_phi_b3), replaces XS / VS
+    uint32_t *XK = nullptr;             // F32 median key parts, KP 32 / 64 (svgd_device.h)
     bool want_b3 = false;               // F32 phi on the bf16 matrix cores (init)
 
     // row-stream path (d <= ROWS_MAX_D)
@@ -268,6 +269,15 @@ struct svgd_ctx {
     // H2D copy-engine round trips and cross-queue waits on the host
     // gradient's path (cfg2: phi waited ~70 us for G behind them)
     bool xmirror = false, xh_valid = false, ghost = false, ghost_step = false;
+    // Mean partials from the update epilogue (one rank, row path, not the
+    // symmetric pass): k_phi_reduce leaves X_{t+1}'s per-block column sums in
+    // xsum (xsum_parts blocks) and zeroes nmax, so the next centring skips
+    // k_mean_partial.  xsum_valid from the reduce's enqueue to the next
+    // centring; cleared by anything else that moves X (svgd_set_particles, a
+    // redo).  SVGD_XSUM=0 turns it off.
+    double *xsum = nullptr;
+    int xsum_parts = 0;
+    bool xsum_valid = false, xsum_written = false;
     double *h_xm = nullptr, *h_xm_dev = nullptr;
     unsigned long long *h_cnt = nullptr;
     double *h_scal = nullptr;
@@ -622,12 +632,15 @@ int mark_median_end(svgd_ctx *c)
 
 int center(svgd_ctx *c, const SelState *st_init = nullptr)
 {
-    HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc,
-                                 c->nrm, c->rowpath ? 1 : 0, c->xf, c->nmax, c->cnt3 + 3, c->stream,
-                                 c->st, st_init));
+    const bool pr = c->xsum_valid; // the last update epilogue's partials (svgd_ctx::xsum)
+    c->xsum_valid = false;
+    HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, pr ? c->xsum : c->partial,
+                                 pr ? c->xsum_parts : c->nparts, c->xc, c->nrm, c->rowpath ? 1 : 0,
+                                 c->xf, c->nmax, c->cnt3 + 3, c->stream, c->st, st_init, pr));
     if (c->dtype == SVGD_F32) {
         HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
         HIPCHK(c, launch_cvt_f32(c->nrm, c->np, c->nrmf, c->stream));
+        if (c->XK) HIPCHK(c, launch_swz_keys_b3(c->xcf, c->KP, c->np, c->XK, c->stream));
     }
     return SVGD_OK;
 }
@@ -680,7 +693,7 @@ hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t
     if (c->dtype == SVGD_F32)
         return launch_pair_tiles_f32(c->KP, mode, grid, c->xcf, c->nrmf, c->n, c->pnb, c->tile0,
                                      c->tile0 + c->own_tiles, regions, cap, c->counts, c->below,
-                                     c->st, c->ghist, bp, dbg, c->stream);
+                                     c->st, c->ghist, bp, dbg, c->XK, c->stream);
     return launch_pair_tiles(c->KP, mode, grid, c->xc, c->nrm, c->n, c->pnb, c->tile0,
                              c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
                              c->ghist, bp, dbg, c->stream);
@@ -877,8 +890,8 @@ int median_begin(svgd_ctx *c)
             c->sample_alloc = S;
         }
         if (tile_sample)
-            HIPCHK(c, launch_sample_tiles(c->KP, c->xc, c->nrm, c->xcf, c->nrmf, n, S / (TB * TB),
-                                          c->sample_keys, c->stream));
+            HIPCHK(c, launch_sample_tiles(c->KP, c->xc, c->nrm, c->xcf, c->nrmf, c->XK, n,
+                                          S / (TB * TB), c->sample_keys, c->stream));
         // sharded (P > 1, scattered pairs): rank r draws pairs [S r/P, S (r+1)/P)
         // of the one counter-based sequence and the bracket's histograms are
         // all-reduced -- the same sample, hence the same bracket, as on one rank
@@ -962,9 +975,9 @@ int collect_counts(svgd_ctx *c)
                                    c->counts, c->below, c->st, c->bpart, c->mcol_bf16, c->stream));
     else if (!c->rowpath && c->dtype == SVGD_F32 && c->mcol)
         // fp32 tile path: k_pair_tiles' keys, rows held in VGPRs, no LDS
-        HIPCHK(c, launch_pair_tcol(c->KP, c->collect_grid, c->xcf, c->nrmf, c->n, c->pnb, c->tile0,
-                                   c->tile0 + c->own_tiles, c->regions, c->reg_cap, c->counts,
-                                   c->below, c->st, c->bpart, c->stream));
+        HIPCHK(c, launch_pair_tcol(c->KP, c->collect_grid, c->xcf, c->nrmf, c->XK, c->n, c->pnb,
+                                   c->tile0, c->tile0 + c->own_tiles, c->regions, c->reg_cap,
+                                   c->counts, c->below, c->st, c->bpart, c->stream));
     else
         HIPCHK(c, pair_pass(c, 0, c->collect_grid, c->regions, c->reg_cap, nullptr));
     HIPCHK(c, launch_counts_reduce(c->below, c->counts, c->nregions, c->reg_cap, c->st, c->bpart,
@@ -1338,14 +1351,20 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         // the second half's phi runs (svgd_step_host_model copies it down and
         // starts its gradient there)
         const int64_t h = c->split_h, d = c->dim;
-        OptArgs o2 = *opt;
+        OptArgs o1 = *opt, o2 = *opt;
+        o1.nmax_zero = nullptr; // the second part's phi still reads nmax
+        if (o2.xsum) {
+            o2.xsum += phi_reduce_blocks((int)d, h) * d;
+            c->xsum_parts = (int)(phi_reduce_blocks((int)d, h) + phi_reduce_blocks((int)d, c->nrows - h));
+            c->xsum_written = true;
+        }
         o2.X += h * d;
         o2.m += h * d;
         o2.v += h * d;
         if (o2.bak) o2.bak += h * d;
         if (o2.xh) o2.xh += h * d;
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, h, c->n, c->S2, c->part, h,
-                                  1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, opt, c->stream, k1,
+                                  1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, &o1, c->stream, k1,
                                   c->phi_kind));
         HIPCHK(c, hipEventRecord(c->ev_xhalf, c->stream));
         hipEvent_t k2 = diag_begin(c, c->stream);
@@ -1354,12 +1373,16 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
                                   c->part, c->nrows - h, 1.0 / (double)c->n, nullptr, nullptr, c->nmax,
                                   c->phi + h * d, &o2, c->stream, k3, c->phi_kind));
         if (k2) c->ev_diag.push_back({k2, k3, DG_PHI_KERNEL, true});
-    } else if (c->rowpath)
+    } else if (c->rowpath) {
+        if (opt && opt->xsum) {
+            c->xsum_parts = (int)phi_reduce_blocks(c->dim, c->nrows);
+            c->xsum_written = true;
+        }
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
                                   mat ? c->sc_sgn : nullptr, mat ? nullptr : c->nmax, c->phi, opt,
                                   c->stream, k1, mat ? 0 : c->phi_kind));
-    else if (phis)
+    } else if (phis)
         HIPCHK(c, c->B3 ? launch_phi_b3(c->KP, c->NCB, c->B3, c->cvf, c->scal, c->row0, c->nrows, ntl,
                                         c->dim, 1.0 / (double)c->n, mat ? c->wv : nullptr, c->xc, c->KP,
                                         c->phi, opt, c->stream)
@@ -1457,7 +1480,13 @@ int run_phi_opt(svgd_ctx *c)
     const bool fused = c->rowpath || phi_streamed(c);
     c->phi_end = nullptr;
     c->xh_valid = false;
+    c->xsum_valid = c->xsum_written = false;
+    if (c->xsum && c->rowpath && !c->sym) {
+        o.xsum = c->xsum;
+        o.nmax_zero = c->nmax;
+    }
     CHK(run_phi(c, fused ? &o : nullptr));
+    c->xsum_valid = c->xsum_written;
     if (!fused) {
         HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
         c->phi_end = nullptr;
@@ -1609,6 +1638,7 @@ int resolve_pending(svgd_ctx *c)
     c->t -= 1;
     c->spec_step = false;
     c->last_fast = false;
+    c->xsum_valid = false; // X_t is back: its partials are not the epilogue's
     CHK(scale_begin(c));
     CHK(scale_finish(c));
     CHK(run_phi_opt(c));
@@ -1704,6 +1734,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         CHK(dalloc(c, &c->xcf, c->np * c->KP));
         CHK(dalloc(c, &c->nrmf, c->np));
         CHK(dalloc(c, &c->cvf, c->np));
+        // KP 32 / 64: the median keys on the bf16 matrix cores (their parts)
+        if (const int64_t w = median_key_part_words(c->KP, c->np)) CHK(dalloc(c, &c->XK, w));
     }
     if (c->rowpath) {
         // column splits: enough workgroups to fill every CU at the kernel's occupancy
@@ -1797,6 +1829,9 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             CHK(dalloc(c, &c->symok, 1));
             c->sym = true;
         }
+        bool want_xsum = c->world == 1 && c->sim_world <= 1 && !c->sym;
+        if (const char *e = std::getenv("SVGD_XSUM")) want_xsum = want_xsum && std::atoi(e) != 0;
+        if (want_xsum) CHK(dalloc(c, &c->xsum, (phi_reduce_blocks(dim, c->nrows) + 2) * dim));
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
@@ -2008,6 +2043,8 @@ int svgd_destroy(svgd_ctx *c)
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
     if (c->B3) (void)hipFree(c->B3);
+    if (c->XK) (void)hipFree(c->XK);
+    if (c->xsum) (void)hipFree(c->xsum);
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
@@ -2202,6 +2239,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     c->have_particles = true;
     c->xhalf_ready = false;
     c->xh_valid = false;
+    c->xsum_valid = false;
     c->trk_n = c->trk_nerr = 0; // new particles: the median history restarts
     return SVGD_OK;
 }

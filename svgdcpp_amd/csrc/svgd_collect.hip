@@ -569,13 +569,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
 // cycles).  Candidates (the band, ~0.3 %) go straight to the block's region.
 // Rows / columns >= n carry norm -inf: never below, never candidates.
 constexpr int TC_STG = 512; // staged band values per wave (k_pair_tcol)
+#ifndef SVGD_TCOL_PIPE
+#define SVGD_TCOL_PIPE 0
+#endif
 
+// KP 32 / 64 (B3K): the bf16 part-product keys (svgd_device.h "F32 pair
+// keys"): per tile 6 KP/32 x 4 bf16 MFMAs of 16 cycles instead of KP x 4 f32
+// ones of 32; the wave's column parts in VGPRs (from the key parts xk), the
+// tile row's parts in LDS (read once per row block and tile); a wrapped tile
+// (J < I) swaps the operand roles, which transposes the lane map.
 template <int KP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_tcol(
-    const float *__restrict__ xc, const float *__restrict__ nrm, int64_t n, int64_t nb, int64_t t0,
-    int64_t t1, SinkCollect sc)
+    const float *__restrict__ xc, const float *__restrict__ nrm, const uint32_t *__restrict__ xk,
+    int64_t n, int64_t nb, int64_t t0, int64_t t1, SinkCollect sc)
 {
-    constexpr int KK = KP / 4;
+    constexpr bool B3K = kb3_keys(KP);
+    constexpr int NDB = KP / 32;
+    constexpr int KK = B3K ? 1 : KP / 4;
     __shared__ uint32_t sBk[NBK];
     __shared__ uint32_t sCnt;
     __shared__ unsigned long long sBelow[4];
@@ -615,11 +625,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     // the load would make the compiler wait for it (and the whole prefetch)
     struct Cols {
         float A[KK];
+        uint4 A3[B3K ? NDB : 1][3];
         f4 nv;
+        float nq; // B3K: the norm of column j0 + ql (transposed lane map)
     };
     auto load_cols = [&](int J, Cols &c) {
         const int64_t j0 = (int64_t)J * TB + 16 * w;
-        if constexpr (KP % 16 == 0) { // kslot order: 16-byte loads
+        if constexpr (B3K) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(xk + ((int64_t)J * 4 + w) * kb3_block_words(KP)) + lane;
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) c.A3[db][q] = p[(db * 3 + q) * 64];
+            c.nq = nrm[j0 + ql];
+        } else if constexpr (KP % 16 == 0) { // kslot order: 16-byte loads
             const float *xcol = xc + (j0 + ql) * KP + 4 * kq;
 #pragma unroll
             for (int u = 0; u < KK / 4; ++u) {
@@ -717,7 +736,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 
     // the tile row's B operands, shared by the block's 4 waves (written at a
     // row change, between barriers: every wave follows the same schedule)
-    __shared__ float sB[4 * KK * 64];
+    __shared__ float sB[B3K ? 1 : 4 * KK * 64];
+    __shared__ uint4 sB3[B3K ? 4 * NDB * 3 * 64 : 1]; // [rb][db][part][lane]
+    __shared__ __attribute__((aligned(16))) float sNr[B3K ? 64 : 1]; // -n_i of the row (masked)
     float hr[4];
     // one tile (I, J): 4 x KK MFMAs, then the classification
     auto tile = [&](const Pos &p, const Cols &c) {
@@ -728,20 +749,65 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         f4 acc[4];
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) acc[rb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        // B3K: a wrapped tile (J < I) puts the rows (larger indices) in the A role
+        const bool swp = B3K && p.J < p.I;
+        if constexpr (B3K) {
+            auto gram = [&](auto swp_tag) {
+                constexpr bool SW = decltype(swp_tag)::value;
+                // the row block's parts from LDS; SVGD_TCOL_PIPE: row block
+                // rb + 1's reads issued before rb's MFMAs
+                uint4 rp[2][NDB][3];
+                auto rows_of = [&](int rb, uint4 (&r)[NDB][3]) {
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk)
+                    for (int db = 0; db < NDB; ++db)
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(c.A[kk], sB[(rb * KK + kk) * 64 + lane],
-                                                               acc[rb], 0, 0, 0);
+                        for (int q = 0; q < 3; ++q) r[db][q] = sB3[((rb * NDB + db) * 3 + q) * 64 + lane];
+                };
+                if (SVGD_TCOL_PIPE) rows_of(0, rp[0]);
+#pragma unroll
+                for (int rb = 0; rb < 4; ++rb) {
+                    uint4 (&cur)[NDB][3] = rp[SVGD_TCOL_PIPE ? rb & 1 : 0];
+                    if (!SVGD_TCOL_PIPE) rows_of(rb, cur);
+                    else if (rb + 1 < 4) rows_of(rb + 1, rp[(rb + 1) & 1]);
+#pragma unroll
+                    for (int tm = 0; tm < 6; ++tm)
+#pragma unroll
+                        for (int db = 0; db < NDB; ++db)
+                            acc[rb] = SW ? kb3_mfma(cur[db][KB3_TA[tm]], c.A3[db][KB3_TB[tm]], acc[rb])
+                                         : kb3_mfma(c.A3[db][KB3_TA[tm]], cur[db][KB3_TB[tm]], acc[rb]);
+                }
+            };
+            if (swp)
+                gram(std::true_type{});
+            else
+                gram(std::false_type{});
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+                for (int rb = 0; rb < 4; ++rb)
+                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(c.A[kk], sB[(rb * KK + kk) * 64 + lane],
+                                                                   acc[rb], 0, 0, 0);
+        }
         const bool diag = p.s == 0;
+        const float hq = B3K && j0 - 4 * kq + ql < n32 ? -c.nq : ninf; // column 16 w + ql
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
             // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): the same roundings,
-            // half the instructions
+            // half the instructions; (-n_i) + (-n_j) in either lane map
             typedef float f2 __attribute__((ext_vector_type(2)));
-            const f2 hh = {hr[rb], hr[rb]}, two = {2.0f, 2.0f};
-            const f2 t01 = hh + f2{hc[0], hc[1]}, t23 = hh + f2{hc[2], hc[3]};
+            const f2 two = {2.0f, 2.0f};
+            f2 t01, t23;
+            if (B3K && swp) { // row 16 rb + 4 kq + r, column ql
+                const f4 hn = *reinterpret_cast<const f4 *>(sNr + 16 * rb + 4 * kq);
+                const f2 qq = {hq, hq};
+                t01 = f2{hn[0], hn[1]} + qq;
+                t23 = f2{hn[2], hn[3]} + qq;
+            } else {
+                const f2 hh = {hr[rb], hr[rb]};
+                t01 = hh + f2{hc[0], hc[1]};
+                t23 = hh + f2{hc[2], hc[3]};
+            }
             const f2 v01 = __builtin_elementwise_fma(two, f2{acc[rb][0], acc[rb][1]}, t01);
             const f2 v23 = __builtin_elementwise_fma(two, f2{acc[rb][2], acc[rb][3]}, t23);
             const f4 v = {v01[0], v01[1], v23[0], v23[1]};
@@ -777,9 +843,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     auto rows = [&](int I) {
         const int ib = I * TB;
         __syncthreads(); // every wave is done with the previous row
-        for (int e = tid; e < 4 * KK * 64; e += 256) {
-            const int l = e & 63, kk = (e >> 6) % KK, rb = (e >> 6) / KK;
-            sB[e] = xc[(int64_t)(ib + 16 * rb + (l & 15)) * KP + kslot<float, KP>(kk, l >> 4)];
+        if constexpr (B3K) {
+            // the 4 row blocks' parts are contiguous in xk: a straight copy
+            const uint4 *src = reinterpret_cast<const uint4 *>(xk + (int64_t)I * 4 * kb3_block_words(KP));
+            for (int e = tid; e < 4 * NDB * 3 * 64; e += 256) sB3[e] = src[e];
+            if (tid < 64) sNr[tid] = ib + tid < n32 ? -nrm[ib + tid] : ninf;
+        } else {
+            for (int e = tid; e < 4 * KK * 64; e += 256) {
+                const int l = e & 63, kk = (e >> 6) % KK, rb = (e >> 6) / KK;
+                sB[e] = xc[(int64_t)(ib + 16 * rb + (l & 15)) * KP + kslot<float, KP>(kk, l >> 4)];
+            }
         }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
@@ -850,16 +923,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 
 #define SVGD_TCOL_CASE(KPv)                                                                  \
     case KPv:                                                                                \
-        hipLaunchKernelGGL((k_pair_tcol<KPv>), dim3(grid), dim3(256), 0, stream, xc, nrm, n, nb, \
-                           t0, t1, sc);                                                      \
+        hipLaunchKernelGGL((k_pair_tcol<KPv>), dim3(grid), dim3(256), 0, stream, xc, nrm, xk, n, \
+                           nb, t0, t1, sc);                                                  \
         break;
 
-hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, int64_t n,
-                            int64_t nb, int64_t t0, int64_t t1, uint64_t *regions, int64_t cap,
-                            uint32_t *counts, unsigned long long *below, const SelState *st,
-                            uint32_t *bpart, hipStream_t stream)
+hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, const uint32_t *xk,
+                            int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                            int64_t cap, uint32_t *counts, unsigned long long *below,
+                            const SelState *st, uint32_t *bpart, hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
+    if (kb3_keys(KP) && !xk) return hipErrorInvalidValue;
     SinkCollect sc{st, regions, cap, counts, below, nullptr, nullptr, bpart};
     switch (KP) {
         SVGD_TCOL_CASE(4)

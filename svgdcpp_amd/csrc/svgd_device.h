@@ -69,6 +69,55 @@ __device__ __forceinline__ void tile_coords(int64_t nb, int64_t t, int64_t *I, i
     *J = slot == 0 ? *I : (*I + slot) % nb;
 }
 
+// ------------------------------------------ F32 pair keys for d > 16 (B3) --
+//
+// SVGD_F32 with KP in {32, 64}: the Gram of every pair key is formed on the
+// bf16 matrix cores (16x the fp32 MFMA rate) from the exact three-part bf16
+// split of the fp32 centred coordinates, x = h + m + l, with the six part
+// products that reach 2^-24 of each product (as k_phi_b3).  The key of a
+// pair i < j is DEFINED by this sequence, and every pass over the keys (the
+// matrix-core collect k_pair_tcol, k_pair_tiles' collect / radix / debug /
+// sample modes) runs it, so they agree bit for bit:
+//   dot = 0; for tm = 0..5 (mm, hl, lh, hm, mh, hh), for db = 0..KP/32 - 1:
+//     dot = v_mfma_f32_16x16x32_bf16(A = part KB3_TA[tm] of x_j, k-chunk db,
+//                                    B = part KB3_TB[tm] of x_i, k-chunk db, dot)
+//   s = max(fma(-2, dot, n_i + n_j), 0)
+// with x_j the particle of the LARGER index: the hm / mh terms are not
+// symmetric under the swap of the operand roles, so a tile whose column
+// block precedes its row block (the plan's wrapped tiles) swaps them.
+// Parts (k_swz_keys_b3, once per step from xcf), per 16-row block b:
+//   XK[b][db][part][lane][e] = part of xcf[16 b + lane % 16][32 db + 8 (lane / 16) + e]
+// (the A and B operand lane maps of the 16x16x32 MFMA coincide).
+constexpr int KB3_TA[6] = {1, 0, 2, 0, 1, 0}, KB3_TB[6] = {1, 2, 0, 1, 0, 0};
+__host__ __device__ constexpr bool kb3_keys(int KP) { return KP == 32 || KP == 64; }
+__host__ __device__ constexpr int kb3_block_words(int KP) { return (KP / 32) * 3 * 256; }
+typedef __bf16 kb3_bf16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f4_t kb3_mfma(uint4 a, uint4 b, f4_t c)
+{
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(kb3_bf16x8_t, a),
+                                                   __builtin_bit_cast(kb3_bf16x8_t, b), c, 0, 0, 0);
+}
+// One 16 x 16 block of dots from the parts in memory (global or LDS): pa =
+// the larger-index block's parts, pb = the other's, each at + lane * 4.
+template <int KP> __device__ __forceinline__ f4_t kb3_dot(const uint32_t *pa, const uint32_t *pb)
+{
+    constexpr int NDB = KP / 32;
+    uint4 a[NDB][3], b[NDB][3];
+#pragma unroll
+    for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+            a[db][p] = *reinterpret_cast<const uint4 *>(pa + (db * 3 + p) * 256);
+            b[db][p] = *reinterpret_cast<const uint4 *>(pb + (db * 3 + p) * 256);
+        }
+    f4_t dot = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int tm = 0; tm < 6; ++tm)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) dot = kb3_mfma(a[db][KB3_TA[tm]], b[db][KB3_TB[tm]], dot);
+    return dot;
+}
+
 struct SinkCollect {
     const SelState *st; // bracket [st->lo_key, st->hi_key)
     uint64_t *region; // this block's region (capacity cap)

@@ -49,7 +49,8 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
                               unsigned long long *bzero, hipStream_t stream,
-                              SelState *st_out = nullptr, const SelState *st_init = nullptr);
+                              SelState *st_out = nullptr, const SelState *st_init = nullptr,
+                              bool partials_ready = false);
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);
@@ -69,13 +70,19 @@ hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, co
                                  int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                                  int64_t cap, uint32_t *counts, unsigned long long *below,
                                  const SelState *st, unsigned long long *ghist, uint32_t *bpart,
-                                 double *dbg_out, hipStream_t stream);
+                                 double *dbg_out, const uint32_t *xk, hipStream_t stream);
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream);
 // Sampled median keys on the tile path: ntiles random (block, block) pairs of
 // distinct full 64-particle blocks, all 64 x 64 keys each (xcf/nrmf: fp32 path)
+// xk: the F32 key parts when KP is 32 or 64 (launch_swz_keys_b3), else null
 hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, const float *xcf,
-                               const float *nrmf, int64_t n, int64_t ntiles, uint64_t *keys,
-                               hipStream_t stream);
+                               const float *nrmf, const uint32_t *xk, int64_t n, int64_t ntiles,
+                               uint64_t *keys, hipStream_t stream);
+// The F32 median's key parts for KP = 32 / 64 (svgd_device.h "F32 pair keys"):
+// np / 16 blocks of kb3_block_words(KP) dwords from xcf (stride KP); np % 16 == 0
+hipError_t launch_swz_keys_b3(const float *xcf, int KP, int64_t np, uint32_t *XK, hipStream_t stream);
+// dwords of those parts for np rows; 0 when the keys at this KP are the fp32-MFMA ones
+int64_t median_key_part_words(int KP, int64_t np);
 // bak (optional, 3 cnt doubles): X_t, m_t, v_t of the cnt elements, saved in the pass
 // One optimizer step over cnt = rows x d elements of this rank (X, m, v at
 // the rank's rows): Adam (kind 0) / AdaGrad (1) / RMSProp (2) + clamp.
@@ -87,7 +94,15 @@ struct OptArgs {
     const double *lower, *upper; // clamp bounds (both or neither)
     double *bak;                 // X_t, m_t, v_t saved here when set (speculative step)
     double *xh = nullptr;        // X_{t+1} also stored here when set (pinned host mirror)
+    // k_phi_reduce only: per-block column sums of X_{t+1} (its rows, in row
+    // order) at xsum[block * d + k] -- the next step's mean partials, so its
+    // centring needs no k_mean_partial -- and *nmax_zero = 0 (k_center's
+    // atomicMax target; set on the LAST reduce launch of a step only)
+    double *xsum = nullptr;
+    unsigned long long *nmax_zero = nullptr;
 };
+// Blocks of k_phi_reduce (= mean partials written through OptArgs::xsum) for nrows rows
+int64_t phi_reduce_blocks(int d, int64_t nrows);
 hipError_t launch_opt_update(const OptArgs &o, const double *g, hipStream_t stream);
 // mode 0: collect keys in [st->lo_key, st->hi_key) into per-block regions and count
 // keys below lo_key; mode 1: radix histogram pass over all pairs (fallback);
@@ -263,11 +278,12 @@ hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
                             unsigned long long *below, const SelState *st, uint32_t *bpart,
                             bool bf16, hipStream_t stream);
 // fp32 tile-path collect (k_pair_tiles<float> MODE 0 on the matrix cores,
-// same keys): one region per block; KP in {4, 8, 12, 16, 32, 64}
-hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, int64_t n,
-                            int64_t nb, int64_t t0, int64_t t1, uint64_t *regions, int64_t cap,
-                            uint32_t *counts, unsigned long long *below, const SelState *st,
-                            uint32_t *bpart, hipStream_t stream);
+// same keys): one region per block; KP in {4, 8, 12, 16, 32, 64}; xk: the
+// key parts at KP 32 / 64 (bf16 part-product keys), else unused
+hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, const uint32_t *xk,
+                            int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
+                            int64_t cap, uint32_t *counts, unsigned long long *below,
+                            const SelState *st, uint32_t *bpart, hipStream_t stream);
 // F32 tile phi, streamed (k_phi_f32s): operand-ordered fp32 copies of the
 // columns (XS, VS: ntiles = ceil(n / 32) tiles of 32 particles; XS holds
 // ntiles * 32 * KP floats, VS ntiles * 2 * (VW/16 + 1) * 256) made by

@@ -549,7 +549,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(SVGD_PH
 
 // bak (optional, the speculative step): bak[0..cnt) = X_t, bak[cnt..2cnt) =
 // m_t, bak[2cnt..3cnt) = v_t of these elements, written in the same pass.
-__device__ __forceinline__ void opt_elem(const OptArgs &o, int64_t e, double ge)
+__device__ __forceinline__ double opt_elem(const OptArgs &o, int64_t e, double ge)
 {
 #pragma clang fp contract(off)
     double *__restrict__ m = o.m, *__restrict__ v = o.v, *__restrict__ X = o.X;
@@ -582,6 +582,7 @@ __device__ __forceinline__ void opt_elem(const OptArgs &o, int64_t e, double ge)
     }
     X[e] = x;
     if (o.xh) o.xh[e] = x; // the host gradient's copy of X_{t+1} (no D2H copy)
+    return x;
 }
 
 __global__ void k_opt_update(OptArgs o, const double *__restrict__ g)
@@ -616,9 +617,13 @@ template <class T, int KP, int MODE>
 __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
                                                    const T *__restrict__ nrm, int64_t n,
                                                    int64_t nb, int64_t t0, int64_t t1,
-                                                   SinkCollect sc, SinkHist sh, SinkDebug sd)
+                                                   SinkCollect sc, SinkHist sh, SinkDebug sd,
+                                                   const uint32_t *__restrict__ xk)
 {
     typedef typename Acc4<T>::type A4;
+    // F32 at KP 32 / 64: the bf16 part-product keys from the key parts xk
+    // (svgd_device.h), no X tiles in LDS
+    constexpr bool B3K = sizeof(T) == 4 && kb3_keys(KP);
     // fp64: the X tiles j-major with row stride LDK (an odd multiple of 4
     // doubles: the MFMA operand reads of 16 rows x 4 columns hit distinct
     // banks, the fill is a straight 16-byte copy) -- 70 KB instead of 80 KB
@@ -626,7 +631,7 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     // fp32 keeps the k-major tiles (its kslot order would conflict j-major)
     constexpr bool JM = sizeof(T) == 8 && (KP / 4) % 2 == 0;
     constexpr int LDK = PhiTile<T, KP>::LDK;
-    constexpr int XT = JM ? TB * LDK : KP * LDP;
+    constexpr int XT = B3K ? 4 : JM ? TB * LDK : KP * LDP;
     __shared__ __attribute__((aligned(16))) T sXI[XT];
     __shared__ __attribute__((aligned(16))) T sXJ[XT];
     __shared__ T sNI[TB], sNJ[TB];
@@ -699,7 +704,8 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     uint4 preQ[PQ];
     T preN = (T)0;
     auto fetch = [&](int64_t Jn) {
-        if constexpr (JM) {
+        if constexpr (B3K) {
+        } else if constexpr (JM) {
 #pragma unroll
             for (int u = 0; u < PQ; ++u)
                 preQ[u] = reinterpret_cast<const uint4 *>(xc + Jn * TB * KP)[tid + 256 * u];
@@ -725,7 +731,8 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
     for (int64_t t = tb; t < te; ++t) {
         __syncthreads();
         if (I != curI) {
-            if constexpr (JM) {
+            if constexpr (B3K) {
+            } else if constexpr (JM) {
                 for (int e = tid; e < TB * KP / EP; e += 256)
                     put(sXI, e, reinterpret_cast<const uint4 *>(xc + I * TB * KP)[e]);
             } else {
@@ -736,7 +743,8 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
             }
             if (tid < TB) sNI[tid] = nrm[I * TB + tid];
         }
-        if constexpr (JM) {
+        if constexpr (B3K) {
+        } else if constexpr (JM) {
 #pragma unroll
             for (int u = 0; u < PQ; ++u) put(sXJ, tid + 256 * u, preQ[u]);
         } else {
@@ -756,27 +764,37 @@ __global__ __launch_bounds__(256) void k_pair_tiles(const T *__restrict__ xc,
         }
 
         const bool full = Ic != Jc && (Ic + 1) * TB <= n && (Jc + 1) * TB <= n;
-        T bI[KP / 4];
+        T bI[B3K ? 1 : KP / 4];
+        if constexpr (!B3K) {
 #pragma unroll
-        for (int kk = 0; kk < KP / 4; ++kk)
-            bI[kk] = JM ? sXI[(w * 16 + lo) * LDK + kslot<T, KP>(kk, hi)]
-                        : sXI[kslot<T, KP>(kk, hi) * LDP + w * 16 + lo];
-        const int il = w * 16 + lo;
-        const int64_t i = Ic * TB + il;
-        const T ni = sNI[il];
+            for (int kk = 0; kk < KP / 4; ++kk)
+                bI[kk] = JM ? sXI[(w * 16 + lo) * LDK + kslot<T, KP>(kk, hi)]
+                            : sXI[kslot<T, KP>(kk, hi) * LDP + w * 16 + lo];
+        }
+        // B3K, a wrapped tile (J < I): the rows take the A role (larger
+        // indices), so the lane map is transposed: row 4 hi + r, column lo
+        const bool swp = B3K && Jc < Ic;
 
 #pragma unroll
         for (int js = 0; js < 4; ++js) {
             A4 dot = {0, 0, 0, 0};
+            if constexpr (B3K) {
+                const uint32_t *pr = xk + (Ic * 4 + w) * kb3_block_words(KP) + lane * 4;
+                const uint32_t *pc = xk + (Jc * 4 + js) * kb3_block_words(KP) + lane * 4;
+                dot = kb3_dot<KP>(swp ? pr : pc, swp ? pc : pr);
+            } else {
 #pragma unroll
-            for (int kk = 0; kk < KP / 4; ++kk)
-                dot = mfma16(JM ? sXJ[(js * 16 + lo) * LDK + kslot<T, KP>(kk, hi)]
-                                : sXJ[kslot<T, KP>(kk, hi) * LDP + js * 16 + lo],
-                             bI[kk], dot);
+                for (int kk = 0; kk < KP / 4; ++kk)
+                    dot = mfma16(JM ? sXJ[(js * 16 + lo) * LDK + kslot<T, KP>(kk, hi)]
+                                    : sXJ[kslot<T, KP>(kk, hi) * LDP + js * 16 + lo],
+                                 bI[kk], dot);
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int jl = js * 16 + acc_row<T>(hi, r);
-                const int64_t j = Jc * TB + jl;
+                const int jl = swp ? js * 16 + lo : js * 16 + acc_row<T>(hi, r);
+                const int il = swp ? w * 16 + acc_row<T>(hi, r) : w * 16 + lo;
+                const int64_t i = Ic * TB + il, j = Jc * TB + jl;
+                const T ni = sNI[il];
                 if constexpr (MODE == 0) {
                     // off-diagonal tiles of two full blocks (all but a few):
                     // every pair is valid
@@ -3146,6 +3164,34 @@ __global__ void k_swz_b3(const double *__restrict__ x, const double *__restrict_
     }
 }
 
+// The key parts of the F32 median (d > 16, svgd_device.h "F32 pair keys"):
+// one thread per (16-row block, 32-k chunk, lane), 8 coordinates split
+// into their three bf16 parts (round to nearest: exact, as k_swz_b3).
+template <int KP>
+__global__ __launch_bounds__(256) void k_swz_keys_b3(const float *__restrict__ xcf, int64_t nblk,
+                                                     uint32_t *__restrict__ XK)
+{
+    constexpr int NDB = KP / 32;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nblk * NDB * 64;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int lane = (int)(e & 63);
+        const int64_t r = e >> 6;
+        const int db = (int)(r % NDB);
+        const int64_t b = r / NDB;
+        const float4 *src = reinterpret_cast<const float4 *>(xcf + (16 * b + (lane & 15)) * KP + 32 * db + 8 * (lane >> 4));
+        const float4 p = src[0], q = src[1];
+        float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+        uint4 *o = reinterpret_cast<uint4 *>(XK + (b * NDB + db) * 3 * 256) + lane;
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+            uint32_t w[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[k] = b3_split_pair(v[2 * k], v[2 * k + 1]);
+            o[part * 64] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
 typedef __bf16 b16x8_t __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ f4_t mfma_b3(uint4 a, uint4 b, f4_t c)
 {
@@ -3361,15 +3407,31 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
         sm[e] = acc;
     }
     __syncthreads();
+    __shared__ double sx[256]; // X_{t+1} of the block's rows (OptArgs::xsum)
     for (int o = threadIdx.x; o < rows * d; o += blockDim.x) {
         const int r = o / d, k = o - r * d;
         const int64_t li = rb + r;
         const double w = wv ? wv[(row0 + li) * d + k] : two_a * rec[(row0 + li) * RS + k];
         const double ph = inv_n * (sm[r * DP + k] + w * sm[r * DP + d]);
         phi[li * d + k] = ph;
-        if (do_opt) opt_elem(opt, li * d + k, ph);
+        if (do_opt) {
+            const double x = opt_elem(opt, li * d + k, ph);
+            if (opt.xsum) sx[o] = x; // (rows * d < 256: one element per thread)
+        }
+    }
+    if (do_opt && opt.xsum) {
+        // the next step's mean partials: this block's column sums in row order
+        if (opt.nmax_zero && blockIdx.x == 0 && threadIdx.x == 0) *opt.nmax_zero = 0;
+        __syncthreads();
+        if (threadIdx.x < d) {
+            double c = 0.0;
+            for (int r = 0; r < rows; ++r) c += sx[r * d + threadIdx.x];
+            opt.xsum[(int64_t)blockIdx.x * d + threadIdx.x] = c;
+        }
     }
 }
+
+int64_t phi_reduce_blocks(int d, int64_t nrows) { return (nrows + phi_red_rows(d) - 1) / phi_red_rows(d); }
 
 // Median pair sweep, row-stream form: each wave walks a contiguous run of the
 // rank's block tiles (plan.cpp); lane = particle i of the row block, j of the
@@ -4184,16 +4246,16 @@ hipError_t launch_phi_f32(int KP, int NCB, const float *xg, const float *cvec, c
     if (KP == KPv) {                                                                         \
         if (mode == 0)                                                                       \
             hipLaunchKernelGGL((k_pair_tiles<T, KPv, 0>), dim3(grid), dim3(256), 0, stream,  \
-                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd, xk);                          \
         else if (mode == 1)                                                                  \
             hipLaunchKernelGGL((k_pair_tiles<T, KPv, 1>), dim3(grid), dim3(256), 0, stream,  \
-                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd, xk);                          \
         else if (mode == 2)                                                                  \
             hipLaunchKernelGGL((k_pair_tiles<T, KPv, 2>), dim3(grid), dim3(256), 0, stream,  \
-                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd, xk);                          \
         else                                                                                 \
             hipLaunchKernelGGL((k_pair_tiles<T, KPv, 3>), dim3(grid), dim3(256), 0, stream,  \
-                               xc, nrm, n, nb, t0, t1, sc, sh, sd);                          \
+                               xc, nrm, n, nb, t0, t1, sc, sh, sd, xk);                          \
         return hipGetLastError();                                                            \
     }
 
@@ -4203,9 +4265,12 @@ static hipError_t launch_pair_tiles_t(int KP, int mode, int grid, const T *xc, c
                                       uint64_t *regions, int64_t cap, uint32_t *counts,
                                       unsigned long long *below, const SelState *st,
                                       unsigned long long *ghist, uint32_t *bpart, double *dbg_out,
-                                      hipStream_t stream, uint64_t *sample_out = nullptr)
+                                      hipStream_t stream, uint64_t *sample_out = nullptr,
+                                      const uint32_t *xk = nullptr)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
+    // F32 keys at KP 32 / 64 are the bf16 part-product keys: their parts are required
+    if (sizeof(T) == 4 && kb3_keys(KP) && !xk) return hipErrorInvalidValue;
     SinkCollect sc{st, regions, cap, counts, below, nullptr, nullptr, mode == 0 ? bpart : nullptr};
     SinkHist sh{st, ghist};
     SinkDebug sd{dbg_out, n, sample_out};
@@ -4233,22 +4298,22 @@ hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, co
                                  int64_t n, int64_t nb, int64_t t0, int64_t t1, uint64_t *regions,
                                  int64_t cap, uint32_t *counts, unsigned long long *below,
                                  const SelState *st, unsigned long long *ghist, uint32_t *bpart,
-                                 double *dbg_out, hipStream_t stream)
+                                 double *dbg_out, const uint32_t *xk, hipStream_t stream)
 {
     return launch_pair_tiles_t<float>(KP, mode, grid, xc, nrm, n, nb, t0, t1, regions, cap,
-                                      counts, below, st, ghist, bpart, dbg_out, stream);
+                                      counts, below, st, ghist, bpart, dbg_out, stream, nullptr, xk);
 }
 
 hipError_t launch_sample_tiles(int KP, const double *xc, const double *nrm, const float *xcf,
-                               const float *nrmf, int64_t n, int64_t ntiles, uint64_t *keys,
-                               hipStream_t stream)
+                               const float *nrmf, const uint32_t *xk, int64_t n, int64_t ntiles,
+                               uint64_t *keys, hipStream_t stream)
 {
     if (n / TB < 2 || ntiles <= 0) return hipErrorInvalidValue;
     const int grid = (int)(ntiles < 1024 ? ntiles : 1024);
     if (xcf)
         return launch_pair_tiles_t<float>(KP, 3, grid, xcf, nrmf, n, 0, 0, ntiles, nullptr, 0,
                                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                          stream, keys);
+                                          stream, keys, xk);
     return launch_pair_tiles_t<double>(KP, 3, grid, xc, nrm, n, 0, 0, ntiles, nullptr, 0, nullptr,
                                        nullptr, nullptr, nullptr, nullptr, nullptr, stream, keys);
 }
@@ -4292,6 +4357,21 @@ hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, co
 
 bool phi_b3_supported(int KP, int NCB) { return (KP == 32 || KP == 64) && NCB >= 1 && NCB <= 5; }
 int64_t phi_b3_tile_words(int KP, int NCB) { return (int64_t)(6 * (KP / 32) + 3 * NCB + 2) * 256; }
+
+int64_t median_key_part_words(int KP, int64_t np) { return kb3_keys(KP) ? (np / 16) * kb3_block_words(KP) : 0; }
+
+hipError_t launch_swz_keys_b3(const float *xcf, int KP, int64_t np, uint32_t *XK, hipStream_t stream)
+{
+    if (!kb3_keys(KP) || np % 16 || np <= 0) return hipErrorInvalidValue;
+    const int64_t tot = (np / 16) * (KP / 32) * 64;
+    int64_t g = (tot + 255) / 256;
+    if (g > 8192) g = 8192;
+    if (KP == 32)
+        hipLaunchKernelGGL(k_swz_keys_b3<32>, dim3(g), dim3(256), 0, stream, xcf, np / 16, XK);
+    else
+        hipLaunchKernelGGL(k_swz_keys_b3<64>, dim3(g), dim3(256), 0, stream, xcf, np / 16, XK);
+    return hipGetLastError();
+}
 
 hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const double *cvec,
                          int64_t n, int64_t ntiles, uint32_t *B3, hipStream_t stream)
@@ -4352,12 +4432,15 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
                               unsigned long long *bzero, hipStream_t stream, SelState *st_out,
-                              const SelState *st_init)
+                              const SelState *st_init, bool partials_ready)
 {
     const SelState sinit = st_init ? *st_init : SelState{};
     if (!st_init) st_out = nullptr;
-    hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial,
-                       xf ? nmax_bits : nullptr);
+    // partials_ready: the last update epilogue left X's column partials (and
+    // zeroed nmax_bits) -- k_phi_reduce's OptArgs::xsum
+    if (!partials_ready)
+        hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial,
+                           xf ? nmax_bits : nullptr);
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
 #define SVGD_CENTER_CASE(Dv)                                                                  \
