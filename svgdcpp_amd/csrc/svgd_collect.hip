@@ -53,6 +53,13 @@ constexpr int MC_NG = 4;    // 16-row blocks per classification group
 #ifndef SVGD_MCOL_STAGE
 #define SVGD_MCOL_STAGE 1
 #endif
+// Off-diagonal classification form: 0 = lane masks (v_cmp into SGPRs, the
+// below count and the band OR on the scalar unit), 1 = sign bits on the
+// vector unit (v_pk_add_f32 of TLf - v and THf - v, a per-lane below count,
+// the band as (THf - v) & ~(TLf - v): no scalar work per block)
+#ifndef SVGD_MCOL_CLS
+#define SVGD_MCOL_CLS 0
+#endif
 
 __device__ __forceinline__ float f32_up(double x)
 {
@@ -113,6 +120,28 @@ __device__ __forceinline__ unsigned long long mcol_classify4(const f4_t &v, floa
                  : "scc");
     return any;
 }
+// SVGD_MCOL_CLS = 1: the same classes from sign bits.  For finite v and
+// thresholds, fl(T - v) < 0 (sign set, -0 included) <=> v > T (a difference of
+// distinct floats is never +0), T = +inf gives +inf (never), v = -inf (padding)
+// gives +inf (never); so the sign of TLf - v is "below" and the sign of
+// (THf - v) & ~(TLf - v) "band", as mcol_classify4's masks.  cnt += the
+// lane's below values; b[r] carry the band bits in their signs.
+__device__ __forceinline__ void mcol_classify4v(const f4_t &v, float tl, float th, uint32_t &cnt,
+                                                uint32_t (&b)[4])
+{
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 tl2 = {tl, tl}, th2 = {th, th};
+    const f2 v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
+    const f2 a01 = tl2 - v01, a23 = tl2 - v23, t01 = th2 - v01, t23 = th2 - v23;
+    const uint32_t a[4] = {__float_as_uint(a01[0]), __float_as_uint(a01[1]), __float_as_uint(a23[0]),
+                           __float_as_uint(a23[1])};
+    const uint32_t t[4] = {__float_as_uint(t01[0]), __float_as_uint(t01[1]), __float_as_uint(t23[0]),
+                           __float_as_uint(t23[1])};
+    cnt += (a[0] >> 31) + (a[1] >> 31) + (a[2] >> 31) + (a[3] >> 31);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b[r] = t[r] & ~a[r];
+}
+
 // Diagonal tiles (1 in nb/2 of them): lanes with xl > c (j > i) only.
 // Returns the band lanes of the value.
 __device__ __forceinline__ unsigned long long mcol_classify_diag(float v, float tl, float th, int xl,
@@ -226,6 +255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     uint64_t *wregion = sc.region + wreg * sc.cap;
     int64_t wcnt = 0;             // keys written to the region
     unsigned long long below = 0; // below count (scalar: classified + exact)
+    uint32_t vbelow = 0;          // SVGD_MCOL_CLS = 1: this lane's classified below values
     int scnt = 0;                 // staged band pairs
     bool ovf = false;             // a group outgrew the staging area
 
@@ -478,6 +508,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                                               16 * (g0 + g) - jl0 - r, nbelow);
                                     any |= h[r];
                                 }
+                            } else if constexpr (SVGD_MCOL_CLS == 1) {
+                                uint32_t bv[4];
+                                mcol_classify4v(acc[g], Bg[g][TI], Bg[g][TI + 1], vbelow, bv);
+                                any = __ballot((int)(bv[0] | bv[1] | bv[2] | bv[3]) < 0);
+                                if (__builtin_expect(any != 0, 0)) {
+                                    // the lane masks the staging takes (rare)
+#pragma unroll
+                                    for (int r = 0; r < 4; ++r) h[r] = __ballot((int)bv[r] < 0);
+                                }
                             } else {
                                 any = mcol_classify4(acc[g], Bg[g][TI], Bg[g][TI + 1], nbelow, h);
                             }
@@ -536,6 +575,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
         } while (advance(pos));
     }
 
+    if (SVGD_MCOL_CLS == 1) { // the lanes' classified below counts
+        unsigned long long vb = vbelow;
+        for (int o = 32; o > 0; o >>= 1) vb += __shfl_xor(vb, o);
+        below += vb;
+    }
     if (lane == 0) {
         sc.below_out[wreg] = below;
         // an overflowed staging area reports an overflowed region: the host

@@ -25,13 +25,4 @@ head -6 $O/rocprof_cfg5_kernel_timed.txt
 CONFIGS="cfg2" bash tools/gpu_timeline.sh || exit 1
 cp gpurun_out/timeline/cfg2.txt $O/step_timeline_cfg2.txt
 cat $O/step_timeline_cfg2.txt
-LIB=svgdcpp_amd/libsvgdcpp_amd.so
-cp $LIB $O/.cur.so
-for i in 1 2; do
-  for v in tcol0 tcolpipe; do
-    cp tools/ablibs/$v.so $LIB
-    b ab_${v}_$i 300 --config cfg5 --steps 20 --warmup 3 --no-cpu --repeats 3 || { cp $O/.cur.so $LIB; exit 1; }
-  done
-done
-cp $O/.cur.so $LIB
 echo r4m done
