@@ -271,13 +271,17 @@ struct svgd_ctx {
     bool xmirror = false, xh_valid = false, ghost = false, ghost_step = false;
     // Mean partials from the update epilogue (one rank, row path, not the
     // symmetric pass): k_phi_reduce leaves X_{t+1}'s per-block column sums in
-    // xsum (xsum_parts blocks) and zeroes nmax, so the next centring skips
-    // k_mean_partial.  xsum_valid from the reduce's enqueue to the next
-    // centring; cleared by anything else that moves X (svgd_set_particles, a
-    // redo).  SVGD_XSUM=0 turns it off.
-    double *xsum = nullptr;
-    int xsum_parts = 0;
-    bool xsum_valid = false, xsum_written = false;
+    // xsum (xsum_parts blocks) and zeroes nmax, so the next centrings skip
+    // k_mean_partial (a repeated centring of the same X re-forms the same
+    // max into nmax).  Two buffers: xsum_cur holds the current X's partials
+    // (valid from the reduce's enqueue until anything else moves X: the next
+    // update, svgd_set_particles), the other the previous X's -- which a
+    // redo (X_t restored) returns to, so a redone step centres exactly as
+    // the first attempt did.  SVGD_XSUM=0 turns it off.
+    double *xsum = nullptr; // 2 x xsum_stride
+    int64_t xsum_stride = 0;
+    int xsum_parts[2] = {0, 0}, xsum_cur = 0;
+    bool xsum_ok[2] = {false, false}, xsum_written = false;
     double *h_xm = nullptr, *h_xm_dev = nullptr;
     unsigned long long *h_cnt = nullptr;
     double *h_scal = nullptr;
@@ -632,10 +636,13 @@ int mark_median_end(svgd_ctx *c)
 
 int center(svgd_ctx *c, const SelState *st_init = nullptr)
 {
-    const bool pr = c->xsum_valid; // the last update epilogue's partials (svgd_ctx::xsum)
-    c->xsum_valid = false;
-    HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, pr ? c->xsum : c->partial,
-                                 pr ? c->xsum_parts : c->nparts, c->xc, c->nrm, c->rowpath ? 1 : 0,
+    // the last update epilogue's partials (svgd_ctx::xsum): they stay valid
+    // while X does, so every centring of one X forms the same mean
+    const int xs = c->xsum_cur;
+    const bool pr = c->xsum && c->xsum_ok[xs];
+    HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np,
+                                 pr ? c->xsum + xs * c->xsum_stride : c->partial,
+                                 pr ? c->xsum_parts[xs] : c->nparts, c->xc, c->nrm, c->rowpath ? 1 : 0,
                                  c->xf, c->nmax, c->cnt3 + 3, c->stream, c->st, st_init, pr));
     if (c->dtype == SVGD_F32) {
         HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
@@ -1355,7 +1362,8 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         o1.nmax_zero = nullptr; // the second part's phi still reads nmax
         if (o2.xsum) {
             o2.xsum += phi_reduce_blocks((int)d, h) * d;
-            c->xsum_parts = (int)(phi_reduce_blocks((int)d, h) + phi_reduce_blocks((int)d, c->nrows - h));
+            c->xsum_parts[1 - c->xsum_cur] =
+                (int)(phi_reduce_blocks((int)d, h) + phi_reduce_blocks((int)d, c->nrows - h));
             c->xsum_written = true;
         }
         o2.X += h * d;
@@ -1375,7 +1383,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         if (k2) c->ev_diag.push_back({k2, k3, DG_PHI_KERNEL, true});
     } else if (c->rowpath) {
         if (opt && opt->xsum) {
-            c->xsum_parts = (int)phi_reduce_blocks(c->dim, c->nrows);
+            c->xsum_parts[1 - c->xsum_cur] = (int)phi_reduce_blocks(c->dim, c->nrows);
             c->xsum_written = true;
         }
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
@@ -1480,13 +1488,20 @@ int run_phi_opt(svgd_ctx *c)
     const bool fused = c->rowpath || phi_streamed(c);
     c->phi_end = nullptr;
     c->xh_valid = false;
-    c->xsum_valid = c->xsum_written = false;
+    // X_{t+1}'s partials go to the other buffer (X_t's stay for a redo)
+    const int xn = 1 - c->xsum_cur;
+    c->xsum_ok[xn] = c->xsum_written = false;
     if (c->xsum && c->rowpath && !c->sym) {
-        o.xsum = c->xsum;
+        o.xsum = c->xsum + xn * c->xsum_stride;
         o.nmax_zero = c->nmax;
     }
     CHK(run_phi(c, fused ? &o : nullptr));
-    c->xsum_valid = c->xsum_written;
+    if (c->xsum_written) {
+        c->xsum_ok[xn] = true;
+        c->xsum_cur = xn;
+    } else {
+        c->xsum_ok[c->xsum_cur] = false; // X moved without partials
+    }
     if (!fused) {
         HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
         c->phi_end = nullptr;
@@ -1638,7 +1653,8 @@ int resolve_pending(svgd_ctx *c)
     c->t -= 1;
     c->spec_step = false;
     c->last_fast = false;
-    c->xsum_valid = false; // X_t is back: its partials are not the epilogue's
+    // X_t is back: so are its partials (the failed update wrote the other buffer)
+    if (c->xsum_written) c->xsum_cur = 1 - c->xsum_cur;
     CHK(scale_begin(c));
     CHK(scale_finish(c));
     CHK(run_phi_opt(c));
@@ -1831,7 +1847,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         }
         bool want_xsum = c->world == 1 && c->sim_world <= 1 && !c->sym;
         if (const char *e = std::getenv("SVGD_XSUM")) want_xsum = want_xsum && std::atoi(e) != 0;
-        if (want_xsum) CHK(dalloc(c, &c->xsum, (phi_reduce_blocks(dim, c->nrows) + 2) * dim));
+        if (want_xsum) {
+            c->xsum_stride = (phi_reduce_blocks(dim, c->nrows) + 2) * dim;
+            CHK(dalloc(c, &c->xsum, 2 * c->xsum_stride));
+        }
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
@@ -2239,7 +2258,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     c->have_particles = true;
     c->xhalf_ready = false;
     c->xh_valid = false;
-    c->xsum_valid = false;
+    c->xsum_ok[0] = c->xsum_ok[1] = false;
     c->trk_n = c->trk_nerr = 0; // new particles: the median history restarts
     return SVGD_OK;
 }

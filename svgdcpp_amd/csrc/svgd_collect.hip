@@ -616,6 +616,10 @@ constexpr int TC_STG = 512; // staged band values per wave (k_pair_tcol)
 #ifndef SVGD_TCOL_PIPE
 #define SVGD_TCOL_PIPE 0
 #endif
+// waves per SIMD asked of the bf16-key form (KP 32 / 64)
+#ifndef SVGD_TCOL_WPE
+#define SVGD_TCOL_WPE 2
+#endif
 
 // KP 32 / 64 (B3K): the bf16 part-product keys (svgd_device.h "F32 pair
 // keys"): per tile 6 KP/32 x 4 bf16 MFMAs of 16 cycles instead of KP x 4 f32
@@ -623,7 +627,7 @@ constexpr int TC_STG = 512; // staged band values per wave (k_pair_tcol)
 // tile row's parts in LDS (read once per row block and tile); a wrapped tile
 // (J < I) swaps the operand roles, which transposes the lane map.
 template <int KP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_tcol(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kb3_keys(KP) ? SVGD_TCOL_WPE : 4, 8))) void k_pair_tcol(
     const float *__restrict__ xc, const float *__restrict__ nrm, const uint32_t *__restrict__ xk,
     int64_t n, int64_t nb, int64_t t0, int64_t t1, SinkCollect sc)
 {

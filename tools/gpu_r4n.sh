@@ -17,7 +17,7 @@ b() { # name timeout args...
   tail -1 $O/$name.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); dg=d.get('diag_ms_per_step') or {}; print('$name', round(d['ms_per_step'],4), 'runs', [round(x,3) for x in d['repeats']['ms_per_step']], 'phases', {k: round(v,4) for k,v in (d.get('phases_ms_per_step') or {}).items()}, 'trk', d.get('tracked_brackets'), 'clk', (d.get('gpu_diag') or {}).get('gfxclk_mhz_median'))"
 }
 for i in 1 2; do
-  for v in tcol0 tcolpipe; do
+  for v in tcol0 tcolpipe tcolw3; do
     cp tools/ablibs/$v.so $LIB
     b ${v}_cfg5_$i 300 --config cfg5 --steps 20 --warmup 3 --no-cpu --repeats 3
   done
