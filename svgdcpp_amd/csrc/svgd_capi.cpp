@@ -646,7 +646,7 @@ int center(svgd_ctx *c, const SelState *st_init = nullptr)
                                  c->xf, c->nmax, c->cnt3 + 3, c->stream, c->st, st_init, pr));
     if (c->dtype == SVGD_F32) {
         HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
-        HIPCHK(c, launch_cvt_f32(c->nrm, c->np, c->nrmf, c->stream));
+        HIPCHK(c, launch_cvt_nrm_f32(c->nrm, c->n, c->np, c->nrmf, c->stream));
         if (c->XK) HIPCHK(c, launch_swz_keys_b3(c->xcf, c->KP, c->np, c->XK, c->stream));
     }
     return SVGD_OK;
@@ -1845,7 +1845,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             CHK(dalloc(c, &c->symok, 1));
             c->sym = true;
         }
-        bool want_xsum = c->world == 1 && c->sim_world <= 1 && !c->sym;
+        // only while k_center_d takes all the partials in one LDS sweep (its
+        // sequential loop over thousands of partials cost cfg3 0.17 ms)
+        bool want_xsum = c->world == 1 && c->sim_world <= 1 && !c->sym &&
+                         (phi_reduce_blocks(dim, c->nrows) + 1) * dim <= 1024;
         if (const char *e = std::getenv("SVGD_XSUM")) want_xsum = want_xsum && std::atoi(e) != 0;
         if (want_xsum) {
             c->xsum_stride = (phi_reduce_blocks(dim, c->nrows) + 2) * dim;

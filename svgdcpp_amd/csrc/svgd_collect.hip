@@ -613,27 +613,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
 // cycles).  Candidates (the band, ~0.3 %) go straight to the block's region.
 // Rows / columns >= n carry norm -inf: never below, never candidates.
 constexpr int TC_STG = 512; // staged band values per wave (k_pair_tcol)
-#ifndef SVGD_TCOL_PIPE
-#define SVGD_TCOL_PIPE 0
-#endif
-// waves per SIMD asked of the bf16-key form (KP 32 / 64)
-#ifndef SVGD_TCOL_WPE
-#define SVGD_TCOL_WPE 2
-#endif
 
-// KP 32 / 64 (B3K): the bf16 part-product keys (svgd_device.h "F32 pair
-// keys"): per tile 6 KP/32 x 4 bf16 MFMAs of 16 cycles instead of KP x 4 f32
-// ones of 32; the wave's column parts in VGPRs (from the key parts xk), the
-// tile row's parts in LDS (read once per row block and tile); a wrapped tile
-// (J < I) swaps the operand roles, which transposes the lane map.
 template <int KP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kb3_keys(KP) ? SVGD_TCOL_WPE : 4, 8))) void k_pair_tcol(
-    const float *__restrict__ xc, const float *__restrict__ nrm, const uint32_t *__restrict__ xk,
-    int64_t n, int64_t nb, int64_t t0, int64_t t1, SinkCollect sc)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_pair_tcol(
+    const float *__restrict__ xc, const float *__restrict__ nrm, int64_t n, int64_t nb, int64_t t0,
+    int64_t t1, SinkCollect sc)
 {
-    constexpr bool B3K = kb3_keys(KP);
-    constexpr int NDB = KP / 32;
-    constexpr int KK = B3K ? 1 : KP / 4;
+    constexpr int KK = KP / 4;
     __shared__ uint32_t sBk[NBK];
     __shared__ uint32_t sCnt;
     __shared__ unsigned long long sBelow[4];
@@ -673,20 +659,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kb3_keys(KP
     // the load would make the compiler wait for it (and the whole prefetch)
     struct Cols {
         float A[KK];
-        uint4 A3[B3K ? NDB : 1][3];
         f4 nv;
-        float nq; // B3K: the norm of column j0 + ql (transposed lane map)
     };
     auto load_cols = [&](int J, Cols &c) {
         const int64_t j0 = (int64_t)J * TB + 16 * w;
-        if constexpr (B3K) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(xk + ((int64_t)J * 4 + w) * kb3_block_words(KP)) + lane;
-#pragma unroll
-            for (int db = 0; db < NDB; ++db)
-#pragma unroll
-                for (int q = 0; q < 3; ++q) c.A3[db][q] = p[(db * 3 + q) * 64];
-            c.nq = nrm[j0 + ql];
-        } else if constexpr (KP % 16 == 0) { // kslot order: 16-byte loads
+        if constexpr (KP % 16 == 0) { // kslot order: 16-byte loads
             const float *xcol = xc + (j0 + ql) * KP + 4 * kq;
 #pragma unroll
             for (int u = 0; u < KK / 4; ++u) {
@@ -784,9 +761,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kb3_keys(KP
 
     // the tile row's B operands, shared by the block's 4 waves (written at a
     // row change, between barriers: every wave follows the same schedule)
-    __shared__ float sB[B3K ? 1 : 4 * KK * 64];
-    __shared__ uint4 sB3[B3K ? 4 * NDB * 3 * 64 : 1]; // [rb][db][part][lane]
-    __shared__ __attribute__((aligned(16))) float sNr[B3K ? 64 : 1]; // -n_i of the row (masked)
+    __shared__ float sB[4 * KK * 64];
     float hr[4];
     // one tile (I, J): 4 x KK MFMAs, then the classification
     auto tile = [&](const Pos &p, const Cols &c) {
@@ -797,65 +772,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kb3_keys(KP
         f4 acc[4];
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) acc[rb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-        // B3K: a wrapped tile (J < I) puts the rows (larger indices) in the A role
-        const bool swp = B3K && p.J < p.I;
-        if constexpr (B3K) {
-            auto gram = [&](auto swp_tag) {
-                constexpr bool SW = decltype(swp_tag)::value;
-                // the row block's parts from LDS; SVGD_TCOL_PIPE: row block
-                // rb + 1's reads issued before rb's MFMAs
-                uint4 rp[2][NDB][3];
-                auto rows_of = [&](int rb, uint4 (&r)[NDB][3]) {
 #pragma unroll
-                    for (int db = 0; db < NDB; ++db)
+        for (int kk = 0; kk < KK; ++kk)
 #pragma unroll
-                        for (int q = 0; q < 3; ++q) r[db][q] = sB3[((rb * NDB + db) * 3 + q) * 64 + lane];
-                };
-                if (SVGD_TCOL_PIPE) rows_of(0, rp[0]);
-#pragma unroll
-                for (int rb = 0; rb < 4; ++rb) {
-                    uint4 (&cur)[NDB][3] = rp[SVGD_TCOL_PIPE ? rb & 1 : 0];
-                    if (!SVGD_TCOL_PIPE) rows_of(rb, cur);
-                    else if (rb + 1 < 4) rows_of(rb + 1, rp[(rb + 1) & 1]);
-#pragma unroll
-                    for (int tm = 0; tm < 6; ++tm)
-#pragma unroll
-                        for (int db = 0; db < NDB; ++db)
-                            acc[rb] = SW ? kb3_mfma(cur[db][KB3_TA[tm]], c.A3[db][KB3_TB[tm]], acc[rb])
-                                         : kb3_mfma(c.A3[db][KB3_TA[tm]], cur[db][KB3_TB[tm]], acc[rb]);
-                }
-            };
-            if (swp)
-                gram(std::true_type{});
-            else
-                gram(std::false_type{});
-        } else {
-#pragma unroll
-            for (int kk = 0; kk < KK; ++kk)
-#pragma unroll
-                for (int rb = 0; rb < 4; ++rb)
-                    acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(c.A[kk], sB[(rb * KK + kk) * 64 + lane],
-                                                                   acc[rb], 0, 0, 0);
-        }
+            for (int rb = 0; rb < 4; ++rb)
+                acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(c.A[kk], sB[(rb * KK + kk) * 64 + lane],
+                                                               acc[rb], 0, 0, 0);
         const bool diag = p.s == 0;
-        const float hq = B3K && j0 - 4 * kq + ql < n32 ? -c.nq : ninf; // column 16 w + ql
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
             // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): the same roundings,
-            // half the instructions; (-n_i) + (-n_j) in either lane map
+            // half the instructions
             typedef float f2 __attribute__((ext_vector_type(2)));
-            const f2 two = {2.0f, 2.0f};
-            f2 t01, t23;
-            if (B3K && swp) { // row 16 rb + 4 kq + r, column ql
-                const f4 hn = *reinterpret_cast<const f4 *>(sNr + 16 * rb + 4 * kq);
-                const f2 qq = {hq, hq};
-                t01 = f2{hn[0], hn[1]} + qq;
-                t23 = f2{hn[2], hn[3]} + qq;
-            } else {
-                const f2 hh = {hr[rb], hr[rb]};
-                t01 = hh + f2{hc[0], hc[1]};
-                t23 = hh + f2{hc[2], hc[3]};
-            }
+            const f2 hh = {hr[rb], hr[rb]}, two = {2.0f, 2.0f};
+            const f2 t01 = hh + f2{hc[0], hc[1]}, t23 = hh + f2{hc[2], hc[3]};
             const f2 v01 = __builtin_elementwise_fma(two, f2{acc[rb][0], acc[rb][1]}, t01);
             const f2 v23 = __builtin_elementwise_fma(two, f2{acc[rb][2], acc[rb][3]}, t23);
             const f4 v = {v01[0], v01[1], v23[0], v23[1]};
@@ -891,16 +821,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kb3_keys(KP
     auto rows = [&](int I) {
         const int ib = I * TB;
         __syncthreads(); // every wave is done with the previous row
-        if constexpr (B3K) {
-            // the 4 row blocks' parts are contiguous in xk: a straight copy
-            const uint4 *src = reinterpret_cast<const uint4 *>(xk + (int64_t)I * 4 * kb3_block_words(KP));
-            for (int e = tid; e < 4 * NDB * 3 * 64; e += 256) sB3[e] = src[e];
-            if (tid < 64) sNr[tid] = ib + tid < n32 ? -nrm[ib + tid] : ninf;
-        } else {
-            for (int e = tid; e < 4 * KK * 64; e += 256) {
-                const int l = e & 63, kk = (e >> 6) % KK, rb = (e >> 6) / KK;
-                sB[e] = xc[(int64_t)(ib + 16 * rb + (l & 15)) * KP + kslot<float, KP>(kk, l >> 4)];
-            }
+        for (int e = tid; e < 4 * KK * 64; e += 256) {
+            const int l = e & 63, kk = (e >> 6) % KK, rb = (e >> 6) / KK;
+            sB[e] = xc[(int64_t)(ib + 16 * rb + (l & 15)) * KP + kslot<float, KP>(kk, l >> 4)];
         }
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
@@ -967,12 +890,344 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kb3_keys(KP
         for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
 }
 
+
+// ======================= F32 bf16-key collect (KP 32 / 64: d > 16, SVGD_F32) ==
+//
+// The bracket collect pass over the bf16 part-product keys (svgd_device.h
+// "F32 pair keys"; the keys k_pair_tiles<float> forms at these KP): per
+// 64 x 16 wave tile 4 x 6 KP/32 v_mfma_f32_16x16x32_bf16 of 16 cycles (the
+// fp32 form: 4 x KP/4 f32 MFMAs of 32).  The wave's 16 columns' parts in
+// VGPRs (from xk, the next tile's loading during the current one's MFMAs),
+// the tile row's 4 row blocks' parts in LDS (one 16-byte read per row
+// block, part and k chunk); a wrapped tile (J < I) gives the rows (the larger
+// indices) the A role, which transposes the lane map: row 4 kq + r, column ql.
+// Each tile kind (plain, wrapped, diagonal) is its own straight-line code.
+// Norms come from nrmf, whose padding rows hold +inf (launch_cvt_nrm_f32):
+// a padding row or column gives v = -inf, never below, never in the band.
+// Band values are staged one 16-byte entry per lane and row block (its 4
+// values, NaN where not a band value: a band value is never NaN), so a row
+// block with band values costs one masked-free store; the flush keys them.
+constexpr int TC3_ENT = 448; // staged entries per wave (+ 64 spill slots); a tile adds <= 256
+
+// XCD-banded tile schedule of the tile-path collects (k_pair_tcol's, as a
+// struct): the rank's tile rows I (plan.cpp: row I holds slots
+// 0..cnt(I)-1, J = I + slot mod nb) in bands of R rows dealt round-robin to
+// the 8 XCDs; inside a band the XCD's P blocks sweep the slots together
+// (block q keeps row I = band + q % R and takes slots q / R, q / R + S, ...).
+struct TileSched {
+    int nG, R, S, rr, ph, nb32, Ia, Ib, nbands;
+    int64_t t0, t1, half, c1, c2;
+    struct Pos {
+        int k, I, s, J, hi;
+    };
+    __device__ TileSched(int64_t nb, int64_t t0_, int64_t t1_) : t0(t0_), t1(t1_)
+    {
+        const int G = gridDim.x;
+        nG = (G % 8 == 0) ? 8 : 1;
+        const int P = G / nG, q = blockIdx.x / nG;
+        R = 32;
+        while (P % R) R >>= 1;
+        S = P / R;
+        rr = q % R;
+        ph = q / R;
+        nb32 = (int)nb;
+        const int64_t H = (nb - 1) / 2;
+        half = (nb & 1) == 0 ? nb / 2 : 0;
+        c1 = H + 2;
+        c2 = H + 1;
+        Ia = 0;
+        Ib = -1;
+        if (t1 > t0) {
+            int64_t I64, Jd;
+            tile_coords(nb, t0, &I64, &Jd);
+            Ia = (int)I64;
+            tile_coords(nb, t1 - 1, &I64, &Jd);
+            Ib = (int)I64;
+        }
+        nbands = (Ib - Ia + 1 + R - 1) / R;
+    }
+    __device__ Pos first() const { return Pos{(int)(blockIdx.x % nG), 0, 0, 0, 0}; }
+    // the first tile at or after band p.k (64-bit plan arithmetic once per row)
+    __device__ bool enter_row(Pos &p) const
+    {
+        for (; p.k < nbands; p.k += nG) {
+            const int I = Ia + p.k * R + rr;
+            if (I > Ib) continue;
+            const int64_t rs = I < half ? I * c1 : half * c1 + (I - half) * c2;
+            const int lo = (int)max<int64_t>(0, t0 - rs);
+            const int hi = (int)min<int64_t>(I < half ? c1 : c2, t1 - rs);
+            const int s = lo <= ph ? ph : ph + (lo - ph + S - 1) / S * S;
+            if (s < hi) {
+                p.I = I;
+                p.s = s;
+                p.hi = hi;
+                p.J = I + s >= nb32 ? I + s - nb32 : I + s;
+                return true;
+            }
+        }
+        return false;
+    }
+    __device__ bool advance(Pos &p) const
+    {
+        p.s += S;
+        if (p.s < p.hi) {
+            p.J = p.I + p.s >= nb32 ? p.I + p.s - nb32 : p.I + p.s;
+            return true;
+        }
+        p.k += nG;
+        return enter_row(p);
+    }
+};
+
+// 1 in the lanes whose bit is set in the wave mask m (one v_cndmask)
+__device__ __forceinline__ uint32_t lane_bit(unsigned long long m)
+{
+    uint32_t b;
+    asm volatile("v_cndmask_b32_e64 %0, 0, 1, %1" : "=v"(b) : "s"(m));
+    return b;
+}
+// v where the mask bit is set, else x (one v_cndmask)
+__device__ __forceinline__ float lane_sel(unsigned long long m, float v, float x)
+{
+    float r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(v), "s"(m));
+    return r;
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) void k_pair_tcol3(
+    const float *__restrict__ nrm, const uint32_t *__restrict__ xk, int64_t n, int64_t nb, int64_t t0,
+    int64_t t1, SinkCollect sc)
+{
+    constexpr int NDB = KP / 32;
+    static_assert(kb3_keys(KP), "the bf16-key collect takes KP 32 / 64");
+    __shared__ uint32_t sBk[NBK];
+    __shared__ uint32_t sCnt;
+    __shared__ unsigned long long sBelow[4];
+    __shared__ uint4 sB3[4 * NDB * 3 * 64];                   // [rb][db][part][lane]
+    __shared__ __attribute__((aligned(16))) float sNr[64];   // -n_i of the tile row
+    __shared__ f4 sStage[4][TC3_ENT + 64];                   // + the spill zone
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int kq = lane >> 4, ql = lane & 15;
+
+    const uint64_t lo_key = sc.st->lo_key, hi_key = sc.st->hi_key;
+    const double binv = sc.st->binv;
+    const double lo_d = __longlong_as_double((long long)lo_key);
+    const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
+                                                        : __longlong_as_double((long long)hi_key);
+    // the smallest floats >= the bracket's doubles (as k_pair_tiles), negated
+    // (k_pair_tcol's classification: v = fma(2, dot, -n_i - n_j) = -s)
+    float loT = (float)lo_d, hiT = (float)hi_d;
+    if ((double)loT < lo_d) loT = __int_as_float(__float_as_int(loT) + 1);
+    if ((double)hiT < hi_d) hiT = __int_as_float(__float_as_int(hiT) + 1);
+    const float tl = loT > 0.0f ? -loT : __builtin_inff();
+    const float th = hiT > 0.0f ? -hiT : __builtin_inff();
+    const float qnan = __builtin_nanf("");
+    f4 *stage = sStage[w];
+    int scnt = 0; // staged entries of this wave
+    if (tid == 0) sCnt = 0;
+    if (sc.bpart)
+        for (int e = tid; e < NBK; e += 256) sBk[e] = 0;
+    __syncthreads();
+
+    uint64_t *region = sc.region + (int64_t)blockIdx.x * sc.cap;
+    uint32_t below = 0; // scalar
+    const int xl = 4 * kq - ql; // j - i = xl + r + 16 (w - rb) on diagonal tiles
+
+    // staged entries -> keys (s = max(-v, 0), as k_pair_tiles' fmax) in the
+    // block's region (one LDS atomic per value slot and 64 entries) and the
+    // bucket histogram
+    auto flush = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); // other lanes' staging stores
+        for (int q0 = 0; q0 < scnt; q0 += 64) {
+            const f4 e = q0 + lane < scnt ? stage[q0 + lane] : f4{qnan, qnan, qnan, qnan};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float v = e[r];
+                const bool keep = v == v;
+                const unsigned long long mk = __ballot(keep);
+                if (!mk) continue;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&sCnt, (uint32_t)__popcll(mk));
+                base = __shfl(base, 0);
+                if (keep) {
+                    const uint64_t key = key_of((double)(v >= 0.0f ? 0.0f : -v));
+                    const int64_t pos = (int64_t)base + __popcll(mk & ((1ull << lane) - 1ull));
+                    if (pos < sc.cap) region[pos] = key;
+                    if (sc.bpart) atomicAdd(&sBk[kbucket(key, lo_key, binv)], 1u);
+                }
+            }
+        }
+        scnt = 0;
+    };
+
+    struct Cols {
+        uint4 A3[NDB][3];
+        f4 nv;    // norms of columns j0 + 4 kq + r (plain lane map)
+        float nq; // norm of column j0 + ql (transposed lane map)
+    };
+    auto load_cols = [&](int J, Cols &c) {
+        const int64_t j0 = (int64_t)J * TB + 16 * w;
+        const uint4 *p = reinterpret_cast<const uint4 *>(xk + ((int64_t)J * 4 + w) * kb3_block_words(KP)) + lane;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) c.A3[db][q] = p[(db * 3 + q) * 64];
+        c.nv = *reinterpret_cast<const f4 *>(nrm + j0 + 4 * kq);
+        c.nq = nrm[j0 + ql];
+    };
+
+    float hr[4]; // -n_i of row 16 rb + ql (plain lane map)
+    auto rows = [&](int I) {
+        const int ib = I * TB;
+        __syncthreads(); // every wave is done with the previous row
+        // the 4 row blocks' parts are contiguous in xk: a straight copy
+        const uint4 *src = reinterpret_cast<const uint4 *>(xk + (int64_t)I * 4 * kb3_block_words(KP));
+        for (int e = tid; e < 4 * NDB * 3 * 64; e += 256) sB3[e] = src[e];
+        if (tid < 64) sNr[tid] = -nrm[ib + tid];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) hr[rb] = -nrm[ib + 16 * rb + ql];
+        __syncthreads();
+        __builtin_amdgcn_s_waitcnt(0x0F70); // (vmcnt(0): the waits in the loop cover one column buffer)
+    };
+
+    // one tile of a kind: SW = wrapped (rows in the A role), DG = diagonal
+    auto tile = [&](auto sw_tag, auto dg_tag, const Cols &c) {
+        constexpr bool SW = decltype(sw_tag)::value, DG = decltype(dg_tag)::value;
+        f4 acc[4];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+            acc[rb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+            uint4 rp[NDB][3];
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) rp[db][q] = sB3[((rb * NDB + db) * 3 + q) * 64 + lane];
+#pragma unroll
+            for (int tm = 0; tm < 6; ++tm)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db)
+                    acc[rb] = SW ? kb3_mfma(rp[db][KB3_TA[tm]], c.A3[db][KB3_TB[tm]], acc[rb])
+                                 : kb3_mfma(c.A3[db][KB3_TA[tm]], rp[db][KB3_TB[tm]], acc[rb]);
+        }
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+            // (-n_i) + (-n_j), packed, then v = fma(2, dot, .) (v_pk_fma_f32)
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 two = {2.0f, 2.0f};
+            f2 t01, t23;
+            if constexpr (SW) { // row 16 rb + 4 kq + r, column ql
+                const f4 hn = *reinterpret_cast<const f4 *>(sNr + 16 * rb + 4 * kq);
+                const f2 qq = {-c.nq, -c.nq};
+                t01 = f2{hn[0], hn[1]} + qq;
+                t23 = f2{hn[2], hn[3]} + qq;
+            } else {
+                const f2 hh = {hr[rb], hr[rb]};
+                t01 = hh + f2{-c.nv[0], -c.nv[1]};
+                t23 = hh + f2{-c.nv[2], -c.nv[3]};
+            }
+            const f2 v01 = __builtin_elementwise_fma(two, f2{acc[rb][0], acc[rb][1]}, t01);
+            const f2 v23 = __builtin_elementwise_fma(two, f2{acc[rb][2], acc[rb][3]}, t23);
+            const f4 v = {v01[0], v01[1], v23[0], v23[1]};
+            unsigned long long h[4], any = 0;
+            uint32_t nbl = 0;
+            if constexpr (DG) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    h[r] = mcol_classify_diag(v[r], tl, th, xl, 16 * rb - 16 * w - r, nbl);
+                    any |= h[r];
+                }
+            } else {
+                any = mcol_classify4(v, tl, th, nbl, h);
+            }
+            below += nbl;
+            // band values (~1 % of the pairs): one entry per lane holding any
+            if (__builtin_expect(any != 0, 0)) {
+                const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(any >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
+                const f4 e = {lane_sel(h[0], v[0], qnan), lane_sel(h[1], v[1], qnan),
+                              lane_sel(h[2], v[2], qnan), lane_sel(h[3], v[3], qnan)};
+                // every lane stores: lanes without band values into the spill zone
+                stage[lane_bit(any) ? scnt + (int)pre : TC3_ENT + lane] = e;
+                scnt += __popcll(any);
+            }
+        }
+    };
+
+    // Per row: its parts, then its slots two at a time over two column
+    // buffers; the next tile's columns load during the current tile's MFMAs
+    // (block 0 when there is none, so the wait never includes it)
+    const TileSched ts(nb, t0, t1);
+    TileSched::Pos p0 = ts.first();
+    auto run = [&](const TileSched::Pos &p, const Cols &c) {
+        if (scnt > TC3_ENT - 256) flush(); // (one call site: the tile kinds share it)
+        if (p.s == 0)
+            tile(std::false_type{}, std::true_type{}, c);
+        else if (p.J < p.I)
+            tile(std::true_type{}, std::false_type{}, c);
+        else
+            tile(std::false_type{}, std::false_type{}, c);
+    };
+    if (ts.enter_row(p0)) {
+        Cols c0, c1;
+        load_cols(p0.J, c0);
+        for (bool live = true; live;) {
+            rows(p0.I);
+            for (;;) {
+                TileSched::Pos p1 = p0;
+                const bool m1 = ts.advance(p1);
+                load_cols(m1 ? p1.J : 0, c1);
+                __builtin_amdgcn_sched_barrier(0); // the prefetch issues before the MFMAs
+                run(p0, c0);
+                if (!m1) {
+                    live = false;
+                    break;
+                }
+                if (p1.I != p0.I) { // next row: its first columns are in c1
+                    p0 = p1;
+                    c0 = c1;
+                    break;
+                }
+                TileSched::Pos p2 = p1;
+                const bool m2 = ts.advance(p2);
+                load_cols(m2 ? p2.J : 0, c0);
+                __builtin_amdgcn_sched_barrier(0);
+                run(p1, c1);
+                if (!m2) {
+                    live = false;
+                    break;
+                }
+                const bool row_end = p2.I != p1.I;
+                p0 = p2;
+                if (row_end) break;
+            }
+        }
+    }
+
+    if (scnt) flush();
+    if (lane == 0) sBelow[w] = below;
+    __syncthreads();
+    if (tid == 0) {
+        sc.below_out[blockIdx.x] = sBelow[0] + sBelow[1] + sBelow[2] + sBelow[3];
+        sc.count_out[blockIdx.x] = sCnt;
+    }
+    if (sc.bpart)
+        for (int e = tid; e < NBK; e += 256) sc.bpart[(int64_t)blockIdx.x * NBK + e] = sBk[e];
+}
+
+
 // ============================================================ launcher ==
 
 #define SVGD_TCOL_CASE(KPv)                                                                  \
     case KPv:                                                                                \
-        hipLaunchKernelGGL((k_pair_tcol<KPv>), dim3(grid), dim3(256), 0, stream, xc, nrm, xk, n, \
-                           nb, t0, t1, sc);                                                  \
+        hipLaunchKernelGGL((k_pair_tcol<KPv>), dim3(grid), dim3(256), 0, stream, xc, nrm, n, nb, \
+                           t0, t1, sc);                                                      \
+        break;
+#define SVGD_TCOL3_CASE(KPv)                                                                 \
+    case KPv:                                                                                \
+        hipLaunchKernelGGL((k_pair_tcol3<KPv>), dim3(grid), dim3(256), 0, stream, nrm, xk, n, nb, \
+                           t0, t1, sc);                                                      \
         break;
 
 hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm, const uint32_t *xk,
@@ -988,8 +1243,8 @@ hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm,
         SVGD_TCOL_CASE(8)
         SVGD_TCOL_CASE(12)
         SVGD_TCOL_CASE(16)
-        SVGD_TCOL_CASE(32)
-        SVGD_TCOL_CASE(64)
+        SVGD_TCOL3_CASE(32)
+        SVGD_TCOL3_CASE(64)
     default:
         return hipErrorInvalidValue;
     }

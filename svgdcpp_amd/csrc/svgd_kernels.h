@@ -72,6 +72,8 @@ hipError_t launch_pair_tiles_f32(int KP, int mode, int grid, const float *xc, co
                                  const SelState *st, unsigned long long *ghist, uint32_t *bpart,
                                  double *dbg_out, const uint32_t *xk, hipStream_t stream);
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream);
+// fp32 copy of the norms with +inf in the padding rows [n, np)
+hipError_t launch_cvt_nrm_f32(const double *src, int64_t n, int64_t np, float *dst, hipStream_t stream);
 // Sampled median keys on the tile path: ntiles random (block, block) pairs of
 // distinct full 64-particle blocks, all 64 x 64 keys each (xcf/nrmf: fp32 path)
 // xk: the F32 key parts when KP is 32 or 64 (launch_swz_keys_b3), else null

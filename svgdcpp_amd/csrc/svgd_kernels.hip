@@ -4419,6 +4419,24 @@ hipError_t launch_phi_b3(int KP, int NCB, const uint32_t *B3, const float *crow,
 }
 #undef SVGD_PHIB3_CASE
 
+// fp32 norms for the tile-path median passes: rows [n, np) get +inf, so a
+// padding particle's v = fma(2, dot, -n_i - n_j) is -inf (never below, never
+// a candidate) without a mask in k_pair_tcol3
+__global__ void k_cvt_nrm_f32(const double *__restrict__ src, int64_t n, int64_t np, float *__restrict__ dst)
+{
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < np; e += (int64_t)gridDim.x * blockDim.x)
+        dst[e] = e < n ? (float)src[e] : __builtin_inff();
+}
+
+hipError_t launch_cvt_nrm_f32(const double *src, int64_t n, int64_t np, float *dst, hipStream_t stream)
+{
+    if (np <= 0) return hipSuccess;
+    int64_t g = (np + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_cvt_nrm_f32, dim3(g), dim3(256), 0, stream, src, n, np, dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_t stream)
 {
     if (cnt <= 0) return hipSuccess;

@@ -1,5 +1,5 @@
 """Print the kernel timeline (start offset, gap, duration) of one step of a
-rocprofv3 kernel trace (steps start at k_mean_partial): the middle step of
+rocprofv3 kernel trace (steps start at the centring): the middle step of
 the trace, which lies in bench.py's timed repeats (the diagnostic pass with
 its extra events comes after them).  Also prints the median step span over
 all steps.  With a second argument (the run's memory-copy trace CSV) the
@@ -10,7 +10,11 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-idx = [i for i, r in enumerate(rows) if 'k_mean_partial' in r['Kernel_Name']]
+# a step starts at its centring (k_center / k_center_d), or at the
+# k_mean_partial right before it (steps whose mean partials the previous
+# update epilogue did not leave)
+idx = [i - 1 if i > 0 and 'k_mean_partial' in rows[i - 1]['Kernel_Name'] else i
+       for i, r in enumerate(rows) if 'k_center' in r['Kernel_Name']]
 spans = [(int(rows[j - 1]['End_Timestamp']) - int(rows[i]['Start_Timestamp'])) / 1e3
          for i, j in zip(idx, idx[1:])]
 m = (len(idx) - 1) // 2
