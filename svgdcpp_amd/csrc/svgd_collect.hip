@@ -898,8 +898,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
 // 64 x 16 wave tile 4 x 6 KP/32 v_mfma_f32_16x16x32_bf16 of 16 cycles (the
 // fp32 form: 4 x KP/4 f32 MFMAs of 32).  The wave's 16 columns' parts in
 // VGPRs (from xk, the next tile's loading during the current one's MFMAs),
-// the tile row's 4 row blocks' parts in LDS (one 16-byte read per row
-// block, part and k chunk); a wrapped tile (J < I) gives the rows (the larger
+// the tile row's 4 row blocks' parts in VGPRs too, for the whole run of
+// tiles sharing the row (no LDS reads per tile); a wrapped tile (J < I) gives the rows (the larger
 // indices) the A role, which transposes the lane map: row 4 kq + r, column ql.
 // Each tile kind (plain, wrapped, diagonal) is its own straight-line code.
 // Norms come from nrmf, whose padding rows hold +inf (launch_cvt_nrm_f32):
@@ -1004,8 +1004,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
     __shared__ uint32_t sBk[NBK];
     __shared__ uint32_t sCnt;
     __shared__ unsigned long long sBelow[4];
-    __shared__ uint4 sB3[4 * NDB * 3 * 64];                   // [rb][db][part][lane]
-    __shared__ __attribute__((aligned(16))) float sNr[64];   // -n_i of the tile row
     __shared__ f4 sStage[4][TC3_ENT + 64];                   // + the spill zone
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1078,17 +1076,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         c.nq = nrm[j0 + ql];
     };
 
+    // the tile row's 4 row blocks' parts and norms, in VGPRs for the whole
+    // run of tiles that share the row (~nb / 2): no LDS reads per tile
+    uint4 rp[4][NDB][3];
     float hr[4]; // -n_i of row 16 rb + ql (plain lane map)
+    f4 hn[4];    // -n_i of rows 16 rb + 4 kq + r (transposed lane map)
     auto rows = [&](int I) {
         const int ib = I * TB;
-        __syncthreads(); // every wave is done with the previous row
-        // the 4 row blocks' parts are contiguous in xk: a straight copy
-        const uint4 *src = reinterpret_cast<const uint4 *>(xk + (int64_t)I * 4 * kb3_block_words(KP));
-        for (int e = tid; e < 4 * NDB * 3 * 64; e += 256) sB3[e] = src[e];
-        if (tid < 64) sNr[tid] = -nrm[ib + tid];
+        const uint4 *src = reinterpret_cast<const uint4 *>(xk + (int64_t)I * 4 * kb3_block_words(KP)) + lane;
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb) hr[rb] = -nrm[ib + 16 * rb + ql];
-        __syncthreads();
+        for (int rb = 0; rb < 4; ++rb) {
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) rp[rb][db][q] = src[((rb * NDB + db) * 3 + q) * 64];
+            hr[rb] = -nrm[ib + 16 * rb + ql];
+            hn[rb] = -*reinterpret_cast<const f4 *>(nrm + ib + 16 * rb + 4 * kq);
+        }
         __builtin_amdgcn_s_waitcnt(0x0F70); // (vmcnt(0): the waits in the loop cover one column buffer)
     };
 
@@ -1097,20 +1101,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
         constexpr bool SW = decltype(sw_tag)::value, DG = decltype(dg_tag)::value;
         f4 acc[4];
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb) {
-            acc[rb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
-            uint4 rp[NDB][3];
+        for (int rb = 0; rb < 4; ++rb) acc[rb] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+        // term by term across the 4 row blocks' chains (each chain keeps the
+        // key's order: tm, then db)
+#pragma unroll
+        for (int tm = 0; tm < 6; ++tm)
 #pragma unroll
             for (int db = 0; db < NDB; ++db)
 #pragma unroll
-                for (int q = 0; q < 3; ++q) rp[db][q] = sB3[((rb * NDB + db) * 3 + q) * 64 + lane];
-#pragma unroll
-            for (int tm = 0; tm < 6; ++tm)
-#pragma unroll
-                for (int db = 0; db < NDB; ++db)
-                    acc[rb] = SW ? kb3_mfma(rp[db][KB3_TA[tm]], c.A3[db][KB3_TB[tm]], acc[rb])
-                                 : kb3_mfma(c.A3[db][KB3_TA[tm]], rp[db][KB3_TB[tm]], acc[rb]);
-        }
+                for (int rb = 0; rb < 4; ++rb)
+                    acc[rb] = SW ? kb3_mfma(rp[rb][db][KB3_TA[tm]], c.A3[db][KB3_TB[tm]], acc[rb])
+                                 : kb3_mfma(c.A3[db][KB3_TA[tm]], rp[rb][db][KB3_TB[tm]], acc[rb]);
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb) {
             // (-n_i) + (-n_j), packed, then v = fma(2, dot, .) (v_pk_fma_f32)
@@ -1118,10 +1119,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
             const f2 two = {2.0f, 2.0f};
             f2 t01, t23;
             if constexpr (SW) { // row 16 rb + 4 kq + r, column ql
-                const f4 hn = *reinterpret_cast<const f4 *>(sNr + 16 * rb + 4 * kq);
                 const f2 qq = {-c.nq, -c.nq};
-                t01 = f2{hn[0], hn[1]} + qq;
-                t23 = f2{hn[2], hn[3]} + qq;
+                t01 = f2{hn[rb][0], hn[rb][1]} + qq;
+                t23 = f2{hn[rb][2], hn[rb][3]} + qq;
             } else {
                 const f2 hh = {hr[rb], hr[rb]};
                 t01 = hh + f2{-c.nv[0], -c.nv[1]};

@@ -18,7 +18,7 @@ b() { # name timeout args...
   tail -1 $O/$name.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', round(d['ms_per_step'],4), 'runs', [round(x,3) for x in d['repeats']['ms_per_step']], 'med', round(d['phases_ms_per_step']['median_incl_step_gap'],4), 'clk', (d.get('gpu_timed') or {}).get('gfxclk_mhz_median'))"
 }
 for i in 1 2; do
-  for v in head tcol3; do
+  for v in head tcol3 tcol3r; do
     cp tools/ablibs/$v.so $LIB
     b ${v}_cfg5_$i 300 --config cfg5 --steps 20 --warmup 3 --no-cpu --repeats 3
   done
