@@ -271,10 +271,11 @@ int svgd_model_neg_hess_sum(void *model, const double *X, int64_t nrows, double 
  * round trip hides behind the device median.  Same result as the split
  * calls.  Not for SVGD_SCALE_HESSIAN (that step also needs the caller's
  * Hessian sum).  On a shard of <= 1 MiB the previous update's epilogue
- * leaves X_t in a context-private pinned buffer instead of a copy, and with
- * one rank the record prep reads G_t from the pinned G buffer (no copies;
- * SVGD_X_MIRROR=0 / SVGD_G_HOSTREAD=0 disable either): the buffers of
- * svgd_host_buffers are then not guaranteed to hold X_t afterwards. */
+ * leaves X_t in a context-private pinned buffer instead of a copy
+ * (SVGD_X_MIRROR=0 disables it; SVGD_G_HOSTREAD=1, one rank, also has the
+ * record prep read G_t from the pinned G buffer instead of its copies): the
+ * buffers of svgd_host_buffers are then not guaranteed to hold X_t
+ * afterwards. */
 int svgd_step_host_model(svgd_ctx *ctx, const void *model);
 
 /* Mirror a built-in Gaussian-sum model (svgd_model_create) on the device

@@ -1902,7 +1902,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     {
         const bool small = hb <= XMIRROR_MAX;
         c->xmirror = small;
-        c->ghost = small && c->plan_world == 1;
+        // the G host read (prep reading h_g over PCIe) measured 2-4 us per
+        // step slower than the G copies at cfg2 (profiles/r04_g_hostread_ab.txt):
+        // opt-in
+        c->ghost = false;
         if (const char *e = std::getenv("SVGD_X_MIRROR")) c->xmirror = std::atoi(e) != 0;
         if (const char *e = std::getenv("SVGD_G_HOSTREAD")) c->ghost = c->plan_world == 1 && std::atoi(e) != 0;
     }
