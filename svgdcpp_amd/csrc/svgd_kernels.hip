@@ -549,40 +549,52 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(SVGD_PH
 
 // bak (optional, the speculative step): bak[0..cnt) = X_t, bak[cnt..2cnt) =
 // m_t, bak[2cnt..3cnt) = v_t of these elements, written in the same pass.
-__device__ __forceinline__ double opt_elem(const OptArgs &o, int64_t e, double ge)
+// An element's optimizer state, loaded ahead of the phi value it needs
+// (k_phi_reduce issues these loads before its partial sums)
+struct OptIn {
+    double m, v, x;
+};
+__device__ __forceinline__ OptIn opt_load(const OptArgs &o, int64_t e)
+{
+    return OptIn{o.kind == 0 ? o.m[e] : 0.0, o.v[e], o.X[e]};
+}
+__device__ __forceinline__ double opt_apply(const OptArgs &o, int64_t e, double ge, const OptIn &in)
 {
 #pragma clang fp contract(off)
-    double *__restrict__ m = o.m, *__restrict__ v = o.v, *__restrict__ X = o.X;
     if (o.bak) {
-        o.bak[e] = X[e];
-        o.bak[o.cnt + e] = m[e];
-        o.bak[2 * o.cnt + e] = v[e];
+        o.bak[e] = in.x;
+        o.bak[o.cnt + e] = o.kind == 0 ? in.m : o.m[e];
+        o.bak[2 * o.cnt + e] = in.v;
     }
     double delta;
     if (o.kind == 0) { // Adam.hpp:75-83
-        const double me = o.b1 * m[e] + (1 - o.b1) * ge;
-        const double ve = o.b2 * v[e] + (1 - o.b2) * (ge * ge);
-        m[e] = me;
-        v[e] = ve;
+        const double me = o.b1 * in.m + (1 - o.b1) * ge;
+        const double ve = o.b2 * in.v + (1 - o.b2) * (ge * ge);
+        o.m[e] = me;
+        o.v[e] = ve;
         delta = (o.lr * (1.0 / (o.eps + sqrt(ve / o.c2)))) * (me / o.c1);
     } else if (o.kind == 1) { // AdaGrad.hpp:60-65
-        const double ve = v[e] + ge * ge;
-        v[e] = ve;
+        const double ve = in.v + ge * ge;
+        o.v[e] = ve;
         delta = (o.lr * (1.0 / (o.eps + sqrt(ve)))) * ge;
     } else { // RMSProp.hpp:69-74 (beta passed as b1)
-        const double ve = o.b1 * v[e] + (1 - o.b1) * (ge * ge);
-        v[e] = ve;
+        const double ve = o.b1 * in.v + (1 - o.b1) * (ge * ge);
+        o.v[e] = ve;
         delta = (o.lr * (1.0 / (o.eps + sqrt(ve)))) * ge;
     }
-    double x = X[e] + delta; // SVGD.hpp:393
+    double x = in.x + delta; // SVGD.hpp:393
     if (o.lower) {           // SVGD.hpp:396-399: min(upper) then max(lower)
         const int k = (int)(e % o.d);
         x = x < o.upper[k] ? x : o.upper[k];
         x = x > o.lower[k] ? x : o.lower[k];
     }
-    X[e] = x;
+    o.X[e] = x;
     if (o.xh) o.xh[e] = x; // the host gradient's copy of X_{t+1} (no D2H copy)
     return x;
+}
+__device__ __forceinline__ double opt_elem(const OptArgs &o, int64_t e, double ge)
+{
+    return opt_apply(o, e, ge, opt_load(o, e));
 }
 
 __global__ void k_opt_update(OptArgs o, const double *__restrict__ g)
@@ -3384,12 +3396,24 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
 {
     if (skip && *skip) return;
     __shared__ double sm[256];
-    const double two_a = 2.0 * (*a_ptr);
     const int DP = d + 1;
     const int RB = phi_red_rows(d);
     const int64_t rb = (int64_t)blockIdx.x * RB;
     const int rows = (int)min<int64_t>(RB, nrows - rb);
     if (rows <= 0) return;
+    // this thread's output element (rows * d < 256: at most one), its
+    // weight and optimizer state loaded before the partial sums (one memory
+    // round trip fewer)
+    const int o = threadIdx.x;
+    const bool own = o < rows * d;
+    const int r_o = own ? o / d : 0, k_o = own ? o - r_o * d : 0;
+    const int64_t li_o = rb + r_o;
+    double w_o = 0.0;
+    OptIn in_o{0.0, 0.0, 0.0};
+    if (own) {
+        w_o = wv ? wv[(row0 + li_o) * d + k_o] : 2.0 * (*a_ptr) * rec[(row0 + li_o) * RS + k_o];
+        if (do_opt) in_o = opt_load(opt, li_o * d + k_o);
+    }
     const int e = threadIdx.x;
     if (e < rows * DP) {
         const double *p = part + rb * DP + e;
@@ -3408,15 +3432,12 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
     }
     __syncthreads();
     __shared__ double sx[256]; // X_{t+1} of the block's rows (OptArgs::xsum)
-    for (int o = threadIdx.x; o < rows * d; o += blockDim.x) {
-        const int r = o / d, k = o - r * d;
-        const int64_t li = rb + r;
-        const double w = wv ? wv[(row0 + li) * d + k] : two_a * rec[(row0 + li) * RS + k];
-        const double ph = inv_n * (sm[r * DP + k] + w * sm[r * DP + d]);
-        phi[li * d + k] = ph;
+    if (own) {
+        const double ph = inv_n * (sm[r_o * DP + k_o] + w_o * sm[r_o * DP + d]);
+        phi[li_o * d + k_o] = ph;
         if (do_opt) {
-            const double x = opt_elem(opt, li * d + k, ph);
-            if (opt.xsum) sx[o] = x; // (rows * d < 256: one element per thread)
+            const double x = opt_apply(opt, li_o * d + k_o, ph, in_o);
+            if (opt.xsum) sx[o] = x;
         }
     }
     if (do_opt && opt.xsum) {
