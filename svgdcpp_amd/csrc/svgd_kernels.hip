@@ -3107,6 +3107,11 @@ __device__ __forceinline__ uint32_t b3_trunc_pair(float &x0, float &x1)
 #ifndef SVGD_B3_TRUNC
 #define SVGD_B3_TRUNC 1
 #endif
+// waves 4-7 VALU-first (below): measured 6 % slower per clock at cfg5
+// (profiles/r04_b3_ab.txt), so off
+#ifndef SVGD_B3_STAGGER
+#define SVGD_B3_STAGGER 0
+#endif
 __device__ __forceinline__ uint32_t b3_split_pair(float &x0, float &x1)
 {
     // bf16(x0) | bf16(x1) << 16 (round to nearest even), and the residuals
@@ -3285,39 +3290,38 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     // on the VALU while those are in the matrix pipe.  The DMA of tile t+1
     // goes to buffer (t+1) % 3, whose tile (t-2) every wave finished before
     // this iteration's barrier.
+    // Stagger (SVGD_B3_STAGGER, 8-wave blocks): waves 4-7 share the SIMDs of
+    // waves 0-3 and would run the same MFMA / VALU phases in lockstep; they
+    // keep tile t-1's Gram in registers across the barrier and run each
+    // iteration VALU-first -- P(t-1), P.V(t-1), then Gram(t) -- so one wave
+    // of each SIMD pair forms P while the other is in the matrix pipe.  The
+    // same MFMAs in the same order per wave: results bit for bit unchanged.
     uint4 aP[3] = {};
-    if (ntiles > 0) issue(0, 0);
-    for (int64_t t = 0; t < ntiles; ++t) {
-        const int b = (int)(t % 3);
-        wait_vmcnt<0>();
-        __syncthreads();
-        if (t + 1 < ntiles) issue(t + 1, b == 2 ? 0 : b + 1);
-        const uint32_t *lb = sbuf + b * BUF;
-        // Gram: dot[js][db] (4 independent chains at KP = 64), term by term
-        f4_t dot[2][NDB];
+    auto gram = [&](const uint32_t *lb, f4_t (&dot)[2][NDB]) {
 #pragma unroll
         for (int js = 0; js < 2; ++js)
 #pragma unroll
             for (int db = 0; db < NDB; ++db) dot[js][db] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
-        {
-            uint4 aX[2][NDB][3];
+        uint4 aX[2][NDB][3];
+#pragma unroll
+        for (int js = 0; js < 2; ++js)
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+                for (int part = 0; part < 3; ++part)
+                    aX[js][db][part] =
+                        *reinterpret_cast<const uint4 *>(lb + ((js * NDB + db) * 3 + part) * 256 + lane * 4);
+        // dot[js][db] (4 independent chains at KP = 64), term by term
+#pragma unroll
+        for (int tm = 0; tm < 6; ++tm)
 #pragma unroll
             for (int js = 0; js < 2; ++js)
 #pragma unroll
                 for (int db = 0; db < NDB; ++db)
-#pragma unroll
-                    for (int part = 0; part < 3; ++part)
-                        aX[js][db][part] =
-                            *reinterpret_cast<const uint4 *>(lb + ((js * NDB + db) * 3 + part) * 256 + lane * 4);
-#pragma unroll
-            for (int tm = 0; tm < 6; ++tm)
-#pragma unroll
-                for (int js = 0; js < 2; ++js)
-#pragma unroll
-                    for (int db = 0; db < NDB; ++db)
-                        dot[js][db] = mfma_b3(aX[js][db][TA[tm]], bR[db][TB_[tm]], dot[js][db]);
-        }
-        if (t > 0) pv_mfma(sbuf + (b == 0 ? 2 : b - 1) * BUF, aP);
+                    dot[js][db] = mfma_b3(aX[js][db][TA[tm]], bR[db][TB_[tm]], dot[js][db]);
+    };
+    // P of a tile from its Gram (its c_j in LDS buffer lb) -> aP, row sums
+    auto form_p = [&](const uint32_t *lb, const f4_t (&dot)[2][NDB]) {
         float pv[8]; // P[i = lo][j = 16js + 4hi + r] at k-slot 4js + r
 #pragma unroll
         for (int js = 0; js < 2; ++js) {
@@ -3332,22 +3336,49 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
 #pragma unroll
             for (int q = 0; q < 8; ++q) ps += pv[q];
         }
-        {
-            uint32_t wd[3][4];
+        uint32_t wd[3][4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float x0 = pv[2 * q], x1 = pv[2 * q + 1];
+        for (int q = 0; q < 4; ++q) {
+            float x0 = pv[2 * q], x1 = pv[2 * q + 1];
 #pragma unroll
-                for (int part = 0; part < 3; ++part)
-                    wd[part][q] = SVGD_B3_TRUNC ? b3_trunc_pair(x0, x1) : b3_split_pair(x0, x1);
-            }
-#pragma unroll
-            for (int part = 0; part < 3; ++part) aP[part] = make_uint4(wd[part][0], wd[part][1], wd[part][2], wd[part][3]);
+            for (int part = 0; part < 3; ++part)
+                wd[part][q] = SVGD_B3_TRUNC ? b3_trunc_pair(x0, x1) : b3_split_pair(x0, x1);
         }
-    }
-    if (ntiles > 0) { // the last tile's P.V (its buffer is intact: no DMA after it)
-        const int b = (int)((ntiles - 1) % 3);
-        pv_mfma(sbuf + b * BUF, aP);
+#pragma unroll
+        for (int part = 0; part < 3; ++part) aP[part] = make_uint4(wd[part][0], wd[part][1], wd[part][2], wd[part][3]);
+    };
+    auto buf = [&](int64_t t) { return sbuf + (int)(t % 3) * BUF; };
+    const bool lag = SVGD_B3_STAGGER && NW == 8 && w >= 4;
+    if (ntiles > 0) issue(0, 0);
+    if (!lag) {
+        for (int64_t t = 0; t < ntiles; ++t) {
+            const int b = (int)(t % 3);
+            wait_vmcnt<0>();
+            __syncthreads();
+            if (t + 1 < ntiles) issue(t + 1, b == 2 ? 0 : b + 1);
+            f4_t dot[2][NDB];
+            gram(buf(t), dot);
+            if (t > 0) pv_mfma(buf(t - 1), aP);
+            form_p(buf(t), dot);
+        }
+        if (ntiles > 0) pv_mfma(buf(ntiles - 1), aP); // (its buffer is intact: no DMA after it)
+    } else {
+        f4_t dotc[2][NDB]; // tile t-1's Gram, carried across the barrier
+        for (int64_t t = 0; t < ntiles; ++t) {
+            const int b = (int)(t % 3);
+            wait_vmcnt<0>();
+            __syncthreads();
+            if (t + 1 < ntiles) issue(t + 1, b == 2 ? 0 : b + 1);
+            if (t > 0) {
+                form_p(buf(t - 1), dotc);
+                pv_mfma(buf(t - 1), aP);
+            }
+            gram(buf(t), dotc);
+        }
+        if (ntiles > 0) {
+            form_p(buf(ntiles - 1), dotc);
+            pv_mfma(buf(ntiles - 1), aP);
+        }
     }
 
     // epilogue (fp64): acc lane map row i = 4 hi + q, column c = lo (+16 cb)
