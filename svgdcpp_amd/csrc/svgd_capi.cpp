@@ -640,13 +640,18 @@ int center(svgd_ctx *c, const SelState *st_init = nullptr)
     // while X does, so every centring of one X forms the same mean
     const int xs = c->xsum_cur;
     const bool pr = c->xsum && c->xsum_ok[xs];
+    // F32 at KP 32 / 64: the centring writes the fp32 copies itself
+    const bool fused = c->dtype == SVGD_F32 && !c->rowpath && (c->KP == 32 || c->KP == 64);
     HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np,
                                  pr ? c->xsum + xs * c->xsum_stride : c->partial,
                                  pr ? c->xsum_parts[xs] : c->nparts, c->xc, c->nrm, c->rowpath ? 1 : 0,
-                                 c->xf, c->nmax, c->cnt3 + 3, c->stream, c->st, st_init, pr));
+                                 c->xf, c->nmax, c->cnt3 + 3, c->stream, c->st, st_init, pr,
+                                 fused ? c->xcf : nullptr, fused ? c->nrmf : nullptr));
     if (c->dtype == SVGD_F32) {
-        HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
-        HIPCHK(c, launch_cvt_nrm_f32(c->nrm, c->n, c->np, c->nrmf, c->stream));
+        if (!fused) {
+            HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
+            HIPCHK(c, launch_cvt_nrm_f32(c->nrm, c->n, c->np, c->nrmf, c->stream));
+        }
         if (c->XK) HIPCHK(c, launch_swz_keys_b3(c->xcf, c->KP, c->np, c->XK, c->stream));
     }
     return SVGD_OK;

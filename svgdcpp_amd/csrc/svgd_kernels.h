@@ -50,7 +50,10 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
                               unsigned long long *bzero, hipStream_t stream,
                               SelState *st_out = nullptr, const SelState *st_init = nullptr,
-                              bool partials_ready = false);
+                              bool partials_ready = false, float *xcf = nullptr,
+                              float *nrmf = nullptr);
+// (xcf / nrmf, KP 32 or 64: also the fp32 copies of xc and nrm, nrmf +inf in
+// the padding rows -- launch_cvt_f32 / launch_cvt_nrm_f32 in the same pass)
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);

@@ -332,6 +332,89 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
     }
 }
 
+// k_center for the tile path, KP = 32 / 64 (d > 16): the same values bit for
+// bit (xc = X - mu, |xc|^2 as one fma chain over k ascending, the zero pads
+// adding nothing), but the mean from the partials in one LDS sweep, the
+// row's X loads unrolled and issued before the mean is formed (the generic
+// loop, KP a run-time value, was a chain of dependent round trips: 77 us at
+// N = 65536, d = 64), 16-byte record stores -- and, for SVGD_F32, the fp32
+// copies the median passes read (xcf = fl(xc), nrmf = fl(|xc|^2), +inf in
+// the padding rows: launch_cvt_nrm_f32) in the same pass, two launches fewer.
+template <int KP>
+__global__ __launch_bounds__(256) void k_center_t(const double *__restrict__ X, int64_t n, int d,
+                                                  const double *__restrict__ partial, int nparts,
+                                                  int64_t np, double *__restrict__ xc,
+                                                  double *__restrict__ nrm, float *__restrict__ xcf,
+                                                  float *__restrict__ nrmf, unsigned long long *bzero,
+                                                  SelState *st_out, SelState st_init)
+{
+    if (bzero && blockIdx.x == 0)
+        for (int e = threadIdx.x; e < NBK; e += blockDim.x) bzero[e] = 0;
+    if (st_out && blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_init;
+    __shared__ double mu[KP];
+    __shared__ double sP[4096];
+    const int64_t jstride = (int64_t)gridDim.x * blockDim.x;
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the first row's X loaded before the mean (its latency overlaps the
+    // partials'; the grid usually gives each thread one row)
+    double v[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) v[k] = (j < n && k < d) ? X[j * d + k] : 0.0;
+    if (nparts * d <= 4096) {
+        for (int e = threadIdx.x; e < nparts * d; e += blockDim.x) sP[e] = partial[e];
+        __syncthreads();
+        if (threadIdx.x < d) {
+            double s = 0.0; // partials added in b order, as k_center
+            int b = 0;
+            for (; b + 8 <= nparts; b += 8) {
+                double v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = sP[(b + u) * d + threadIdx.x];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) s += v[u];
+            }
+            for (; b < nparts; ++b) s += sP[b * d + threadIdx.x];
+            mu[threadIdx.x] = s / (double)n;
+        }
+    } else if (threadIdx.x < d) {
+        const int k = threadIdx.x;
+        double s = 0.0;
+        for (int b0 = 0; b0 < nparts; b0 += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = b0 + u < nparts ? partial[(b0 + u) * d + k] : 0.0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (b0 + u < nparts) s += v[u];
+        }
+        mu[k] = s / (double)n;
+    }
+    __syncthreads();
+    for (bool first = true; j < np; j += jstride, first = false) {
+        const bool live = j < n;
+        if (!first) {
+#pragma unroll
+            for (int k = 0; k < KP; ++k) v[k] = (live && k < d) ? X[j * d + k] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < KP; ++k) v[k] = (live && k < d) ? v[k] - mu[k] : 0.0;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) s = fma(v[k], v[k], s);
+        nrm[j] = s;
+        double2 *o = reinterpret_cast<double2 *>(xc + j * KP);
+#pragma unroll
+        for (int q = 0; q < KP / 2; ++q) o[q] = make_double2(v[2 * q], v[2 * q + 1]);
+        if (xcf) {
+            float4 *of = reinterpret_cast<float4 *>(xcf + j * KP);
+#pragma unroll
+            for (int q = 0; q < KP / 4; ++q)
+                of[q] = make_float4((float)v[4 * q], (float)v[4 * q + 1], (float)v[4 * q + 2], (float)v[4 * q + 3]);
+            nrmf[j] = live ? (float)s : __builtin_inff();
+        }
+    }
+}
+
 // V_j = [G_j - 2a xc_j, 1, 0...] (row stride 16*NCB), c_j = -a log2e |xc_j|^2.
 __global__ void k_prep_v(const double *__restrict__ xc, const double *__restrict__ G,
                          const double *__restrict__ nrm, const double *__restrict__ a_ptr,
@@ -4502,7 +4585,7 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
                               unsigned long long *bzero, hipStream_t stream, SelState *st_out,
-                              const SelState *st_init, bool partials_ready)
+                              const SelState *st_init, bool partials_ready, float *xcf, float *nrmf)
 {
     const SelState sinit = st_init ? *st_init : SelState{};
     if (!st_init) st_out = nullptr;
@@ -4529,6 +4612,16 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
         }
     }
 #undef SVGD_CENTER_CASE
+    if (!xf && !nrm_in_slot && (KP == 32 || KP == 64) && d <= KP && np % 2 == 0) {
+        if (KP == 32)
+            hipLaunchKernelGGL((k_center_t<32>), dim3(g), dim3(256), 0, stream, X, n, d, partial, nparts, np,
+                               xc, nrm, xcf, nrmf, bzero, st_out, sinit);
+        else
+            hipLaunchKernelGGL((k_center_t<64>), dim3(g), dim3(256), 0, stream, X, n, d, partial, nparts, np,
+                               xc, nrm, xcf, nrmf, bzero, st_out, sinit);
+        return hipGetLastError();
+    }
+    if (xcf) return hipErrorInvalidValue; // (the fp32 copies: KP 32 / 64 only)
     hipLaunchKernelGGL(k_center, dim3(g), dim3(256), 0, stream, X, n, d, KP, partial, nparts, np,
                        xc, nrm, nrm_in_slot, xf, med_f32_stride(d), nmax_bits, bzero, st_out, sinit);
     return hipGetLastError();
