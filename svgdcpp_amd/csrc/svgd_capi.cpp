@@ -770,9 +770,13 @@ bool trk_predict(svgd_ctx *c, double Mq, double band_samp, uint64_t *lo_key, uin
     if (c->trk_nerr == 0) e = std::fabs(m1 - m2) / m1; // no error seen yet: the drift itself
     for (int k = 0; k < c->trk_nerr; ++k) e = std::max(e, c->trk_err[k]);
     const double w = std::max(c->trk_err_mult * e, c->trk_min_w);
+    const double band = c->trk_dens * (2.0 * w * pred) / Mq;
+    static const bool dbg = std::getenv("SVGD_DEBUG_TRK") != nullptr;
+    if (dbg)
+        std::fprintf(stderr, "trk: pred %.6g err %.3g w %.3g band %.3g band_samp %.3g -> %s\n", pred, e, w,
+                     band, band_samp, (w < 0.05 && band <= band_samp) ? "predict" : "sample");
     if (!(w < 0.05)) return false;
     const double lo = pred * (1.0 - w), hi = pred * (1.0 + w);
-    const double band = c->trk_dens * (hi - lo) / Mq;
     if (!(band <= band_samp)) return false;
     *lo_key = __builtin_bit_cast(uint64_t, lo);
     *hi_key = __builtin_bit_cast(uint64_t, hi) + 1;
