@@ -13,7 +13,7 @@ fault_guard gpurun_out/prof_r4/bench.log
 python3 tools/kstats.py gpurun_out/prof_r4/run_kernel_stats.csv > $O/rocprof_kernel_stats.txt
 python3 tools/ktimed.py gpurun_out/prof_r4/run_kernel_trace.csv 3 > $O/rocprof_kernel_timed.txt
 python3 tools/step_timeline.py gpurun_out/prof_r4/run_kernel_trace.csv > $O/step_timeline_cfg3.txt
-tail -1 gpurun_out/prof_r4/bench.log > $O/bench_rocprof_run.json
+grep "^{" gpurun_out/prof_r4/bench.log | tail -1 > $O/bench_rocprof_run.json
 head -4 $O/rocprof_kernel_timed.txt
 STEPS=5 WARMUP=2 TAG=_r4cfg4 BENCH_ARGS="--config cfg4 --repeats 1" bash tools/profile.sh > /dev/null || exit 1
 python3 tools/ktimed.py gpurun_out/prof_r4cfg4/run_kernel_trace.csv 2 > $O/rocprof_cfg4_kernel_timed.txt
