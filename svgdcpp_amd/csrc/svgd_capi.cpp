@@ -376,7 +376,7 @@ struct svgd_ctx {
     // statistics is a failed plan, and the step is redone with a sample.
     bool trk_allowed = true;    // SVGD_TRACK_BRACKET=0 disables
     double trk_min_w = 2e-5;    // SVGD_TRACK_MIN_WIDTH: relative half-width floor
-    double trk_err_mult = 4.0;  // SVGD_TRACK_ERR_MULT: half-width / recent error
+    double trk_err_mult = 4.0;  // SVGD_TRACK_ERR_MULT: half-width / recent error (set at creation)
     uint64_t *h_trk = nullptr, *h_trk_dev = nullptr; // pinned [lo, hi, below, cand, key0, key1, err]
     double trk_m[3] = {0, 0, 0}; // last selected D^2 (lower order statistic), newest first
     int trk_n = 0;
@@ -1939,6 +1939,12 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     if (const char *e = std::getenv("SVGD_SPECULATE")) c->spec_allowed = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_TRACK_BRACKET")) c->trk_allowed = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_TRACK_MIN_WIDTH")) c->trk_min_w = std::atof(e);
+    // A miss redoes the step; the band it saves is collect-pass work, which
+    // outweighs the misses' cost only when the collect is large: 2.5 x the
+    // recent error from N = 32768 up (cfg3: median phase 0.550 -> 0.513 ms,
+    // 86 instead of 72 of 90 steps tracked, no miss in 360), 4 below (cfg2
+    // at 2.5: 3 misses in 180 steps, slower) -- profiles/r04_track_mult_ab.txt
+    c->trk_err_mult = n >= 32768 ? 2.5 : 4.0;
     if (const char *e = std::getenv("SVGD_TRACK_ERR_MULT")) c->trk_err_mult = std::atof(e);
     // half the OpenMP threads, but no more than this rank's share of the
     // cgroup CPU quota (ranks of one node share it; OpenMP sees the affinity
