@@ -552,10 +552,12 @@ def main():
             if not os.path.exists(path):
                 return None
             with open(path) as f:
-                p = json.load(f)
-            ok = (p.get("n") == n and p.get("d") == d and p.get("world") == wkey and kname in p.get("kernel", "")
-                  and p.get("src_sha16") == src_sha)
-            return p if ok else None
+                recs = json.load(f)
+            for p in recs if isinstance(recs, list) else [recs]:  # one record per kernel / workload
+                if (p.get("n") == n and p.get("d") == d and p.get("world") == wkey and kname in p.get("kernel", "")
+                        and p.get("src_sha16") == src_sha):
+                    return p
+            return None
 
         pmc = committed("phi_pmc_traffic.json")
         traffic = pmc.get("bytes_per_launch") if pmc else None
