@@ -271,11 +271,34 @@ def _cpu_sample(o, X0, mus, covs, rows):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(X0, mus, covs, rows, rows_1t, repeats=3):
+def accuracy_rows(n):
+    """Rows whose phi_hat the line checks against the oracle: both ends and
+    512 around n / 2 (as tests/test_gpu_fullsize.py samples them)."""
+    return [(0, 256), (n // 2 - 256, n // 2 + 256), (n - 256, n)]
+
+
+def phi_accuracy(o, X0, G0, a0, phi0, dtype):
+    """The device's phi_hat of X0 (untimed, before the warm-up) on the
+    accuracy rows against the oracle's fp64 phi_hat from the same (X, G, a):
+    the observed error, next to the bar the GPU tests assert."""
+    err, ref_max = 0.0, 0.0
+    for r0, r1 in accuracy_rows(X0.shape[0]):
+        ref = o.phi(X0, G0, a0, rows=(r0, r1))
+        err = max(err, float(np.max(np.abs(phi0[r0:r1] - ref))))
+        ref_max = max(ref_max, float(np.max(np.abs(ref))))
+    out = {"rows": sum(r1 - r0 for r0, r1 in accuracy_rows(X0.shape[0])), "scale_a": a0,
+           "phi_max_abs_err": err, "phi_max_abs": ref_max, "phi_err_rel_to_max": err / ref_max if ref_max else None,
+           "reference": "oracle fp64 phi_hat (SVGD.hpp:407-454) of the same X, G, a"}
+    out["bar"] = "<= 1e-4 max|phi| (F32, SURVEY A.9)" if dtype == "f32" else "<= 1e-10 absolute (fp64)"
+    return out
+
+
+def cpu_baseline(X0, mus, covs, rows, rows_1t, repeats=3, acc=None):
     """Oracle (CPU port of the reference arithmetic) on a row sample of one step:
     median work of `rows` rows, their log-gradients, phi_hat and Adam -- with
     the OpenMP threads of this box (OMP_NUM_THREADS) and with one thread;
-    `repeats` timings each, the median reported."""
+    `repeats` timings each, the median reported.  acc = (G0, a0, phi0, dtype):
+    also the device's phi_hat accuracy on a row sample (phi_accuracy)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as o
 
@@ -291,9 +314,11 @@ def cpu_baseline(X0, mus, covs, rows, rows_1t, repeats=3):
     dts = sorted(_cpu_sample(o, X0, mus, covs, rows) for _ in range(repeats))
     o.set_threads(1)
     dt1s = sorted(_cpu_sample(o, X0, mus, covs, rows_1t) for _ in range(repeats))
+    accuracy = phi_accuracy(o, X0, *acc) if acc is not None else None
     o.set_threads(keep)
     dt, dt1 = dts[len(dts) // 2], dt1s[len(dt1s) // 2]
     return {
+        "accuracy": accuracy,
         "value": rows / dt,
         "repeats": {"n": repeats, "rule": "median", "value_runs": [rows / t for t in dts],
                     "value_1thread_runs": [rows_1t / t for t in dt1s]},
@@ -329,23 +354,48 @@ def _kernel_src_sha():
     return h.hexdigest()[:16]
 
 
-def spawn_ranks(nproc):
+def spawn_ranks(nproc, argv=None, poll=0.05, grace=20.0):
     """`bench.py --gpus N` without a launcher: start N rank processes (one per
-    GPU) before anything touches a GPU, wait, exit with the worst status."""
+    GPU) before anything touches a GPU and poll them.  The first rank that
+    exits non-zero ends the others (a dead rank would leave them blocked in a
+    collective until an outside timeout, with no line written): SIGTERM, then
+    SIGKILL after `grace` seconds.  Returns 0, or the first failure's status
+    (128 + signal for a rank killed by a signal)."""
     import socket
     import subprocess
 
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
+    argv = [os.path.abspath(__file__)] + sys.argv[1:] if argv is None else argv
     procs = []
     for r in range(nproc):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc),
                    LOCAL_WORLD_SIZE=str(nproc), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
+        procs.append(subprocess.Popen([sys.executable] + argv, env=env))
+    alive, rc = list(procs), 0
+    while alive and rc == 0:
+        for p in list(alive):
+            r = p.poll()
+            if r is None:
+                continue
+            alive.remove(p)
+            if r != 0:
+                rc = r if r > 0 else 128 - r
+                print(f"bench.py: rank {procs.index(p)} exited with status {r}; ending the other ranks",
+                      file=sys.stderr, flush=True)
+                break
+        else:
+            time.sleep(poll)
+    for p in alive:
+        p.terminate()
+    deadline = time.time() + grace
+    for p in alive:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
     return rc
 
 
@@ -414,6 +464,13 @@ def main():
     model = S.GaussianSum(list(mus), list(covs))
     if args.device_model:
         ctx.set_device_model(model)
+    # the device's phi_hat of X0 for the accuracy record of the CPU leg
+    # (untimed, before the warm-up; it moves no particles)
+    acc = None
+    if world == 1 and args.sim_world <= 1 and not args.no_cpu:
+        G0 = model.log_model_grad(X0)
+        a0, _ = ctx.median_scale()
+        acc = (G0, a0, ctx.phi(G0, a0), dtype)
 
     def step():
         if args.device_model:
@@ -619,6 +676,8 @@ def main():
             "gpu_diag": gpu_diag,
             "median_path": ["direct", "bracket", "fallback", "rebracket"][path],
             "scale_a": a,
+            # every SVGD_* variable of this run (library knobs; none by default)
+            "env_knobs": {k: v for k, v in sorted(os.environ.items()) if k.startswith("SVGD_")},
         }
         if b3:
             out["roofline"].update(b3)
@@ -646,7 +705,8 @@ def main():
             out["metric"] = (f"particle-updates/s, {desc}"
                              f"{', device grad log p' if args.device_model else ''} (not the headline config)")
         if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows or cfg["cpu_rows"], args.cpu_rows_1t)
+            out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows or cfg["cpu_rows"], args.cpu_rows_1t,
+                                               acc=acc)
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist is not None:

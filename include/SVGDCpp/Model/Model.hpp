@@ -433,6 +433,13 @@ private:
         out.op_ = op;
         out.lhs_ = CloneSharedPointer();
         out.rhs_ = obj.CloneSharedPointer();
+        // a derived model that overrides the evaluation virtuals but not
+        // CloneSharedPointer would be sliced to a base Model here (and fail
+        // only later, inside SVGD::Run): refuse it now
+        if (typeid(*out.lhs_) != typeid(*this) || typeid(*out.rhs_) != typeid(obj))
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
+                                        "[Argument Error] A derived model must override CloneSharedPointer "
+                                        "(returning a copy of its own type) to be composed.");
         return out;
     }
 

@@ -212,7 +212,13 @@ int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *c
  *   TRK_MISS         of those, steps redone because the bracket missed
  *   SIM_WORLD        simulated world of a measurement context (svgd_create_sim), else 1
  *   CPU_QUOTA        CPUs of the cgroup quota (0: none); a rank's gradient
- *                    threads are at most CPU_QUOTA / world (or / SIM_WORLD) */
+ *                    threads are at most CPU_QUOTA / world (or / SIM_WORLD)
+ *   SPLIT_STEPS      steps whose phi + update ran in two row parts (the first
+ *                    part's X_{t+1} feeding the next host gradient early)
+ *   MIRROR_STEPS     host-model steps whose gradient read X_t from the
+ *                    update's pinned mirror instead of a copy
+ *   SPEC_STEPS       steps whose median took the speculative device plan
+ *   G_COMM           1 if the G all-gather has its own communicator and stream */
 #define SVGD_DIAG_STEPS 0
 #define SVGD_DIAG_PHI_KERNEL_MS 1
 #define SVGD_DIAG_PHI_KERNEL_N 2
@@ -232,7 +238,11 @@ int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *c
 #define SVGD_DIAG_TRK_MISS 16
 #define SVGD_DIAG_SIM_WORLD 17
 #define SVGD_DIAG_CPU_QUOTA 18
-#define SVGD_DIAG_LEN 19
+#define SVGD_DIAG_SPLIT_STEPS 19
+#define SVGD_DIAG_MIRROR_STEPS 20
+#define SVGD_DIAG_SPEC_STEPS 21
+#define SVGD_DIAG_G_COMM 22
+#define SVGD_DIAG_LEN 23
 int svgd_get_diagnostics(svgd_ctx *ctx, double *out, int cap);
 /* Name and template arguments of the phi kernel this context launches, as
  * rocprofv3 prints them (e.g. "k_phi_rows<8, 4, 8, 8192, 8>"): the key under
@@ -272,10 +282,8 @@ int svgd_model_neg_hess_sum(void *model, const double *X, int64_t nrows, double 
  * calls.  Not for SVGD_SCALE_HESSIAN (that step also needs the caller's
  * Hessian sum).  On a shard of <= 1 MiB the previous update's epilogue
  * leaves X_t in a context-private pinned buffer instead of a copy
- * (SVGD_X_MIRROR=0 disables it; SVGD_G_HOSTREAD=1, one rank, also has the
- * record prep read G_t from the pinned G buffer instead of its copies): the
- * buffers of svgd_host_buffers are then not guaranteed to hold X_t
- * afterwards. */
+ * (SVGD_X_MIRROR=0 disables it): the buffers of svgd_host_buffers are then
+ * not guaranteed to hold X_t afterwards. */
 int svgd_step_host_model(svgd_ctx *ctx, const void *model);
 
 /* Mirror a built-in Gaussian-sum model (svgd_model_create) on the device

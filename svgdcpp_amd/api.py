@@ -23,6 +23,7 @@ batched log_model_grad).
 """
 from __future__ import annotations
 
+import copy
 import ctypes
 import enum
 import math
@@ -110,6 +111,9 @@ class Model:
             n1 = len(self._lhs.GetParameters())
             if len(params) != n1 + len(self._rhs.GetParameters()):
                 raise DimensionMismatchException("Number of parameters does not match the model.")
+            # copy on write: copies of this composition share its operands
+            # (the reference's composed model keeps its own parameters, :70-81)
+            self._lhs, self._rhs = _clone_model(self._lhs), _clone_model(self._rhs)
             self._lhs.UpdateParameters(list(params[:n1]))
             self._rhs.UpdateParameters(list(params[n1:]))
             return
@@ -198,7 +202,9 @@ class Model:
             raise UnsetException("One of the model functions is unset; functional composition "
                                  "requires both model functions to be set.")
         out = Model(self.dimension_)
-        out._op, out._lhs, out._rhs = op, self, other
+        # copies of the operands: updating the composition's parameters must
+        # not change the models it was built from (Model.hpp:70-81)
+        out._op, out._lhs, out._rhs = op, _clone_model(self), _clone_model(other)
         return out
 
     def __add__(self, other):  # Model.hpp:55-92
@@ -341,6 +347,24 @@ class MultivariateNormal(GaussianSum):
 
     def GetNormalizationConstant(self):  # MultivariateNormal.hpp:182-186
         return 1.0 / ((2.0 * math.pi) ** (self.dimension_ / 2.0) * math.sqrt(np.linalg.det(self.covs_[0])))
+
+
+def _clone_model(model):
+    """A copy of a model that shares no mutable state with it: parameter
+    lists and Gaussian components copied, a GaussianSum's C++ host model
+    rebuilt (its handle is owned by one object), composed operands cloned in
+    turn.  Other attributes of a user subclass are copied shallowly, as a C++
+    copy constructor copies its members."""
+    c = copy.copy(model)
+    c.model_parameters_ = [np.array(q, copy=True) for q in model.model_parameters_]
+    if isinstance(model, GaussianSum):
+        c.means_ = [m.copy() for m in model.means_]
+        c.covs_ = [v.copy() for v in model.covs_]
+        c._handle = None  # (never free the original's)
+        c._build()
+    if model._lhs is not None:
+        c._lhs, c._rhs = _clone_model(model._lhs), _clone_model(model._rhs)
+    return c
 
 
 def _builtin_grad(model):

@@ -200,7 +200,7 @@ struct svgd_ctx {
     int S2 = 0, S2b = 0;
     hipEvent_t ev_xhalf = nullptr;
     int R = 2; // rows per lane of k_phi_rows
-    int phi_kind = 0; // 0 k_phi_rows (4 waves), 1 k_phi_rows_s (scalar columns), 2 k_phi_rows (8 waves, column-split)
+    int phi_kind = 0; // 0 k_phi_rows (4 waves: matrix scales), 2 k_phi_rows (8 waves, column-split)
     // symmetric phi pass (k_phi_sym, one rank, d <= 8): geometry and buffers
     bool sym = false;
     int symB = 0, symSRS = 0, symNSUB = 0, sym_grid = 0, sym_rslots = 0;
@@ -260,15 +260,12 @@ struct svgd_ctx {
 
     // pinned host
     double *h_x = nullptr, *h_g = nullptr;
-    double *h_g_dev = nullptr; // its device address (coherent memory)
     // svgd_step_host_model on a small shard (<= XMIRROR_MAX bytes): the update
     // epilogue also stores X_{t+1} into h_xm (xmirror; xh_valid while X has not
     // changed otherwise since; a buffer of its own: h_x, the caller's, is
-    // never written by the device behind its back), and a single rank's record prep reads G_t
-    // straight from h_g (ghost, ghost_step for the step that does) -- no D2H /
-    // H2D copy-engine round trips and cross-queue waits on the host
-    // gradient's path (cfg2: phi waited ~70 us for G behind them)
-    bool xmirror = false, xh_valid = false, ghost = false, ghost_step = false;
+    // never written by the device behind its back) -- no D2H copy-engine round
+    // trip and cross-queue wait on the host gradient's path
+    bool xmirror = false, xh_valid = false;
     // Mean partials from the update epilogue (one rank, row path, not the
     // symmetric pass): k_phi_reduce leaves X_{t+1}'s per-block column sums in
     // xsum (xsum_parts blocks) and zeroes nmax, so the next centrings skip
@@ -392,6 +389,10 @@ struct svgd_ctx {
     // 1 its keys are in h_trk / h_cnt, 2 it took another path (history restarts)
     int trk_sync = 0;
     int64_t trk_steps = 0, trk_miss = 0;
+    // path counters (svgd_get_diagnostics): steps whose phi ran in two row
+    // parts, host-model steps whose gradient read the update's pinned mirror,
+    // speculative steps
+    int64_t n_split = 0, n_mirror = 0, n_spec = 0;
 };
 
 namespace {
@@ -1206,7 +1207,6 @@ int check_results(svgd_ctx *c)
 // G shard -> device on the copy stream (ready at ev_g) ...
 int upload_g_begin(svgd_ctx *c, const double *G_shard)
 {
-    c->ghost_step = false;
     const size_t bytes = sizeof(double) * (size_t)c->nrows * c->dim;
     if (!G_shard) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null log-gradient buffer.");
     if (c->nrows > 0) {
@@ -1227,7 +1227,6 @@ int upload_g_begin(svgd_ctx *c, const double *G_shard)
 // compute stream once it needs G.
 int upload_g_finish(svgd_ctx *c)
 {
-    if (c->ghost_step) return SVGD_OK; // one rank, G read from h_g by the record prep
     if (c->gcomm) {
         // the issue-order invariant (svgd_ctx): with a median pending, every
         // comm call of scale_begin precedes this gcomm call on every rank
@@ -1255,9 +1254,6 @@ int upload_g(svgd_ctx *c, const double *G_shard)
     CHK(upload_g_begin(c, G_shard));
     return upload_g_finish(c);
 }
-
-// G_t as the phi chain reads it (all n rows)
-const double *gin(const svgd_ctx *c) { return c->ghost_step ? c->h_g_dev : c->G; }
 
 bool matrix_scale(const svgd_ctx *c)
 {
@@ -1316,16 +1312,16 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         if (*c->h_err == 1 && !c->rowpath)
             return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] The kernel scale matrix is not finite.");
         if (c->rowpath)
-            HIPCHK(c, launch_prep_rec_mat(c->xc, gin(c), c->sc_M, c->sc_L, c->sc_sgn, c->n, c->np,
+            HIPCHK(c, launch_prep_rec_mat(c->xc, c->G, c->sc_M, c->sc_L, c->sc_sgn, c->n, c->np,
                                           c->dim, c->KP, c->RS, c->rec, c->wv, c->stream));
         else
-            HIPCHK(c, launch_prep_v_mat(c->xc, gin(c), c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
+            HIPCHK(c, launch_prep_v_mat(c->xc, c->G, c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
                                         c->VW, c->zc, c->V, c->cvec, c->wv, c->stream));
     } else if (c->rowpath)
-        HIPCHK(c, launch_prep_rec(c->xc, gin(c), c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->RS,
+        HIPCHK(c, launch_prep_rec(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->RS,
                                   c->rec, c->stream));
     else
-        HIPCHK(c, launch_prep_v(c->xc, gin(c), c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
+        HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
                                 c->V, c->cvec, c->stream));
     // F32: the streamed kernel's operand-ordered column copies (k_swz_f32), or
     // the row-major fp32 copies of the generic tile kernel
@@ -1348,11 +1344,12 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     const bool sym = c->sym && !mat;
     const bool split = c->split_rows && c->in_host_step && c->rowpath && !mat && !sym && opt;
     c->xhalf_ready = split;
+    c->n_split += split ? 1 : 0;
     hipEvent_t k0 = sym ? (c->tlevel >= 2 ? take_ev(c) : nullptr) : diag_begin(c, c->stream);
     hipEvent_t k1 = k0 ? take_ev(c) : nullptr;
     if (sym) {
         c->mark = c->phi_end = nullptr;
-        SymArgs sa{c->dim,    c->xc,        c->KP,          gin(c),        c->nrm,       c->scal,
+        SymArgs sa{c->dim,    c->xc,        c->KP,          c->G,        c->nrm,       c->scal,
                    c->nmax,   c->n,         c->sym_nb,      c->sym_units, c->srec,     c->symok,
                    c->rowpart, c->sym_rslots, c->colpart,   c->sym_grid, c->row0,      c->nrows,
                    1.0 / (double)c->n, c->phi};
@@ -1683,6 +1680,7 @@ int plan_step(svgd_ctx *c)
     c->spec_step = c->spec_allowed && c->last_fast && c->scale_method == SVGD_SCALE_MEDIAN &&
                    c->bucket_cap >= c->spec_cap;
     if (c->spec_step && !c->bak) CHK(dalloc(c, &c->bak, 3 * std::max<int64_t>(1, c->nrows) * c->dim));
+    c->n_spec += c->spec_step ? 1 : 0;
     return SVGD_OK;
 }
 
@@ -1772,19 +1770,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             const int r = std::atoi(e);
             if (r == 1 || r == 2 || r == 4) c->R = r;
         }
-        // A/B knob: the scalar-column variant of the phi row stream (R rows per lane)
-        if (const char *e = std::getenv("SVGD_PHI_SMEM")) {
-            const int r = std::atoi(e);
-            if (phi_rows_s_supported(dim, r)) {
-                c->phi_kind = 1;
-                c->R = r;
-            }
-        }
-        // default: 8-wave work-groups, 8192-entry table, columns split over the
-        // waves (kind 2); SVGD_PHI_T8K=0 selects the 4-wave kernel (kind 0)
-        bool t8k = true;
-        if (const char *e = std::getenv("SVGD_PHI_T8K")) t8k = std::atoi(e) != 0;
-        if (t8k && c->phi_kind == 0 && phi_rows_t8k_supported(dim, c->R)) c->phi_kind = 2;
+        // 8-wave work-groups, 8192-entry table, columns split over the waves
+        // (kind 2); the 4-wave kernel (kind 0) serves the full-matrix scales
+        // (signature rows) and an R the 8-wave build does not have
+        if (phi_rows_t8k_supported(dim, c->R)) c->phi_kind = 2;
         const int64_t resident = (int64_t)phi_rows_blocks_per_cu(dim, c->R, c->phi_kind) * ncu;
         const int64_t rows_wg = c->phi_kind == 2 ? phi_rows_t8k_rows(c->R) : 256 * (int64_t)c->R;
         const int64_t iblocks = std::max<int64_t>(1, (c->nrows + rows_wg - 1) / rows_wg);
@@ -1902,21 +1891,15 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
     CHK(dalloc(c, &c->ccount, 1));
     const size_t hb = sizeof(double) * (size_t)std::max<int64_t>(1, c->nrows) * dim;
-    // coherent: the device writes h_x (mirror) and reads h_g (ghost) uncached
     HIPCHK(c, hipHostMalloc((void **)&c->h_x, hb, hipHostMallocDefault));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocCoherent));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_xm, hb, hipHostMallocCoherent));
-    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_xm_dev, c->h_xm, 0));
-    HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_g_dev, c->h_g, 0));
-    {
-        const bool small = hb <= XMIRROR_MAX;
-        c->xmirror = small;
-        // the G host read (prep reading h_g over PCIe) measured 2-4 us per
-        // step slower than the G copies at cfg2 (profiles/r04_g_hostread_ab.txt):
-        // opt-in
-        c->ghost = false;
-        if (const char *e = std::getenv("SVGD_X_MIRROR")) c->xmirror = std::atoi(e) != 0;
-        if (const char *e = std::getenv("SVGD_G_HOSTREAD")) c->ghost = c->plan_world == 1 && std::atoi(e) != 0;
+    HIPCHK(c, hipHostMalloc((void **)&c->h_g, hb, hipHostMallocDefault));
+    c->xmirror = hb <= XMIRROR_MAX;
+    if (const char *e = std::getenv("SVGD_X_MIRROR")) c->xmirror = std::atoi(e) != 0;
+    if (c->xmirror) {
+        // coherent: the update epilogue writes it uncached (the host reads it
+        // once the step's end event has passed); only a mirroring context pins it
+        HIPCHK(c, hipHostMalloc((void **)&c->h_xm, hb, hipHostMallocCoherent));
+        HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_xm_dev, c->h_xm, 0));
     }
     HIPCHK(c, hipHostMalloc((void **)&c->h_cnt, (CNT_LEN + 3) * sizeof(unsigned long long),
                             hipHostMallocDefault));
@@ -2448,11 +2431,9 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
             }
         }
     }
-    // one rank and a small G: the record prep reads h_g (no G copies)
-    const bool ghost = c->ghost;
-    c->ghost_step = ghost;
     // the gradient's input: X_t from the last update's mirror, or its copy
     const double *hx = c->xh_valid ? c->h_xm : c->h_x;
+    c->n_mirror += c->xh_valid && rows > 0 ? 1 : 0;
     // the gradient thread: each chunk waits for its X_t copy, evaluates the
     // model and queues its G copy on the copy stream (the calling thread only
     // touches `stream` until it waits for this job)
@@ -2464,7 +2445,7 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
     const clk::time_point t_post = clk::now();
     std::array<hipEvent_t, XCH> xw;
     std::copy(xwait, xwait + (rows > 0 ? nch : 0), xw.begin());
-    c->worker->post([c, m, d, rows, nch, chunk, ms_since, t_post, xw, ghost, hx](std::string &msg) -> int {
+    c->worker->post([c, m, d, rows, nch, chunk, ms_since, t_post, xw, hx](std::string &msg) -> int {
         for (int q = 0; q < nch && rows > 0; ++q) {
             int64_t r0, r1;
             chunk(q, &r0, &r1);
@@ -2482,7 +2463,6 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
             }
             c->h_xwait_ms += ms_since(tw, tg);
             c->h_grad_ms += ms_since(tg, clk::now());
-            if (ghost) continue;
             e = hipMemcpyAsync(c->G + (size_t)(c->row0 + r0) * d, c->h_g + r0 * d,
                                sizeof(double) * (size_t)(r1 - r0) * d, hipMemcpyHostToDevice,
                                c->cstream);
@@ -2490,11 +2470,6 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
                 msg = std::string("SVGDCpp: [HIP Error] G chunk copy: ") + hipGetErrorString(e);
                 return SVGD_ERR_HIP;
             }
-        }
-        if (ghost) { // h_g complete before the prep that reads it is queued
-            std::atomic_thread_fence(std::memory_order_seq_cst);
-            c->h_job_ms += ms_since(t_post, clk::now());
-            return SVGD_OK;
         }
         hipError_t e = hipEventRecord(c->ev_g, c->cstream);
         // the gradient thread waits for its copies to land (the device is
@@ -2540,7 +2515,6 @@ int svgd_step(svgd_ctx *c, const double *G_shard)
         return fail(c, SVGD_ERR_ARG,
                     "[Argument Error] Null log-gradient buffer and no device model set.");
     CHK(svgd_begin_step(c, nullptr));
-    c->ghost_step = false;
     HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
                                 c->dm_mu, c->dm_prec, c->G + (size_t)c->row0 * c->dim, c->stream));
     c->mark = nullptr; // (the gradient kernel runs after the median's end event)
@@ -2580,7 +2554,6 @@ int svgd_device_logp_grad(svgd_ctx *c, double *G_shard_out)
     CHK(resolve_pending(c));
     if (c->dm_k == 0) return fail(c, SVGD_ERR_UNSET, "[Unset Error] No device model set.");
     if (!G_shard_out) return fail(c, SVGD_ERR_ARG, "[Argument Error] Null output buffer.");
-    c->ghost_step = false;
     HIPCHK(c, launch_gauss_grad(c->X + (size_t)c->row0 * c->dim, c->nrows, c->dim, c->dm_k,
                                 c->dm_mu, c->dm_prec, c->phi, c->stream));
     HIPCHK(c, hipMemcpyAsync(G_shard_out, c->phi, sizeof(double) * (size_t)c->nrows * c->dim,
@@ -2685,12 +2658,17 @@ int svgd_get_diagnostics(svgd_ctx *c, double *out, int cap)
                                      (double)c->trk_steps,
                                      (double)c->trk_miss,
                                      (double)c->sim_world,
-                                     (double)c->cpu_quota};
+                                     (double)c->cpu_quota,
+                                     (double)c->n_split,
+                                     (double)c->n_mirror,
+                                     (double)c->n_spec,
+                                     c->gcomm ? 1.0 : 0.0};
     for (int i = 0; i < cap && i < SVGD_DIAG_LEN; ++i) out[i] = v[i];
     for (int k = 0; k < 4; ++k) c->dg_ms[k] = 0, c->dg_cnt[k] = 0;
     c->h_grad_ms = c->h_xwait_ms = c->h_job_ms = c->h_wait_ms = 0;
     c->h_steps = 0;
     c->trk_steps = c->trk_miss = 0;
+    c->n_split = c->n_mirror = c->n_spec = 0;
     return cap < SVGD_DIAG_LEN ? cap : SVGD_DIAG_LEN;
 }
 
@@ -2736,8 +2714,6 @@ int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
     } else if (c->rowpath) {
         if (c->phi_kind == 2)
             std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 8, 8192, 8>", d, c->R);
-        else if (c->phi_kind == 1)
-            std::snprintf(s, sizeof s, "k_phi_rows_s<%d, %d>", d, c->R);
         else
             std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 4, 4096, 1>", d, c->R);
     } else if (c->dtype == SVGD_F32 && c->B3) {

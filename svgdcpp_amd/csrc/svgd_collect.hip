@@ -650,7 +650,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     __syncthreads();
 
     uint64_t *region = sc.region + (int64_t)blockIdx.x * sc.cap;
-    uint32_t below = 0; // scalar
+    // scalar, 64-bit: one wave may classify more than 2^32 pairs (a small
+    // collect grid, or large N at d > 16)
+    unsigned long long below = 0;
     const int xl = 4 * kq - ql; // j - i = xl + r + 16 (w - rb) on diagonal tiles
     const float ninf = -__builtin_inff();
 
@@ -1030,7 +1032,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
     __syncthreads();
 
     uint64_t *region = sc.region + (int64_t)blockIdx.x * sc.cap;
-    uint32_t below = 0; // scalar
+    // scalar, 64-bit: one wave may classify more than 2^32 pairs (a small
+    // collect grid, or large N at d > 16)
+    unsigned long long below = 0;
     const int xl = 4 * kq - ql; // j - i = xl + r + 16 (w - rb) on diagonal tiles
 
     // staged entries -> keys (s = max(-v, 0), as k_pair_tiles' fmax) in the

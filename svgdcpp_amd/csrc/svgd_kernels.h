@@ -251,8 +251,6 @@ bool phi_sym_geom(int d, int *B, int *SRS, int *NSUB);
 int phi_sym_blocks_per_cu(int d);
 hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0, hipEvent_t ev_k1,
                           hipStream_t stream);
-// kind 1: the scalar-column variant k_phi_rows_s (phi_rows_s_supported)
-bool phi_rows_s_supported(int d, int R);
 // kind 2: k_phi_rows with 8-wave work-groups and the mask-free 8192-entry exp table
 bool phi_rows_t8k_supported(int d, int R);
 int phi_rows_t8k_rows(int R); // rows per work-group of kind 2

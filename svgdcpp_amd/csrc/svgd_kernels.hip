@@ -2857,158 +2857,6 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
     }
 }
 
-// ------------------------------------ phi row stream, scalar column loads --
-//
-// k_phi_rows with the column records read by the scalar unit (s_load into
-// SGPRs; the FMAs take the column operand straight from SGPRs) instead of
-// LDS DMA + 9 broadcast ds_read per column: no column registers in VGPRs
-// (R up to 6 rows per lane at 2 waves/SIMD) and no LDS instructions for the
-// columns -- the issue slots they took go to the VALU.  Same arithmetic,
-// same order: bit-identical partials.
-typedef const __attribute__((address_space(4))) double cdouble_t;
-
-template <int D> struct ColRecS {
-    double x[D], v[D], c;
-    __device__ __forceinline__ void load(const cdouble_t *rj)
-    {
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            x[k] = rj[k];
-            v[k] = rj[D + k];
-        }
-        c = rj[2 * D];
-    }
-};
-
-template <int D, int R, bool FOLD>
-__device__ __forceinline__ void phi_rows_pair_s(const ColRecS<D> &q, const double (&xs)[R][D],
-                                                const double (&ci)[R], double (&acc)[R][D],
-                                                double (&acc1)[R], const double *tab)
-{
-    double u[R], K[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) u[r] = FOLD ? q.c : ci[r] + q.c;
-#pragma unroll
-    for (int k = 0; k < D; ++k)
-#pragma unroll
-        for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], q.x[k], u[r]);
-    if constexpr (!FOLD) {
-#pragma unroll
-        for (int r = 0; r < R; ++r) u[r] = fmin(fmax(u[r], -EXP_U_CLAMP), EXP_U_CLAMP);
-    }
-    double f[R], T[R];
-    int ki[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const double k = __builtin_rint(u[r]);
-        f[r] = u[r] - k;
-        ki[r] = (int)k;
-        T[r] = tab[ki[r] & (EXP_TB - 1)];
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) K[r] = exp2_4096_poly(f[r]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) K[r] = K[r] * tab_scale(T[r], ki[r]);
-#pragma unroll
-    for (int k = 0; k < D; ++k)
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][k] = fma(K[r], q.v[k], acc[r][k]);
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc1[r] += K[r];
-}
-
-template <int D, int R>
-__global__ __launch_bounds__(256) void k_phi_rows_s(const double *__restrict__ rec,
-                                                   const double *__restrict__ a_ptr, int64_t row0,
-                                                   int64_t nrows, int64_t n, int S,
-                                                   double *__restrict__ part, int64_t ldp,
-                                                   const double *__restrict__ sgn,
-                                                   const unsigned long long *__restrict__ nmax_bits,
-                                                   const int *__restrict__ skip)
-{
-    constexpr int RS = RecLayout<D>::RS;
-    __shared__ double tab[EXP_TB];
-    if (skip && *skip) return;
-#pragma unroll
-    for (int e = 0; e < EXP_TB / 256; ++e)
-        tab[e * 256 + threadIdx.x] = tab_biased(EXP2_TAB4096[e * 256 + threadIdx.x], e * 256 + threadIdx.x);
-    __syncthreads();
-
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t iblk = blockIdx.x / S;
-    const int s = (int)(blockIdx.x - iblk * S);
-    const int64_t rbase = iblk * (256 * R) + w * (64 * R);
-    const double alpha = 8192.0 * LOG2E * (*a_ptr);
-
-    double xs[R][D], ci[R], acc[R][D], acc1[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        int64_t li = rbase + 64 * r + lane;
-        if (li >= nrows) li = nrows - 1;
-        const double *ri = rec + (row0 + li) * RS;
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            xs[r][k] = (sgn ? alpha * sgn[k] : alpha) * ri[k];
-            acc[r][k] = 0.0;
-        }
-        ci[r] = ri[2 * D];
-        acc1[r] = 0.0;
-    }
-
-    const int64_t j0 = n * s / S, j1 = n * (s + 1) / S;
-    const cdouble_t *crec = (const cdouble_t *)(rec);
-    constexpr double FOLD_MAX = 400.0;
-    const bool nowrap =
-        nmax_bits && LOG2E * (*a_ptr) * __longlong_as_double((long long)*nmax_bits) <= 300.0;
-    bool fold_ok = sgn == nullptr && nowrap;
-#pragma unroll
-    for (int r = 0; r < R; ++r) fold_ok = fold_ok && ci[r] >= -4096.0 * FOLD_MAX;
-    const bool fold = __all(fold_ok);
-    auto stream_columns = [&](auto fold_tag) {
-        constexpr bool FOLD = decltype(fold_tag)::value;
-        if (j0 >= j1) return;
-        // two SGPR copies of the column record: column j+1's scalar loads are
-        // in flight while column j is computed (rec has >= 64 padded rows
-        // past n, so the look-ahead past j1 - 1 stays inside the array)
-        ColRecS<D> qa, qb;
-        qa.load(crec + j0 * RS);
-        int64_t j = j0;
-        for (; j + 2 <= j1; j += 2) {
-            qb.load(crec + (j + 1) * RS);
-            phi_rows_pair_s<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
-            qa.load(crec + (j + 2) * RS);
-            phi_rows_pair_s<D, R, FOLD>(qb, xs, ci, acc, acc1, tab);
-        }
-        if (j < j1) phi_rows_pair_s<D, R, FOLD>(qa, xs, ci, acc, acc1, tab);
-    };
-    if (fold) {
-        stream_columns(std::true_type{});
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const double k = __builtin_rint(ci[r]);
-            const int ki = (int)k;
-            const double g = exp2_4096_poly(ci[r] - k) * tab_scale(tab[ki & (EXP_TB - 1)], ki);
-#pragma unroll
-            for (int k2 = 0; k2 < D; ++k2) acc[r][k2] *= g;
-            acc1[r] *= g;
-        }
-    } else {
-        stream_columns(std::false_type{});
-    }
-
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int64_t li = rbase + 64 * r + lane;
-        if (li < nrows) {
-            double *o = part + ((int64_t)s * ldp + li) * (D + 1);
-#pragma unroll
-            for (int k = 0; k < D; ++k) o[k] = acc[r][k];
-            o[D] = acc1[r];
-        }
-    }
-}
-
 // ------------------------------------------- fp32 tile phi, streamed (F32) --
 //
 // k_phi<float>'s arithmetic (Gram on v_mfma_f32_16x16x4f32, P = 2^t by
@@ -4197,25 +4045,6 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
     return hipGetLastError();
 }
 
-// scalar-column variant (k_phi_rows_s): d = 8, R in {4, 5}
-static hipError_t launch_rows_s(int d, int R, int grid, const double *rec, const double *a_ptr,
-                                int64_t row0, int64_t nrows, int64_t n, int S, double *part,
-                                int64_t ldp, const double *sgn, const unsigned long long *nmax,
-                                hipStream_t stream, const int *skip)
-{
-    if (d == 8 && R == 4)
-        hipLaunchKernelGGL((k_phi_rows_s<8, 4>), dim3(grid), dim3(256), 0, stream, rec, a_ptr, row0,
-                           nrows, n, S, part, ldp, sgn, nmax, skip);
-    else if (d == 8 && R == 5)
-        hipLaunchKernelGGL((k_phi_rows_s<8, 5>), dim3(grid), dim3(256), 0, stream, rec, a_ptr, row0,
-                           nrows, n, S, part, ldp, sgn, nmax, skip);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
-bool phi_rows_s_supported(int d, int R) { return d == 8 && (R == 4 || R == 5); }
-
 // kind 2: k_phi_rows with 8 waves, the 8192-entry table and the columns split
 // over the 8 waves (WC = 8: one 64 R-row group per work-group); R = 4 for
 // d <= 8, 2 above (the register budget)
@@ -4258,8 +4087,6 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
     const int grid = (int)(((nrows + rows_wg - 1) / rows_wg) * S);
     hipError_t e = kind == 2 ? launch_rows_t8k(d, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                                nmax_bits, stream, skip)
-                   : kind == 1 ? launch_rows_s(d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
-                                             nmax_bits, stream, skip)
                              : launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                       nmax_bits, nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
                                       SinkDebug{}, stream, skip);
@@ -4947,11 +4774,6 @@ int phi_rows_blocks_per_cu(int d, int R, int kind)
             break;
         }
 #undef SVGD_T8K_OCC
-        return (e == hipSuccess && nb > 0) ? nb : 1;
-    }
-    if (kind == 1) {
-        if (d == 8 && R == 4) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows_s<8, 4>, 256, 0);
-        if (d == 8 && R == 5) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_phi_rows_s<8, 5>, 256, 0);
         return (e == hipSuccess && nb > 0) ? nb : 1;
     }
     switch (d) {

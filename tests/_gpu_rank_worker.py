@@ -38,8 +38,8 @@ def run(rank, world, name, n, d, steps, q, env=None):
             scales.append(ctx.last_scale()[:3])
         X = ctx.get_particles()
         shard = (ctx.row0, ctx.row1)
-        trk = ctx.diagnostics()["trk_steps"]
+        diag = ctx.diagnostics()
         ctx.close()
-        q.put(("ok", rank, X, scales, shard, trk))
+        q.put(("ok", rank, X, scales, shard, diag))
     except Exception:
         q.put(("err", rank, traceback.format_exc(), None, None, None))

@@ -585,6 +585,16 @@ public:
     }
 };
 
+// the same closed forms without a CloneSharedPointer override: composing it
+// would slice it to a base Model, so the composition refuses it at once
+class NoCloneQuad : public Model
+{
+public:
+    NoCloneQuad() : Model(2) {}
+    double EvaluateModel(const Eigen::VectorXd &x) override { return 1.0 + x(0) * x(0); }
+    Eigen::VectorXd EvaluateModelGrad(const Eigen::VectorXd &x) override { return Eigen::Vector2d(2.0 * x(0), 0.0); }
+};
+
 // grad (and Hessian) of m at x against central differences of the level below
 static void CheckDerivatives(Model &m, const Eigen::VectorXd &x, bool hess)
 {
@@ -674,6 +684,9 @@ static void TestModelComposition()
     // method-3 derived models compose (through CloneSharedPointer), also
     // with Gaussian forms and inside deeper compositions
     ShiftedQuad sqd;
+    NoCloneQuad ncq;
+    CHECK(Throws<std::invalid_argument>([&] { Model bad = ncq + lin; }));
+    CHECK(Throws<std::invalid_argument>([&] { Model bad = lin * ncq; }));
     Eigen::Matrix2d cov;
     cov << 1.2, 0.3, 0.3, 0.8;
     MultivariateNormal mvn(Eigen::Vector2d(0.2, -0.1), cov);

@@ -17,7 +17,7 @@ import _gpu_rank_worker as W
 pytestmark = pytest.mark.gpu
 
 
-def _run_ranks(world, n, d, steps, env=None, trk=None):
+def _run_ranks(world, n, d, steps, env=None, trk=None, diags=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     name = "svgd_" + uuid.uuid4().hex[:12]
@@ -27,11 +27,13 @@ def _run_ranks(world, n, d, steps, env=None, trk=None):
     out = {}
     try:
         for _ in range(world):
-            status, rank, X, scales, shard, ntrk = q.get(timeout=300)
+            status, rank, X, scales, shard, diag = q.get(timeout=300)
             assert status == "ok", X
             out[rank] = (X, scales, shard)
             if trk is not None:
-                trk[rank] = ntrk
+                trk[rank] = diag["trk_steps"]
+            if diags is not None:
+                diags[rank] = diag
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -77,6 +79,38 @@ def test_sharded_tracked_brackets_bit_identical(world, n):
         Xb, sb, _ = sampled[rank]
         assert np.array_equal(Xa, Xb), rank
         assert sa == sb, rank
+
+
+@pytest.mark.parametrize("world,n", [(4, 12007), (8, 20011)])
+def test_default_multirank_path_row_parts(world, n):
+    """The path a rank of P >= 4 takes by default at cfg3:
+    phi + update in two row parts (rows per rank > 2048 x the gradient
+    threads: SVGD_HOST_THREADS=1 here, as a rank of 8 on a 16-CPU box has 2),
+    the next gradient reading the update's pinned X mirror, speculative steps
+    with tracked median brackets, and every step's collective sequence hashed
+    and compared across ranks (SVGD_DEBUG_COLL=1) -- against one rank of the
+    same problem: the first scale bit-exact, later ones to the rounding of
+    X_t (1e-13), positions <= 1e-10 (phi's column splits differ)."""
+    d, steps = 5, 10
+    diags = {}
+    multi = _run_ranks(world, n, d, steps, {"SVGD_HOST_THREADS": "1", "SVGD_DEBUG_COLL": "1"}, diags=diags)
+    single = _run_ranks(1, n, d, steps, {"SVGD_HOST_THREADS": "1"})[0]
+    X1, s1, _ = single
+    for rank, (X, scales, (r0, r1)) in multi.items():
+        dg = diags[rank]
+        assert dg["ranks"] == world, dg
+        # every step but a redone one (a redo runs phi whole) in row parts;
+        # all but the first read X_t from the mirror; tracked brackets
+        assert dg["split_steps"] >= steps - 2, (rank, dg)
+        assert dg["mirror_steps"] >= steps - 3, (rank, dg)
+        assert dg["spec_steps"] >= steps - 3 and dg["trk_steps"] >= 3, (rank, dg)
+        assert scales[0][0] == s1[0][0], (rank, scales, s1)
+        np.testing.assert_allclose([s[0] for s in scales], [s[0] for s in s1], rtol=1e-13)
+        np.testing.assert_allclose(X, X1, rtol=0, atol=1e-10)
+    # the ranks' trajectories are one trajectory
+    Xs = [multi[r][0] for r in range(world)]
+    assert all(np.array_equal(Xs[0], x) for x in Xs[1:])
+    assert len({tuple(s[0] for s in multi[r][1]) for r in range(world)}) == 1
 
 
 def test_measurement_context_refuses_results():

@@ -62,24 +62,21 @@ def test_phi_random_shapes(oracle, n, d):
 
 @pytest.mark.parametrize("n,d", [(1, 2), (5, 8), (200, 8), (1000, 8), (2049, 8), (4000, 2),
                                  (777, 3), (130, 12), (70, 16)])
-def test_phi_row_kernel_variants(oracle, monkeypatch, n, d):
-    """The row stream's two work-group shapes: the default (kind 2: 8 waves
-    splitting one row group's columns, their sums added in LDS in wave order)
-    and the 4-wave kernel (SVGD_PHI_T8K=0, one partial per wave's rows).  Both
-    against the oracle; against each other only the summation order differs."""
+def test_phi_row_kernel(oracle, n, d):
+    """The row stream (8 waves splitting one row group's columns, their sums
+    added in LDS in wave order) against the oracle, and deterministic.  (The
+    4-wave kernel it replaced serves the full-matrix scales and is covered by
+    tests/test_gpu_matrix_scale.py.)"""
     X = oracle.splitmix((n, d), 2.0, 500 + n + d)
     G = oracle.splitmix((n, d), 1.0, 600 + n + d)
     a = 0.29
     ref = oracle.phi(X, G, a)
-    out = {}
-    for v in ("1", "0"):
-        monkeypatch.setenv("SVGD_PHI_T8K", v)
-        c = _ctx(X)
-        out[v] = c.phi(G, a)
-        assert np.array_equal(out[v], c.phi(G, a))  # deterministic
-        c.close()
-        assert np.max(np.abs(out[v] - ref)) <= PHI_TOL, v
-    assert np.max(np.abs(out["1"] - out["0"])) <= 1e-12
+    c = _ctx(X)
+    assert c.phi_kernel_name().startswith("k_phi_rows<%d, %d, 8, 8192, 8>" % (d, 4 if d <= 8 else 2))
+    out = c.phi(G, a)
+    assert np.array_equal(out, c.phi(G, a))  # deterministic
+    c.close()
+    assert np.max(np.abs(out - ref)) <= PHI_TOL
 
 
 @pytest.mark.parametrize("n,d", [(300, 32), (1111, 32), (1111, 48), (300, 64), (1111, 64), (1111, 17),

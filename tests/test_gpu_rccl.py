@@ -22,7 +22,7 @@ from svgdcpp_amd import _capi as C
 pytestmark = pytest.mark.gpu
 
 
-def _run(oracle, n, d, steps, rccl, monkeypatch, bucket_cap=None, sample=None):
+def _run(oracle, n, d, steps, rccl, monkeypatch, bucket_cap=None, sample=None, diag=None):
     if bucket_cap is not None:
         monkeypatch.setenv("SVGD_BUCKET_CAP", str(bucket_cap))
     uid = S.Context.unique_id() if rccl else None
@@ -34,11 +34,17 @@ def _run(oracle, n, d, steps, rccl, monkeypatch, bucket_cap=None, sample=None):
     c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
     if sample:
         c.check(c.lib.svgd_set_median_tuning(c.h, -1, sample, -1))
+    if diag is not None:
+        c.diagnostics()
+        c.check(c.lib.svgd_set_timing(c.h, 2))  # count the collectives
     scales = []
     for _ in range(steps):
         c.step_with_model(model)
         scales.append(c.last_scale())
     X = c.get_particles()
+    if diag is not None:
+        diag.update(c.diagnostics())
+        c.check(c.lib.svgd_set_timing(c.h, 0))
     c.close()
     return X, scales
 
@@ -55,10 +61,32 @@ def test_rccl_one_rank_step_bit_identical(oracle, monkeypatch, n, d, bucket_cap)
 
 
 def test_rccl_one_rank_tracked_brackets(oracle, monkeypatch):
-    """16 steps through the one-rank RCCL communicator (G all-gather on its
-    own communicator and stream, tracked median brackets from the fourth
-    speculative step on) against the same steps without one: bit-identical."""
-    Xa, sa = _run(oracle, 6000, 8, 16, True, monkeypatch)
+    """16 steps through the one-rank RCCL communicator (every collective on
+    the compute stream, tracked median brackets from the fourth speculative
+    step on) against the same steps without one: bit-identical."""
+    dg = {}
+    Xa, sa = _run(oracle, 6000, 8, 16, True, monkeypatch, diag=dg)
     Xb, sb = _run(oracle, 6000, 8, 16, False, monkeypatch)
     assert sa == sb
     assert np.array_equal(Xa, Xb)
+    assert dg["ranks"] == 1 and dg["g_comm"] == 0 and dg["gather_g_n"] == 0
+    assert dg["coll_n"] >= 16 * 3 and dg["trk_steps"] >= 3
+
+
+@pytest.mark.parametrize("n,d", [(6000, 8), (700, 24)])
+def test_rccl_one_rank_split_g_communicator(oracle, monkeypatch, n, d):
+    """SVGD_G_COMM=1: the G all-gather on its own communicator (ncclCommSplit
+    of the context's, the split's success agreed by a min all-reduce) and its
+    own stream, beside the median chain, the phi chain waiting on its event
+    -- 16 steps against the same steps without any communicator:
+    bit-identical, and the diagnostics show the split communicator carried
+    one G all-gather per step."""
+    monkeypatch.setenv("SVGD_G_COMM", "1")
+    dg = {}
+    Xa, sa = _run(oracle, n, d, 16, True, monkeypatch, diag=dg)
+    monkeypatch.delenv("SVGD_G_COMM")
+    Xb, sb = _run(oracle, n, d, 16, False, monkeypatch)
+    assert sa == sb
+    assert np.array_equal(Xa, Xb)
+    assert dg["g_comm"] == 1 and dg["ranks"] == 1, dg
+    assert dg["gather_g_n"] == 16, dg

@@ -143,6 +143,21 @@ def test_parameters_route_through_composition():  # Model.hpp:70-74, 377-406
     assert m.EvaluateModel(x) == pytest.approx(float(np.sum(newp[0] * x)) * float(x @ newp[3] @ x))
     with pytest.raises(api.DimensionMismatchException):
         m.UpdateParameters(newp[:3])
+    # the operands are copies (Model.hpp:70-81; tests/cpp/test_api.cpp): the
+    # update leaves a and b, and other compositions of them, untouched
+    assert a.EvaluateModel(x) == pytest.approx(float(np.sum(PARAMS[0].reshape(-1) * x)))
+    assert b.EvaluateModel(x) == pytest.approx(float(x @ PARAMS[1] @ x))
+    m2 = a + b
+    c2 = m2 * a  # a composition of a composition
+    m2.UpdateParameters(newp)
+    assert a.GetParameters()[0].tolist() == PARAMS[0].tolist()
+    assert c2.EvaluateModel(x) == pytest.approx((float(np.sum(PARAMS[0].reshape(-1) * x)) + float(x @ PARAMS[1] @ x))
+                                                * float(np.sum(PARAMS[0].reshape(-1) * x)))
+    # a copy of a composition keeps its parameters when the original's change
+    m3 = a * b
+    m3b = api._clone_model(m3)
+    m3.UpdateParameters(newp)
+    assert m3b.EvaluateModel(x) == pytest.approx(a.EvaluateModel(x) * b.EvaluateModel(x))
 
 
 def test_gaussian_operands():
@@ -167,3 +182,8 @@ def test_gaussian_operands():
     assert len(s.GetParameters()) == 4
     s.UpdateParameters(g2.GetParameters() + g1.GetParameters())
     assert s.EvaluateModel(x) == pytest.approx(p)
+    # a Gaussian operand of a composition is copied (its own C++ host model)
+    m.UpdateParameters([np.array([3.0, 3.0]), np.eye(2)] + sq.GetParameters())
+    np.testing.assert_allclose(g1.log_model_grad(x[None])[0],
+                               -np.linalg.solve([[1.0, 0.2], [0.2, 0.8]], x - np.array([0.0, 1.0])), rtol=1e-12)
+    np.testing.assert_allclose(m.EvaluateLogModelGrad(x), -(x - 3.0) + sq.EvaluateLogModelGrad(x), rtol=1e-10)
