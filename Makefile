@@ -1,7 +1,7 @@
 # Top-level build of the MI355X (gfx950) SVGD library and test/bench helpers.
 #   make            -> svgdcpp_amd/libsvgdcpp_amd.so (HIP kernels + C ABI, links RCCL)
 #   make oracle     -> oracle/liboracle.so (CPU restatement; test infrastructure)
-#   make cpp        -> build/{mvn_example,gmm_example,test_api} (SVGDCpp-compatible C++ API)
+#   make cpp        -> build/{mvn_example,gmm_example,svgd_run_bench,test_api,test_dist} (SVGDCpp-compatible C++ API)
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
@@ -45,7 +45,7 @@ oracle:
 CPP_FLAGS := -O2 -std=c++17 -Wall -fopenmp -Iinclude
 CPP_LINK := -Lsvgdcpp_amd -lsvgdcpp_amd -Wl,-rpath,'$$ORIGIN/../svgdcpp_amd' -Wl,--allow-shlib-undefined
 CPP_HDRS := $(wildcard include/SVGDCpp/*.hpp include/SVGDCpp/*/*.hpp) include/Core include/Model include/Kernel include/Optimizer
-CPP_BINS := build/mvn_example build/gmm_example build/test_api
+CPP_BINS := build/mvn_example build/gmm_example build/svgd_run_bench build/test_api build/test_dist
 
 cpp: $(CPP_BINS)
 
@@ -54,6 +54,10 @@ build/%: examples/%.cpp $(CPP_HDRS) $(LIB)
 	$(CXX) $(CPP_FLAGS) $< -o $@ $(CPP_LINK)
 
 build/test_api: tests/cpp/test_api.cpp $(CPP_HDRS) $(LIB)
+	@mkdir -p build
+	$(CXX) $(CPP_FLAGS) $< -o $@ $(CPP_LINK)
+
+build/test_dist: tests/cpp/test_dist.cpp $(CPP_HDRS) $(LIB)
 	@mkdir -p build
 	$(CXX) $(CPP_FLAGS) $< -o $@ $(CPP_LINK)
 

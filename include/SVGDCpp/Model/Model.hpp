@@ -369,6 +369,18 @@ public:
 
     int GetDimension() const { return dimension_; }
 
+    /** The C++ host model of a built-in Gaussian form (svgd_model_create;
+     *  built on first use), for svgd_step_host_model / svgd_set_device_model;
+     *  nullptr for any other model. */
+    const void *HostModelHandle()
+    {
+        if (!IsGaussianForm())
+            return nullptr;
+        if (!handle_)
+            Build();
+        return handle_.get();
+    }
+
     /** A built-in Gaussian form (MultivariateNormal or a sum of them): the
      *  batched C++ host gradient, the device model of svgd_set_device_model. */
     bool IsGaussianForm() const { return !means_.empty() && !model_fun_ && !lhs_; }

@@ -11,8 +11,21 @@
  *   host               G = grad log p(X_t) from the Model plugin (Model.hpp:335)
  *   svgd_finish_step   phi_hat (SVGD.hpp:407-454), optimizer increment, clamp (:393-399)
  *
+ * A built-in Gaussian model (MultivariateNormal or an operator+ sum of them,
+ * exactly those types) under the Median or Constant scale takes the one-call
+ * step svgd_step_host_model instead: the X_t copy, the host gradient and the
+ * G upload pipelined in row chunks behind the device median on a worker
+ * thread -- the path bench.py measures; same result bit for bit.
+ *
  * The coordinate matrix stays on the device during Run() and is written back
  * to *CoordinateMatrixPtr at the end (the reference mutates it every step).
+ *
+ * Extensions in SVGDOptions (defaults keep the reference's behaviour): the
+ * HIP device, the compute dtype of the O(N^2) work (SVGD_F64 / SVGD_F32),
+ * and a sharded run -- World ranks, this process's Rank and the 128-byte
+ * RCCL UniqueId (svgd_get_unique_id on one rank, broadcast by the caller):
+ * every rank passes the full coordinate matrix, owns rows [row0, row1) of
+ * the step and ends Run() with all of them (svgd_create_dist).
  * Requirements of the device path: the kernel is a GaussianRBFKernel
  * (Median, Hessian or Constant scale) and the optimizer is Adam, AdaGrad or
  * RMSProp.  With the Hessian scale, the kernel's model sums -hess log p(X_t)
@@ -35,14 +48,16 @@
 #include <fstream>
 #include <exception>
 #include <sstream>
+#include <typeinfo>
 
 #include "Core.hpp"
 #include "Kernel/GaussianRBFKernel.hpp"
 #include "Kernel/Kernel.hpp"
 #include "Model/Model.hpp"
+#include "Model/MultivariateNormal.hpp"
 #include "Optimizer/Optimizer.hpp"
 
-/** SVGD.hpp:27-52 (+ Device: HIP device index of the context). */
+/** SVGD.hpp:27-52 (+ Device, ComputeDtype, World / Rank / UniqueId). */
 struct SVGDOptions
 {
     size_t Dimension;
@@ -60,6 +75,16 @@ struct SVGDOptions
     /** Extension: significant digits of the logged matrices (0 = the stream
      *  default, 6, as the reference writes them). */
     int IntermediateMatricesPrecision = 0;
+    /** Extension: compute dtype of the O(N^2) work, SVGD_F64 (the
+     *  reference's precision) or SVGD_F32 (svgd_capi.h). */
+    int ComputeDtype = SVGD_F64;
+    /** Extension: a sharded run over World processes (one GPU each); this
+     *  process is Rank.  UniqueId: the 128 bytes of svgd_get_unique_id from
+     *  one rank (empty: World must be 1, or the host shared-memory rehearsal
+     *  backend SVGD_HOSTCOMM is set). */
+    int World = 1;
+    int Rank = 0;
+    std::vector<unsigned char> UniqueId;
     SVGDOptions() {}
 };
 
@@ -69,7 +94,7 @@ public:
     SVGD(const SVGDOptions &o)
         : SVGD(o.Dimension, o.NumIterations, o.CoordinateMatrixPtr, o.KernelPtr, o.ModelPtr, o.OptimizerPtr,
                o.LowerBound, o.UpperBound, o.Parallel, o.LogIntermediateMatrices, o.IntermediateMatricesOutputPath,
-               o.Device)
+               o.Device, o.ComputeDtype, o.World, o.Rank, o.UniqueId)
     {
         log_precision_ = o.IntermediateMatricesPrecision;
     }
@@ -86,7 +111,9 @@ public:
          const std::shared_ptr<Kernel> &kernel_ptr, const std::shared_ptr<Model> &model_ptr,
          const std::shared_ptr<Optimizer> &optimizer_ptr, const Eigen::VectorXd &bound_lower,
          const Eigen::VectorXd &bound_upper, const bool &parallel = false, const bool &log_intermediate_matrices = false,
-         const std::string &intermediate_matrices_output_path = "log.txt", int device = 0)
+         const std::string &intermediate_matrices_output_path = "log.txt", int device = 0,
+         int compute_dtype = SVGD_F64, int world = 1, int rank = 0,
+         const std::vector<unsigned char> &unique_id = {})
         : dimension_((int)coord_mat_ptr->rows()), num_iterations_(iter), parallel_(parallel),
           log_intermediate_matrices_(log_intermediate_matrices),
           intermediate_matrices_output_path_(intermediate_matrices_output_path)
@@ -143,11 +170,20 @@ public:
         if (optimizer_ptr_->Kind() < 0)
             throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
                                         "[Argument Error] The device path requires Adam, AdaGrad or RMSProp.");
+        if (!unique_id.empty() && unique_id.size() != 128)
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX + "[Argument Error] The RCCL unique id has 128 bytes.");
+        if (world > 1 && log_intermediate_matrices_)
+            throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
+                                        "[Argument Error] Intermediate matrices are logged by single-GPU runs only.");
 
         svgd_ctx *c = nullptr;
-        const int rc = svgd_create(&c, dimension_, (int64_t)num_particles_, SVGD_F64, device);
+        const int rc = world > 1 || !unique_id.empty()
+                           ? svgd_create_dist(&c, dimension_, (int64_t)num_particles_, compute_dtype, device, world,
+                                              rank, unique_id.empty() ? nullptr : unique_id.data())
+                           : svgd_create(&c, dimension_, (int64_t)num_particles_, compute_dtype, device);
         ctx_.reset(c, [](svgd_ctx *p) { svgd_destroy(p); });
         Check(rc);
+        Check(svgd_shard(c, &row0_, &row1_));
     }
 
     SVGD(const SVGD &) = delete;
@@ -223,20 +259,47 @@ public:
      *  host path of any other kernel. */
     bool UsesDevicePath() const { return rbf_ptr_ != nullptr; }
 
+    /** True when Step() takes the one-call pipelined step (svgd_step_host_model):
+     *  a built-in Gaussian model of exactly the Model / MultivariateNormal
+     *  type (a subclass may override the gradient or Step(): it keeps the
+     *  split calls), the Median or Constant scale, no matrix logging. */
+    bool UsesPipelinedStep() const
+    {
+        if (!UsesDevicePath() || log_intermediate_matrices_ || !model_ptr_->IsGaussianForm())
+            return false;
+        const Model &m = *model_ptr_;
+        if (typeid(m) != typeid(Model) && typeid(m) != typeid(MultivariateNormal))
+            return false;
+        return rbf_ptr_->GetScaleMethod() != GaussianRBFKernel::ScaleMethod::Hessian;
+    }
+
+    /** Rows [row0, row1) of the particles this rank steps (all of them on one GPU). */
+    int64_t ShardBegin() const { return row0_; }
+    int64_t ShardEnd() const { return row1_; }
+
 protected:
-    /** SVGD.hpp:373-400 on the device; the model gradient stays on the host. */
+    /** SVGD.hpp:373-400 on the device; the model gradient stays on the host
+     *  (this rank's rows).  A built-in Gaussian model takes the pipelined
+     *  one-call step (UsesPipelinedStep); any other model the split calls
+     *  with its LogModelGradBatch between them. */
     void Step(double *hx, double *hg)
     {
         svgd_ctx *c = ctx_.get();
         model_ptr_->Step();
+        if (UsesPipelinedStep())
+        {
+            Check(svgd_step_host_model(c, model_ptr_->HostModelHandle()));
+            return;
+        }
+        const int64_t rows = row1_ - row0_;
         Check(svgd_begin_step(c, hx));
         if (rbf_ptr_->GetScaleMethod() == GaussianRBFKernel::ScaleMethod::Hessian)
         {
             std::vector<double> H((size_t)dimension_ * dimension_);
-            rbf_ptr_->GetTargetModel()->NegHessSumBatch(hx, (int64_t)num_particles_, H.data());
+            rbf_ptr_->GetTargetModel()->NegHessSumBatch(hx, rows, H.data());
             Check(svgd_set_step_hessian_sum(c, H.data()));
         }
-        model_ptr_->LogModelGradBatch(hx, (int64_t)num_particles_, hg);
+        model_ptr_->LogModelGradBatch(hx, rows, hg);
         Check(svgd_finish_step(c, hg));
     }
 
@@ -462,6 +525,7 @@ protected:
     bool log_intermediate_matrices_ = false;
     bool initialized_ = false;
     int log_precision_ = 0;
+    int64_t row0_ = 0, row1_ = 0;
     std::vector<double> lower_, upper_;
     std::shared_ptr<Kernel> kernel_ptr_;
     std::shared_ptr<GaussianRBFKernel> rbf_ptr_;

@@ -151,3 +151,40 @@ def test_cpp_device_log_matches_oracle(oracle, tmp_path, which):
         cov = 5.0 * np.array([[0.2260, 0.1652], [0.1652, 0.6779]])
         _check_log(oracle, which, tmp_path, lambda X: oracle.logp_grad_gmm(X, mu[None], cov[None]),
                    lambda X: oracle.median_scale(X)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipelined", ["1", "0"])
+def test_cpp_sharded_run_matches_one_rank(tmp_path, pipelined):
+    """SVGDOptions World / Rank (C++ API, SVGD.hpp:27-52 + the extension):
+    two ranks of tests/cpp/test_dist.cpp on one GPU (host shared-memory
+    collectives, SVGD_HOSTCOMM; every step's collective sequence compared
+    across ranks) against the same program on one rank.  pipelined = 1: a
+    built-in Gaussian model (the one-call svgd_step_host_model step); 0: a
+    user subclass (the split begin / LogModelGradBatch of the rank's rows /
+    finish).  Both ranks end with the same matrix; it matches one rank's to
+    fp64 rounding of phi's column splits (<= 1e-10)."""
+    import uuid
+
+    _make_cpp()
+    exe = os.path.join(BUILD, "test_dist")
+    n, d, steps = 9001, 4, 8
+    env = dict(os.environ, SVGD_HOSTCOMM="svgd_cpp_" + uuid.uuid4().hex[:10], SVGD_DEBUG_COLL="1")
+    outs = [str(tmp_path / f"r{r}.bin") for r in range(2)]
+    procs = [subprocess.Popen([exe, "2", str(r), str(n), str(d), str(steps), outs[r], pipelined], env=env,
+                              cwd=BUILD, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+             for r in range(2)]
+    try:
+        logs = [p.communicate(timeout=300)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert all(p.returncode == 0 for p in procs), logs
+    one = str(tmp_path / "one.bin")
+    r = _run([exe, "1", "0", str(n), str(d), str(steps), one, pipelined])
+    assert r.returncode == 0, r.stdout + r.stderr
+    X = [np.fromfile(f, dtype=np.float64).reshape(n, d) for f in outs + [one]]
+    assert np.all(np.isfinite(X[2]))
+    assert np.array_equal(X[0], X[1])
+    assert np.max(np.abs(X[0] - X[2])) <= 1e-10

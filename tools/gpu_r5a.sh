@@ -8,7 +8,7 @@ O=gpurun_out/r5a
 mkdir -p $O
 T="python -u -m pytest -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread"
 timeout -k 10 600 $T -v -s tests/test_gpu_multirank.py tests/test_gpu_rccl.py tests/test_gpu_f32_accuracy.py \
-  tests/test_gpu_host_model_step.py > $O/pytest_new.log 2>&1; rc=$?
+  tests/test_gpu_host_model_step.py tests/test_cpp_api.py > $O/pytest_new.log 2>&1; rc=$?
 echo "new tests rc=$rc"; tail -3 $O/pytest_new.log; fault_guard $O/pytest_new.log
 [ $rc -ne 0 ] && { grep -E "^FAILED|Error|assert" $O/pytest_new.log | head -20; exit $rc; }
 grep -E "b3 |keys b3|cfg5 rows" $O/pytest_new.log | head -12
@@ -20,4 +20,7 @@ timeout -k 10 600 python bench.py --steps 20 --warmup 3 > $O/bench.log 2>&1 || {
 fault_guard $O/bench.log
 tail -1 $O/bench.log > $O/bench.json
 python3 -c "import json; d=json.load(open('$O/bench.json')); print('cfg3', round(d['ms_per_step'],4), d['value'], d['roofline']['frac'], d['cpu_baseline']['accuracy'], d['env_knobs'])"
+(cd build && timeout -k 10 300 ./svgd_run_bench > ../$O/bench_cpp.log 2>&1) || { tail -5 $O/bench_cpp.log; exit 1; }
+fault_guard $O/bench_cpp.log
+grep '^{' $O/bench_cpp.log | tail -1 > $O/bench_cpp.json; cut -c1-400 $O/bench_cpp.json
 echo r5a done
