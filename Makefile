@@ -32,7 +32,7 @@ $(SRC_DIR)/plan.o: $(SRC_DIR)/plan.cpp $(HDRS)
 $(SRC_DIR)/hostcomm.o: $(SRC_DIR)/hostcomm.cpp $(SRC_DIR)/hostcomm.h
 	$(HIPCC) -O2 -std=c++17 -fPIC -Wall -c $< -o $@
 
-$(SRC_DIR)/host_models.o: $(SRC_DIR)/host_models.cpp $(SRC_DIR)/host_grad_block.inc $(HDRS)
+$(SRC_DIR)/host_models.o: $(SRC_DIR)/host_models.cpp $(SRC_DIR)/host_grad_block.inc $(SRC_DIR)/host_grad_soa8.inc $(HDRS)
 	$(CXX) -O3 -std=c++17 -fPIC -fopenmp -Wall -Wno-psabi -c $< -o $@
 
 $(LIB): $(OBJS)
@@ -47,7 +47,12 @@ CPP_LINK := -Lsvgdcpp_amd -lsvgdcpp_amd -Wl,-rpath,'$$ORIGIN/../svgdcpp_amd' -Wl
 CPP_HDRS := $(wildcard include/SVGDCpp/*.hpp include/SVGDCpp/*/*.hpp) include/Core include/Model include/Kernel include/Optimizer
 CPP_BINS := build/mvn_example build/gmm_example build/svgd_run_bench build/test_api build/test_dist
 
-cpp: $(CPP_BINS)
+cpp: $(CPP_BINS) build/host_grad_bench
+
+# host gradient builds side by side (tools/bench_host_grad.cpp; host only)
+build/host_grad_bench: tools/bench_host_grad.cpp $(SRC_DIR)/host_models.o $(SRC_DIR)/host_models.h
+	@mkdir -p build
+	$(CXX) -O2 -std=c++17 -fopenmp $< $(SRC_DIR)/host_models.o -o $@
 
 build/%: examples/%.cpp $(CPP_HDRS) $(LIB)
 	@mkdir -p build

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <omp.h>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -78,6 +79,16 @@ namespace gb_avx2 {
 }
 #pragma GCC pop_options
 
+// AVX-512 hosts (the MI355X boxes' EPYC 9575F): 8 particles per call, one
+// per vector lane (host_grad_soa8.inc) -- about a quarter of the AVX2
+// block's instructions at d = 8, k = 4
+#pragma GCC push_options
+#pragma GCC target("avx512f,avx512dq,fma")
+namespace gb_avx512 {
+#include "host_grad_soa8.inc"
+}
+#pragma GCC pop_options
+
 typedef void (*GradBlockFn)(const HostModel *, const double *, int64_t, int, double *, double *, double *,
                             double *);
 GradBlockFn pick_grad_block()
@@ -86,22 +97,44 @@ GradBlockFn pick_grad_block()
     return (__builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) ? gb_avx2::logp_grad_block
                                                                            : gb_base::logp_grad_block;
 }
+bool have_avx512()
+{
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
+           __builtin_cpu_supports("fma");
+}
 
+// variant: 0 the host's best, 1 the 4-particle block (AVX2 / baseline), 2 SoA8 (AVX-512)
 static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, double *G,
-                           int nthreads)
+                           int nthreads, int variant = 0)
 {
     static const GradBlockFn block = pick_grad_block();
+    static const bool avx512 = have_avx512();
     const int d = m->d, k = m->k;
     if (nthreads <= 0) nthreads = omp_get_max_threads();
+    const bool soa8 = variant == 2 || (variant == 0 && avx512);
+    if (soa8 && !avx512) return; // (variant 2 forced on a host without AVX-512: refused by the caller)
 #pragma omp parallel num_threads(nthreads)
     {
-        std::vector<double> diff((size_t)GB_NP * d), gc((size_t)GB_NP * k * d), q((size_t)GB_NP * k);
-        const int64_t nblk = (nrows + GB_NP - 1) / GB_NP;
+        if (soa8) {
+            // 64-byte aligned by hand: outside the AVX-512 target a 64-byte
+            // vector type is not 64-byte aligned by the allocator
+            const size_t bytes = sizeof(double) * 8 * ((size_t)(2 + k) * d + k);
+            double *ws = static_cast<double *>(std::aligned_alloc(64, (bytes + 63) / 64 * 64));
+            const int64_t nblk = (nrows + 7) / 8;
 #pragma omp for schedule(static)
-        for (int64_t b = 0; b < nblk; ++b) {
-            const int64_t i0 = b * GB_NP;
-            block(m, X, i0, (int)std::min<int64_t>(GB_NP, nrows - i0), G, diff.data(), gc.data(),
-                  q.data());
+            for (int64_t b = 0; b < nblk; ++b)
+                gb_avx512::logp_grad_soa8(m, X, b * 8, (int)std::min<int64_t>(8, nrows - b * 8), G, ws);
+            std::free(ws);
+        } else {
+            std::vector<double> diff((size_t)GB_NP * d), gc((size_t)GB_NP * k * d), q((size_t)GB_NP * k);
+            const int64_t nblk = (nrows + GB_NP - 1) / GB_NP;
+#pragma omp for schedule(static)
+            for (int64_t b = 0; b < nblk; ++b) {
+                const int64_t i0 = b * GB_NP;
+                block(m, X, i0, (int)std::min<int64_t>(GB_NP, nrows - i0), G, diff.data(), gc.data(),
+                      q.data());
+            }
         }
     }
 }
@@ -112,6 +145,14 @@ int model_logp_grad_threads(const HostModel *m, const double *X, int64_t nrows, 
 {
     if (!m || (!X && nrows > 0) || (!G && nrows > 0)) return SVGD_ERR_ARG;
     logp_grad_rows(m, X, nrows, G, nthreads);
+    return SVGD_OK;
+}
+int model_logp_grad_variant(const HostModel *m, const double *X, int64_t nrows, double *G, int nthreads,
+                            int variant)
+{
+    if (!m || (!X && nrows > 0) || (!G && nrows > 0) || variant < 0 || variant > 2) return SVGD_ERR_ARG;
+    if (variant == 2 && !have_avx512()) return SVGD_ERR_ARG;
+    logp_grad_rows(m, X, nrows, G, nthreads, variant);
     return SVGD_OK;
 }
 } // namespace svgd_amd

@@ -14,4 +14,9 @@ struct HostModel {
 // svgd_model_logp_grad on nthreads OpenMP threads (<= 0: the OpenMP default)
 int model_logp_grad_threads(const HostModel *m, const double *X, int64_t nrows, double *G,
                             int nthreads);
+// A/B and tests: variant 1 the 4-particle block (AVX2 or baseline build),
+// 2 the 8-lane structure-of-arrays block (AVX-512 hosts only; else
+// SVGD_ERR_ARG), 0 the host's best (what every other call uses)
+int model_logp_grad_variant(const HostModel *m, const double *X, int64_t nrows, double *G, int nthreads,
+                            int variant);
 } // namespace svgd_amd
