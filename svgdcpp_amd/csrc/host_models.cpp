@@ -147,6 +147,7 @@ int model_logp_grad_threads(const HostModel *m, const double *X, int64_t nrows, 
     logp_grad_rows(m, X, nrows, G, nthreads);
     return SVGD_OK;
 }
+bool host_grad_avx512() { return have_avx512(); }
 int model_logp_grad_variant(const HostModel *m, const double *X, int64_t nrows, double *G, int nthreads,
                             int variant)
 {

@@ -266,19 +266,21 @@ struct svgd_ctx {
     // never written by the device behind its back) -- no D2H copy-engine round
     // trip and cross-queue wait on the host gradient's path
     bool xmirror = false, xh_valid = false;
-    // Mean partials from the update epilogue (one rank, row path, not the
-    // symmetric pass): k_phi_reduce leaves X_{t+1}'s per-block column sums in
-    // xsum (xsum_parts blocks) and zeroes nmax, so the next centrings skip
-    // k_mean_partial (a repeated centring of the same X re-forms the same
-    // max into nmax).  Two buffers: xsum_cur holds the current X's partials
-    // (valid from the reduce's enqueue until anything else moves X: the next
-    // update, svgd_set_particles), the other the previous X's -- which a
-    // redo (X_t restored) returns to, so a redone step centres exactly as
-    // the first attempt did.  SVGD_XSUM=0 turns it off.
-    double *xsum = nullptr; // 2 x xsum_stride
-    int64_t xsum_stride = 0;
-    int xsum_parts[2] = {0, 0}, xsum_cur = 0;
-    bool xsum_ok[2] = {false, false}, xsum_written = false;
+    // The centring fold (row path, d <= 16): X version xver (+1 per update,
+    // -1 for a redo's restore, +1 and the history cleared by
+    // svgd_set_particles) is centred on the mean of version xver - 1 when its
+    // column partials are at hand -- the ones that version's centring left in
+    // cpart[(xver - 1) & 1] -- so the centring is one launch at any P (else
+    // k_mean_partial's exact mean first).  Every rank centres the same
+    // all-gathered X the same way; a repeated centring of one version (a phi
+    // or scale call, a redo) finds the same partials, so it forms the same
+    // centre.  nmax (max |xc|^2) has a slot per version parity: a centring
+    // fills its own and zeroes the other for the next.
+    int64_t xver = 0;
+    double *cpart = nullptr; // 2 x cpart_stride
+    int64_t cpart_stride = 0;
+    int cpart_n[2] = {0, 0};
+    int64_t cpart_ver[2] = {-1, -1};
     double *h_xm = nullptr, *h_xm_dev = nullptr;
     unsigned long long *h_cnt = nullptr;
     double *h_scal = nullptr;
@@ -635,19 +637,27 @@ int mark_median_end(svgd_ctx *c)
     return SVGD_OK;
 }
 
+// max |xc|^2 of the current X version (its parity slot)
+unsigned long long *nmax_cur(const svgd_ctx *c) { return c->nmax ? c->nmax + (c->xver & 1) : nullptr; }
+
 int center(svgd_ctx *c, const SelState *st_init = nullptr)
 {
-    // the last update epilogue's partials (svgd_ctx::xsum): they stay valid
-    // while X does, so every centring of one X forms the same mean
-    const int xs = c->xsum_cur;
-    const bool pr = c->xsum && c->xsum_ok[xs];
+    // the fold (svgd_ctx::cpart): the previous version's partials as the centre
+    const int64_t v = c->xver;
+    const int ps = (int)((v - 1) & 1), cs = (int)(v & 1);
+    const bool have = c->cpart && c->cpart_ver[ps] == v - 1;
     // F32 at KP 32 / 64: the centring writes the fp32 copies itself
     const bool fused = c->dtype == SVGD_F32 && !c->rowpath && (c->KP == 32 || c->KP == 64);
-    HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np,
-                                 pr ? c->xsum + xs * c->xsum_stride : c->partial,
-                                 pr ? c->xsum_parts[xs] : c->nparts, c->xc, c->nrm, c->rowpath ? 1 : 0,
-                                 c->xf, c->nmax, c->cnt3 + 3, c->stream, c->st, st_init, pr,
-                                 fused ? c->xcf : nullptr, fused ? c->nrmf : nullptr));
+    HIPCHK(c, launch_mean_center(c->X, c->n, c->dim, c->KP, c->np, c->partial, c->nparts, c->xc, c->nrm,
+                                 c->rowpath ? 1 : 0, c->xf, nmax_cur(c), c->cnt3 + 3, c->stream, c->st,
+                                 st_init, have ? c->cpart + ps * c->cpart_stride : nullptr,
+                                 have ? c->cpart_n[ps] : 0, c->cpart ? c->cpart + cs * c->cpart_stride : nullptr,
+                                 c->nmax ? c->nmax + (1 - cs) : nullptr, fused ? c->xcf : nullptr,
+                                 fused ? c->nrmf : nullptr));
+    if (c->cpart) {
+        c->cpart_ver[cs] = v;
+        c->cpart_n[cs] = center_fold_grid(c->dim, c->np);
+    }
     if (c->dtype == SVGD_F32) {
         if (!fused) {
             HIPCHK(c, launch_cvt_f32(c->xc, c->np * c->KP, c->xcf, c->stream));
@@ -699,7 +709,7 @@ hipError_t pair_pass(svgd_ctx *c, int mode, int grid, uint64_t *regions, int64_t
     // the collect pass (mode 0) also histograms its candidates in key-range buckets
     uint32_t *bp = mode == 0 ? c->bpart : nullptr;
     if (c->rowpath)
-        return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->xf, c->nmax, c->n,
+        return launch_pair_rows(c->dim, c->KP, mode, grid, c->xc, c->nrm, c->xf, nmax_cur(c), c->n,
                                 c->pnb, c->tile0,
                                 c->tile0 + c->own_tiles, regions, cap, c->counts, c->below, c->st,
                                 c->ghist, bp, dbg, c->stream);
@@ -987,7 +997,7 @@ int collect_counts(svgd_ctx *c)
     if (c->rowpath && c->mcol && c->med_path != SVGD_MEDIAN_DIRECT && c->band_est <= MCOL_MAX_BAND)
         // bracket collect: fp32 MFMA classification, exact keys for the band
         // (a thin band only: each band pair is staged and finished one by one)
-        HIPCHK(c, launch_pair_mcol(c->dim, c->collect_grid, c->xc, c->xf, c->nmax, c->n, c->pnb,
+        HIPCHK(c, launch_pair_mcol(c->dim, c->collect_grid, c->xc, c->xf, nmax_cur(c), c->n, c->pnb,
                                    c->tile0, c->tile0 + c->own_tiles, c->regions, c->reg_cap,
                                    c->counts, c->below, c->st, c->bpart, c->mcol_bf16, c->stream));
     else if (!c->rowpath && c->dtype == SVGD_F32 && c->mcol)
@@ -1350,14 +1360,14 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     if (sym) {
         c->mark = c->phi_end = nullptr;
         SymArgs sa{c->dim,    c->xc,        c->KP,          c->G,        c->nrm,       c->scal,
-                   c->nmax,   c->n,         c->sym_nb,      c->sym_units, c->srec,     c->symok,
+                   nmax_cur(c),   c->n,         c->sym_nb,      c->sym_units, c->srec,     c->symok,
                    c->rowpart, c->sym_rslots, c->colpart,   c->sym_grid, c->row0,      c->nrows,
                    1.0 / (double)c->n, c->phi};
         HIPCHK(c, launch_phi_sym(sa, opt, k0, k1, c->stream));
         // the row stream takes the step instead when the records' flag says
         // the symmetric form would leave its range (symok = 0)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
-                                  c->ldp, 1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, opt,
+                                  c->ldp, 1.0 / (double)c->n, nullptr, nullptr, nmax_cur(c), c->phi, opt,
                                   c->stream, nullptr, c->phi_kind, c->symok));
     } else if (c->rowpath && split) {
         // two row halves: the first half's X_{t+1} is final at ev_xhalf, while
@@ -1365,36 +1375,25 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         // starts its gradient there)
         const int64_t h = c->split_h, d = c->dim;
         OptArgs o1 = *opt, o2 = *opt;
-        o1.nmax_zero = nullptr; // the second part's phi still reads nmax
-        if (o2.xsum) {
-            o2.xsum += phi_reduce_blocks((int)d, h) * d;
-            c->xsum_parts[1 - c->xsum_cur] =
-                (int)(phi_reduce_blocks((int)d, h) + phi_reduce_blocks((int)d, c->nrows - h));
-            c->xsum_written = true;
-        }
         o2.X += h * d;
         o2.m += h * d;
         o2.v += h * d;
         if (o2.bak) o2.bak += h * d;
         if (o2.xh) o2.xh += h * d;
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, h, c->n, c->S2, c->part, h,
-                                  1.0 / (double)c->n, nullptr, nullptr, c->nmax, c->phi, &o1, c->stream, k1,
+                                  1.0 / (double)c->n, nullptr, nullptr, nmax_cur(c), c->phi, &o1, c->stream, k1,
                                   c->phi_kind));
         HIPCHK(c, hipEventRecord(c->ev_xhalf, c->stream));
         hipEvent_t k2 = diag_begin(c, c->stream);
         hipEvent_t k3 = k2 ? take_ev(c) : nullptr;
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0 + h, c->nrows - h, c->n, c->S2b,
-                                  c->part, c->nrows - h, 1.0 / (double)c->n, nullptr, nullptr, c->nmax,
+                                  c->part, c->nrows - h, 1.0 / (double)c->n, nullptr, nullptr, nmax_cur(c),
                                   c->phi + h * d, &o2, c->stream, k3, c->phi_kind));
         if (k2) c->ev_diag.push_back({k2, k3, DG_PHI_KERNEL, true});
     } else if (c->rowpath) {
-        if (opt && opt->xsum) {
-            c->xsum_parts[1 - c->xsum_cur] = (int)phi_reduce_blocks(c->dim, c->nrows);
-            c->xsum_written = true;
-        }
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
                                   c->ldp, 1.0 / (double)c->n, mat ? c->wv : nullptr,
-                                  mat ? c->sc_sgn : nullptr, mat ? nullptr : c->nmax, c->phi, opt,
+                                  mat ? c->sc_sgn : nullptr, mat ? nullptr : nmax_cur(c), c->phi, opt,
                                   c->stream, k1, mat ? 0 : c->phi_kind));
     } else if (phis)
         HIPCHK(c, c->B3 ? launch_phi_b3(c->KP, c->NCB, c->B3, c->cvf, c->scal, c->row0, c->nrows, ntl,
@@ -1494,25 +1493,13 @@ int run_phi_opt(svgd_ctx *c)
     const bool fused = c->rowpath || phi_streamed(c);
     c->phi_end = nullptr;
     c->xh_valid = false;
-    // X_{t+1}'s partials go to the other buffer (X_t's stay for a redo)
-    const int xn = 1 - c->xsum_cur;
-    c->xsum_ok[xn] = c->xsum_written = false;
-    if (c->xsum && c->rowpath && !c->sym) {
-        o.xsum = c->xsum + xn * c->xsum_stride;
-        o.nmax_zero = c->nmax;
-    }
     CHK(run_phi(c, fused ? &o : nullptr));
-    if (c->xsum_written) {
-        c->xsum_ok[xn] = true;
-        c->xsum_cur = xn;
-    } else {
-        c->xsum_ok[c->xsum_cur] = false; // X moved without partials
-    }
     if (!fused) {
         HIPCHK(c, launch_opt_update(o, c->phi, c->stream));
         c->phi_end = nullptr;
     }
     c->xh_valid = o.xh != nullptr;
+    c->xver += 1; // X_{t+1} (the centring fold's version)
     // this rank's rows of X_{t+1} are final here: the next step's X_t copy
     // down (host gradient) need not wait for the X all-gather (P > 1)
     if (c->phi_end) {
@@ -1659,8 +1646,7 @@ int resolve_pending(svgd_ctx *c)
     c->t -= 1;
     c->spec_step = false;
     c->last_fast = false;
-    // X_t is back: so are its partials (the failed update wrote the other buffer)
-    if (c->xsum_written) c->xsum_cur = 1 - c->xsum_cur;
+    c->xver -= 1; // X_t is back (its centre's partials were never overwritten)
     CHK(scale_begin(c));
     CHK(scale_finish(c));
     CHK(run_phi_opt(c));
@@ -1810,7 +1796,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         }
         CHK(dalloc(c, &c->rec, c->np * c->RS));
         CHK(dalloc(c, &c->xf, c->np * med_f32_stride(dim)));
-        CHK(dalloc(c, &c->nmax, 1));
+        CHK(dalloc(c, &c->nmax, 2)); // one slot per X version parity (center)
         CHK(dalloc(c, &c->part, std::max({(int64_t)c->S * c->ldp, (int64_t)c->S2 * c->split_h,
                                           (int64_t)c->S2b * (c->nrows - c->split_h)}) * (dim + 1)));
         // symmetric phi pass: one rank (a pair feeds two particles, which
@@ -1843,15 +1829,9 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             CHK(dalloc(c, &c->symok, 1));
             c->sym = true;
         }
-        // only while k_center_d takes all the partials in one LDS sweep (its
-        // sequential loop over thousands of partials cost cfg3 0.17 ms)
-        bool want_xsum = c->world == 1 && c->sim_world <= 1 && !c->sym &&
-                         (phi_reduce_blocks(dim, c->nrows) + 1) * dim <= 1024;
-        if (const char *e = std::getenv("SVGD_XSUM")) want_xsum = want_xsum && std::atoi(e) != 0;
-        if (want_xsum) {
-            c->xsum_stride = (phi_reduce_blocks(dim, c->nrows) + 2) * dim;
-            CHK(dalloc(c, &c->xsum, 2 * c->xsum_stride));
-        }
+        // the centring fold (svgd_ctx::cpart)
+        c->cpart_stride = (int64_t)center_fold_grid(dim, c->np) * dim;
+        CHK(dalloc(c, &c->cpart, 2 * c->cpart_stride));
     } else {
         CHK(dalloc(c, &c->V, c->np * c->VW));
         if (f32) CHK(dalloc(c, &c->Vf, c->np * c->VW));
@@ -1944,17 +1924,21 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     }
     if (const char *e = std::getenv("SVGD_HOST_THREADS")) c->host_threads = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SVGD_DEBUG_COLL")) c->dbg_coll = std::atoi(e) != 0;
-    // phi in row halves when a rank of 4 or more has more than 2048 rows per
-    // gradient thread: then the host gradient (~18 us per 1000 rows and
-    // thread at cfg3's GMM) outlasts the device's median phase of a P-GPU
-    // step and phi waited for G; with halves the first half's gradient runs
-    // beside the second half's phi (cost: one launch pair and one event more
-    // per step).  Measured per-rank share of cfg3 (profiles/r04_sim_world):
-    // P = 8 at 2 threads 0.714 -> 0.656 ms, P = 4 at 4 threads 1.135 ->
-    // 1.098; P = 2 at 8 threads 2.020 -> 2.052 (its phi is long enough to hide
-    // the gradient whole: not split)
-    c->split_rows = c->rowpath && c->split_h > 0 && c->plan_world >= 4 &&
-                    c->nrows > 2048 * (int64_t)std::max(1, c->host_threads);
+    // phi in row halves when a rank of 4 or more has more rows per gradient
+    // thread than the device's median phase hides: then phi waited for G;
+    // with halves the first half's gradient runs beside the second half's
+    // phi (cost: a second phi launch and reduce, ~20 us at P = 8).  AVX2
+    // gradient block (~18 us per 1000 rows and thread at cfg3's GMM): split
+    // above 2048 rows per thread (profiles/r04_sim_world: P = 8 at 2 threads
+    // 0.714 -> 0.656 ms).  AVX-512 block (~7 us per 1000 rows and thread on
+    // the EPYC 9575F): the whole-rows step wins at P = 8 and 4
+    // (profiles/r05_sim_split_ab.txt: 0.580 vs 0.598 ms, 1.052 vs 1.077 ms),
+    // split above 8192 rows per thread.
+    {
+        const int64_t per_thread = svgd_amd::host_grad_avx512() ? 8192 : 2048;
+        c->split_rows = c->rowpath && c->split_h > 0 && c->plan_world >= 4 &&
+                        c->nrows > per_thread * (int64_t)std::max(1, c->host_threads);
+    }
     if (const char *e = std::getenv("SVGD_PHI_SPLIT")) c->split_rows = c->rowpath && c->split_h > 0 && std::atoi(e) != 0;
     HIPCHK(c, hipEventCreateWithFlags(&c->ev_xhalf, hipEventDisableTiming));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2067,7 +2051,7 @@ int svgd_destroy(svgd_ctx *c)
         if (p) (void)hipFree(p);
     if (c->B3) (void)hipFree(c->B3);
     if (c->XK) (void)hipFree(c->XK);
-    if (c->xsum) (void)hipFree(c->xsum);
+    if (c->cpart) (void)hipFree(c->cpart);
     for (double *p : dbufs)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
@@ -2262,7 +2246,8 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     c->have_particles = true;
     c->xhalf_ready = false;
     c->xh_valid = false;
-    c->xsum_ok[0] = c->xsum_ok[1] = false;
+    c->xver += 1;
+    c->cpart_ver[0] = c->cpart_ver[1] = -1; // new particles: centred on their own mean
     c->trk_n = c->trk_nerr = 0; // new particles: the median history restarts
     return SVGD_OK;
 }

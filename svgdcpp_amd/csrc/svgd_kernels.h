@@ -39,18 +39,26 @@ constexpr int NBK = 2048;
 // the step's own total, the speculative one the adaptive spec cap.
 constexpr int CAPG = 262144;
 
-// xc = X - mean (stride KP, zero padded), nrm = |xc|^2; nrm_in_slot also
+// xc = X - mu (stride KP, zero padded), nrm = |xc|^2; nrm_in_slot also
 // stores |xc|^2 at xc[j*KP + d] (the row-stream median record).
 // xf (optional, d <= 16): fp32 median records [xc | -|xc|^2/2 | 0..] of stride
 // med_f32_stride(d); nmax_bits: max |xc|^2 as double bits (atomicMax).
 // bzero (optional): NBK counters zeroed (the step's collect-pass bucket counts)
 // st_init (optional): written to *st_out by the launch (a predicted bracket)
+// The centre mu: the exact mean of X (k_mean_partial into partial[nparts],
+// which also zeroes nmax_bits), or -- the fold, d <= 16 on the row path, one
+// launch -- the mean of another X from its column partials pin[nin] (the
+// ones a previous centring left: the previous particles' mean).  Row path:
+// pout (optional) <- this X's column partials (center_fold_grid(d, np)
+// blocks of d) and *nmax_zero = 0 (the next centring's max target).
+int center_fold_grid(int d, int64_t np);
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
                               unsigned long long *bzero, hipStream_t stream,
                               SelState *st_out = nullptr, const SelState *st_init = nullptr,
-                              bool partials_ready = false, float *xcf = nullptr,
+                              const double *pin = nullptr, int nin = 0, double *pout = nullptr,
+                              unsigned long long *nmax_zero = nullptr, float *xcf = nullptr,
                               float *nrmf = nullptr);
 // (xcf / nrmf, KP 32 or 64: also the fp32 copies of xc and nrm, nrmf +inf in
 // the padding rows -- launch_cvt_f32 / launch_cvt_nrm_f32 in the same pass)
@@ -99,15 +107,7 @@ struct OptArgs {
     const double *lower, *upper; // clamp bounds (both or neither)
     double *bak;                 // X_t, m_t, v_t saved here when set (speculative step)
     double *xh = nullptr;        // X_{t+1} also stored here when set (pinned host mirror)
-    // k_phi_reduce only: per-block column sums of X_{t+1} (its rows, in row
-    // order) at xsum[block * d + k] -- the next step's mean partials, so its
-    // centring needs no k_mean_partial -- and *nmax_zero = 0 (k_center's
-    // atomicMax target; set on the LAST reduce launch of a step only)
-    double *xsum = nullptr;
-    unsigned long long *nmax_zero = nullptr;
 };
-// Blocks of k_phi_reduce (= mean partials written through OptArgs::xsum) for nrows rows
-int64_t phi_reduce_blocks(int d, int64_t nrows);
 hipError_t launch_opt_update(const OptArgs &o, const double *g, hipStream_t stream);
 // mode 0: collect keys in [st->lo_key, st->hi_key) into per-block regions and count
 // keys below lo_key; mode 1: radix histogram pass over all pairs (fallback);

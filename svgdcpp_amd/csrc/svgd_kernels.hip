@@ -18,6 +18,7 @@
 // f64 MFMA: v_mfma_f64_16x16x4_f64.  A/B lane maps: A[i = l&15][k = l>>4],
 // B[k = l>>4][j = l&15]; C/D: col = l&15, row = (l>>4) + 4*reg.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <type_traits>
 #include <stdint.h>
 
@@ -220,73 +221,85 @@ __global__ void k_center(const double *__restrict__ X, int64_t n, int d, int KP,
     }
 }
 
+// The centre of a centring from `nin` column-sum partials (nin * D <= 4096,
+// staged in sP): mu[k] = (sum of the partials) / n, every block summing them
+// in the same fixed order -- T threads per column take partials q, q + T, ...
+// in turn, then their T sums meet in a fixed tree -- so the centre is
+// bit-identical in every block and on every rank.
+template <int D>
+__device__ __forceinline__ void center_mean(const double *__restrict__ pin, int nin, int64_t n, double *sP,
+                                            double *mu)
+{
+    constexpr int T = D <= 2 ? 128 : D <= 4 ? 64 : D <= 8 ? 32 : 16; // threads per column
+    for (int e = threadIdx.x; e < nin * D; e += blockDim.x) sP[e] = pin[e];
+    __syncthreads();
+    __shared__ double sT[T * D];
+    const int k = threadIdx.x / T, q = threadIdx.x - k * T;
+    if (k < D) {
+        double s = 0.0;
+        for (int b = q; b < nin; b += T) s += sP[b * D + k];
+        sT[k * T + q] = s;
+    }
+    __syncthreads();
+    for (int h = T / 2; h > 0; h >>= 1) {
+        if (k < D && q < h) sT[k * T + q] += sT[k * T + q + h];
+        __syncthreads();
+    }
+    if (threadIdx.x < D) mu[threadIdx.x] = sT[threadIdx.x * T] / (double)n;
+    __syncthreads();
+}
+
 // k_center for d <= 16 with the median record stride KP = med_rec_stride(D):
-// the same values bit for bit, but the row's X loads unrolled (all in flight
-// together instead of one dependent load-store round trip per column: the
-// generic loop was latency-bound at 20 us for N = 65536, d = 8) and the
-// records written with 16-byte stores.
+// xc = X - mu, |xc|^2, the median records, max |xc|^2, with the row's X
+// loads unrolled and issued before the centre is formed (one row ahead: the
+// generic loop was latency-bound at 20 us for N = 65536, d = 8) and 16-byte
+// record stores.  The centre mu is the mean of the partials `pin`: those of
+// k_mean_partial (the exact mean of this X), or -- one launch per step --
+// those this kernel left for the previous X (its mean: any fixed centre near
+// the particles keeps the centred Gram form accurate, and the distances and
+// kernel values are translation invariant).  pout: this block's column sums
+// of its rows of X (the next centring's partials, gridDim.x * D values).
+// nmax_zero: the other max |xc|^2 slot, zeroed for the next centring.
 template <int D>
 __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, int64_t n,
-                                                  const double *__restrict__ partial, int nparts,
+                                                  const double *__restrict__ pin, int nin,
                                                   int64_t np, double *__restrict__ xc,
                                                   double *__restrict__ nrm, int nrm_in_slot,
                                                   float *__restrict__ xf,
                                                   unsigned long long *nmax_bits,
+                                                  unsigned long long *nmax_zero, double *__restrict__ pout,
                                                   unsigned long long *bzero, SelState *st_out,
                                                   SelState st_init)
 {
     constexpr int KP = med_rec_stride(D), KF = med_f32_stride(D);
     if (bzero && blockIdx.x == 0)
         for (int e = threadIdx.x; e < NBK; e += blockDim.x) bzero[e] = 0;
-    if (st_out && blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_init; // predicted bracket
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (st_out) *st_out = st_init; // predicted bracket
+        if (nmax_zero) *nmax_zero = 0;
+    }
     __shared__ double mu[D];
-    __shared__ double sP[1024];
-    // the first row's X is loaded before the mean (its latency overlaps the
+    __shared__ double sP[4096];
+    // the first row's X is loaded before the centre (its latency overlaps the
     // partials'), each later row's one iteration ahead
     const int64_t jstride = (int64_t)gridDim.x * blockDim.x;
     int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    double xn[D];
+    double xn[D], rs[D];
 #pragma unroll
-    for (int k = 0; k < D; ++k) xn[k] = j < n ? X[j * D + k] : 0.0;
-    if (nparts * D <= 1024) {
-        // every partial loaded at once (one coalesced sweep), then added in
-        // b order from LDS: the same sums as the loop below without its
-        // nparts / 8 dependent global round trips
-        for (int e = threadIdx.x; e < nparts * D; e += blockDim.x) sP[e] = partial[e];
-        __syncthreads();
-        if (threadIdx.x < D) {
-            double s = 0.0;
-            int b = 0;
-            for (; b + 8 <= nparts; b += 8) {
-                double v[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = sP[(b + u) * D + threadIdx.x];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) s += v[u];
-            }
-            for (; b < nparts; ++b) s += sP[b * D + threadIdx.x];
-            mu[threadIdx.x] = s / (double)n;
-        }
-    } else if (threadIdx.x < D) {
-        const int k = threadIdx.x;
-        double s = 0.0; // partials added in b order, as k_center
-        for (int b0 = 0; b0 < nparts; b0 += 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = b0 + u < nparts ? partial[(b0 + u) * D + k] : 0.0;
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (b0 + u < nparts) s += v[u];
-        }
-        mu[k] = s / (double)n;
+    for (int k = 0; k < D; ++k) {
+        xn[k] = j < n ? X[j * D + k] : 0.0;
+        rs[k] = 0.0;
     }
-    __syncthreads();
+    center_mean<D>(pin, nin, n, sP, mu);
     unsigned long long bmax = 0;
     for (; j < np; j += jstride) {
         double v[KP];
         const bool live = j < n;
 #pragma unroll
-        for (int k = 0; k < D; ++k) v[k] = xn[k];
+        for (int k = 0; k < D; ++k) {
+            v[k] = xn[k];
+            rs[k] += xn[k]; // (zero past n)
+        }
         const int64_t jn = j + jstride;
 #pragma unroll
         for (int k = 0; k < D; ++k) xn[k] = jn < n ? X[jn * D + k] : 0.0;
@@ -320,6 +333,20 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
             bmax = m > bmax ? m : bmax;
         }
     }
+    __shared__ double wsum[4][D];
+    if (pout) {
+        // the block's column sums of X: a fixed butterfly per wave, then the
+        // 4 waves in order
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            double t = rs[k];
+            for (int o2 = 32; o2 > 0; o2 >>= 1) t += __shfl_xor(t, o2);
+            rs[k] = t;
+        }
+        if ((threadIdx.x & 63) == 0)
+#pragma unroll
+            for (int k = 0; k < D; ++k) wsum[threadIdx.x >> 6][k] = rs[k];
+    }
     if (xf) {
         __shared__ unsigned long long wmax[4];
         if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = bmax;
@@ -329,7 +356,12 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
             for (int w = 0; w < (int)(blockDim.x >> 6); ++w) m = wmax[w] > m ? wmax[w] : m;
             atomicMax(nmax_bits, m);
         }
+    } else {
+        __syncthreads();
     }
+    if (pout && threadIdx.x < D)
+        pout[(int64_t)blockIdx.x * D + threadIdx.x] =
+            ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) + wsum[3][threadIdx.x];
 }
 
 // k_center for the tile path, KP = 32 / 64 (d > 16): the same values bit for
@@ -3393,28 +3425,13 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
         sm[e] = acc;
     }
     __syncthreads();
-    __shared__ double sx[256]; // X_{t+1} of the block's rows (OptArgs::xsum)
     if (own) {
         const double ph = inv_n * (sm[r_o * DP + k_o] + w_o * sm[r_o * DP + d]);
         phi[li_o * d + k_o] = ph;
-        if (do_opt) {
-            const double x = opt_apply(opt, li_o * d + k_o, ph, in_o);
-            if (opt.xsum) sx[o] = x;
-        }
-    }
-    if (do_opt && opt.xsum) {
-        // the next step's mean partials: this block's column sums in row order
-        if (opt.nmax_zero && blockIdx.x == 0 && threadIdx.x == 0) *opt.nmax_zero = 0;
-        __syncthreads();
-        if (threadIdx.x < d) {
-            double c = 0.0;
-            for (int r = 0; r < rows; ++r) c += sx[r * d + threadIdx.x];
-            opt.xsum[(int64_t)blockIdx.x * d + threadIdx.x] = c;
-        }
+        if (do_opt) opt_apply(opt, li_o * d + k_o, ph, in_o);
     }
 }
 
-int64_t phi_reduce_blocks(int d, int64_t nrows) { return (nrows + phi_red_rows(d) - 1) / phi_red_rows(d); }
 
 // Median pair sweep, row-stream form: each wave walks a contiguous run of the
 // rank's block tiles (plan.cpp); lane = particle i of the row block, j of the
@@ -4408,25 +4425,39 @@ hipError_t launch_cvt_f32(const double *src, int64_t cnt, float *dst, hipStream_
     return hipGetLastError();
 }
 
+int center_fold_grid(int d, int64_t np)
+{
+    int64_t g = (np + 255) / 256;
+    return (int)std::min<int64_t>(g, 4096 / std::max(1, d));
+}
+
 hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t np,
                               double *partial, int nparts, double *xc, double *nrm,
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
                               unsigned long long *bzero, hipStream_t stream, SelState *st_out,
-                              const SelState *st_init, bool partials_ready, float *xcf, float *nrmf)
+                              const SelState *st_init, const double *pin, int nin, double *pout,
+                              unsigned long long *nmax_zero, float *xcf, float *nrmf)
 {
     const SelState sinit = st_init ? *st_init : SelState{};
     if (!st_init) st_out = nullptr;
-    // partials_ready: the last update epilogue left X's column partials (and
-    // zeroed nmax_bits) -- k_phi_reduce's OptArgs::xsum
-    if (!partials_ready)
+    // pin: the column partials of another X (the fold, k_center_d only), else
+    // the exact mean of this X from k_mean_partial's (which also zeroes
+    // nmax_bits, the max target of this centring)
+    const bool fold = pin && d <= 16 && KP == med_rec_stride(d);
+    if (!fold) {
         hipLaunchKernelGGL(k_mean_partial, dim3(nparts), dim3(256), 0, stream, X, n, d, partial,
                            xf ? nmax_bits : nullptr);
+        pin = partial;
+        nin = nparts;
+    }
     int64_t g = (np + 255) / 256;
     if (g > 4096) g = 4096;
+    const int gd = center_fold_grid(d, np);
 #define SVGD_CENTER_CASE(Dv)                                                                  \
     case Dv:                                                                                  \
-        hipLaunchKernelGGL((k_center_d<Dv>), dim3(g), dim3(256), 0, stream, X, n, partial,    \
-                           nparts, np, xc, nrm, nrm_in_slot, xf, nmax_bits, bzero, st_out, sinit); \
+        hipLaunchKernelGGL((k_center_d<Dv>), dim3(gd), dim3(256), 0, stream, X, n, pin, nin,   \
+                           np, xc, nrm, nrm_in_slot, xf, nmax_bits, nmax_zero, pout, bzero, st_out, \
+                           sinit);                                                            \
         return hipGetLastError();
     if (d <= 16 && KP == med_rec_stride(d)) {
         switch (d) {

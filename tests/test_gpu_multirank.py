@@ -81,27 +81,34 @@ def test_sharded_tracked_brackets_bit_identical(world, n):
         assert sa == sb, rank
 
 
-@pytest.mark.parametrize("world,n", [(4, 12007), (8, 20011)])
-def test_default_multirank_path_row_parts(world, n):
-    """The path a rank of P >= 4 takes by default at cfg3:
-    phi + update in two row parts (rows per rank > 2048 x the gradient
-    threads: SVGD_HOST_THREADS=1 here, as a rank of 8 on a 16-CPU box has 2),
-    the next gradient reading the update's pinned X mirror, speculative steps
-    with tracked median brackets, and every step's collective sequence hashed
-    and compared across ranks (SVGD_DEBUG_COLL=1) -- against one rank of the
-    same problem: the first scale bit-exact, later ones to the rounding of
+@pytest.mark.parametrize("world,n,split", [(4, 12007, "auto"), (8, 20011, "auto"), (4, 12007, "1"),
+                                           (8, 20011, "1")])
+def test_default_multirank_path_row_parts(world, n, split):
+    """The path a rank of P >= 4 takes at cfg3: the next
+    gradient reading the update's pinned X mirror, speculative steps with
+    tracked median brackets, every step's collective sequence hashed and
+    compared across ranks (SVGD_DEBUG_COLL=1) -- with phi + update whole
+    (split "auto": the policy's choice at SVGD_HOST_THREADS=1, a rank of 8 on
+    a 16-CPU box has 2 threads) and in two row parts (SVGD_PHI_SPLIT=1, the
+    first part's X_{t+1} feeding the gradient early) -- against one rank of
+    the same problem: the first scale bit-exact, later ones to the rounding of
     X_t (1e-13), positions <= 1e-10 (phi's column splits differ)."""
     d, steps = 5, 10
     diags = {}
-    multi = _run_ranks(world, n, d, steps, {"SVGD_HOST_THREADS": "1", "SVGD_DEBUG_COLL": "1"}, diags=diags)
+    env = {"SVGD_HOST_THREADS": "1", "SVGD_DEBUG_COLL": "1"}
+    if split != "auto":
+        env["SVGD_PHI_SPLIT"] = split
+    multi = _run_ranks(world, n, d, steps, env, diags=diags)
     single = _run_ranks(1, n, d, steps, {"SVGD_HOST_THREADS": "1"})[0]
     X1, s1, _ = single
     for rank, (X, scales, (r0, r1)) in multi.items():
         dg = diags[rank]
         assert dg["ranks"] == world, dg
-        # every step but a redone one (a redo runs phi whole) in row parts;
-        # all but the first read X_t from the mirror; tracked brackets
-        assert dg["split_steps"] >= steps - 2, (rank, dg)
+        # forced split: every step but a redone one (a redo runs phi whole)
+        # in row parts; all but the first read X_t from the mirror; tracked
+        # brackets
+        if split == "1":
+            assert dg["split_steps"] >= steps - 2, (rank, dg)
         assert dg["mirror_steps"] >= steps - 3, (rank, dg)
         assert dg["spec_steps"] >= steps - 3 and dg["trk_steps"] >= 3, (rank, dg)
         assert scales[0][0] == s1[0][0], (rank, scales, s1)
