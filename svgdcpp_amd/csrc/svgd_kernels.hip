@@ -333,19 +333,12 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
             bmax = m > bmax ? m : bmax;
         }
     }
-    __shared__ double wsum[4][D];
+    // the block's column sums of X (pout): every thread's row sums to LDS
+    // (sP is free again), then thread k < D adds column k's 256 in thread order
     if (pout) {
-        // the block's column sums of X: a fixed butterfly per wave, then the
-        // 4 waves in order
+        __syncthreads(); // every block-mate is past its reads of sP
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-            double t = rs[k];
-            for (int o2 = 32; o2 > 0; o2 >>= 1) t += __shfl_xor(t, o2);
-            rs[k] = t;
-        }
-        if ((threadIdx.x & 63) == 0)
-#pragma unroll
-            for (int k = 0; k < D; ++k) wsum[threadIdx.x >> 6][k] = rs[k];
+        for (int k = 0; k < D; ++k) sP[k * 256 + threadIdx.x] = rs[k];
     }
     if (xf) {
         __shared__ unsigned long long wmax[4];
@@ -359,9 +352,17 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
     } else {
         __syncthreads();
     }
-    if (pout && threadIdx.x < D)
-        pout[(int64_t)blockIdx.x * D + threadIdx.x] =
-            ((wsum[0][threadIdx.x] + wsum[1][threadIdx.x]) + wsum[2][threadIdx.x]) + wsum[3][threadIdx.x];
+    if (pout && threadIdx.x < D) {
+        const double *col = sP + threadIdx.x * 256;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0; // four fixed interleaved chains
+        for (int t = 0; t < 256; t += 4) {
+            a0 += col[t];
+            a1 += col[t + 1];
+            a2 += col[t + 2];
+            a3 += col[t + 3];
+        }
+        pout[(int64_t)blockIdx.x * D + threadIdx.x] = (a0 + a1) + (a2 + a3);
+    }
 }
 
 // k_center for the tile path, KP = 32 / 64 (d > 16): the same values bit for
@@ -3410,18 +3411,27 @@ __global__ __launch_bounds__(256) void k_phi_reduce(const double *__restrict__ p
     }
     const int e = threadIdx.x;
     if (e < rows * DP) {
+        // 16 splits' loads in flight at once (one memory round trip at S <= 16,
+        // the usual case), added in s order
         const double *p = part + rb * DP + e;
         const int64_t st = ldp * DP;
         double acc = 0.0;
         int s = 0;
-        for (; s + 8 <= S; s += 8) {
-            double v[8];
+        for (; s + 16 <= S; s += 16) {
+            double v[16];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = p[(s + q) * st];
+            for (int q = 0; q < 16; ++q) v[q] = p[(s + q) * st];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc += v[q];
+            for (int q = 0; q < 16; ++q) acc += v[q];
         }
-        for (; s < S; ++s) acc += p[s * st];
+        if (s < S) {
+            double v[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) v[q] = s + q < S ? p[(s + q) * st] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 16; ++q)
+                if (s + q < S) acc += v[q];
+        }
         sm[e] = acc;
     }
     __syncthreads();
