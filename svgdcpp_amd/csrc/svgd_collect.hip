@@ -177,6 +177,14 @@ __device__ __forceinline__ uint32_t mcol_code4(const unsigned long long (&h)[4])
     return c0 | c1 | c2 | c3;
 }
 
+// a (lanes in mask) or b (the others), straight from a scalar lane mask
+__device__ __forceinline__ uint32_t mcol_sel(unsigned long long mask, uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %[r], %[b], %[a], %[m]" : [r] "=v"(r) : [a] "v"(a), [b] "v"(b), [m] "s"(mask));
+    return r;
+}
+
 // Row operands of one 16-row block for one lane: B (KK fp32) | TLf | THf | pad.
 template <int D> struct McolRow {
     static constexpr int KK = (D + 3) / 4;
@@ -488,9 +496,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                     if (scnt > MC_STG / 2) flush(ib, jbase);
                     if (jb + 4 < njb) load_cols(jb + 4, An, hqn);
                     const int jl0 = 16 * jb;
+                    // the lane's part of a staged entry for this column block
+                    // (row offset | the lane's 4-column offset << 16)
+                    const uint32_t ebase = (uint32_t)ql | ((uint32_t)(jl0 + 4 * kq) << 16);
                     float Bg[MC_NG][BW], Bn[MC_NG][BW];
                     f4 acc[MC_NG], accn[MC_NG];
                     group_mfma(0, hq, A, Bg, acc);
+                    // unrolled: the next group's accumulators and row values
+                    // take other registers instead of being copied each group
+#pragma unroll
                     for (int g0 = 0; g0 < NI; g0 += MC_NG) {
                         if (g0 + MC_NG < NI) group_mfma(g0 + MC_NG, hq, A, Bn, accn);
                         uint32_t nbelow = 0;
@@ -531,10 +545,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                     const uint32_t code = mcol_code4(h);
                                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
                                         (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
-                                    uint32_t idx = code ? (uint32_t)scnt + pre : (uint32_t)(MC_STG + lane);
-                                    idx = min(idx, (uint32_t)(MC_STG + lane));
-                                    stage[idx] = (16u * (g0 + g) + ql) | ((uint32_t)(jl0 + 4 * kq) << 16) |
-                                                 (code << 28);
+                                    // a lane holding band values (its bit in any) takes the next
+                                    // slot, the others the spill zone
+                                    const uint32_t idx = min(mcol_sel(any, (uint32_t)scnt + pre, (uint32_t)(MC_STG + lane)),
+                                                             (uint32_t)(MC_STG + lane));
+                                    stage[idx] = (ebase + 16u * (g0 + g)) | (code << 28);
                                     scnt += __popcll(any);
                                 }
                             } else if ((SVGD_MCOL_ABL == 0 || SVGD_MCOL_ABL == 3) && __builtin_expect(any != 0, 0)) {

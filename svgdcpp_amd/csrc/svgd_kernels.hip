@@ -2605,12 +2605,22 @@ __device__ __forceinline__ void sym_step(const double *rj, const double (&xs)[R]
     // step would hold a second column record -- the registers are all taken)
     __builtin_amdgcn_sched_barrier(0);
     double u[R];
+    // 16-byte LDS reads of the lane's record (ds_read_b128: 16-lane groups,
+    // the odd 16-byte record stride conflict-free).  The records are 16-byte
+    // aligned (SRS even, whole-KiB buffers), but without the hint the
+    // compiler emits ds_read2_b64 pairs, whose 32-bank rule puts records r
+    // and r + 8 on the same banks: every record read 2-way conflicted.
+    const double2 *r2 = reinterpret_cast<const double2 *>(__builtin_assume_aligned(rj, 16));
     {
         // the column's coordinates first, its weights only once the Gram is
         // issued (the two never hold registers at the same time)
-        double xj[D];
+        double xj[D + (D & 1)];
 #pragma unroll
-        for (int k = 0; k < D; ++k) xj[k] = rj[k];
+        for (int q = 0; q < (D + 1) / 2; ++q) {
+            const double2 t = r2[q];
+            xj[2 * q] = t.x;
+            xj[2 * q + 1] = t.y;
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) u[r] = fma(xs[r][0], xj[0], EXP_UB); // biased: u >= 0
 #pragma unroll
@@ -2619,9 +2629,18 @@ __device__ __forceinline__ void sym_step(const double *rj, const double (&xs)[R]
             for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], xj[k], u[r]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    double wj[DP];
+    double wj[DP + 1];
+    if constexpr (D % 2 == 0) { // W at a 16-byte boundary: (D + 2) / 2 reads
 #pragma unroll
-    for (int k = 0; k < DP; ++k) wj[k] = rj[D + k];
+        for (int q = 0; q < (DP + 1) / 2; ++q) {
+            const double2 t = r2[D / 2 + q];
+            wj[2 * q] = t.x;
+            wj[2 * q + 1] = t.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < DP; ++k) wj[k] = rj[D + k];
+    }
     double f[R], T[R], E[R];
     int ki[R];
 #pragma unroll
