@@ -1801,9 +1801,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
                                           (int64_t)c->S2b * (c->nrows - c->split_h)}) * (dim + 1)));
         // symmetric phi pass: one rank (a pair feeds two particles, which
         // ranks would have to exchange), isotropic scales, d <= 8
-        bool want_sym = c->world == 1 && phi_sym_supported(dim);
+        // (default since round 5: with 16-byte record reads cfg3 phi 3.60 ->
+        // 3.08 ms, profiles/r05_sym_ab.txt; SVGD_PHI_SYM=0 keeps the row stream)
+        bool want_sym = c->plan_world == 1 && phi_sym_supported(dim);
         if (const char *e = std::getenv("SVGD_PHI_SYM")) want_sym = want_sym && std::atoi(e) != 0;
-        else want_sym = false; // (opt-in until measured)
         if (want_sym && phi_sym_geom(dim, &c->symB, &c->symSRS, &c->symNSUB)) {
             const int64_t B = c->symB;
             c->sym_nb = (n + B - 1) / B;
