@@ -62,11 +62,13 @@ def test_phi_random_shapes(oracle, n, d):
 
 @pytest.mark.parametrize("n,d", [(1, 2), (5, 8), (200, 8), (1000, 8), (2049, 8), (4000, 2),
                                  (777, 3), (130, 12), (70, 16)])
-def test_phi_row_kernel(oracle, n, d):
+def test_phi_row_kernel(oracle, monkeypatch, n, d):
     """The row stream (8 waves splitting one row group's columns, their sums
-    added in LDS in wave order) against the oracle, and deterministic.  (The
-    4-wave kernel it replaced serves the full-matrix scales and is covered by
-    tests/test_gpu_matrix_scale.py.)"""
+    added in LDS in wave order; SVGD_PHI_SYM=0 -- one rank at d <= 8 takes
+    the symmetric pass by default, tests/test_gpu_sym.py) against the oracle,
+    and deterministic.  (The 4-wave kernel it replaced serves the full-matrix
+    scales and is covered by tests/test_gpu_matrix_scale.py.)"""
+    monkeypatch.setenv("SVGD_PHI_SYM", "0")
     X = oracle.splitmix((n, d), 2.0, 500 + n + d)
     G = oracle.splitmix((n, d), 1.0, 600 + n + d)
     a = 0.29

@@ -1,4 +1,5 @@
-"""Symmetric phi pass (k_phi_sym, SVGD_PHI_SYM=1): parity with the CPU oracle
+"""Symmetric phi pass (k_phi_sym: the default for one rank at d <= 8; SVGD_PHI_SYM=1
+forces it here, =0 selects the row stream): parity with the CPU oracle
 through the C ABI.  GPU only.
 
 Each unordered pair's kernel value feeds both particles (SVGD.hpp:453 with
