@@ -1801,10 +1801,15 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
                                           (int64_t)c->S2b * (c->nrows - c->split_h)}) * (dim + 1)));
         // symmetric phi pass: one rank (a pair feeds two particles, which
         // ranks would have to exchange), isotropic scales, d <= 8
-        // (default since round 5: with 16-byte record reads cfg3 phi 3.60 ->
-        // 3.08 ms, profiles/r05_sym_ab.txt; SVGD_PHI_SYM=0 keeps the row stream)
+        // (default since round 5 from N = 32768 up: with 16-byte record reads
+        // cfg3 phi 3.59 -> 3.08 ms, step 4.12 -> 3.68 ms, cfg4 65.5 -> 56.5
+        // ms; at cfg2, N = 16384, its extra launches outweigh the saving,
+        // 0.200 vs 0.265 ms -- profiles/r05_sym_ab.txt.  SVGD_PHI_SYM=1 / 0
+        // forces it on / off)
         bool want_sym = c->plan_world == 1 && phi_sym_supported(dim);
-        if (const char *e = std::getenv("SVGD_PHI_SYM")) want_sym = want_sym && std::atoi(e) != 0;
+        if (n < 32768) want_sym = false;
+        if (const char *e = std::getenv("SVGD_PHI_SYM"))
+            want_sym = c->plan_world == 1 && phi_sym_supported(dim) && std::atoi(e) != 0;
         if (want_sym && phi_sym_geom(dim, &c->symB, &c->symSRS, &c->symNSUB)) {
             const int64_t B = c->symB;
             c->sym_nb = (n + B - 1) / B;
