@@ -1327,10 +1327,10 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         else
             HIPCHK(c, launch_prep_v_mat(c->xc, c->G, c->sc_M, c->sc_L, c->n, c->np, c->dim, c->KP,
                                         c->VW, c->zc, c->V, c->cvec, c->wv, c->stream));
-    } else if (c->rowpath)
+    } else if (c->rowpath && !c->sym) // (the symmetric pass's prep writes these when it does not apply)
         HIPCHK(c, launch_prep_rec(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->RS,
                                   c->rec, c->stream));
-    else
+    else if (!c->rowpath)
         HIPCHK(c, launch_prep_v(c->xc, c->G, c->nrm, c->scal, c->n, c->np, c->dim, c->KP, c->VW,
                                 c->V, c->cvec, c->stream));
     // F32: the streamed kernel's operand-ordered column copies (k_swz_f32), or
@@ -1362,7 +1362,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         SymArgs sa{c->dim,    c->xc,        c->KP,          c->G,        c->nrm,       c->scal,
                    nmax_cur(c),   c->n,         c->sym_nb,      c->sym_units, c->srec,     c->symok,
                    c->rowpart, c->sym_rslots, c->colpart,   c->sym_grid, c->row0,      c->nrows,
-                   1.0 / (double)c->n, c->phi};
+                   1.0 / (double)c->n, c->phi, c->rec, c->RS};
         HIPCHK(c, launch_phi_sym(sa, opt, k0, k1, c->stream));
         // the row stream takes the step instead when the records' flag says
         // the symmetric form would leave its range (symok = 0)

@@ -245,6 +245,8 @@ struct SymArgs {
     int64_t row0, nrows;
     double inv_n;
     double *phi;
+    double *rec; // the row stream's records, written by the record prep when symok = 0
+    int RS;
 };
 bool phi_sym_supported(int d);
 bool phi_sym_geom(int d, int *B, int *SRS, int *NSUB);

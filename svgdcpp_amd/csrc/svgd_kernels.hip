@@ -2561,17 +2561,40 @@ __device__ __forceinline__ void sym_lds_barrier()
 }
 
 // records: srec_j = [xc_j | w_j (G_j - 2a xc_j) | w_j | 0..] (zero past n),
-// w_j = exp(-a |xc_j|^2); symok = (a log2e max|xc|^2 <= 300)
+// w_j = exp(-a |xc_j|^2); symok = (a log2e max|xc|^2 <= 300).  When the
+// symmetric form does not apply (every block sees the same flag), the row
+// stream's records rec (k_prep_rec's values, rows [0, n); its padding rows
+// stay zero) are written instead -- no k_prep_rec launch on the usual path.
 template <int D>
 __global__ void k_prep_sym(const double *__restrict__ xc, int KP, const double *__restrict__ G,
                            const double *__restrict__ nrm, const double *__restrict__ a_ptr,
                            const unsigned long long *__restrict__ nmax_bits, int64_t n, int64_t npad,
-                           double *__restrict__ srec, int *__restrict__ symok)
+                           double *__restrict__ srec, int *__restrict__ symok, double *__restrict__ rec,
+                           int RS)
 {
     using Gm = SymGeom<D>;
     const double a = *a_ptr;
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        *symok = LOG2E * a * __longlong_as_double((long long)*nmax_bits) <= 300.0 ? 1 : 0;
+    const bool ok = LOG2E * a * __longlong_as_double((long long)*nmax_bits) <= 300.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *symok = ok ? 1 : 0;
+    if (!ok) { // the row stream's records (k_prep_rec, same expressions)
+        const int64_t tot = n * RS;
+        for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+             e += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t j = e / RS;
+            const int k = (int)(e - j * RS);
+            double v = 0.0;
+            if (k < D)
+                v = xc[j * KP + k];
+            else if (k < 2 * D)
+                v = G[j * D + (k - D)] - 2.0 * a * xc[j * KP + (k - D)];
+            else if (k == 2 * D)
+                v = -4096.0 * a * LOG2E * nrm[j];
+            else if (k == 2 * D + 1)
+                v = -4096.0 * a * LOG2E * nrm[j] + EXP_UB;
+            rec[e] = v;
+        }
+        return;
+    }
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < npad;
          j += (int64_t)gridDim.x * blockDim.x) {
         double *o = srec + j * Gm::SRS;
@@ -2888,12 +2911,24 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
             tile_coords(nb, gu0 / NSUB, &I0, &J0);
             acc += rowpart[(((int64_t)g * rslots + (P - I0)) * B + pl) * DP + k];
         }
-        // column role: tiles (I, P), slot s >= 1
-        for (int64_t sl = 1; sl <= (nb - 1) / 2 + 1; ++sl) {
-            const int64_t I = ((P - sl) % nb + nb) % nb;
-            if (I == P || sl >= sym_cnt(nb, I)) continue;
-            const int64_t t = sym_base(nb, I) + sl;
-            acc += colpart[(t * B + pl) * DP + k];
+        // column role: tiles (I, P), slot s >= 1, added in slot order; 16
+        // slots' loads in flight at a time (one dependent load per slot left
+        // this kernel latency-bound: 54 us at cfg3)
+        const int64_t smax = (nb - 1) / 2 + 1;
+        for (int64_t s0 = 1; s0 <= smax; s0 += 16) {
+            double v[16];
+            bool ok[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int64_t sl = s0 + u;
+                int64_t I = P - sl;
+                if (I < 0) I += nb;
+                ok[u] = sl <= smax && I != P && sl < sym_cnt(nb, I);
+                v[u] = ok[u] ? colpart[((sym_base(nb, I) + sl) * B + pl) * DP + k] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (ok[u]) acc += v[u];
         }
         sm[e] = acc;
     }
@@ -4781,7 +4816,7 @@ int phi_sym_blocks_per_cu(int d)
         int64_t g = (npad + 255) / 256;                                                       \
         if (g > 4096) g = 4096;                                                               \
         hipLaunchKernelGGL((k_prep_sym<Dv>), dim3(g), dim3(256), 0, stream, a.xc, a.KP, a.G,   \
-                           a.nrm, a.a_ptr, a.nmax, a.n, npad, a.srec, a.symok);               \
+                           a.nrm, a.a_ptr, a.nmax, a.n, npad, a.srec, a.symok, a.rec, a.RS);  \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k0 && (e = hipEventRecord(ev_k0, stream)) != hipSuccess) return e;             \
         hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(SYM_NW * 64), 0, stream, a.srec, a.a_ptr, \
