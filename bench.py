@@ -647,7 +647,10 @@ def main():
                 # avg_launch_ms: HIP events around the phi kernel launch alone
                 # (diagnostic pass after the timed runs; k_phi_rows without
                 # its reduce), so it is comparable with rocprof's kernel mean
-                "kernel": ("k_phi_rows (fused RBF + grad + phi contraction, fp64 VALU row stream)"
+                "kernel": ("k_phi_sym (fused RBF + grad + phi contraction, symmetric: one Gram and one exp "
+                           "per unordered pair feed both particles; fp64 VALU)"
+                           if kname.startswith("k_phi_sym") else
+                           "k_phi_rows (fused RBF + grad + phi contraction, fp64 VALU row stream)"
                            if row_kernel else
                            "k_phi_b3 (fused RBF + grad + phi contraction, fp32-accurate on the bf16 "
                            "matrix cores: three-part operands, six part products)"

@@ -204,8 +204,10 @@ struct svgd_ctx {
     // symmetric phi pass (k_phi_sym, one rank, d <= 8): geometry and buffers
     bool sym = false;
     int symB = 0, symSRS = 0, symNSUB = 0, sym_grid = 0, sym_rslots = 0;
-    int64_t sym_nb = 0, sym_units = 0;
+    int64_t sym_nb = 0, sym_units = 0, sym_u0 = 0, sym_u1 = 0; // all units, this rank's [u0, u1)
     double *srec = nullptr, *rowpart = nullptr, *colpart = nullptr;
+    double *contrib = nullptr; // P > 1: every particle's sums from this rank's units (reduce-scattered)
+    int *sym_tab = nullptr;    // the finish's row-role tables (SymArgs::wgI0 | blkg)
     int *symok = nullptr;
     int64_t ldp = 0;
 
@@ -529,7 +531,7 @@ void diag_end(svgd_ctx *c, hipStream_t s, hipEvent_t a, int kind, bool own_a = t
 
 // Every collective this rank issues goes into the step's sequence hash (the
 // SVGD_DEBUG_COLL cross-rank check of the issue-order invariant, svgd_ctx).
-enum { CO_GATHER_ROWS = 1, CO_REDUCE_U64 = 2, CO_GATHER_U64 = 3, CO_REDUCE_F64 = 4, CO_GCOMM = 16 };
+enum { CO_GATHER_ROWS = 1, CO_REDUCE_U64 = 2, CO_GATHER_U64 = 3, CO_REDUCE_F64 = 4, CO_RS_ROWS = 5, CO_GCOMM = 16 };
 void coll_note(svgd_ctx *c, int op, size_t cnt)
 {
     uint64_t h = c->coll_sig ? c->coll_sig : 0xcbf29ce484222325ull;
@@ -597,6 +599,27 @@ int allgather_u64(svgd_ctx *c, uint64_t *buf, size_t cnt)
     } else {
         NCCLCHK(c, ncclAllGather(buf + (size_t)c->rank * cnt, buf, cnt, ncclUint64, c->comm,
                                  c->stream));
+    }
+    diag_end(c, c->stream, d0, DG_COLL);
+    return SVGD_OK;
+}
+
+// In-place reduce-scatter (sum) of `w` doubles per row: buf holds world x
+// chunk rows, rank r gets the sums of its chunk at buf + r * chunk * w.  The
+// host-shm rehearsal path all-reduces the whole buffer (same result there).
+int reduce_scatter_rows(svgd_ctx *c, double *buf, size_t w)
+{
+    if (!c->comm && !c->hcomm) return SVGD_OK; // one rank / simulated world: no exchange
+    c->mark = c->phi_end = nullptr;
+    const size_t cnt = (size_t)c->chunk * w;
+    coll_note(c, CO_RS_ROWS, cnt);
+    hipEvent_t d0 = diag_begin(c, c->stream);
+    if (c->hcomm) {
+        if (hostcomm_allreduce_f64(c->hcomm, buf, cnt * (size_t)c->world, c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
+    } else {
+        NCCLCHK(c, ncclReduceScatter(buf, buf + (size_t)c->rank * cnt, cnt, ncclDouble, ncclSum, c->comm,
+                                     c->stream));
     }
     diag_end(c, c->stream, d0, DG_COLL);
     return SVGD_OK;
@@ -1360,10 +1383,19 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     if (sym) {
         c->mark = c->phi_end = nullptr;
         SymArgs sa{c->dim,    c->xc,        c->KP,          c->G,        c->nrm,       c->scal,
-                   nmax_cur(c),   c->n,         c->sym_nb,      c->sym_units, c->srec,     c->symok,
-                   c->rowpart, c->sym_rslots, c->colpart,   c->sym_grid, c->row0,      c->nrows,
-                   1.0 / (double)c->n, c->phi, c->rec, c->RS};
+                   nmax_cur(c),   c->n,         c->sym_nb,      c->sym_u0,   c->sym_u1,    c->srec,
+                   c->symok,  c->rowpart,   c->sym_rslots,  c->colpart,  c->sym_grid,  c->row0,
+                   c->nrows,  1.0 / (double)c->n, c->phi, c->rec, c->RS, c->contrib,
+                   c->sym_tab, c->sym_tab + c->sym_grid};
         HIPCHK(c, launch_phi_sym(sa, opt, k0, k1, c->stream));
+        if (c->contrib) {
+            // every rank's sums of its rows (issued whether or not symok: the
+            // ranks' collective sequences must not depend on device data)
+            CHK(reduce_scatter_rows(c, c->contrib, (size_t)(c->dim + 1)));
+            HIPCHK(c, launch_sym_apply(c->dim, c->contrib + (size_t)c->row0 * (c->dim + 1), c->srec, c->scal,
+                                       c->symok, c->row0, c->nrows, 1.0 / (double)c->n, c->phi, opt,
+                                       c->stream));
+        }
         // the row stream takes the step instead when the records' flag says
         // the symmetric form would leave its range (symok = 0)
         HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
@@ -1806,33 +1838,60 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         // ms; at cfg2, N = 16384, its extra launches outweigh the saving,
         // 0.200 vs 0.265 ms -- profiles/r05_sym_ab.txt.  SVGD_PHI_SYM=1 / 0
         // forces it on / off)
+        // P > 1 (opt-in, SVGD_PHI_SYM=1): rank r runs the units
+        // [U r / P, U (r+1) / P), sums every particle's partials from them and
+        // a reduce-scatter hands each rank its rows' totals
         bool want_sym = c->plan_world == 1 && phi_sym_supported(dim);
         if (n < 32768) want_sym = false;
-        if (const char *e = std::getenv("SVGD_PHI_SYM"))
-            want_sym = c->plan_world == 1 && phi_sym_supported(dim) && std::atoi(e) != 0;
+        int sym_env = -1; // 2 (a test knob): the P > 1 form (sums, reduce-scatter, apply) at any P
+        if (const char *e = std::getenv("SVGD_PHI_SYM")) {
+            sym_env = std::atoi(e);
+            want_sym = phi_sym_supported(dim) && sym_env != 0;
+        }
         if (want_sym && phi_sym_geom(dim, &c->symB, &c->symSRS, &c->symNSUB)) {
             const int64_t B = c->symB;
             c->sym_nb = (n + B - 1) / B;
             const int64_t T = c->sym_nb * (c->sym_nb + 1) / 2;
             c->sym_units = T * c->symNSUB;
+            const int64_t P = c->plan_world, r = c->sim_world > 1 ? 0 : c->rank;
+            c->sym_u0 = c->sym_units * r / P;
+            c->sym_u1 = c->sym_units * (r + 1) / P;
+            const int64_t V = c->sym_u1 - c->sym_u0;
             const int64_t slots = (int64_t)phi_sym_blocks_per_cu(dim) * ncu;
-            c->sym_grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->sym_units, slots));
+            c->sym_grid = (int)std::max<int64_t>(1, std::min<int64_t>(V, slots));
             // row blocks a work-group visits (its unit range is contiguous in
-            // the plan's row-major tile order)
+            // the plan's row-major tile order; G <= V: none is empty), and
+            // per row block the work-groups that visit it (for the finish)
             int rs = 1;
+            const int64_t nbs = c->sym_nb;
+            std::vector<int> tab((size_t)c->sym_grid + 2 * (size_t)nbs);
+            int *wgI0 = tab.data(), *blkg = tab.data() + c->sym_grid;
+            for (int64_t P = 0; P < nbs; ++P) {
+                blkg[2 * P] = INT32_MAX;
+                blkg[2 * P + 1] = -1;
+            }
             for (int64_t g = 0; g < c->sym_grid; ++g) {
-                const int64_t u0 = c->sym_units * g / c->sym_grid, u1 = c->sym_units * (g + 1) / c->sym_grid;
-                if (u1 <= u0) continue;
+                const int64_t u0 = c->sym_u0 + V * g / c->sym_grid, u1 = c->sym_u0 + V * (g + 1) / c->sym_grid;
                 int64_t I0, J0, I1, J1;
                 svgd_plan_pair_tile(n, (int)B, 1, 0, u0 / c->symNSUB, &I0, &J0);
                 svgd_plan_pair_tile(n, (int)B, 1, 0, (u1 - 1) / c->symNSUB, &I1, &J1);
                 rs = std::max<int>(rs, (int)(I1 - I0 + 1));
+                wgI0[g] = (int)I0;
+                for (int64_t P = I0; P <= I1; ++P) {
+                    blkg[2 * P] = std::min<int>(blkg[2 * P], (int)g);
+                    blkg[2 * P + 1] = std::max<int>(blkg[2 * P + 1], (int)g);
+                }
             }
             c->sym_rslots = rs;
+            CHK(dalloc(c, &c->sym_tab, (int64_t)tab.size()));
+            HIPCHK(c, hipMemcpyAsync(c->sym_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice,
+                                     c->stream)); // (after dalloc's memset on the same stream)
+            HIPCHK(c, hipStreamSynchronize(c->stream));
             CHK(dalloc(c, &c->srec, c->sym_nb * B * c->symSRS));
             CHK(dalloc(c, &c->rowpart, (int64_t)c->sym_grid * rs * B * (dim + 1)));
             CHK(dalloc(c, &c->colpart, T * B * (dim + 1)));
             CHK(dalloc(c, &c->symok, 1));
+            if (P > 1 || sym_env == 2) CHK(dalloc(c, &c->contrib, std::max<int64_t>(c->np, c->world * c->chunk) * (dim + 1)));
             c->sym = true;
         }
         // the centring fold (svgd_ctx::cpart)
@@ -2000,7 +2059,8 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
                 std::max<size_t>((size_t)c->chunk * c->dim, (size_t)c->dim * c->dim) * sizeof(double),
                 2 * RADIX * sizeof(unsigned long long)),
             std::max<size_t>((CAPG + 1) * sizeof(uint64_t), (3 + NBK) * sizeof(uint64_t)));
-        if (hostcomm_create(&c->hcomm, std::getenv("SVGD_HOSTCOMM"), world, rank, slot))
+        const size_t slot_rs = c->contrib ? (size_t)world * c->chunk * (c->dim + 1) * sizeof(double) : 0;
+        if (hostcomm_create(&c->hcomm, std::getenv("SVGD_HOSTCOMM"), world, rank, std::max(slot, slot_rs)))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host communicator setup failed.");
         return SVGD_OK;
     }
@@ -2051,7 +2111,7 @@ int svgd_destroy(svgd_ctx *c)
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
-                       c->sc_sgn,  c->sc_work, c->bak, c->srec, c->rowpart, c->colpart};
+                       c->sc_sgn,  c->sc_work, c->bak, c->srec, c->rowpart, c->colpart, c->contrib};
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf, c->XS, c->VS};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
@@ -2062,7 +2122,7 @@ int svgd_destroy(svgd_ctx *c)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
                      c->xf,          c->nmax,    c->sc_err, c->cbuf, c->ccount, c->d_status,
-                     c->bpart,       c->gseg, c->symok};
+                     c->bpart,       c->gseg, c->symok, c->sym_tab};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_xm, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk};

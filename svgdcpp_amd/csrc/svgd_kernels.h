@@ -235,7 +235,7 @@ struct SymArgs {
     int KP;
     const double *G, *nrm, *a_ptr;
     const unsigned long long *nmax;
-    int64_t n, nbs, units; // particles, blocks of B, (tile, sub-tile) units
+    int64_t n, nbs, u0, u1; // particles, blocks of B, this rank's (tile, sub-tile) units [u0, u1)
     double *srec;          // nbs * B records of SRS doubles
     int *symok;
     double *rowpart;       // grid x rslots x B x (d+1)
@@ -247,7 +247,19 @@ struct SymArgs {
     double *phi;
     double *rec; // the row stream's records, written by the record prep when symok = 0
     int RS;
+    // P > 1: the finish writes every particle's sums from this rank's units
+    // here (n x (d+1), the reduce-scatter's input) instead of phi
+    double *contrib = nullptr;
+    // the finish's row-role tables: wgI0[g] = work-group g's first row block,
+    // blkg[2P], blkg[2P+1] = the work-groups whose units meet row block P
+    // (g1 < g0: none)
+    const int *wgI0 = nullptr, *blkg = nullptr;
 };
+// P > 1: phi + the optimizer for rows [row0, row0 + nrows) from S (their
+// reduce-scattered sums, nrows x (d+1)); nothing unless *symok
+hipError_t launch_sym_apply(int d, const double *S, const double *srec, const double *a_ptr,
+                            const int *symok, int64_t row0, int64_t nrows, double inv_n, double *phi,
+                            const OptArgs *opt, hipStream_t stream);
 bool phi_sym_supported(int d);
 bool phi_sym_geom(int d, int *B, int *SRS, int *NSUB);
 int phi_sym_blocks_per_cu(int d);

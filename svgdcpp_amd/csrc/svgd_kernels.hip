@@ -2740,7 +2740,7 @@ __device__ __forceinline__ void sym_phases(const char *cb, int grp, int tl, int 
 
 template <int D>
 __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_phi_sym(
-    const double *__restrict__ srec, const double *__restrict__ a_ptr, int64_t nb, int64_t U,
+    const double *__restrict__ srec, const double *__restrict__ a_ptr, int64_t nb, int64_t U0, int64_t U1,
     const int *__restrict__ symok, double *__restrict__ rowpart, int rslots, double *__restrict__ colpart)
 {
     using Gm = SymGeom<D>;
@@ -2763,8 +2763,9 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     __syncthreads();
 
     const double alpha = 8192.0 * LOG2E * (*a_ptr);
-    const int64_t Gn = gridDim.x;
-    const int64_t u0 = U * (int64_t)blockIdx.x / Gn, u1 = U * ((int64_t)blockIdx.x + 1) / Gn;
+    // this work-group's contiguous run of the rank's units [U0, U1)
+    const int64_t Gn = gridDim.x, V = U1 - U0;
+    const int64_t u0 = U0 + V * (int64_t)blockIdx.x / Gn, u1 = U0 + V * ((int64_t)blockIdx.x + 1) / Gn;
     const int npw = (NP - w + SYM_NW - 1) / SYM_NW; // this wave's DMA pieces per sub-tile
     // (tile, sub-tile) cursor: the plan's tile t = (I, J), J = I + slot mod nb
     // (plan.cpp); advanced incrementally (no 64-bit divisions per sub-tile)
@@ -2876,14 +2877,20 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
 // phi_p = (1/N) w_p (S_p[0..d) + 2a xc_p S_p[d]) for this rank's rows, S_p =
 // every row and column partial of p in a fixed order, then the optimizer.
 // A block owns 256 / (d+1) particles, one thread per (particle, component).
+// The partials are those of the units [U0, U1) (this rank's) run by G
+// work-groups.  contrib (P > 1): instead of phi, S_p of EVERY particle from
+// this rank's units alone -> contrib[p * DP + k] (rows [row0, row0 + nrows)
+// = all N), the input of the reduce-scatter; k_sym_apply then forms phi.
 template <int D>
 __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ rowpart,
                                                     const double *__restrict__ colpart, int rslots,
                                                     const double *__restrict__ srec,
                                                     const double *__restrict__ a_ptr, int64_t nb,
-                                                    int64_t U, int G, const int *__restrict__ symok,
-                                                    int64_t row0, int64_t nrows, double inv_n,
-                                                    double *__restrict__ phi, OptArgs opt, int do_opt)
+                                                    int64_t U0, int64_t U1, const int *__restrict__ wgI0,
+                                                    const int *__restrict__ blkg,
+                                                    const int *__restrict__ symok, int64_t row0,
+                                                    int64_t nrows, double inv_n, double *__restrict__ phi,
+                                                    OptArgs opt, int do_opt, double *__restrict__ contrib)
 {
     using Gm = SymGeom<D>;
     constexpr int B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP, RB = 256 / DP;
@@ -2898,24 +2905,49 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
         const int64_t p = row0 + rb + pl_;
         const int64_t P = p / B, pl = p - P * B;
         double acc = 0.0;
-        // row role: the work-groups whose unit range meets row block P's units
-        const int64_t ub = sym_base(nb, P) * NSUB, ue = ub + sym_cnt(nb, P) * NSUB;
-        int64_t g = ub * G / U;
-        while (g > 0 && U * g / G > ub) --g;
-        while (g + 1 < G && U * (g + 1) / G <= ub) ++g;
-        for (; g < G; ++g) {
-            const int64_t gu0 = U * g / G, gu1 = U * (g + 1) / G;
-            if (gu0 >= ue) break;
-            if (gu1 <= ub || gu0 >= gu1) continue;
-            int64_t I0, J0;
-            tile_coords(nb, gu0 / NSUB, &I0, &J0);
-            acc += rowpart[(((int64_t)g * rslots + (P - I0)) * B + pl) * DP + k];
+        // row role: the work-groups g0 .. g1 whose unit ranges meet row block
+        // P (host tables, svgd_ctx::sym_tab: wgI0[g] = g's first row block),
+        // in work-group order, 16 loads in flight (at P = 8 a row block
+        // spans ~48 work-groups)
+        const int g0 = blkg[2 * P], g1 = blkg[2 * P + 1];
+        for (int gb = g0; gb <= g1; gb += 16) {
+            double v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int g = gb + u;
+                v[u] = g <= g1 ? rowpart[(((int64_t)g * rslots + (P - wgI0[g])) * B + pl) * DP + k] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (gb + u <= g1) acc += v[u];
         }
         // column role: tiles (I, P), slot s >= 1, added in slot order; 16
         // slots' loads in flight at a time (one dependent load per slot left
-        // this kernel latency-bound: 54 us at cfg3)
+        // this kernel latency-bound: 54 us at cfg3).  A rank's units (P > 1)
+        // span the row blocks Ia .. Ib only: then the loop runs over those
+        // (slot P - I) when they are fewer than the slots
         const int64_t smax = (nb - 1) / 2 + 1;
-        for (int64_t s0 = 1; s0 <= smax; s0 += 16) {
+        int64_t Ia, Ib, Jx;
+        tile_coords(nb, U0 / NSUB, &Ia, &Jx);
+        tile_coords(nb, (U1 - 1) / NSUB, &Ib, &Jx);
+        if (Ib - Ia + 1 < smax) {
+            for (int64_t i0 = Ia; i0 <= Ib; i0 += 16) {
+                double v[16];
+                bool ok[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) {
+                    const int64_t I = i0 + u;
+                    int64_t sl = P - I;
+                    if (sl < 0) sl += nb;
+                    const int64_t t = sym_base(nb, I) + sl, unit = t * NSUB + pl / SYM_SUB;
+                    ok[u] = I <= Ib && sl >= 1 && sl < sym_cnt(nb, I) && unit >= U0 && unit < U1;
+                    v[u] = ok[u] ? colpart[(t * B + pl) * DP + k] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (ok[u]) acc += v[u];
+            }
+        } else for (int64_t s0 = 1; s0 <= smax; s0 += 16) {
             double v[16];
             bool ok[16];
 #pragma unroll
@@ -2923,15 +2955,21 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
                 const int64_t sl = s0 + u;
                 int64_t I = P - sl;
                 if (I < 0) I += nb;
-                ok[u] = sl <= smax && I != P && sl < sym_cnt(nb, I);
-                v[u] = ok[u] ? colpart[((sym_base(nb, I) + sl) * B + pl) * DP + k] : 0.0;
+                const int64_t t = sym_base(nb, I) + sl, unit = t * NSUB + pl / SYM_SUB;
+                ok[u] = sl <= smax && I != P && sl < sym_cnt(nb, I) && unit >= U0 && unit < U1;
+                v[u] = ok[u] ? colpart[(t * B + pl) * DP + k] : 0.0;
             }
 #pragma unroll
             for (int u = 0; u < 16; ++u)
                 if (ok[u]) acc += v[u];
         }
+        if (contrib) {
+            contrib[p * DP + k] = acc;
+            return;
+        }
         sm[e] = acc;
     }
+    if (contrib) return;
     __syncthreads();
     const double two_a = 2.0 * (*a_ptr);
     for (int o = threadIdx.x; o < rows * D; o += blockDim.x) {
@@ -2941,6 +2979,30 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
         const double ph = inv_n * (rec[2 * D] * (sm[r * DP + k] + two_a * rec[k] * sm[r * DP + D]));
         phi[li * D + k] = ph;
         if (do_opt) opt_elem(opt, li * D + k, ph);
+    }
+}
+
+// P > 1: phi and the optimizer for this rank's rows from S (the
+// reduce-scattered sums of every rank's contributions, chunk x DP).
+template <int D>
+__global__ __launch_bounds__(256) void k_sym_apply(const double *__restrict__ S, const double *__restrict__ srec,
+                                                   const double *__restrict__ a_ptr,
+                                                   const int *__restrict__ symok, int64_t row0, int64_t nrows,
+                                                   double inv_n, double *__restrict__ phi, OptArgs opt,
+                                                   int do_opt)
+{
+    using Gm = SymGeom<D>;
+    constexpr int SRS = Gm::SRS, DP = Gm::DP;
+    if (!*symok) return;
+    const double two_a = 2.0 * (*a_ptr);
+    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < nrows * D;
+         o += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t li = o / D;
+        const int k = (int)(o - li * D);
+        const double *rec = srec + (row0 + li) * SRS;
+        const double ph = inv_n * (rec[2 * D] * (S[li * DP + k] + two_a * rec[k] * S[li * DP + D]));
+        phi[o] = ph;
+        if (do_opt) opt_elem(opt, o, ph);
     }
 }
 
@@ -4820,16 +4882,37 @@ int phi_sym_blocks_per_cu(int d)
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k0 && (e = hipEventRecord(ev_k0, stream)) != hipSuccess) return e;             \
         hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(SYM_NW * 64), 0, stream, a.srec, a.a_ptr, \
-                           a.nbs, a.units, a.symok, a.rowpart, a.rslots, a.colpart);          \
+                           a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.rslots, a.colpart);       \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k1 && (e = hipEventRecord(ev_k1, stream)) != hipSuccess) return e;             \
         constexpr int RB = 256 / Gm::DP;                                                      \
-        hipLaunchKernelGGL((k_sym_finish<Dv>), dim3((a.nrows + RB - 1) / RB), dim3(256), 0,    \
+        const int64_t fr0 = a.contrib ? 0 : a.row0, fn = a.contrib ? a.n : a.nrows;           \
+        hipLaunchKernelGGL((k_sym_finish<Dv>), dim3((fn + RB - 1) / RB), dim3(256), 0,         \
                            stream, a.rowpart, a.colpart, a.rslots, a.srec, a.a_ptr, a.nbs,     \
-                           a.units, a.grid, a.symok, a.row0, a.nrows, a.inv_n, a.phi,          \
-                           opt ? *opt : OptArgs{}, opt ? 1 : 0);                              \
+                           a.u0, a.u1, a.wgI0, a.blkg, a.symok, fr0, fn, a.inv_n, a.phi,       \
+                           opt ? *opt : OptArgs{}, opt ? 1 : 0, a.contrib);                   \
         return hipGetLastError();                                                             \
     }
+
+#define SVGD_SYM_APPLY_CASE(Dv)                                                               \
+    case Dv:                                                                                  \
+        hipLaunchKernelGGL((k_sym_apply<Dv>), dim3(g), dim3(256), 0, stream, S, srec, a_ptr, symok, \
+                           row0, nrows, inv_n, phi, opt ? *opt : OptArgs{}, opt ? 1 : 0);      \
+        return hipGetLastError();
+
+hipError_t launch_sym_apply(int d, const double *S, const double *srec, const double *a_ptr,
+                            const int *symok, int64_t row0, int64_t nrows, double inv_n, double *phi,
+                            const OptArgs *opt, hipStream_t stream)
+{
+    if (nrows <= 0) return hipSuccess;
+    const int64_t g = std::min<int64_t>((nrows * d + 255) / 256, 4096);
+    switch (d) {
+        SVGD_SYM_APPLY_CASE(1) SVGD_SYM_APPLY_CASE(2) SVGD_SYM_APPLY_CASE(3) SVGD_SYM_APPLY_CASE(4)
+        SVGD_SYM_APPLY_CASE(5) SVGD_SYM_APPLY_CASE(6) SVGD_SYM_APPLY_CASE(7) SVGD_SYM_APPLY_CASE(8)
+    default:
+        return hipErrorInvalidValue;
+    }
+}
 
 hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0, hipEvent_t ev_k1,
                           hipStream_t stream)

@@ -38,7 +38,8 @@ def run(rank, world, name, n, d, steps, q, env=None):
             scales.append(ctx.last_scale()[:3])
         X = ctx.get_particles()
         shard = (ctx.row0, ctx.row1)
-        diag = ctx.diagnostics()
+        diag = dict(ctx.diagnostics())
+        diag["phi_kernel"] = ctx.phi_kernel_name()
         ctx.close()
         q.put(("ok", rank, X, scales, shard, diag))
     except Exception:

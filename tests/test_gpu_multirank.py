@@ -120,6 +120,29 @@ def test_default_multirank_path_row_parts(world, n, split):
     assert len({tuple(s[0] for s in multi[r][1]) for r in range(world)}) == 1
 
 
+@pytest.mark.parametrize("world,n,d", [(2, 3001, 5), (3, 6007, 8), (4, 12007, 2)])
+def test_sharded_symmetric_phi(world, n, d):
+    """The symmetric phi pass sharded (SVGD_PHI_SYM=1 at P > 1): rank r runs
+    the pair units [U r / P, U (r+1) / P), sums every particle's partials from
+    them, and the reduce-scatter (here the host backend's all-reduce) hands
+    each rank its rows' totals for k_sym_apply -- against one rank on the row
+    stream: the first scale bit-exact, positions <= 1e-10 (the pair sums are
+    grouped differently, fp64 rounding)."""
+    steps = 4
+    diags = {}
+    multi = _run_ranks(world, n, d, steps, {"SVGD_PHI_SYM": "1", "SVGD_DEBUG_COLL": "1"}, diags=diags)
+    single = _run_ranks(1, n, d, steps, {"SVGD_PHI_SYM": "0"}, diags=(d1 := {}))[0]
+    assert d1[0]["phi_kernel"].startswith("k_phi_rows"), d1
+    X1, s1, _ = single
+    for rank, (X, scales, _) in multi.items():
+        assert diags[rank]["phi_kernel"].startswith("k_phi_sym"), diags[rank]
+        assert scales[0][0] == s1[0][0], (rank, scales, s1)
+        np.testing.assert_allclose([s[0] for s in scales], [s[0] for s in s1], rtol=1e-13)
+        np.testing.assert_allclose(X, X1, rtol=0, atol=1e-10)
+    Xs = [multi[r][0] for r in range(world)]
+    assert all(np.array_equal(Xs[0], x) for x in Xs[1:])
+
+
 def test_measurement_context_refuses_results():
     """svgd_create_sim (bench.py --sim-world): rank 0's share of a P-rank step,
     measurement only -- it steps, but every call that hands results back

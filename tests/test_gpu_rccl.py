@@ -90,3 +90,19 @@ def test_rccl_one_rank_split_g_communicator(oracle, monkeypatch, n, d):
     assert np.array_equal(Xa, Xb)
     assert dg["g_comm"] == 1 and dg["ranks"] == 1, dg
     assert dg["gather_g_n"] == 16, dg
+
+
+def test_rccl_one_rank_symmetric_reduce_scatter(oracle, monkeypatch):
+    """SVGD_PHI_SYM=2: the sharded symmetric form (every particle's sums from
+    the rank's pair units, the in-place ncclReduceScatter, k_sym_apply) on the
+    one-rank communicator, 6 steps: bit-identical to the same form without a
+    communicator and to the one-rank symmetric pass (SVGD_PHI_SYM=1: the same
+    partials summed in the same order, phi formed by the same expression)."""
+    n, d = 6000, 8
+    monkeypatch.setenv("SVGD_PHI_SYM", "2")
+    Xa, sa = _run(oracle, n, d, 6, True, monkeypatch)
+    Xb, sb = _run(oracle, n, d, 6, False, monkeypatch)
+    monkeypatch.setenv("SVGD_PHI_SYM", "1")
+    Xc, sc = _run(oracle, n, d, 6, False, monkeypatch)
+    assert sa == sb == sc
+    assert np.array_equal(Xa, Xb) and np.array_equal(Xa, Xc)
