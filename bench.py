@@ -571,6 +571,7 @@ def main():
             "host_grad": per_step(diag["host_grad_ms"], diag["steps"]),
         }
         mine["n_ranks_seen"] = int(diag["ranks"])
+    mine["phi_kernel"] = ctx.phi_kernel_name()
     per_rank = [mine]
     if dist is not None:
         per_rank = [None] * world

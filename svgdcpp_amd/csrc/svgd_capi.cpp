@@ -1831,17 +1831,20 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         CHK(dalloc(c, &c->nmax, 2)); // one slot per X version parity (center)
         CHK(dalloc(c, &c->part, std::max({(int64_t)c->S * c->ldp, (int64_t)c->S2 * c->split_h,
                                           (int64_t)c->S2b * (c->nrows - c->split_h)}) * (dim + 1)));
-        // symmetric phi pass: one rank (a pair feeds two particles, which
-        // ranks would have to exchange), isotropic scales, d <= 8
-        // (default since round 5 from N = 32768 up: with 16-byte record reads
+        // symmetric phi pass: isotropic scales, d <= 8 (a pair feeds two
+        // particles).  One rank: default since round 5 from N = 32768 up (with 16-byte record reads
         // cfg3 phi 3.59 -> 3.08 ms, step 4.12 -> 3.68 ms, cfg4 65.5 -> 56.5
         // ms; at cfg2, N = 16384, its extra launches outweigh the saving,
         // 0.200 vs 0.265 ms -- profiles/r05_sym_ab.txt.  SVGD_PHI_SYM=1 / 0
         // forces it on / off)
-        // P > 1 (opt-in, SVGD_PHI_SYM=1): rank r runs the units
-        // [U r / P, U (r+1) / P), sums every particle's partials from them and
-        // a reduce-scatter hands each rank its rows' totals
-        bool want_sym = c->plan_world == 1 && phi_sym_supported(dim);
+        // P > 1: rank r runs the units [U r / P, U (r+1) / P), sums every
+        // particle's partials from them and a reduce-scatter (N (d+1) doubles)
+        // hands each rank its rows' totals.  Default up to P = 4: the cfg3
+        // shares (sim-world, profiles/r05_sim_sym.txt) P = 2 2.008 -> 1.875
+        // ms, P = 4 1.066 -> 1.003, against a reduce-scatter of 4.7 MB
+        // (P = 2: 2.4 MB over one xGMI link, ~35 us; P = 4: 1.2 MB per peer
+        // link, ~20 us); P = 8 0.587 -> 0.582, less than its ~20 us exchange
+        bool want_sym = c->plan_world <= 4 && phi_sym_supported(dim);
         if (n < 32768) want_sym = false;
         int sym_env = -1; // 2 (a test knob): the P > 1 form (sums, reduce-scatter, apply) at any P
         if (const char *e = std::getenv("SVGD_PHI_SYM")) {

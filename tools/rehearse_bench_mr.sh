@@ -21,9 +21,9 @@ import json, sys
 d = json.load(open(sys.argv[1])); n = int(sys.argv[2])
 pr = d["per_rank"]
 rows = [(r["rank"], r["rows"], r["diag_ms_per_step"]["phi_launches_per_step"], r["n_ranks_seen"],
-         r["tracked_brackets"]) for r in pr]
+         r["tracked_brackets"], r.get("phi_kernel")) for r in pr]
 print("n_gpus", d["n_gpus"], "ranks", len(pr), "env", d.get("env_knobs"))
 for r in rows:
-    print("rank %d rows %d phi_launches %d ranks_seen %d trk %s" % r)
+    print("rank %d rows %d phi_launches %d ranks_seen %d trk %s phi %s" % r)
 assert d["n_gpus"] == n and len(pr) == n and all(r[3] == n for r in rows)
 PY
