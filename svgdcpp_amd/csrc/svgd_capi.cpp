@@ -203,11 +203,13 @@ struct svgd_ctx {
     int phi_kind = 0; // 0 k_phi_rows (4 waves: matrix scales), 2 k_phi_rows (8 waves, column-split)
     // symmetric phi pass (k_phi_sym, one rank, d <= 8): geometry and buffers
     bool sym = false;
-    int symB = 0, symSRS = 0, symNSUB = 0, sym_grid = 0, sym_rslots = 0;
+    int symB = 0, symSRS = 0, symNSUB = 0, sym_grid = 0;
     int64_t sym_nb = 0, sym_units = 0, sym_u0 = 0, sym_u1 = 0; // all units, this rank's [u0, u1)
+    int sym_fS = 1; // the row stream's column splits when it takes the step (symok = 0)
+    int64_t sym_SM = 0, sym_Ia = 0, sym_Ib = 0; // colpart slots per column block; units' row-block span
     double *srec = nullptr, *rowpart = nullptr, *colpart = nullptr;
     double *contrib = nullptr; // P > 1: every particle's sums from this rank's units (reduce-scattered)
-    int *sym_tab = nullptr;    // the finish's row-role tables (SymArgs::wgI0 | blkg)
+    int *sym_tab = nullptr;    // the symmetric pass's row-block tables (SymArgs::blkg | rbase)
     int *symok = nullptr;
     int64_t ldp = 0;
 
@@ -1384,23 +1386,25 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         c->mark = c->phi_end = nullptr;
         SymArgs sa{c->dim,    c->xc,        c->KP,          c->G,        c->nrm,       c->scal,
                    nmax_cur(c),   c->n,         c->sym_nb,      c->sym_u0,   c->sym_u1,    c->srec,
-                   c->symok,  c->rowpart,   c->sym_rslots,  c->colpart,  c->sym_grid,  c->row0,
+                   c->symok,  c->rowpart,   c->colpart,     c->sym_grid, c->row0,
                    c->nrows,  1.0 / (double)c->n, c->phi, c->rec, c->RS, c->contrib,
-                   c->sym_tab, c->sym_tab + c->sym_grid};
-        HIPCHK(c, launch_phi_sym(sa, opt, k0, k1, c->stream));
+                   c->sym_tab, c->sym_tab + 2 * c->sym_nb,
+                   c->sym_SM, c->sym_Ia, c->sym_Ib, c->part, c->sym_fS, c->ldp};
+        HIPCHK(c, launch_phi_sym(sa, k0, k1, c->stream));
+        // the row stream takes the step instead when the records' flag says
+        // the symmetric form would leave its range (symok = 0): its kernel
+        // alone, in one wave of work-groups (a no-op launch on the usual path
+        // costs little), its partials summed by the finish / k_sym_apply
+        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->sym_fS, c->part,
+                                  c->ldp, 1.0 / (double)c->n, nullptr, nullptr, nmax_cur(c), c->phi, opt,
+                                  c->stream, nullptr, c->phi_kind, c->symok, false));
+        HIPCHK(c, launch_sym_finish(sa, opt, c->stream));
         if (c->contrib) {
             // every rank's sums of its rows (issued whether or not symok: the
             // ranks' collective sequences must not depend on device data)
             CHK(reduce_scatter_rows(c, c->contrib, (size_t)(c->dim + 1)));
-            HIPCHK(c, launch_sym_apply(c->dim, c->contrib + (size_t)c->row0 * (c->dim + 1), c->srec, c->scal,
-                                       c->symok, c->row0, c->nrows, 1.0 / (double)c->n, c->phi, opt,
-                                       c->stream));
+            HIPCHK(c, launch_sym_apply(sa, c->contrib + (size_t)c->row0 * (c->dim + 1), opt, c->stream));
         }
-        // the row stream takes the step instead when the records' flag says
-        // the symmetric form would leave its range (symok = 0)
-        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->S, c->part,
-                                  c->ldp, 1.0 / (double)c->n, nullptr, nullptr, nmax_cur(c), c->phi, opt,
-                                  c->stream, nullptr, c->phi_kind, c->symok));
     } else if (c->rowpath && split) {
         // two row halves: the first half's X_{t+1} is final at ev_xhalf, while
         // the second half's phi runs (svgd_step_host_model copies it down and
@@ -1856,19 +1860,18 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             c->sym_nb = (n + B - 1) / B;
             const int64_t T = c->sym_nb * (c->sym_nb + 1) / 2;
             c->sym_units = T * c->symNSUB;
-            const int64_t P = c->plan_world, r = c->sim_world > 1 ? 0 : c->rank;
-            c->sym_u0 = c->sym_units * r / P;
-            c->sym_u1 = c->sym_units * (r + 1) / P;
+            const int64_t Pw = c->plan_world, r = c->sim_world > 1 ? 0 : c->rank;
+            c->sym_u0 = c->sym_units * r / Pw;
+            c->sym_u1 = c->sym_units * (r + 1) / Pw;
             const int64_t V = c->sym_u1 - c->sym_u0;
             const int64_t slots = (int64_t)phi_sym_blocks_per_cu(dim) * ncu;
             c->sym_grid = (int)std::max<int64_t>(1, std::min<int64_t>(V, slots));
             // row blocks a work-group visits (its unit range is contiguous in
             // the plan's row-major tile order; G <= V: none is empty), and
             // per row block the work-groups that visit it (for the finish)
-            int rs = 1;
             const int64_t nbs = c->sym_nb;
-            std::vector<int> tab((size_t)c->sym_grid + 2 * (size_t)nbs);
-            int *wgI0 = tab.data(), *blkg = tab.data() + c->sym_grid;
+            std::vector<int> tab(3 * (size_t)nbs);
+            int *blkg = tab.data(), *rbase = blkg + 2 * nbs;
             for (int64_t P = 0; P < nbs; ++P) {
                 blkg[2 * P] = INT32_MAX;
                 blkg[2 * P + 1] = -1;
@@ -1878,23 +1881,40 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
                 int64_t I0, J0, I1, J1;
                 svgd_plan_pair_tile(n, (int)B, 1, 0, u0 / c->symNSUB, &I0, &J0);
                 svgd_plan_pair_tile(n, (int)B, 1, 0, (u1 - 1) / c->symNSUB, &I1, &J1);
-                rs = std::max<int>(rs, (int)(I1 - I0 + 1));
-                wgI0[g] = (int)I0;
                 for (int64_t P = I0; P <= I1; ++P) {
                     blkg[2 * P] = std::min<int>(blkg[2 * P], (int)g);
                     blkg[2 * P + 1] = std::max<int>(blkg[2 * P + 1], (int)g);
                 }
             }
-            c->sym_rslots = rs;
+            // each row block's row-sum records: one per visiting work-group,
+            // contiguous (rbase); the units' row-block span (finish)
+            int64_t nrec = 0;
+            for (int64_t P = 0; P < nbs; ++P) {
+                rbase[P] = (int)nrec;
+                if (blkg[2 * P + 1] >= blkg[2 * P]) nrec += blkg[2 * P + 1] - blkg[2 * P] + 1;
+            }
+            {
+                int64_t J;
+                svgd_plan_pair_tile(n, (int)B, 1, 0, c->sym_u0 / c->symNSUB, &c->sym_Ia, &J);
+                svgd_plan_pair_tile(n, (int)B, 1, 0, (c->sym_u1 - 1) / c->symNSUB, &c->sym_Ib, &J);
+            }
+            c->sym_SM = (nbs - 1) / 2 + 2;
+            // fallback row stream: one wave of work-groups (<= c->S, the part buffer's splits)
+            {
+                const int64_t rows_wg = c->phi_kind == 2 ? phi_rows_t8k_rows(c->R) : 256 * (int64_t)c->R;
+                const int64_t ib = std::max<int64_t>(1, (c->nrows + rows_wg - 1) / rows_wg);
+                c->sym_fS = (int)std::max<int64_t>(1, std::min<int64_t>(c->S, ncu / ib));
+            }
             CHK(dalloc(c, &c->sym_tab, (int64_t)tab.size()));
             HIPCHK(c, hipMemcpyAsync(c->sym_tab, tab.data(), tab.size() * sizeof(int), hipMemcpyHostToDevice,
                                      c->stream)); // (after dalloc's memset on the same stream)
             HIPCHK(c, hipStreamSynchronize(c->stream));
             CHK(dalloc(c, &c->srec, c->sym_nb * B * c->symSRS));
-            CHK(dalloc(c, &c->rowpart, (int64_t)c->sym_grid * rs * B * (dim + 1)));
-            CHK(dalloc(c, &c->colpart, T * B * (dim + 1)));
+            CHK(dalloc(c, &c->rowpart, nrec * B * (dim + 1)));
+            // zeroed here once: entries no unit of this rank writes stay zero
+            CHK(dalloc(c, &c->colpart, nbs * c->sym_SM * B * (dim + 1)));
             CHK(dalloc(c, &c->symok, 1));
-            if (P > 1 || sym_env == 2) CHK(dalloc(c, &c->contrib, std::max<int64_t>(c->np, c->world * c->chunk) * (dim + 1)));
+            if (Pw > 1 || sym_env == 2) CHK(dalloc(c, &c->contrib, std::max<int64_t>(c->np, c->world * c->chunk) * (dim + 1)));
             c->sym = true;
         }
         // the centring fold (svgd_ctx::cpart)

@@ -220,15 +220,18 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
                            hipStream_t stream, hipEvent_t ev_mid = nullptr, int kind = 0,
-                           const int *skip = nullptr);
+                           const int *skip = nullptr, bool reduce = true);
 // skip (optional): the row stream and its reduce do nothing while *skip != 0
-// (the symmetric pass below took the step)
+// (the symmetric pass below took the step).  reduce = false: the row kernel
+// alone (its partials summed by the symmetric finish / apply instead)
 
-// Symmetric phi pass (d <= 8, one rank): each unordered pair's kernel value
-// feeds both particles (k_phi_sym), then k_sym_finish sums the partials in a
-// fixed order, forms phi and applies the optimizer.  Runs only while *symok
-// (set by its record prep: a log2e max|xc|^2 <= 300); otherwise the row
-// stream, launched after it with skip = symok, takes the step.
+// Symmetric phi pass (d <= 8): each unordered pair's kernel value feeds both
+// particles (k_phi_sym, launch_phi_sym), then k_sym_finish (launch_sym_finish)
+// sums the partials in a fixed order, forms phi and applies the optimizer.
+// Runs only while *symok (set by its record prep: a log2e max|xc|^2 <= 300);
+// otherwise the row stream, launched between the two with skip = symok and
+// reduce = false, takes the step: the finish (one rank) or k_sym_apply
+// (P > 1) then sums ITS partials fS x fldp (the k_phi_reduce arithmetic).
 struct SymArgs {
     int d;
     const double *xc;
@@ -238,9 +241,8 @@ struct SymArgs {
     int64_t n, nbs, u0, u1; // particles, blocks of B, this rank's (tile, sub-tile) units [u0, u1)
     double *srec;          // nbs * B records of SRS doubles
     int *symok;
-    double *rowpart;       // grid x rslots x B x (d+1)
-    int rslots;
-    double *colpart;       // tiles x B x (d+1)
+    double *rowpart;       // per row block P, its visiting work-groups' row sums (rbase below) x B x (d+1)
+    double *colpart;       // nbs x SM slots x B x (d+1), by (column block, slot)
     int grid;
     int64_t row0, nrows;
     double inv_n;
@@ -250,21 +252,26 @@ struct SymArgs {
     // P > 1: the finish writes every particle's sums from this rank's units
     // here (n x (d+1), the reduce-scatter's input) instead of phi
     double *contrib = nullptr;
-    // the finish's row-role tables: wgI0[g] = work-group g's first row block,
-    // blkg[2P], blkg[2P+1] = the work-groups whose units meet row block P
-    // (g1 < g0: none)
-    const int *wgI0 = nullptr, *blkg = nullptr;
+    // row-block tables: blkg[2P], blkg[2P+1] = the work-groups whose units
+    // meet row block P (g1 < g0: none), rbase[P] = the first rowpart record of P
+    const int *blkg = nullptr, *rbase = nullptr;
+    int64_t SM = 0;        // colpart slots per column block: (nbs - 1) / 2 + 2
+    int64_t Ia = 0, Ib = 0; // the row blocks this rank's units span
+    // the row stream's partials when it takes the step (symok = 0)
+    const double *fpart = nullptr;
+    int fS = 0;
+    int64_t fldp = 0;
 };
 // P > 1: phi + the optimizer for rows [row0, row0 + nrows) from S (their
-// reduce-scattered sums, nrows x (d+1)); nothing unless *symok
-hipError_t launch_sym_apply(int d, const double *S, const double *srec, const double *a_ptr,
-                            const int *symok, int64_t row0, int64_t nrows, double inv_n, double *phi,
-                            const OptArgs *opt, hipStream_t stream);
+// reduce-scattered sums, nrows x (d+1)), or from the row stream's partials
+// when symok = 0
+hipError_t launch_sym_apply(const SymArgs &a, const double *S, const OptArgs *opt, hipStream_t stream);
 bool phi_sym_supported(int d);
 bool phi_sym_geom(int d, int *B, int *SRS, int *NSUB);
 int phi_sym_blocks_per_cu(int d);
-hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0, hipEvent_t ev_k1,
-                          hipStream_t stream);
+// record prep + k_phi_sym (ev_k0 / ev_k1 around the pair kernel, optional)
+hipError_t launch_phi_sym(const SymArgs &a, hipEvent_t ev_k0, hipEvent_t ev_k1, hipStream_t stream);
+hipError_t launch_sym_finish(const SymArgs &a, const OptArgs *opt, hipStream_t stream);
 // kind 2: k_phi_rows with 8-wave work-groups and the mask-free 8192-entry exp table
 bool phi_rows_t8k_supported(int d, int R);
 int phi_rows_t8k_rows(int R); // rows per work-group of kind 2

@@ -2741,7 +2741,8 @@ __device__ __forceinline__ void sym_phases(const char *cb, int grp, int tl, int 
 template <int D>
 __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_phi_sym(
     const double *__restrict__ srec, const double *__restrict__ a_ptr, int64_t nb, int64_t U0, int64_t U1,
-    const int *__restrict__ symok, double *__restrict__ rowpart, int rslots, double *__restrict__ colpart)
+    const int *__restrict__ symok, double *__restrict__ rowpart, const int *__restrict__ blkg,
+    const int *__restrict__ rbase, double *__restrict__ colpart, int64_t SM)
 {
     using Gm = SymGeom<D>;
     constexpr int R = Gm::R, B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP,
@@ -2803,11 +2804,13 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     };
 
     double xs[R][D], wr[R][DP], acc[R][DP];
-    int64_t curI = -1, firstI = 0;
-    // row sums of block curI -> rowpart slot curI - firstI
+    int64_t curI = -1;
+    // row sums of block curI -> rowpart record rbase[curI] + (this group -
+    // the first group visiting curI): each row block's records contiguous,
+    // in work-group order (the finish reads them as one run)
 #define SYM_FLUSH_ROWS()                                                                        \
     do {                                                                                        \
-        double *o_ = rowpart + ((int64_t)blockIdx.x * rslots + (curI - firstI)) * B * DP;        \
+        double *o_ = rowpart + ((int64_t)rbase[curI] + ((int)blockIdx.x - blkg[2 * curI])) * B * DP; \
         _Pragma("unroll") for (int r = 0; r < R; ++r) {                                         \
             const int lr = (w * R + r) * 64 + lane;                                             \
             _Pragma("unroll") for (int k = 0; k < DP; ++k) o_[lr * DP + k] = acc[r][k];         \
@@ -2827,12 +2830,11 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
             wait_vmcnt<0>();
         }
         sym_lds_barrier(); // every wave's pieces of sub-tile u are in LDS; sCol free
-        const int64_t t = cu.t, I = cu.I, J = cu.J;
+        const int64_t I = cu.I, J = cu.J, slot = cu.slot;
         const int q = cu.q;
         cur_next(cu);
         if (I != curI) {
             if (curI >= 0) SYM_FLUSH_ROWS();
-            else firstI = I;
             curI = I;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -2858,7 +2860,10 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
         sym_lds_barrier();
         // the 8 waves' column sums added in wave order into colpart (off the
         // diagonal), and the slots zeroed for the next sub-tile
-        double *o = colpart + (t * B + (int64_t)q * SYM_SUB) * DP;
+        // column partials by (column block, slot): colpart[J][slot], so a
+        // particle's column terms are one run (the finish); entries no unit of
+        // this rank writes stay zero from the allocation
+        double *o = colpart + ((J * SM + slot) * B + (int64_t)q * SYM_SUB) * DP;
         for (int e = tid; e < SYM_SUB * DP; e += NT) {
             double v = sCol[e];
             sCol[e] = 0.0;
@@ -2874,6 +2879,49 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
 #undef SYM_FLUSH_ROWS
 }
 
+// The row stream's step when the symmetric form does not apply (symok = 0):
+// its partials (launch_phi_rows without its reduce) summed per element in
+// split order and phi_i = (S_i[0..d) + 2a xc_i S_i[d]) / N -- k_phi_reduce's
+// arithmetic in the symmetric finish's block geometry (256 / (d+1) rows).
+struct SymFallback {
+    const double *part; // S x ldp x (d+1)
+    int S;
+    int64_t ldp;
+    const double *rec; // the row records (xc in slots 0..d)
+    int RS;
+};
+template <int D>
+__device__ __forceinline__ double sym_fb_sum(const SymFallback &fb, int64_t rb, int e)
+{
+    constexpr int DP = D + 1;
+    const double *p = fb.part + rb * DP + e;
+    const int64_t st = fb.ldp * DP;
+    double acc = 0.0;
+    for (int s0 = 0; s0 < fb.S; s0 += 16) { // 16 splits' loads in flight, added in s order
+        double v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = s0 + q < fb.S ? p[(s0 + q) * st] : 0.0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (s0 + q < fb.S) acc += v[q];
+    }
+    return acc;
+}
+template <int D>
+__device__ __forceinline__ void sym_fb_phi(const SymFallback &fb, const double *sm, int64_t rb, int rows,
+                                           int64_t row0, double inv_n, double a, double *phi,
+                                           const OptArgs &opt, int do_opt)
+{
+    constexpr int DP = D + 1;
+    for (int o = threadIdx.x; o < rows * D; o += blockDim.x) {
+        const int r = o / D, k = o - r * D;
+        const int64_t li = rb + r;
+        const double w = 2.0 * a * fb.rec[(row0 + li) * fb.RS + k];
+        const double ph = inv_n * (sm[r * DP + k] + w * sm[r * DP + D]);
+        phi[li * D + k] = ph;
+        if (do_opt) opt_elem(opt, li * D + k, ph);
+    }
+}
 // phi_p = (1/N) w_p (S_p[0..d) + 2a xc_p S_p[d]) for this rank's rows, S_p =
 // every row and column partial of p in a fixed order, then the optimizer.
 // A block owns 256 / (d+1) particles, one thread per (particle, component).
@@ -2883,85 +2931,81 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
 // = all N), the input of the reduce-scatter; k_sym_apply then forms phi.
 template <int D>
 __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ rowpart,
-                                                    const double *__restrict__ colpart, int rslots,
+                                                    const double *__restrict__ colpart,
                                                     const double *__restrict__ srec,
                                                     const double *__restrict__ a_ptr, int64_t nb,
-                                                    int64_t U0, int64_t U1, const int *__restrict__ wgI0,
+                                                    int64_t SM, int64_t Ia, int64_t Ib,
                                                     const int *__restrict__ blkg,
+                                                    const int *__restrict__ rbase,
                                                     const int *__restrict__ symok, int64_t row0,
                                                     int64_t nrows, double inv_n, double *__restrict__ phi,
-                                                    OptArgs opt, int do_opt, double *__restrict__ contrib)
+                                                    OptArgs opt, int do_opt, double *__restrict__ contrib,
+                                                    SymFallback fb)
 {
     using Gm = SymGeom<D>;
-    constexpr int B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP, RB = 256 / DP;
-    if (!*symok) return;
+    constexpr int B = Gm::B, SRS = Gm::SRS, DP = Gm::DP, RB = 256 / DP;
+    const bool ok = *symok;
+    if (!ok && contrib) return; // (k_sym_apply takes the row stream's step)
     __shared__ double sm[256];
     const int64_t rb = (int64_t)blockIdx.x * RB;
     const int rows = (int)min<int64_t>(RB, nrows - rb);
     if (rows <= 0) return;
     const int e = threadIdx.x;
+    if (!ok) { // the row stream took the step: its partials, then its phi form
+        if (e < rows * DP) sm[e] = sym_fb_sum<D>(fb, rb, e);
+        __syncthreads();
+        sym_fb_phi<D>(fb, sm, rb, rows, row0, inv_n, *a_ptr, phi, opt, do_opt);
+        return;
+    }
     if (e < rows * DP) {
         const int pl_ = e / DP, k = e - pl_ * DP;
         const int64_t p = row0 + rb + pl_;
         const int64_t P = p / B, pl = p - P * B;
         double acc = 0.0;
-        // row role: the work-groups g0 .. g1 whose unit ranges meet row block
-        // P (host tables, svgd_ctx::sym_tab: wgI0[g] = g's first row block),
-        // in work-group order, 16 loads in flight (at P = 8 a row block
-        // spans ~48 work-groups)
-        const int g0 = blkg[2 * P], g1 = blkg[2 * P + 1];
-        for (int gb = g0; gb <= g1; gb += 16) {
-            double v[16];
+        // row role: the row sums of the work-groups that visited row block P,
+        // one contiguous run (k_phi_sym's rowpart layout), in work-group order
+        {
+            const int cnt = blkg[2 * P + 1] - blkg[2 * P] + 1; // <= 0: none
+            const double *rp = rowpart + ((int64_t)rbase[P] * B + pl) * DP + k;
+            for (int i0 = 0; i0 < cnt; i0 += 16) {
+                double v[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int g = gb + u;
-                v[u] = g <= g1 ? rowpart[(((int64_t)g * rslots + (P - wgI0[g])) * B + pl) * DP + k] : 0.0;
+                for (int u = 0; u < 16; ++u) v[u] = i0 + u < cnt ? rp[(int64_t)(i0 + u) * B * DP] : 0.0;
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (i0 + u < cnt) acc += v[u];
             }
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if (gb + u <= g1) acc += v[u];
         }
-        // column role: tiles (I, P), slot s >= 1, added in slot order; 16
-        // slots' loads in flight at a time (one dependent load per slot left
-        // this kernel latency-bound: 54 us at cfg3).  A rank's units (P > 1)
-        // span the row blocks Ia .. Ib only: then the loop runs over those
-        // (slot P - I) when they are fewer than the slots
-        const int64_t smax = (nb - 1) / 2 + 1;
-        int64_t Ia, Ib, Jx;
-        tile_coords(nb, U0 / NSUB, &Ia, &Jx);
-        tile_coords(nb, (U1 - 1) / NSUB, &Ib, &Jx);
-        if (Ib - Ia + 1 < smax) {
+        // column role: colpart[P][slot], slots 1 .. SM-1 in order (entries no
+        // unit of this rank wrote are zero); a rank whose units span the row
+        // blocks Ia .. Ib only (P > 1) reads the slots P - I of those, fewer
+        // -- 16 loads in flight
+        const double *cp = colpart + ((P * SM) * B + pl) * DP + k;
+        const int64_t cs = (int64_t)B * DP;
+        if (Ib - Ia + 1 >= SM - 1) {
+            for (int64_t s0 = 1; s0 < SM; s0 += 16) {
+                double v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = s0 + u < SM ? cp[(s0 + u) * cs] : 0.0;
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (s0 + u < SM) acc += v[u];
+            }
+        } else {
             for (int64_t i0 = Ia; i0 <= Ib; i0 += 16) {
                 double v[16];
-                bool ok[16];
+                bool okv[16];
 #pragma unroll
                 for (int u = 0; u < 16; ++u) {
-                    const int64_t I = i0 + u;
-                    int64_t sl = P - I;
+                    int64_t sl = P - (i0 + u);
                     if (sl < 0) sl += nb;
-                    const int64_t t = sym_base(nb, I) + sl, unit = t * NSUB + pl / SYM_SUB;
-                    ok[u] = I <= Ib && sl >= 1 && sl < sym_cnt(nb, I) && unit >= U0 && unit < U1;
-                    v[u] = ok[u] ? colpart[(t * B + pl) * DP + k] : 0.0;
+                    okv[u] = i0 + u <= Ib && sl >= 1 && sl < SM;
+                    v[u] = okv[u] ? cp[sl * cs] : 0.0;
                 }
 #pragma unroll
                 for (int u = 0; u < 16; ++u)
-                    if (ok[u]) acc += v[u];
+                    if (okv[u]) acc += v[u];
             }
-        } else for (int64_t s0 = 1; s0 <= smax; s0 += 16) {
-            double v[16];
-            bool ok[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int64_t sl = s0 + u;
-                int64_t I = P - sl;
-                if (I < 0) I += nb;
-                const int64_t t = sym_base(nb, I) + sl, unit = t * NSUB + pl / SYM_SUB;
-                ok[u] = sl <= smax && I != P && sl < sym_cnt(nb, I) && unit >= U0 && unit < U1;
-                v[u] = ok[u] ? colpart[(t * B + pl) * DP + k] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-                if (ok[u]) acc += v[u];
         }
         if (contrib) {
             contrib[p * DP + k] = acc;
@@ -2983,26 +3027,38 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
 }
 
 // P > 1: phi and the optimizer for this rank's rows from S (the
-// reduce-scattered sums of every rank's contributions, chunk x DP).
+// reduce-scattered sums of every rank's contributions, nrows x DP), or from
+// the row stream's partials when it took the step (symok = 0); the finish's
+// block geometry.
 template <int D>
 __global__ __launch_bounds__(256) void k_sym_apply(const double *__restrict__ S, const double *__restrict__ srec,
                                                    const double *__restrict__ a_ptr,
                                                    const int *__restrict__ symok, int64_t row0, int64_t nrows,
                                                    double inv_n, double *__restrict__ phi, OptArgs opt,
-                                                   int do_opt)
+                                                   int do_opt, SymFallback fb)
 {
     using Gm = SymGeom<D>;
-    constexpr int SRS = Gm::SRS, DP = Gm::DP;
-    if (!*symok) return;
+    constexpr int SRS = Gm::SRS, DP = Gm::DP, RB = 256 / DP;
+    __shared__ double sm[256];
+    const bool ok = *symok;
+    const int64_t rb = (int64_t)blockIdx.x * RB;
+    const int rows = (int)min<int64_t>(RB, nrows - rb);
+    if (rows <= 0) return;
+    const int e = threadIdx.x;
+    if (e < rows * DP) sm[e] = ok ? S[rb * DP + e] : sym_fb_sum<D>(fb, rb, e);
+    __syncthreads();
+    if (!ok) {
+        sym_fb_phi<D>(fb, sm, rb, rows, row0, inv_n, *a_ptr, phi, opt, do_opt);
+        return;
+    }
     const double two_a = 2.0 * (*a_ptr);
-    for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < nrows * D;
-         o += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t li = o / D;
-        const int k = (int)(o - li * D);
+    for (int o = threadIdx.x; o < rows * D; o += blockDim.x) {
+        const int r = o / D, k = o - r * D;
+        const int64_t li = rb + r;
         const double *rec = srec + (row0 + li) * SRS;
-        const double ph = inv_n * (rec[2 * D] * (S[li * DP + k] + two_a * rec[k] * S[li * DP + D]));
-        phi[o] = ph;
-        if (do_opt) opt_elem(opt, o, ph);
+        const double ph = inv_n * (rec[2 * D] * (sm[r * DP + k] + two_a * rec[k] * sm[r * DP + D]));
+        phi[li * D + k] = ph;
+        if (do_opt) opt_elem(opt, li * D + k, ph);
     }
 }
 
@@ -4220,7 +4276,7 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                            int64_t ldp, double inv_n, const double *wv, const double *sgn,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
-                           hipStream_t stream, hipEvent_t ev_mid, int kind, const int *skip)
+                           hipStream_t stream, hipEvent_t ev_mid, int kind, const int *skip, bool reduce)
 {
     if (nrows <= 0) {
         if (ev_mid) return hipEventRecord(ev_mid, stream);
@@ -4235,6 +4291,7 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                                       SinkDebug{}, stream, skip);
     if (e != hipSuccess) return e;
     if (ev_mid && (e = hipEventRecord(ev_mid, stream)) != hipSuccess) return e;
+    if (!reduce) return hipSuccess;
     if (d > 16) return hipErrorInvalidValue; // k_phi_reduce's LDS holds d + 1 <= 17
     const int64_t g = (nrows + phi_red_rows(d) - 1) / phi_red_rows(d);
     hipLaunchKernelGGL(k_phi_reduce, dim3(g), dim3(256), 0, stream, part, rec, a_ptr, row0, nrows,
@@ -4882,31 +4939,43 @@ int phi_sym_blocks_per_cu(int d)
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k0 && (e = hipEventRecord(ev_k0, stream)) != hipSuccess) return e;             \
         hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(SYM_NW * 64), 0, stream, a.srec, a.a_ptr, \
-                           a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.rslots, a.colpart);       \
+                           a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.blkg, a.rbase, a.colpart, a.SM); \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k1 && (e = hipEventRecord(ev_k1, stream)) != hipSuccess) return e;             \
-        constexpr int RB = 256 / Gm::DP;                                                      \
+        return hipSuccess;                                                                    \
+    }
+
+#define SVGD_SYM_FINISH_CASE(Dv)                                                              \
+    case Dv: {                                                                                \
+        constexpr int RB = 256 / SymGeom<Dv>::DP;                                             \
         const int64_t fr0 = a.contrib ? 0 : a.row0, fn = a.contrib ? a.n : a.nrows;           \
+        if (fn <= 0) return hipSuccess;                                                       \
         hipLaunchKernelGGL((k_sym_finish<Dv>), dim3((fn + RB - 1) / RB), dim3(256), 0,         \
-                           stream, a.rowpart, a.colpart, a.rslots, a.srec, a.a_ptr, a.nbs,     \
-                           a.u0, a.u1, a.wgI0, a.blkg, a.symok, fr0, fn, a.inv_n, a.phi,       \
-                           opt ? *opt : OptArgs{}, opt ? 1 : 0, a.contrib);                   \
+                           stream, a.rowpart, a.colpart, a.srec, a.a_ptr, a.nbs, a.SM, a.Ia,   \
+                           a.Ib, a.blkg, a.rbase, a.symok, fr0, fn, a.inv_n, a.phi,            \
+                           opt ? *opt : OptArgs{}, opt ? 1 : 0, a.contrib, fb);               \
         return hipGetLastError();                                                             \
     }
 
 #define SVGD_SYM_APPLY_CASE(Dv)                                                               \
-    case Dv:                                                                                  \
-        hipLaunchKernelGGL((k_sym_apply<Dv>), dim3(g), dim3(256), 0, stream, S, srec, a_ptr, symok, \
-                           row0, nrows, inv_n, phi, opt ? *opt : OptArgs{}, opt ? 1 : 0);      \
-        return hipGetLastError();
+    case Dv: {                                                                                \
+        constexpr int RB = 256 / SymGeom<Dv>::DP;                                             \
+        hipLaunchKernelGGL((k_sym_apply<Dv>), dim3((a.nrows + RB - 1) / RB), dim3(256), 0,     \
+                           stream, S, a.srec, a.a_ptr, a.symok, a.row0, a.nrows, a.inv_n,      \
+                           a.phi, opt ? *opt : OptArgs{}, opt ? 1 : 0, fb);                   \
+        return hipGetLastError();                                                             \
+    }
 
-hipError_t launch_sym_apply(int d, const double *S, const double *srec, const double *a_ptr,
-                            const int *symok, int64_t row0, int64_t nrows, double inv_n, double *phi,
-                            const OptArgs *opt, hipStream_t stream)
+static SymFallback sym_fallback(const SymArgs &a)
 {
-    if (nrows <= 0) return hipSuccess;
-    const int64_t g = std::min<int64_t>((nrows * d + 255) / 256, 4096);
-    switch (d) {
+    return SymFallback{a.fpart, a.fS, a.fldp, a.rec, a.RS};
+}
+
+hipError_t launch_sym_apply(const SymArgs &a, const double *S, const OptArgs *opt, hipStream_t stream)
+{
+    if (a.nrows <= 0) return hipSuccess;
+    const SymFallback fb = sym_fallback(a);
+    switch (a.d) {
         SVGD_SYM_APPLY_CASE(1) SVGD_SYM_APPLY_CASE(2) SVGD_SYM_APPLY_CASE(3) SVGD_SYM_APPLY_CASE(4)
         SVGD_SYM_APPLY_CASE(5) SVGD_SYM_APPLY_CASE(6) SVGD_SYM_APPLY_CASE(7) SVGD_SYM_APPLY_CASE(8)
     default:
@@ -4914,11 +4983,21 @@ hipError_t launch_sym_apply(int d, const double *S, const double *srec, const do
     }
 }
 
-hipError_t launch_phi_sym(const SymArgs &a, const OptArgs *opt, hipEvent_t ev_k0, hipEvent_t ev_k1,
-                          hipStream_t stream)
+hipError_t launch_sym_finish(const SymArgs &a, const OptArgs *opt, hipStream_t stream)
+{
+    const SymFallback fb = sym_fallback(a);
+    switch (a.d) {
+        SVGD_SYM_FINISH_CASE(1) SVGD_SYM_FINISH_CASE(2) SVGD_SYM_FINISH_CASE(3) SVGD_SYM_FINISH_CASE(4)
+        SVGD_SYM_FINISH_CASE(5) SVGD_SYM_FINISH_CASE(6) SVGD_SYM_FINISH_CASE(7) SVGD_SYM_FINISH_CASE(8)
+    default:
+        return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_phi_sym(const SymArgs &a, hipEvent_t ev_k0, hipEvent_t ev_k1, hipStream_t stream)
 {
     hipError_t e = hipSuccess;
-    if (a.nrows <= 0) return hipSuccess;
+    if (a.nrows <= 0 && !a.contrib) return hipSuccess; // (P > 1: the rank's units still count)
     switch (a.d) {
         SVGD_SYM_CASE(1) SVGD_SYM_CASE(2) SVGD_SYM_CASE(3) SVGD_SYM_CASE(4)
         SVGD_SYM_CASE(5) SVGD_SYM_CASE(6) SVGD_SYM_CASE(7) SVGD_SYM_CASE(8)
