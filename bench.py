@@ -464,14 +464,6 @@ def main():
     model = S.GaussianSum(list(mus), list(covs))
     if args.device_model:
         ctx.set_device_model(model)
-    # the device's phi_hat of X0 for the accuracy record of the CPU leg
-    # (untimed, before the warm-up; it moves no particles)
-    acc = None
-    if world == 1 and args.sim_world <= 1 and not args.no_cpu:
-        G0 = model.log_model_grad(X0)
-        a0, _ = ctx.median_scale()
-        acc = (G0, a0, ctx.phi(G0, a0), dtype)
-
     def step():
         if args.device_model:
             ctx.step_device()
@@ -709,6 +701,16 @@ def main():
             out["metric"] = (f"particle-updates/s, {desc}"
                              f"{', device grad log p' if args.device_model else ''} (not the headline config)")
         if world == 1 and not args.no_cpu:
+            # the device's phi_hat of X0 for the CPU leg's accuracy record,
+            # after the timed runs (X0 set again: the centring, median and phi
+            # of X0 are those of a fresh context).  Run before the warm-up it
+            # left the first timed runs up to 55 % slower (profiles/r05_acc_prepass_ab.txt)
+            acc = None
+            if args.sim_world <= 1:
+                ctx.set_particles(X0)
+                G0 = model.log_model_grad(X0)
+                a0, _ = ctx.median_scale()
+                acc = (G0, a0, ctx.phi(G0, a0), dtype)
             out["cpu_baseline"] = cpu_baseline(X0, mus, covs, args.cpu_rows or cfg["cpu_rows"], args.cpu_rows_1t,
                                                acc=acc)
         print(json.dumps(out), flush=True)
