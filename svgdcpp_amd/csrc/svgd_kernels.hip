@@ -2516,7 +2516,9 @@ template <int D> struct SymGeom {
     static constexpr int H = (DP % 2 == 1) ? DP : DP + 1;
     static constexpr int SRS = 2 * H;
     static constexpr int SUBB = SYM_SUB * SRS * 8;       // bytes per sub-tile (whole KiB)
-    static constexpr int LDS = 2 * SUBB + 8192 * 8 + SYM_NW * SYM_SUB * DP * 8;
+    static constexpr int SCOL = SYM_NW * SYM_SUB * DP; // doubles of one column-sum buffer
+    // two record buffers, the exp table, two column-sum buffers (d = 8: 154 KiB)
+    static constexpr int LDS = 2 * SUBB + 8192 * 8 + 2 * SCOL * 8;
 };
 
 __device__ __forceinline__ int64_t sym_cnt(int64_t nb, int64_t I)
@@ -2542,15 +2544,6 @@ __device__ __forceinline__ int dpp_ror15_i(int v)
 __device__ __forceinline__ double dpp_ror15(double v)
 {
     return __hiloint2double(dpp_ror15_i(__double2hiint(v)), dpp_ror15_i(__double2loint(v)));
-}
-
-// vmcnt wait with a wave-uniform count (0..3)
-__device__ __forceinline__ void wait_vmcnt_upto3(int n)
-{
-    if (n >= 3) wait_vmcnt<3>();
-    else if (n == 2) wait_vmcnt<2>();
-    else if (n == 1) wait_vmcnt<1>();
-    else wait_vmcnt<0>();
 }
 
 // Barrier that drains only LDS operations (a __syncthreads() would also wait
@@ -2616,42 +2609,48 @@ __global__ void k_prep_sym(const double *__restrict__ xc, int KP, const double *
     }
 }
 
-// One skew step: the lane's R rows against the column record at rj (LDS).
+// One skew step: the lane's R rows against the column record at rj (LDS),
+// whose coordinates xj the previous step already loaded (PRE: after this
+// step's Gram, the next record's coordinates rn are loaded into xj -- their
+// LDS latency then hides behind this step's exp and accumulation instead of
+// stalling the next step's Gram; xj's registers are free after the Gram).
 // SYMM: also the column side into cacc; ROT: then rotate cacc one lane.
-template <int D, int R, bool SYMM, bool ROT>
-__device__ __forceinline__ void sym_step(const double *rj, const double (&xs)[R][D],
-                                         const double (&wr)[R][D + 1], double (&acc)[R][D + 1],
-                                         double (&cacc)[D + 1], const double *tab)
+#ifndef SVGD_SYM_PRE
+#define SVGD_SYM_PRE 1
+#endif
+template <int D>
+__device__ __forceinline__ void sym_load_x(const double *rj, double (&xj)[D + (D & 1)])
 {
-    constexpr int DP = D + 1;
-    // (no scheduling across steps: a step's loads hoisted into the previous
-    // step would hold a second column record -- the registers are all taken)
-    __builtin_amdgcn_sched_barrier(0);
-    double u[R];
     // 16-byte LDS reads of the lane's record (ds_read_b128: 16-lane groups,
     // the odd 16-byte record stride conflict-free).  The records are 16-byte
     // aligned (SRS even, whole-KiB buffers), but without the hint the
     // compiler emits ds_read2_b64 pairs, whose 32-bank rule puts records r
     // and r + 8 on the same banks: every record read 2-way conflicted.
     const double2 *r2 = reinterpret_cast<const double2 *>(__builtin_assume_aligned(rj, 16));
-    {
-        // the column's coordinates first, its weights only once the Gram is
-        // issued (the two never hold registers at the same time)
-        double xj[D + (D & 1)];
 #pragma unroll
-        for (int q = 0; q < (D + 1) / 2; ++q) {
-            const double2 t = r2[q];
-            xj[2 * q] = t.x;
-            xj[2 * q + 1] = t.y;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) u[r] = fma(xs[r][0], xj[0], EXP_UB); // biased: u >= 0
-#pragma unroll
-        for (int k = 1; k < D; ++k)
-#pragma unroll
-            for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], xj[k], u[r]);
+    for (int q = 0; q < (D + 1) / 2; ++q) {
+        const double2 t = r2[q];
+        xj[2 * q] = t.x;
+        xj[2 * q + 1] = t.y;
     }
+}
+template <int D, int R, bool SYMM, bool ROT, bool PRE>
+__device__ __forceinline__ void sym_step(const double *rj, const double *rn, double (&xj)[D + (D & 1)],
+                                         const double (&xs)[R][D], const double (&wr)[R][D + 1],
+                                         double (&acc)[R][D + 1], double (&cacc)[D + 1], const double *tab)
+{
+    constexpr int DP = D + 1;
     __builtin_amdgcn_sched_barrier(0);
+    double u[R];
+    const double2 *r2 = reinterpret_cast<const double2 *>(__builtin_assume_aligned(rj, 16));
+#pragma unroll
+    for (int r = 0; r < R; ++r) u[r] = fma(xs[r][0], xj[0], EXP_UB); // biased: u >= 0
+#pragma unroll
+    for (int k = 1; k < D; ++k)
+#pragma unroll
+        for (int r = 0; r < R; ++r) u[r] = fma(xs[r][k], xj[k], u[r]);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRE) sym_load_x<D>(rn, xj);
     double wj[DP + 1];
     if constexpr (D % 2 == 0) { // W at a 16-byte boundary: (D + 2) / 2 reads
 #pragma unroll
@@ -2716,13 +2715,25 @@ __device__ __forceinline__ void sym_phases(const char *cb, int grp, int tl, int 
 #pragma unroll
         for (int k = 0; k < DP; ++k) cacc[k] = 0.0;
         // 16 steps straight-line: the last one leaves the packet in place
+        double xj[D + (D & 1)];
+        sym_load_x<D>(reinterpret_cast<const double *>(cb + roff), xj);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             if (s < 15) {
-                sym_step<D, R, SYMM, true>(reinterpret_cast<const double *>(cb + roff), xs, wr, acc, cacc, tab);
-                roff = dpp_ror15_i(roff);
+                const int rnext = dpp_ror15_i(roff);
+                if constexpr (SVGD_SYM_PRE) {
+                    sym_step<D, R, SYMM, true, true>(reinterpret_cast<const double *>(cb + roff),
+                                                     reinterpret_cast<const double *>(cb + rnext), xj, xs, wr,
+                                                     acc, cacc, tab);
+                } else {
+                    sym_step<D, R, SYMM, true, false>(reinterpret_cast<const double *>(cb + roff), nullptr, xj,
+                                                      xs, wr, acc, cacc, tab);
+                    sym_load_x<D>(reinterpret_cast<const double *>(cb + rnext), xj);
+                }
+                roff = rnext;
             } else {
-                sym_step<D, R, SYMM, false>(reinterpret_cast<const double *>(cb + roff), xs, wr, acc, cacc, tab);
+                sym_step<D, R, SYMM, false, false>(reinterpret_cast<const double *>(cb + roff), nullptr, xj, xs,
+                                                   wr, acc, cacc, tab);
             }
         }
         if constexpr (SYMM) {
@@ -2750,9 +2761,10 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
     if (!*symok) return; // uniform: the row stream runs instead
     double *tab = reinterpret_cast<double *>(smem + 2 * SUBB);
-    double *sCol = tab + 8192;
+    double *sCol = tab + 8192; // [2][SYM_NW][SYM_SUB][DP]: sub-tile u's column sums in buffer u & 1
+    constexpr int SCOL = Gm::SCOL;
     const int tid = threadIdx.x, lane = tid & 63;
-    for (int e = tid; e < SYM_NW * SYM_SUB * DP; e += NT) sCol[e] = 0.0;
+    for (int e = tid; e < 2 * SCOL; e += NT) sCol[e] = 0.0;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = lane >> 4, tl = lane & 15;
     // the biased 8192-entry table of the row stream (k_phi_rows, TABN 8192)
@@ -2767,7 +2779,6 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     // this work-group's contiguous run of the rank's units [U0, U1)
     const int64_t Gn = gridDim.x, V = U1 - U0;
     const int64_t u0 = U0 + V * (int64_t)blockIdx.x / Gn, u1 = U0 + V * ((int64_t)blockIdx.x + 1) / Gn;
-    const int npw = (NP - w + SYM_NW - 1) / SYM_NW; // this wave's DMA pieces per sub-tile
     // (tile, sub-tile) cursor: the plan's tile t = (I, J), J = I + slot mod nb
     // (plan.cpp); advanced incrementally (no 64-bit divisions per sub-tile)
     struct Cur {
@@ -2818,21 +2829,52 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     } while (0)
 
     if (u0 >= u1) return;
+    // One barrier per sub-tile: the column sums of sub-tile u go to buffer
+    // u & 1 and are added into colpart during sub-tile u + 1 (after its
+    // barrier, when every wave is past sub-tile u), and the DMA of sub-tile
+    // u + 1 is issued right after that barrier (every wave is then done with
+    // the record buffer it refills).  The barrier of sub-tile u + 1 also
+    // orders the zeroing of a column buffer before its next use.
+    // the 8 waves' column sums of a sub-tile added in wave order into
+    // colpart[J][slot] (off the diagonal: a diagonal tile's are dropped), the
+    // buffer zeroed; colpart by (column block, slot), so a particle's column
+    // terms are one run (the finish); entries no unit of this rank writes
+    // stay zero from the allocation
+    auto col_out = [&](double *scw, int64_t Jp, int64_t slotp, int qp, bool diagp) {
+        double *o = colpart + ((Jp * SM + slotp) * B + (int64_t)qp * SYM_SUB) * DP;
+        for (int e = tid; e < SYM_SUB * DP; e += NT) {
+            double v = scw[e];
+            scw[e] = 0.0;
+#pragma unroll
+            for (int ww = 1; ww < SYM_NW; ++ww) {
+                v += scw[ww * SYM_SUB * DP + e];
+                scw[ww * SYM_SUB * DP + e] = 0.0;
+            }
+            if (!diagp) o[e] = v;
+        }
+    };
     Cur cu = cur_at(u0), cn = cu;
     issue(cu, 0);
+    int64_t pJ = 0, pSlot = 0;
+    int pQ = 0;
+    bool pDiag = true, have_prev = false;
     for (int64_t u = u0; u < u1; ++u) {
         const int buf = (int)((u - u0) & 1);
+        wait_vmcnt<0>();   // this wave's pieces of sub-tile u (the only DMA in flight)
+        sym_lds_barrier(); // every wave's pieces are in LDS; every wave is past sub-tile u - 1
         if (u + 1 < u1) {
             cur_next(cn);
             issue(cn, buf ^ 1);
-            wait_vmcnt_upto3(npw); // this wave's pieces of sub-tile u have landed
-        } else {
-            wait_vmcnt<0>();
         }
-        sym_lds_barrier(); // every wave's pieces of sub-tile u are in LDS; sCol free
+        if (have_prev) col_out(sCol + (buf ^ 1) * SCOL, pJ, pSlot, pQ, pDiag);
         const int64_t I = cu.I, J = cu.J, slot = cu.slot;
         const int q = cu.q;
         cur_next(cu);
+        pJ = J;
+        pSlot = slot;
+        pQ = q;
+        pDiag = I == J;
+        have_prev = true;
         if (I != curI) {
             if (curI >= 0) SYM_FLUSH_ROWS();
             curI = I;
@@ -2854,27 +2896,10 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
         // register ranges: the allocator spilled); a diagonal tile's column
         // sums are computed and dropped -- its row side already holds every
         // ordered pair of the square (~2 % of the tiles)
-        sym_phases<D, true>(cb, grp, tl, w, xs, wr, acc, sCol, tab);
-        // every wave is done with buffer buf (the next iteration's DMA
-        // refills it) and its column sums of this sub-tile are in sCol
-        sym_lds_barrier();
-        // the 8 waves' column sums added in wave order into colpart (off the
-        // diagonal), and the slots zeroed for the next sub-tile
-        // column partials by (column block, slot): colpart[J][slot], so a
-        // particle's column terms are one run (the finish); entries no unit of
-        // this rank writes stay zero from the allocation
-        double *o = colpart + ((J * SM + slot) * B + (int64_t)q * SYM_SUB) * DP;
-        for (int e = tid; e < SYM_SUB * DP; e += NT) {
-            double v = sCol[e];
-            sCol[e] = 0.0;
-#pragma unroll
-            for (int ww = 1; ww < SYM_NW; ++ww) {
-                v += sCol[ww * SYM_SUB * DP + e];
-                sCol[ww * SYM_SUB * DP + e] = 0.0;
-            }
-            if (I != J) o[e] = v;
-        }
+        sym_phases<D, true>(cb, grp, tl, w, xs, wr, acc, sCol + buf * SCOL, tab);
     }
+    sym_lds_barrier(); // every wave's column sums of the last sub-tile are in LDS
+    col_out(sCol + ((u1 - 1 - u0) & 1) * SCOL, pJ, pSlot, pQ, pDiag);
     if (curI >= 0) SYM_FLUSH_ROWS();
 #undef SYM_FLUSH_ROWS
 }
