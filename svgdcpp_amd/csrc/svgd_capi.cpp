@@ -1843,13 +1843,14 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         // forces it on / off)
         // P > 1: rank r runs the units [U r / P, U (r+1) / P), sums every
         // particle's partials from them and a reduce-scatter (N (d+1) doubles)
-        // hands each rank its rows' totals.  Default up to P = 4: the cfg3
-        // shares (sim-world, profiles/r05_sim_sym.txt) P = 2 2.008 -> 1.875
-        // ms, P = 4 1.066 -> 1.003, against a reduce-scatter of 4.7 MB
-        // (P = 2: 2.4 MB over one xGMI link, ~35 us; P = 4: 1.2 MB per peer
-        // link, ~20 us); P = 8 0.587 -> 0.582, less than its ~20 us exchange
-        bool want_sym = c->plan_world <= 4 && phi_sym_supported(dim);
-        if (n < 32768) want_sym = false;
+        // hands each rank its rows' totals.  Its phi saving grows as N^2 / P,
+        // the exchange as N: default from N / P >= 16384.  cfg3 shares
+        // (sim-world, profiles/r05_sim_sym.txt) P = 2 2.008 -> 1.875 ms, P = 4
+        // 1.066 -> 1.003 against a reduce-scatter of 4.7 MB (P = 2: 2.4 MB
+        // over one xGMI link, ~35 us; P = 4 ~20-35 us); P = 8 (8192 rows) 0.587
+        // -> 0.582, less than its exchange; cfg4 at P = 8 (32768 rows) 7.92 ->
+        // 6.84 ms against 18.9 MB (~0.1-0.15 ms), profiles/r05_cfg4_sim8_sym.txt
+        bool want_sym = phi_sym_supported(dim) && n >= 32768 && n / c->plan_world >= 16384;
         int sym_env = -1; // 2 (a test knob): the P > 1 form (sums, reduce-scatter, apply) at any P
         if (const char *e = std::getenv("SVGD_PHI_SYM")) {
             sym_env = std::atoi(e);

@@ -14,7 +14,7 @@ N=${1:-2}
 OUT=${2:-gpurun_out/bench_mr$N.json}
 SVGD_BENCH_DEVICE=0 SVGD_HOSTCOMM=svgd_bench_$$ SVGD_DEBUG_COLL=1 OMP_NUM_THREADS=4 timeout -k 10 400 \
   python -m torch.distributed.run --nnodes=1 --nproc-per-node $N --master-addr 127.0.0.1 \
-  --master-port 29531 bench.py --gpus $N --steps 8 --warmup 2 --repeats 2 > gpurun_out/bench_mr$N.log 2>&1 || { tail -20 gpurun_out/bench_mr$N.log; exit 1; }
+  --master-port 29531 bench.py --gpus $N --steps ${STEPS:-8} --warmup 2 --repeats 2 ${BENCH_ARGS:-} > gpurun_out/bench_mr$N.log 2>&1 || { tail -20 gpurun_out/bench_mr$N.log; exit 1; }
 grep '^{"metric"' gpurun_out/bench_mr$N.log | tail -1 > $OUT
 python3 - "$OUT" "$N" <<'PY'
 import json, sys
