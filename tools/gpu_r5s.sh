@@ -6,7 +6,7 @@
 REPO="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$REPO"
 source tools/fault_guard.sh
-O=gpurun_out/r5s
+O=gpurun_out/${OUTDIR:-r5s}
 mkdir -p $O
 STEPS=20 WARMUP=3 TAG=_r5 bash tools/profile.sh > /dev/null || exit 1
 fault_guard gpurun_out/prof_r5/bench.log
