@@ -233,19 +233,22 @@ __device__ __forceinline__ void center_mean(const double *__restrict__ pin, int 
     constexpr int T = D <= 2 ? 128 : D <= 4 ? 64 : D <= 8 ? 32 : 16; // threads per column
     for (int e = threadIdx.x; e < nin * D; e += blockDim.x) sP[e] = pin[e];
     __syncthreads();
-    __shared__ double sT[T * D];
+    __shared__ double sT[D <= 2 ? 64 * D : 1];
     const int k = threadIdx.x / T, q = threadIdx.x - k * T;
-    if (k < D) {
-        double s = 0.0;
+    double s = 0.0;
+    if (k < D)
         for (int b = q; b < nin; b += T) s += sP[b * D + k];
-        sT[k * T + q] = s;
-    }
-    __syncthreads();
-    for (int h = T / 2; h > 0; h >>= 1) {
-        if (k < D && q < h) sT[k * T + q] += sT[k * T + q + h];
+    // the T sums in a fixed tree: partner q + h for h = T/2 .. 1 (T = 128:
+    // the upper wave's sums through LDS first, then within the wave by
+    // shuffles -- a column's T <= 64 threads are one aligned lane group)
+    if constexpr (T == 128) {
+        if (k < D && q >= 64) sT[k * 64 + q - 64] = s;
         __syncthreads();
+        if (k < D && q < 64) s += sT[k * 64 + q];
     }
-    if (threadIdx.x < D) mu[threadIdx.x] = sT[threadIdx.x * T] / (double)n;
+#pragma unroll
+    for (int h = (T > 64 ? 64 : T) / 2; h > 0; h >>= 1) s += __shfl_xor(s, h);
+    if (k < D && q == 0) mu[k] = s / (double)n;
     __syncthreads();
 }
 
@@ -352,16 +355,21 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
     } else {
         __syncthreads();
     }
-    if (pout && threadIdx.x < D) {
-        const double *col = sP + threadIdx.x * 256;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0; // four fixed interleaved chains
-        for (int t = 0; t < 256; t += 4) {
-            a0 += col[t];
-            a1 += col[t + 1];
-            a2 += col[t + 2];
-            a3 += col[t + 3];
+    if (pout) {
+        // column k's 256 row sums: TC threads each add 256 / TC consecutive
+        // ones, then a fixed shuffle tree (a column's threads are one aligned
+        // lane group of a wave)
+        constexpr int TC = D <= 4 ? 64 : D <= 8 ? 32 : 16, NV = 256 / TC;
+        const int kc = threadIdx.x / TC, qc = threadIdx.x - kc * TC;
+        double a = 0.0;
+        if (kc < D) {
+            const double *col = sP + kc * 256 + qc * NV;
+#pragma unroll
+            for (int t = 0; t < NV; ++t) a += col[t];
         }
-        pout[(int64_t)blockIdx.x * D + threadIdx.x] = (a0 + a1) + (a2 + a3);
+#pragma unroll
+        for (int h = TC / 2; h > 0; h >>= 1) a += __shfl_xor(a, h);
+        if (kc < D && qc == 0) pout[(int64_t)blockIdx.x * D + kc] = a;
     }
 }
 

@@ -24,6 +24,8 @@ def run(rank, world, name, n, d, steps, q, env=None):
         from svgdcpp_amd import _capi as C
 
         X0 = O.splitmix((n, d), 3.0, 41)
+        if os.environ.get("SVGD_TEST_OUTLIERS"):  # far particles: a log2e max|xc|^2 > 300
+            X0[:3] += float(os.environ["SVGD_TEST_OUTLIERS"])
         mus = O.splitmix((3, d), 3.0, 42)
         covs = [np.eye(d) * (1.0 + 0.25 * c) for c in range(3)]
         ctx = S.Context(d, n, device=0, world=world, rank=rank)

@@ -143,6 +143,22 @@ def test_sharded_symmetric_phi(world, n, d):
     assert all(np.array_equal(Xs[0], x) for x in Xs[1:])
 
 
+def test_sharded_symmetric_phi_hands_over_to_row_stream():
+    """Far outliers at P > 1 (a log2e max|xc|^2 > 300 on every rank: the
+    flag derives from the all-gathered X): the symmetric form's record prep
+    hands the step to the row stream, whose partials k_sym_apply sums -- the
+    reduce-scatter is still issued (the ranks' sequences never depend on
+    device data, SVGD_DEBUG_COLL=1) -- against one rank on the row stream."""
+    world, n, d, steps = 3, 6007, 8, 3
+    env = {"SVGD_TEST_OUTLIERS": "60", "SVGD_DEBUG_COLL": "1"}
+    multi = _run_ranks(world, n, d, steps, dict(env, SVGD_PHI_SYM="1"))
+    single = _run_ranks(1, n, d, steps, dict(env, SVGD_PHI_SYM="0"))[0]
+    X1, s1, _ = single
+    for rank, (X, scales, _) in multi.items():
+        assert scales[0][0] == s1[0][0], (rank, scales, s1)
+        np.testing.assert_allclose(X, X1, rtol=0, atol=1e-10)
+
+
 def test_measurement_context_refuses_results():
     """svgd_create_sim (bench.py --sim-world): rank 0's share of a P-rank step,
     measurement only -- it steps, but every call that hands results back
