@@ -316,6 +316,17 @@ int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi);
 int64_t svgd_plan_pair_tiles(int64_t n, int block, int world, int rank);
 void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
                          int64_t *row_block, int64_t *col_block);
+/* Symmetric phi pass (k_phi_sym) plan of rank r among `world`: its
+ * (tile, sub-tile) units [*u0, *u1) of the tile plan above with blocks of
+ * `block` rows and `nsub` sub-tiles per tile (equal pair counts per rank),
+ * run by `grid` work-groups in contiguous runs; per row block P (of
+ * nb = ceil(n/block)) blkg[2P] .. blkg[2P+1] = the work-groups visiting it
+ * (blkg[2P+1] < blkg[2P]: none) and rbase[P] = its first row-sum record;
+ * *Ia .. *Ib = the row blocks the rank's units span.  blkg holds 2 nb ints,
+ * rbase nb.  Returns the number of row-sum records.  (The pass replaces the
+ * reference's ComputePhi, SVGD.hpp:407-454, for d <= 8.) */
+int64_t svgd_plan_sym_units(int64_t n, int block, int nsub, int world, int rank, int grid,
+                            int64_t *u0, int64_t *u1, int *blkg, int *rbase, int64_t *Ia, int64_t *Ib);
 /* Median bucket select: from the all-reduced histogram of candidate keys in
  * `nb` ascending key-range buckets, the bucket holding each of the `nsel`
  * (1 or 2) candidate ranks, the rank inside it, and the total count of the

@@ -14,6 +14,7 @@
 // unordered pair of blocks then appears exactly once and every row block
 // has the same number of tiles (+-1), so contiguous tile ranges balance the
 // ranks.
+#include <limits.h>
 #include <stdint.h>
 
 #include "../../include/svgdcpp_amd/svgd_capi.h"
@@ -80,6 +81,51 @@ void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
     }
     *row_block = I;
     *col_block = slot == 0 ? I : (I + slot) % nb;
+}
+
+// The symmetric phi pass's unit plan (svgd_capi.cpp, k_phi_sym / k_sym_finish).
+int64_t svgd_plan_sym_units(int64_t n, int block, int nsub, int world, int rank, int grid,
+                            int64_t *u0, int64_t *u1, int *blkg, int *rbase, int64_t *Ia, int64_t *Ib)
+{
+    if (world < 1) world = 1;
+    const int64_t nb = (n + block - 1) / block;
+    const int64_t U = tiles_total(nb) * nsub;
+    *u0 = U * rank / world;
+    *u1 = U * (rank + 1) / world;
+    const int64_t V = *u1 - *u0;
+    for (int64_t P = 0; P < nb; ++P) {
+        blkg[2 * P] = INT32_MAX;
+        blkg[2 * P + 1] = -1;
+    }
+    *Ia = 0;
+    *Ib = -1;
+    if (V <= 0 || grid < 1) {
+        for (int64_t P = 0; P < nb; ++P) rbase[P] = 0;
+        return 0;
+    }
+    // work-group g takes the contiguous units [u0 + V g / G, u0 + V (g+1) / G)
+    // (G <= V: none is empty) and visits the row blocks of their tiles
+    int64_t J;
+    for (int64_t g = 0; g < grid; ++g) {
+        const int64_t a = *u0 + V * g / grid, b = *u0 + V * (g + 1) / grid;
+        if (b <= a) continue;
+        int64_t I0, I1;
+        svgd_plan_pair_tile(n, block, 1, 0, a / nsub, &I0, &J);
+        svgd_plan_pair_tile(n, block, 1, 0, (b - 1) / nsub, &I1, &J);
+        for (int64_t P = I0; P <= I1; ++P) {
+            if ((int)g < blkg[2 * P]) blkg[2 * P] = (int)g;
+            if ((int)g > blkg[2 * P + 1]) blkg[2 * P + 1] = (int)g;
+        }
+    }
+    // each row block's row-sum records contiguous, in work-group order
+    int64_t nrec = 0;
+    for (int64_t P = 0; P < nb; ++P) {
+        rbase[P] = (int)nrec;
+        if (blkg[2 * P + 1] >= blkg[2 * P]) nrec += blkg[2 * P + 1] - blkg[2 * P] + 1;
+    }
+    svgd_plan_pair_tile(n, block, 1, 0, *u0 / nsub, Ia, &J);
+    svgd_plan_pair_tile(n, block, 1, 0, (*u1 - 1) / nsub, Ib, &J);
+    return nrec;
 }
 
 // Bucket of each selection from the all-reduced key-range bucket counts

@@ -1862,43 +1862,16 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             const int64_t T = c->sym_nb * (c->sym_nb + 1) / 2;
             c->sym_units = T * c->symNSUB;
             const int64_t Pw = c->plan_world, r = c->sim_world > 1 ? 0 : c->rank;
-            c->sym_u0 = c->sym_units * r / Pw;
-            c->sym_u1 = c->sym_units * (r + 1) / Pw;
-            const int64_t V = c->sym_u1 - c->sym_u0;
             const int64_t slots = (int64_t)phi_sym_blocks_per_cu(dim) * ncu;
-            c->sym_grid = (int)std::max<int64_t>(1, std::min<int64_t>(V, slots));
-            // row blocks a work-group visits (its unit range is contiguous in
-            // the plan's row-major tile order; G <= V: none is empty), and
-            // per row block the work-groups that visit it (for the finish)
+            const int64_t Vr = c->sym_units * (r + 1) / Pw - c->sym_units * r / Pw;
+            c->sym_grid = (int)std::max<int64_t>(1, std::min<int64_t>(Vr, slots));
+            // the rank's units, the row blocks each work-group's contiguous run
+            // visits and each row block's contiguous row-sum records (plan.cpp)
             const int64_t nbs = c->sym_nb;
             std::vector<int> tab(3 * (size_t)nbs);
             int *blkg = tab.data(), *rbase = blkg + 2 * nbs;
-            for (int64_t P = 0; P < nbs; ++P) {
-                blkg[2 * P] = INT32_MAX;
-                blkg[2 * P + 1] = -1;
-            }
-            for (int64_t g = 0; g < c->sym_grid; ++g) {
-                const int64_t u0 = c->sym_u0 + V * g / c->sym_grid, u1 = c->sym_u0 + V * (g + 1) / c->sym_grid;
-                int64_t I0, J0, I1, J1;
-                svgd_plan_pair_tile(n, (int)B, 1, 0, u0 / c->symNSUB, &I0, &J0);
-                svgd_plan_pair_tile(n, (int)B, 1, 0, (u1 - 1) / c->symNSUB, &I1, &J1);
-                for (int64_t P = I0; P <= I1; ++P) {
-                    blkg[2 * P] = std::min<int>(blkg[2 * P], (int)g);
-                    blkg[2 * P + 1] = std::max<int>(blkg[2 * P + 1], (int)g);
-                }
-            }
-            // each row block's row-sum records: one per visiting work-group,
-            // contiguous (rbase); the units' row-block span (finish)
-            int64_t nrec = 0;
-            for (int64_t P = 0; P < nbs; ++P) {
-                rbase[P] = (int)nrec;
-                if (blkg[2 * P + 1] >= blkg[2 * P]) nrec += blkg[2 * P + 1] - blkg[2 * P] + 1;
-            }
-            {
-                int64_t J;
-                svgd_plan_pair_tile(n, (int)B, 1, 0, c->sym_u0 / c->symNSUB, &c->sym_Ia, &J);
-                svgd_plan_pair_tile(n, (int)B, 1, 0, (c->sym_u1 - 1) / c->symNSUB, &c->sym_Ib, &J);
-            }
+            const int64_t nrec = svgd_plan_sym_units(n, (int)B, c->symNSUB, (int)Pw, (int)r, c->sym_grid,
+                                                     &c->sym_u0, &c->sym_u1, blkg, rbase, &c->sym_Ia, &c->sym_Ib);
             c->sym_SM = (nbs - 1) / 2 + 2;
             // fallback row stream: one wave of work-groups (<= c->S, the part buffer's splits)
             {

@@ -223,3 +223,66 @@ def test_plan_bucket_select():
     assert lib.svgd_plan_bucket_select(counts.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 3, 1,
                                        r.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), bsel, rin,
                                        ctypes.byref(t)) == -1
+
+
+def _tile(lib, n, block, t):
+    I, J = ctypes.c_int64(), ctypes.c_int64()
+    lib.svgd_plan_pair_tile(n, block, 1, 0, t, ctypes.byref(I), ctypes.byref(J))
+    return I.value, J.value
+
+
+@pytest.mark.parametrize("n,block,world,grid", [(65536, 1536, 1, 256), (65536, 1536, 2, 256),
+                                               (65536, 1536, 4, 256), (65536, 1536, 8, 256),
+                                               (262144, 1536, 8, 256), (16384, 4096, 1, 256),
+                                               (6007, 1536, 3, 5), (3001, 2048, 2, 7), (1537, 1536, 1, 4)])
+def test_plan_sym_units(n, block, world, grid):
+    """The symmetric phi pass's unit plan (svgd_plan_sym_units, used by the
+    context for k_phi_sym / k_sym_finish): the ranks' unit ranges partition
+    every (tile, sub-tile) unit once; each work-group's contiguous run is
+    non-empty; blkg holds exactly the work-groups whose runs visit a row
+    block (a contiguous range); rbase numbers each row block's records
+    contiguously in work-group order; Ia..Ib span the rank's row blocks; and
+    the finish's column-partial index (column block J, slot (J - I) mod nb)
+    is one-to-one over the off-diagonal tiles."""
+    lib = C.lib()
+    nsub = block // 64
+    nb = (n + block - 1) // block
+    T = nb * (nb + 1) // 2
+    U = T * nsub
+    tiles = [_tile(lib, n, block, t) for t in range(T)]
+    slots = {}
+    for t, (I, J) in enumerate(tiles):
+        if I != J:
+            key = (J, (J - I) % nb)
+            assert key not in slots, (key, t, slots.get(key))
+            slots[key] = t
+    assert len(slots) == T - nb
+    cover = []
+    for r in range(world):
+        u0, u1, Ia, Ib = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        blkg = (ctypes.c_int * (2 * nb))()
+        rbase = (ctypes.c_int * nb)()
+        g = min(grid, max(1, U * (r + 1) // world - U * r // world))
+        nrec = lib.svgd_plan_sym_units(n, block, nsub, world, r, g, ctypes.byref(u0), ctypes.byref(u1), blkg,
+                                       rbase, ctypes.byref(Ia), ctypes.byref(Ib))
+        u0, u1 = u0.value, u1.value
+        cover.append((u0, u1))
+        V = u1 - u0
+        visits = {}
+        for wg in range(g):
+            a, b = u0 + V * wg // g, u0 + V * (wg + 1) // g
+            assert b > a
+            for P in {tiles[u // nsub][0] for u in range(a, b)}:
+                visits.setdefault(P, []).append(wg)
+        expect_rec = 0
+        for P in range(nb):
+            lo, hi = blkg[2 * P], blkg[2 * P + 1]
+            got = list(range(lo, hi + 1)) if hi >= lo else []
+            assert got == sorted(visits.get(P, [])), (r, P, got, visits.get(P))
+            assert rbase[P] == expect_rec
+            expect_rec += len(got)
+        assert nrec == expect_rec
+        rows = {tiles[u // nsub][0] for u in range(u0, u1)}
+        assert rows == set(range(Ia.value, Ib.value + 1))
+    assert cover[0][0] == 0 and cover[-1][1] == U
+    assert all(a[1] == b[0] for a, b in zip(cover, cover[1:]))
