@@ -135,3 +135,25 @@ def test_sym_full_size_rows_match_oracle(oracle, sym_env):
         ref = oracle.phi(X, G, a, rows=(r0, r1))
         assert np.max(np.abs(ph[r0:r1] - ref)) <= PHI_TOL, (r0, r1)
     c.close()
+
+
+def test_sym_context_takes_row_stream_for_matrix_scale(oracle, sym_env):
+    """A context planned for the symmetric pass: an isotropic phi (the
+    pass), then a full-matrix scale (the folded form needs an isotropic a:
+    the row stream with the matrix records runs), then isotropic again --
+    each against the oracle."""
+    n, d = 2000, 8
+    X = oracle.splitmix((n, d), 2.0, 501)
+    G = oracle.splitmix((n, d), 1.0, 502)
+    A = np.random.default_rng(3).standard_normal((d, d)) * 0.4
+    M = (A @ A.T + 0.3 * np.eye(d)) / d
+    a = 0.37
+    c = _ctx(X)
+    assert c.phi_kernel_name().startswith("k_phi_sym")
+    ref = oracle.phi(X, G, a)
+    assert np.max(np.abs(c.phi(G, a) - ref)) <= PHI_TOL
+    c.set_scale_matrix(M)
+    assert np.max(np.abs(c.phi(G, 0.0) - oracle.phi_matrix(X, G, M))) <= PHI_TOL
+    c.set_scale(C.SVGD_SCALE_MEDIAN)
+    assert np.max(np.abs(c.phi(G, a) - ref)) <= PHI_TOL
+    c.close()
