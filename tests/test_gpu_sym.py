@@ -90,10 +90,13 @@ def test_sym_far_outliers_fall_back_to_row_stream(oracle, sym_env):
     assert np.max(np.abs(ph - ref)) <= PHI_TOL
 
 
-@pytest.mark.parametrize("opt", ["adam", "adagrad"])
-def test_sym_steps_match_oracle(oracle, sym_env, opt):
-    """Median scale + symmetric phi + optimizer, several steps, each step
-    against the oracle step from the same X_t (scale rel <= 1e-12)."""
+@pytest.mark.parametrize("opt", ["adam", "adagrad", "rmsprop"])
+@pytest.mark.parametrize("bounded", [False, True])
+def test_sym_steps_match_oracle(oracle, sym_env, opt, bounded):
+    """Median scale + symmetric phi + optimizer (+ the bounds clamp,
+    SVGD.hpp:393-399), several steps, each step against the oracle step from
+    the same X_t (scale rel <= 1e-12).  The finish (k_sym_finish) and the
+    sharded apply (k_sym_apply) run the optimizer epilogue themselves."""
     n, d, k = 3000, 8, 4
     X = oracle.splitmix((n, d), 3.0, 0x5EED)
     mus = oracle.splitmix((k, d), 3.0, 0x5EEE)
@@ -103,10 +106,19 @@ def test_sym_steps_match_oracle(oracle, sym_env, opt):
     if opt == "adam":
         c.set_optimizer(C.SVGD_OPT_ADAM, 0.1, 0.9, 0.999, 1e-8)
         ref_opt = oracle.Adam((n, d), 0.1, 0.9, 0.999)
-    else:
+    elif opt == "adagrad":
         c.set_optimizer(C.SVGD_OPT_ADAGRAD, 0.1, 0.0, 0.0, 1e-8)
         ref_opt = oracle.AdaGrad((n, d), 0.1)
+    else:
+        c.set_optimizer(C.SVGD_OPT_RMSPROP, 0.1, 0.9, 0.0, 1e-8)
+        ref_opt = oracle.RMSProp((n, d), 0.1, 0.9)
+    lo = up = None
+    if bounded:  # tight enough that every step clamps some coordinates
+        lo, up = -np.full(d, 2.8), np.full(d, 2.5)
+        c.set_bounds(lo, up)
+    assert c.phi_kernel_name().startswith("k_phi_sym")
     Xt = X.copy()
+    clamped = 0
     for _ in range(4):
         c.step_with_model(model)
         a_dev, _, _ = c.last_scale()
@@ -114,10 +126,14 @@ def test_sym_steps_match_oracle(oracle, sym_env, opt):
         assert a_dev == pytest.approx(a_ref, rel=1e-12)
         G = oracle.logp_grad_gmm(Xt, mus, covs)
         Xr = Xt.copy()
-        oracle.apply_update(Xr, ref_opt.step(oracle.phi(Xt, G, a_dev)))
+        oracle.apply_update(Xr, ref_opt.step(oracle.phi(Xt, G, a_dev)), lo, up)
         X1 = c.get_particles()
         assert np.max(np.abs(X1 - Xr)) <= 1e-9
+        if bounded:
+            assert X1.min() >= -2.8 and X1.max() <= 2.5
+            clamped += int(np.sum(X1 == -2.8) + np.sum(X1 == 2.5))
         Xt = X1
+    assert not bounded or clamped > 0
     c.close()
 
 
