@@ -56,9 +56,11 @@ constexpr int MC_NG = 4;    // 16-row blocks per classification group
 // Off-diagonal classification form: 0 = lane masks (v_cmp into SGPRs, the
 // below count and the band OR on the scalar unit), 1 = sign bits on the
 // vector unit (v_pk_add_f32 of TLf - v and THf - v, a per-lane below count,
-// the band as (THf - v) & ~(TLf - v): no scalar work per block)
+// the band as (THf - v) & ~(TLf - v): no scalar work per block), 2 = the
+// band's centre and half-width (bf16-split form; the f32 form takes 0):
+// mcol_classify4m, cfg3 k_pair_mcol 449 -> 428 us (profiles/r05_mcol_cls2_ab.txt)
 #ifndef SVGD_MCOL_CLS
-#define SVGD_MCOL_CLS 0
+#define SVGD_MCOL_CLS 2
 #endif
 
 __device__ __forceinline__ float f32_up(double x)
@@ -140,6 +142,81 @@ __device__ __forceinline__ void mcol_classify4v(const f4_t &v, float tl, float t
     cnt += (a[0] >> 31) + (a[1] >> 31) + (a[2] >> 31) + (a[3] >> 31);
 #pragma unroll
     for (int r = 0; r < 4; ++r) b[r] = t[r] & ~a[r];
+}
+
+// SVGD_MCOL_CLS = 2: one compare per value.  Per row, with the fp32
+// thresholds TL > TH of the lane-mask form clamped into [-2^42, 2^42] (every
+// value is finite and below 2^41 in magnitude while delta is finite: |v| <=
+// 1.5 nmax + rounding, nmax <= 2^40), TM = fp32((TL + TH) / 2) and
+// W = fp32_up(max(TL - TM, TM - TH) (1 + 2^-22)), and x = fl(v - TM):
+//   x > W   => v - TM > W (1 - 2^-24) >= TL - TM  => v > TL  (below)
+//   x < -W  => v < TM - W (1 - 2^-24) <= TH                 (above)
+// (fl(v - TM) = (v - TM)(1 + e), |e| <= 2^-24; exact when subnormal), so
+// "below" is a subset of the lane-mask form's below, "above" of its above,
+// and the band |x| <= W a superset of its band: the exact fp64 finish
+// decides every staged pair, the keys and counts are the same.  Padding
+// rows: TM = +inf, W = 0 (x is -inf or NaN: never below, never band);
+// padding columns (h = -inf): x = -inf, never band.  delta = inf (nmax >
+// 2^40) keeps the lane-mask form (the caller's uniform branch).
+//   4 v_cmp (below) + min3 / min of |x| + 1 v_cmp (any band lane) on the
+// vector unit, 4 bcnt + 4 add on the scalar unit: 8 scalar operations fewer
+// per 16 x 16 block than mcol_classify4; the band lanes' per-value masks are
+// formed only in the (rare) staging branch (mcol_band4m).
+__device__ __forceinline__ unsigned long long mcol_classify4m(const float (&x)[4], float w, uint32_t &nbelow)
+{
+    unsigned long long l0, l1, l2, l3, any;
+    uint32_t t0, t1;
+    float m;
+    asm volatile("v_cmp_gt_f32_e64 %[l0], %[x0], %[w]\n\t"
+                 "v_cmp_gt_f32_e64 %[l1], %[x1], %[w]\n\t"
+                 "v_min3_f32 %[m], |%[x0]|, |%[x1]|, |%[x2]|\n\t"
+                 "v_cmp_gt_f32_e64 %[l2], %[x2], %[w]\n\t"
+                 "v_cmp_gt_f32_e64 %[l3], %[x3], %[w]\n\t"
+                 "v_min_f32_e64 %[m], %[m], |%[x3]|\n\t"
+                 "s_bcnt1_i32_b64 %[t0], %[l0]\n\t"
+                 "s_bcnt1_i32_b64 %[t1], %[l1]\n\t"
+                 "v_cmp_ge_f32_e64 %[any], %[w], %[m]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t0]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t1]\n\t"
+                 "s_bcnt1_i32_b64 %[t0], %[l2]\n\t"
+                 "s_bcnt1_i32_b64 %[t1], %[l3]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t0]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t1]"
+                 : [nb] "+s"(nbelow), [any] "=&s"(any), [l0] "=&s"(l0), [l1] "=&s"(l1),
+                   [l2] "=&s"(l2), [l3] "=&s"(l3), [t0] "=&s"(t0), [t1] "=&s"(t1), [m] "=&v"(m)
+                 : [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [w] "v"(w)
+                 : "scc");
+    return any;
+}
+// x_r = v_r - TM, two values per packed subtraction
+__device__ __forceinline__ void mcol_sub_centre(const f4_t &v, float tm, float (&x)[4])
+{
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 t = {tm, tm};
+    const f2 x01 = f2{v[0], v[1]} - t, x23 = f2{v[2], v[3]} - t;
+    x[0] = x01[0];
+    x[1] = x01[1];
+    x[2] = x23[0];
+    x[3] = x23[1];
+}
+// the per-value band masks of mcol_classify4m's values (|x_r| <= W)
+__device__ __forceinline__ void mcol_band4m(const float (&x)[4], float w, unsigned long long (&h)[4])
+{
+    asm volatile("v_cmp_ge_f32_e64 %[h0], %[w], |%[x0]|\n\t"
+                 "v_cmp_ge_f32_e64 %[h1], %[w], |%[x1]|\n\t"
+                 "v_cmp_ge_f32_e64 %[h2], %[w], |%[x2]|\n\t"
+                 "v_cmp_ge_f32_e64 %[h3], %[w], |%[x3]|"
+                 : [h0] "=&s"(h[0]), [h1] "=&s"(h[1]), [h2] "=&s"(h[2]), [h3] "=&s"(h[3])
+                 : [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]), [w] "v"(w));
+}
+// (TM, W) of one row from the lane-mask form's fp32 thresholds (TL, TH)
+__device__ __forceinline__ float2 mcol_centre_width(float tl, float th)
+{
+    if (tl == __builtin_inff() && th == __builtin_inff()) return make_float2(__builtin_inff(), 0.0f); // padding row
+    const double L = fmin((double)tl, 0x1p42), H = fmax((double)th, -0x1p42);
+    const float tm = (float)(0.5 * (L + H));
+    const double w = fmax(L - (double)tm, (double)tm - H) * (1.0 + 0x1p-22);
+    return make_float2(tm, f32_up(w));
 }
 
 // Diagonal tiles (1 in nb/2 of them): lanes with xl > c (j > i) only.
@@ -237,6 +314,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     static_assert(!BF || (D <= 8 && RW == 4), "the bf16 split form takes d <= 8");
     __shared__ __attribute__((aligned(16))) float sRow[NI * 64 * RW]; // BF: the B fragments
     __shared__ float2 sThr[BF ? PBLK : 1];                            // BF: (TLf, THf) per row
+    constexpr bool MIDC = BF && SVGD_MCOL_CLS == 2;                   // mcol_classify4m
+    __shared__ float2 sThm[MIDC ? PBLK : 1];                          // (TM, W) per row
     __shared__ uint32_t sStage[4][MC_STG + 64]; // + the spill zone (SVGD_MCOL_STAGE)
     __shared__ uint32_t sBk[NBK];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -403,8 +482,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                             const double m = 0x1p-48 * (ni + nmax);
                             const double TL = lo_key == 0 ? __builtin_inf() : 0.5 * (ni - lo_d + m);
                             const double TH = 0.5 * (ni - hi_d - m);
-                            sThr[e] = make_float2(tv ? f32_up(TL + delta) : __builtin_inff(),
-                                                  tv ? f32_down(TH - delta) : __builtin_inff());
+                            const float2 t = make_float2(tv ? f32_up(TL + delta) : __builtin_inff(),
+                                                         tv ? f32_down(TH - delta) : __builtin_inff());
+                            sThr[e] = t;
+                            if constexpr (MIDC) sThm[e] = mcol_centre_width(t.x, t.y);
                         }
                         continue;
                     }
@@ -449,14 +530,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                 for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
             };
             // one group of MC_NG row blocks: its row operands from LDS, its MFMAs
-            auto group_mfma = [&](int g0, const f4 &hq, const float (&A)[AK],
+            // MID: the row values are (TM, W) (mcol_classify4m), else (TLf, THf)
+            auto group_mfma = [&](auto mid_tag, int g0, const f4 &hq, const float (&A)[AK],
                                   float (&Bg)[MC_NG][BW], f4 (&acc)[MC_NG]) {
+                constexpr bool MID = decltype(mid_tag)::value;
                 if constexpr (BF) {
                     const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(A));
 #pragma unroll
                     for (int g = 0; g < MC_NG; ++g) {
                         const uint4 b = *reinterpret_cast<const uint4 *>(sRow + ((g0 + g) * 64 + lane) * RW);
-                        const float2 t = sThr[16 * (g0 + g) + ql];
+                        const float2 t = MID ? sThm[16 * (g0 + g) + ql] : sThr[16 * (g0 + g) + ql];
                         Bg[g][0] = t.x;
                         Bg[g][1] = t.y;
                         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, b), hq,
@@ -485,8 +568,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
             // classification (phase 2: two compares per value straight into
             // lane masks -- below (v > TLf) counted on the scalar unit, band (v
             // > THf but not below) OR-ed; phase 3, rare: stage the band pairs).
-            auto jloop = [&](auto diag_tag) {
+            auto jloop = [&](auto diag_tag, auto mid_tag) {
                 constexpr bool DIAG = decltype(diag_tag)::value;
+                constexpr bool MID = decltype(mid_tag)::value;
                 float A[AK], An[AK];
                 f4 hq, hqn;
                 if (w < njb) load_cols(w, A, hq);
@@ -501,16 +585,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                     const uint32_t ebase = (uint32_t)ql | ((uint32_t)(jl0 + 4 * kq) << 16);
                     float Bg[MC_NG][BW], Bn[MC_NG][BW];
                     f4 acc[MC_NG], accn[MC_NG];
-                    group_mfma(0, hq, A, Bg, acc);
+                    group_mfma(mid_tag, 0, hq, A, Bg, acc);
                     // unrolled: the next group's accumulators and row values
                     // take other registers instead of being copied each group
 #pragma unroll
                     for (int g0 = 0; g0 < NI; g0 += MC_NG) {
-                        if (g0 + MC_NG < NI) group_mfma(g0 + MC_NG, hq, A, Bn, accn);
+                        if (g0 + MC_NG < NI) group_mfma(mid_tag, g0 + MC_NG, hq, A, Bn, accn);
                         uint32_t nbelow = 0;
 #pragma unroll
                         for (int g = 0; g < MC_NG; ++g) {
                             unsigned long long h[4], any = 0;
+                            float xm[4]; // MID: v - TM
                             if constexpr (SVGD_MCOL_ABL == 2) {
                                 asm volatile("" ::"v"(acc[g][0]), "v"(acc[g][1]), "v"(acc[g][2]),
                                              "v"(acc[g][3]), "v"(Bg[g][TI]), "v"(Bg[g][TI + 1]));
@@ -522,6 +607,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                                               16 * (g0 + g) - jl0 - r, nbelow);
                                     any |= h[r];
                                 }
+                            } else if constexpr (MID) {
+                                mcol_sub_centre(acc[g], Bg[g][TI], xm); // 2 v_pk_add_f32
+                                any = mcol_classify4m(xm, Bg[g][TI + 1], nbelow);
                             } else if constexpr (SVGD_MCOL_CLS == 1) {
                                 uint32_t bv[4];
                                 mcol_classify4v(acc[g], Bg[g][TI], Bg[g][TI + 1], vbelow, bv);
@@ -542,6 +630,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                     // every lane stores: a lane without band values, or an
                                     // entry past the area, lands in the spill zone; the
                                     // flush reports an overflowed area (scnt > MC_STG)
+                                    if constexpr (MID) mcol_band4m(xm, Bg[g][TI + 1], h);
                                     const uint32_t code = mcol_code4(h);
                                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
                                         (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
@@ -559,6 +648,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                 if (scnt + c > MC_STG) { // pathological band: give up
                                     ovf = true;          // (region overflow -> exact fallback)
                                 } else {
+                                    if constexpr (MID) mcol_band4m(xm, Bg[g][TI + 1], h);
                                     const uint32_t code = mcol_code4(h);
                                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
                                         (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
@@ -583,9 +673,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                 }
             };
             if (diag)
-                jloop(std::true_type{});
-            else
-                jloop(std::false_type{});
+                jloop(std::true_type{}, std::false_type{});
+            else if constexpr (MIDC) {
+                // delta = inf (nmax > 2^40): values may exceed mcol_classify4m's range
+                if (delta < __builtin_inf())
+                    jloop(std::false_type{}, std::true_type{});
+                else
+                    jloop(std::false_type{}, std::false_type{});
+            } else
+                jloop(std::false_type{}, std::false_type{});
             if (scnt) flush(ib, jbase);
         } while (advance(pos));
     }
