@@ -542,9 +542,11 @@ def main():
                              "job": per_step(host_timed["host_job_ms"], host_timed["steps"]),
                              "caller_wait": per_step(host_timed["host_wait_ms"], host_timed["steps"]),
                              "threads": host_timed["host_threads"],
-                             # the gradient's threads: min(OMP threads / 2, cgroup quota / ranks)
+                             # the gradient's threads: min(OMP threads / 2, cgroup quota / ranks);
+                             # a --sim-world rank models one GPU's share of a P-GPU node (CPUs are
+                             # leased per GPU): this box's whole quota
                              "cpu_quota": host_timed["cpu_quota"],
-                             "ranks_sharing_quota": int(host_timed["sim_world"]) if args.sim_world > 1 else world},
+                             "ranks_sharing_quota": 1 if args.sim_world > 1 else world},
         # speculative steps whose median bracket was predicted from the last
         # medians (no sample), and of those the ones redone after a miss
         "tracked_brackets": {"steps": int(host_timed["steps"]), "predicted": int(host_timed["trk_steps"]),

@@ -445,10 +445,16 @@ private:
         out.op_ = op;
         out.lhs_ = CloneSharedPointer();
         out.rhs_ = obj.CloneSharedPointer();
-        // a derived model that overrides the evaluation virtuals but not
-        // CloneSharedPointer would be sliced to a base Model here (and fail
-        // only later, inside SVGD::Run): refuse it now
-        if (typeid(*out.lhs_) != typeid(*this) || typeid(*out.rhs_) != typeid(obj))
+        // a derived model that does not override CloneSharedPointer is
+        // sliced to a base Model here.  That is harmless when the slice keeps
+        // the behaviour (functions set with UpdateModel, a Gaussian form, a
+        // composition: all copied members); a derived model that only
+        // overrides the evaluation virtuals would lose them and fail later,
+        // inside SVGD::Run: refuse that one now
+        auto lost = [](const std::shared_ptr<Model> &clone, const Model &src) {
+            return typeid(*clone) != typeid(src) && !clone->HasFunction();
+        };
+        if (lost(out.lhs_, *this) || lost(out.rhs_, obj))
             throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
                                         "[Argument Error] A derived model must override CloneSharedPointer "
                                         "(returning a copy of its own type) to be composed.");

@@ -161,7 +161,13 @@ public:
         rbf_ptr_ = std::dynamic_pointer_cast<GaussianRBFKernel>(kernel_ptr_);
         if (!rbf_ptr_)
         {
-            // generic kernel: the reference's per-pair ComputePhi on the host
+            // generic kernel: the reference's per-pair ComputePhi on the host,
+            // the whole problem in this process -- the sharding options
+            // (World, Rank, UniqueId) would be silently ignored: refuse them
+            if (world > 1 || !unique_id.empty())
+                throw std::invalid_argument(SVGDCPP_LOG_PREFIX +
+                                            "[Argument Error] World, Rank and UniqueId apply to the GaussianRBFKernel "
+                                            "device path only; a generic kernel runs on one host process.");
             std::cout << SVGDCPP_LOG_PREFIX + "Kernel is not a GaussianRBFKernel: phi_hat runs on the host "
                                               "(generic kernel path)."
                       << std::endl;

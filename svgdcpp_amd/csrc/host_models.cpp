@@ -104,8 +104,9 @@ bool have_avx512()
            __builtin_cpu_supports("fma");
 }
 
-// variant: 0 the host's best, 1 the 4-particle block (AVX2 / baseline), 2 SoA8 (AVX-512)
-static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, double *G,
+// variant: 0 the host's best, 1 the 4-particle block (AVX2 / baseline), 2 SoA8 (AVX-512).
+// Returns SVGD_ERR_RUNTIME when a thread's work area cannot be allocated.
+static int logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, double *G,
                            int nthreads, int variant = 0)
 {
     static const GradBlockFn block = pick_grad_block();
@@ -113,7 +114,8 @@ static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, d
     const int d = m->d, k = m->k;
     if (nthreads <= 0) nthreads = omp_get_max_threads();
     const bool soa8 = variant == 2 || (variant == 0 && avx512);
-    if (soa8 && !avx512) return; // (variant 2 forced on a host without AVX-512: refused by the caller)
+    if (soa8 && !avx512) return SVGD_ERR_ARG; // (variant 2 forced on a host without AVX-512: refused by the caller)
+    int failed = 0;
 #pragma omp parallel num_threads(nthreads)
     {
         if (soa8) {
@@ -121,10 +123,16 @@ static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, d
             // vector type is not 64-byte aligned by the allocator
             const size_t bytes = sizeof(double) * 8 * ((size_t)(2 + k) * d + k);
             double *ws = static_cast<double *>(std::aligned_alloc(64, (bytes + 63) / 64 * 64));
+            if (!ws) {
+#pragma omp atomic write
+                failed = 1;
+            }
             const int64_t nblk = (nrows + 7) / 8;
+            // (every thread reaches the worksharing loop; one without its
+            // work area skips its blocks and the call reports the failure)
 #pragma omp for schedule(static)
             for (int64_t b = 0; b < nblk; ++b)
-                gb_avx512::logp_grad_soa8(m, X, b * 8, (int)std::min<int64_t>(8, nrows - b * 8), G, ws);
+                if (ws) gb_avx512::logp_grad_soa8(m, X, b * 8, (int)std::min<int64_t>(8, nrows - b * 8), G, ws);
             std::free(ws);
         } else {
             std::vector<double> diff((size_t)GB_NP * d), gc((size_t)GB_NP * k * d), q((size_t)GB_NP * k);
@@ -137,6 +145,7 @@ static void logp_grad_rows(const HostModel *m, const double *X, int64_t nrows, d
             }
         }
     }
+    return failed ? SVGD_ERR_RUNTIME : SVGD_OK;
 }
 
 namespace svgd_amd {
@@ -144,8 +153,7 @@ int model_logp_grad_threads(const HostModel *m, const double *X, int64_t nrows, 
                             int nthreads)
 {
     if (!m || (!X && nrows > 0) || (!G && nrows > 0)) return SVGD_ERR_ARG;
-    logp_grad_rows(m, X, nrows, G, nthreads);
-    return SVGD_OK;
+    return logp_grad_rows(m, X, nrows, G, nthreads);
 }
 bool host_grad_avx512() { return have_avx512(); }
 int model_logp_grad_variant(const HostModel *m, const double *X, int64_t nrows, double *G, int nthreads,
@@ -153,8 +161,7 @@ int model_logp_grad_variant(const HostModel *m, const double *X, int64_t nrows, 
 {
     if (!m || (!X && nrows > 0) || (!G && nrows > 0) || variant < 0 || variant > 2) return SVGD_ERR_ARG;
     if (variant == 2 && !have_avx512()) return SVGD_ERR_ARG;
-    logp_grad_rows(m, X, nrows, G, nthreads, variant);
-    return SVGD_OK;
+    return logp_grad_rows(m, X, nrows, G, nthreads, variant);
 }
 } // namespace svgd_amd
 
@@ -193,8 +200,7 @@ int svgd_model_logp_grad(void *model, const double *X, int64_t nrows, double *G)
 {
     const HostModel *m = static_cast<const HostModel *>(model);
     if (!m || (!X && nrows > 0) || (!G && nrows > 0)) return SVGD_ERR_ARG;
-    logp_grad_rows(m, X, nrows, G, 0);
-    return SVGD_OK;
+    return logp_grad_rows(m, X, nrows, G, 0);
 }
 
 int svgd_model_neg_hess_sum(void *model, const double *X, int64_t nrows, double *H)

@@ -157,6 +157,29 @@ template <class T> static int allreduce_sum(HostComm *c, T *dbuf, size_t cnt, hi
     return c->barrier();
 }
 
+// In-place reduce-scatter (sum) of `cnt` doubles per rank, ncclReduceScatter's
+// in-place contract: dbuf holds world x cnt, rank r receives the sums of
+// chunk r at dbuf + r * cnt (added in rank order).  Every OTHER chunk of dbuf
+// is overwritten with NaN afterwards: RCCL leaves it undefined, so a caller
+// that reads outside its chunk (a wrong offset) fails here too.
+int hostcomm_reduce_scatter_f64(HostComm *c, double *dbuf, size_t cnt, hipStream_t stream)
+{
+    const size_t all = cnt * (size_t)c->world * sizeof(double), bytes = cnt * sizeof(double);
+    if (all > c->slot) return -2;
+    if (hipStreamSynchronize(stream) != hipSuccess) return -3;
+    if (hipMemcpy(c->slot_ptr(c->rank), dbuf, all, hipMemcpyDeviceToHost) != hipSuccess) return -3;
+    if (c->barrier()) return -1;
+    c->tmp.assign(bytes, 0);
+    double *acc = reinterpret_cast<double *>(c->tmp.data());
+    for (int r = 0; r < c->world; ++r) {
+        const double *v = reinterpret_cast<const double *>(c->slot_ptr(r)) + (size_t)c->rank * cnt;
+        for (size_t i = 0; i < cnt; ++i) acc[i] += v[i];
+    }
+    if (hipMemset(dbuf, 0xff, all) != hipSuccess) return -3; // all-ones bits: NaN
+    if (hipMemcpy(dbuf + (size_t)c->rank * cnt, acc, bytes, hipMemcpyHostToDevice) != hipSuccess) return -3;
+    return c->barrier();
+}
+
 int hostcomm_allreduce_u32(HostComm *c, uint32_t *dbuf, size_t cnt, hipStream_t stream)
 {
     return allreduce_sum(c, dbuf, cnt, stream);

@@ -12,5 +12,6 @@ void hostcomm_destroy(HostComm *c);
 int hostcomm_allgather(HostComm *c, char *dbuf, size_t count_bytes, hipStream_t stream);
 int hostcomm_allreduce_u32(HostComm *c, uint32_t *dbuf, size_t cnt, hipStream_t stream);
 int hostcomm_allreduce_f64(HostComm *c, double *dbuf, size_t cnt, hipStream_t stream);
+int hostcomm_reduce_scatter_f64(HostComm *c, double *dbuf, size_t cnt, hipStream_t stream);
 int hostcomm_allreduce_u64(HostComm *c, unsigned long long *dbuf, size_t cnt, hipStream_t stream);
 } // namespace svgd_amd

@@ -608,7 +608,9 @@ int allgather_u64(svgd_ctx *c, uint64_t *buf, size_t cnt)
 
 // In-place reduce-scatter (sum) of `w` doubles per row: buf holds world x
 // chunk rows, rank r gets the sums of its chunk at buf + r * chunk * w.  The
-// host-shm rehearsal path all-reduces the whole buffer (same result there).
+// host-shm rehearsal path is a true reduce-scatter: the other chunks come
+// back as NaN (RCCL leaves them undefined), so a read outside the rank's
+// chunk fails the multi-rank tests.
 int reduce_scatter_rows(svgd_ctx *c, double *buf, size_t w)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank / simulated world: no exchange
@@ -617,8 +619,8 @@ int reduce_scatter_rows(svgd_ctx *c, double *buf, size_t w)
     coll_note(c, CO_RS_ROWS, cnt);
     hipEvent_t d0 = diag_begin(c, c->stream);
     if (c->hcomm) {
-        if (hostcomm_allreduce_f64(c->hcomm, buf, cnt * (size_t)c->world, c->stream))
-            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host all-reduce failed.");
+        if (hostcomm_reduce_scatter_f64(c->hcomm, buf, cnt, c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host reduce-scatter failed.");
     } else {
         NCCLCHK(c, ncclReduceScatter(buf, buf + (size_t)c->rank * cnt, cnt, ncclDouble, ncclSum, c->comm,
                                      c->stream));
@@ -1390,14 +1392,10 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
                    c->nrows,  1.0 / (double)c->n, c->phi, c->rec, c->RS, c->contrib,
                    c->sym_tab, c->sym_tab + 2 * c->sym_nb,
                    c->sym_SM, c->sym_Ia, c->sym_Ib, c->part, c->sym_fS, c->ldp};
+        // (when the records' flag says the symmetric form would leave its
+        // range, symok = 0, the same launch runs the row stream's work-groups
+        // instead; their partials are summed by the finish / k_sym_apply)
         HIPCHK(c, launch_phi_sym(sa, k0, k1, c->stream));
-        // the row stream takes the step instead when the records' flag says
-        // the symmetric form would leave its range (symok = 0): its kernel
-        // alone, in one wave of work-groups (a no-op launch on the usual path
-        // costs little), its partials summed by the finish / k_sym_apply
-        HIPCHK(c, launch_phi_rows(c->dim, c->R, c->rec, c->scal, c->row0, c->nrows, c->n, c->sym_fS, c->part,
-                                  c->ldp, 1.0 / (double)c->n, nullptr, nullptr, nmax_cur(c), c->phi, opt,
-                                  c->stream, nullptr, c->phi_kind, c->symok, false));
         HIPCHK(c, launch_sym_finish(sa, opt, c->stream));
         if (c->contrib) {
             // every rank's sums of its rows (issued whether or not symok: the
@@ -1873,9 +1871,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             const int64_t nrec = svgd_plan_sym_units(n, (int)B, c->symNSUB, (int)Pw, (int)r, c->sym_grid,
                                                      &c->sym_u0, &c->sym_u1, blkg, rbase, &c->sym_Ia, &c->sym_Ib);
             c->sym_SM = (nbs - 1) / 2 + 2;
-            // fallback row stream: one wave of work-groups (<= c->S, the part buffer's splits)
+            // the row stream's hand-over inside k_phi_sym (symok = 0): its
+            // 8-wave work-groups, one wave of them (<= c->S, the part buffer's splits)
             {
-                const int64_t rows_wg = c->phi_kind == 2 ? phi_rows_t8k_rows(c->R) : 256 * (int64_t)c->R;
+                const int64_t rows_wg = phi_rows_t8k_rows(4);
                 const int64_t ib = std::max<int64_t>(1, (c->nrows + rows_wg - 1) / rows_wg);
                 c->sym_fS = (int)std::max<int64_t>(1, std::min<int64_t>(c->S, ncu / ib));
             }
@@ -1975,13 +1974,17 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     // cgroup CPU quota (ranks of one node share it; OpenMP sees the affinity
     // mask, not the quota) and at most 32 (the gradient of a 65536-row share
     // takes 0.4 ms on 8 threads, hidden behind the device median).  A
-    // measurement context (svgd_create_sim) takes the share of a rank of its
-    // simulated world, as that rank would.
+    // measurement context (svgd_create_sim) models rank 0 of a P-GPU node:
+    // the pool leases CPUs per GPU (16 with each MI355X), so that rank's
+    // share of the node's quota is this one-GPU box's whole quota
+    // (SVGD_HOST_THREADS=2 reproduces the 16-CPU box split 8 ways, the
+    // pessimistic bound of rounds 3-5).
     {
         int t = std::max(1, omp_get_max_threads() / 2);
         const int q = cgroup_cpus();
         c->cpu_quota = q;
-        if (q > 0) t = std::min(t, std::max(1, q / std::max(1, c->plan_world)));
+        const int sharing = c->sim_world > 1 ? 1 : std::max(1, c->plan_world);
+        if (q > 0) t = std::min(t, std::max(1, q / sharing));
         c->host_threads = std::min(t, 32);
     }
     if (const char *e = std::getenv("SVGD_HOST_THREADS")) c->host_threads = std::max(1, std::atoi(e));
@@ -2504,10 +2507,11 @@ int svgd_step_host_model(svgd_ctx *c, const void *model)
                 return SVGD_ERR_HIP;
             }
             const clk::time_point tg = clk::now();
-            if (model_logp_grad_threads(m, hx + r0 * d, r1 - r0, c->h_g + r0 * d,
-                                        c->host_threads)) {
-                msg = "SVGDCpp: [Argument Error] Host model evaluation failed.";
-                return SVGD_ERR_ARG;
+            if (const int rc = model_logp_grad_threads(m, hx + r0 * d, r1 - r0, c->h_g + r0 * d,
+                                                       c->host_threads)) {
+                msg = rc == SVGD_ERR_RUNTIME ? "SVGDCpp: [Runtime Error] Host model evaluation: out of memory."
+                                             : "SVGDCpp: [Argument Error] Host model evaluation failed.";
+                return rc;
             }
             c->h_xwait_ms += ms_since(tw, tg);
             c->h_grad_ms += ms_since(tg, clk::now());

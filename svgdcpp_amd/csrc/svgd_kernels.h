@@ -221,17 +221,17 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
                            const unsigned long long *nmax_bits, double *phi, const OptArgs *opt,
                            hipStream_t stream, hipEvent_t ev_mid = nullptr, int kind = 0,
                            const int *skip = nullptr, bool reduce = true);
-// skip (optional): the row stream and its reduce do nothing while *skip != 0
-// (the symmetric pass below took the step).  reduce = false: the row kernel
-// alone (its partials summed by the symmetric finish / apply instead)
+// skip (optional): the reduce does nothing while *skip != 0.  reduce = false:
+// the row kernel alone
 
 // Symmetric phi pass (d <= 8): each unordered pair's kernel value feeds both
 // particles (k_phi_sym, launch_phi_sym), then k_sym_finish (launch_sym_finish)
 // sums the partials in a fixed order, forms phi and applies the optimizer.
-// Runs only while *symok (set by its record prep: a log2e max|xc|^2 <= 300);
-// otherwise the row stream, launched between the two with skip = symok and
-// reduce = false, takes the step: the finish (one rank) or k_sym_apply
-// (P > 1) then sums ITS partials fS x fldp (the k_phi_reduce arithmetic).
+// The pair pass runs while *symok (set by its record prep: a log2e
+// max|xc|^2 <= 300); otherwise the same launch runs the row stream's
+// work-groups (its 8-wave kernel, fS column splits, on the rank's rows) and
+// the finish (one rank) or k_sym_apply (P > 1) sums ITS partials fS x fldp
+// (the k_phi_reduce arithmetic) -- no second launch on the usual path.
 struct SymArgs {
     int d;
     const double *xc;
@@ -258,7 +258,7 @@ struct SymArgs {
     int64_t SM = 0;        // colpart slots per column block: (nbs - 1) / 2 + 2
     int64_t Ia = 0, Ib = 0; // the row blocks this rank's units span
     // the row stream's partials when it takes the step (symok = 0)
-    const double *fpart = nullptr;
+    double *fpart = nullptr;
     int fS = 0;
     int64_t fldp = 0;
 };

@@ -2039,6 +2039,8 @@ __device__ __forceinline__ double exp2_4096_poly(double f)
 }
 
 constexpr int CH_PHI = 16; // columns per LDS chunk of the phi row stream
+// the 8-wave row stream (kind 2): 8 waves, columns split over the 8 waves
+constexpr int T8K_NW = 8, T8K_WC = 8;
 constexpr int EXP_TB = 4096; // row-stream exp table entries
 // Biased exponent (the 8-wave kernel, TABN = 8192): u' = u + EXP_UB >= 0 on
 // both forms (folded u >= -1001 x 4096, plain |u| <= 1000 x 4096), so
@@ -2271,23 +2273,28 @@ __device__ __forceinline__ void phi_rows_pair(const ColRec<D> &q, const double (
 // groups of 64 R rows): their partial sums are added in LDS in wave order
 // before one partial per work-group goes out -- WC times fewer partials (HBM
 // writes here, reads in k_phi_reduce) for the same number of waves.
-template <int D, int R, int NW = 4, int TABN = EXP_TB, int WC = 1>
-__global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__ rec,
-                                                 const double *__restrict__ a_ptr, int64_t row0,
-                                                 int64_t nrows, int64_t n, int S,
-                                                 double *__restrict__ part, int64_t ldp,
-                                                 const double *__restrict__ sgn,
-                                                 const unsigned long long *__restrict__ nmax_bits,
-                                                 const int *__restrict__ skip)
+// LDS bytes of the row stream's work-group: per-wave double-buffered column
+// chunks, then the 2^(i/4096) table
+template <int D, int NW, int TABN> constexpr int phi_rows_lds()
+{
+    return NW * 2 * (CH_PHI * RecLayout<D>::RS * 8) + TABN * 8;
+}
+
+// The row stream's work-group `bid` of a grid of (row groups) x S blocks, on
+// the caller's LDS (phi_rows_lds bytes): k_phi_rows, and k_phi_sym when the
+// symmetric form does not apply (its hand-over, symok = 0).
+template <int D, int R, int NW, int TABN, int WC>
+__device__ __forceinline__ void phi_rows_body(char *smem, int64_t bid, const double *__restrict__ rec,
+                                              const double *__restrict__ a_ptr, int64_t row0, int64_t nrows,
+                                              int64_t n, int S, double *__restrict__ part, int64_t ldp,
+                                              const double *__restrict__ sgn,
+                                              const unsigned long long *__restrict__ nmax_bits)
 {
     constexpr int RS = RecLayout<D>::RS;
     constexpr int CHB = CH_PHI * RS * 8; // bytes per column chunk (multiple of 1 KiB)
-    if (skip && *skip) return; // the symmetric pass took this step
     // register double buffer of the column record only where it fits without
     // spilling (row state R(2D+2) + two records 2(2D+1) doubles)
     constexpr bool PIPE = (R * (2 * D + 2) + 2 * (2 * D + 1)) * 2 <= 232;
-    // per-wave double-buffered column chunks, then the 2^(i/4096) table
-    __shared__ __attribute__((aligned(16))) char smem[NW * 2 * CHB + TABN * 8];
     double *tab = reinterpret_cast<double *>(smem + NW * 2 * CHB);
 #pragma unroll
     for (int e = 0; e < TABN / (NW * 64); ++e) {
@@ -2305,8 +2312,8 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
     static_assert(NW % WC == 0, "WC must divide NW");
     constexpr int WR = NW / WC; // row groups per work-group
     const int wr = w % WR, wc = w / WR;
-    const int64_t iblk = blockIdx.x / S;
-    const int s = (int)(blockIdx.x - iblk * S);
+    const int64_t iblk = bid / S;
+    const int s = (int)(bid - iblk * S);
     const int64_t rbase = iblk * (WR * 64 * R) + wr * (64 * R); // local row of this wave's lane 0
     // u_ij = c_i + c_j + 8192 a log2e xc_i.xc_j = -4096 a log2e |xc_i - xc_j|^2;
     // the row coordinates are pre-scaled by 8192 a log2e
@@ -2440,7 +2447,7 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
         // slice of 64 rows per row group at a time; coalesced partial rows
         constexpr int RB = WR * 64;  // rows of one slice
         constexpr int EL = RB * (D + 1);
-        static_assert(WC * EL * 8 <= (int)sizeof(smem), "reduction slice exceeds the LDS");
+        static_assert(WC * EL * 8 <= phi_rows_lds<D, NW, TABN>(), "reduction slice exceeds the LDS");
         double *red = reinterpret_cast<double *>(smem);
         __syncthreads();
 #pragma unroll
@@ -2472,6 +2479,19 @@ __global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__
             o[D] = acc1[r];
         }
     }
+}
+
+template <int D, int R, int NW = 4, int TABN = EXP_TB, int WC = 1>
+__global__ __launch_bounds__(NW * 64) void k_phi_rows(const double *__restrict__ rec,
+                                                 const double *__restrict__ a_ptr, int64_t row0,
+                                                 int64_t nrows, int64_t n, int S,
+                                                 double *__restrict__ part, int64_t ldp,
+                                                 const double *__restrict__ sgn,
+                                                 const unsigned long long *__restrict__ nmax_bits)
+{
+    __shared__ __attribute__((aligned(16))) char smem[phi_rows_lds<D, NW, TABN>()];
+    phi_rows_body<D, R, NW, TABN, WC>(smem, blockIdx.x, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
+                                      nmax_bits);
 }
 
 // ==================================================== symmetric phi pass ==
@@ -2757,17 +2777,42 @@ __device__ __forceinline__ void sym_phases(const char *cb, int grp, int tl, int 
     }
 }
 
+// The row stream's hand-over (symok = 0): its 8-wave work-groups (grid of
+// them: row groups of 256 rows x S column splits) over the rank's rows,
+// partials into part (S x ldp x (d+1)).
+struct SymRows {
+    const double *rec;
+    int64_t row0, nrows, n;
+    int S;
+    int64_t grid;
+    double *part;
+    int64_t ldp;
+    const unsigned long long *nmax;
+};
+
 template <int D>
 __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_phi_sym(
     const double *__restrict__ srec, const double *__restrict__ a_ptr, int64_t nb, int64_t U0, int64_t U1,
     const int *__restrict__ symok, double *__restrict__ rowpart, const int *__restrict__ blkg,
-    const int *__restrict__ rbase, double *__restrict__ colpart, int64_t SM)
+    const int *__restrict__ rbase, double *__restrict__ colpart, int64_t SM, SymRows fr)
 {
     using Gm = SymGeom<D>;
     constexpr int R = Gm::R, B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP,
                   SUBB = Gm::SUBB, NP = SUBB / 1024, NT = SYM_NW * 64;
     __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
-    if (!*symok) return; // uniform: the row stream runs instead
+    if (!*symok) {
+        // uniform: the symmetric form would leave its exponent range, the
+        // row stream takes the step in this launch (its work-groups looped
+        // over this grid; the same code, LDS and partials as k_phi_rows)
+        static_assert(T8K_NW == SYM_NW && phi_rows_lds<D, T8K_NW, 8192>() <= Gm::LDS,
+                      "the row stream's work-group must fit the symmetric pass's");
+        for (int64_t b = blockIdx.x; b < fr.grid; b += gridDim.x) {
+            phi_rows_body<D, 4, T8K_NW, 8192, T8K_WC>(smem, b, fr.rec, a_ptr, fr.row0, fr.nrows, fr.n, fr.S,
+                                                      fr.part, fr.ldp, nullptr, fr.nmax);
+            __syncthreads(); // (the next work-group's table fill reuses the LDS)
+        }
+        return;
+    }
     double *tab = reinterpret_cast<double *>(smem + 2 * SUBB);
     double *sCol = tab + 8192; // [2][SYM_NW][SYM_SUB][DP]: sub-tile u's column sums in buffer u & 1
     constexpr int SCOL = Gm::SCOL;
@@ -4217,13 +4262,13 @@ __global__ __launch_bounds__(256) void k_gauss_grad(const double *__restrict__ X
     case Dv:                                                                                 \
         if (kind == 0 && R == 1)                                                             \
             hipLaunchKernelGGL((k_phi_rows<Dv, 1>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);         \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
         else if (kind == 0 && R == 2)                                                        \
             hipLaunchKernelGGL((k_phi_rows<Dv, 2>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);         \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
         else if (kind == 0)                                                                  \
             hipLaunchKernelGGL((k_phi_rows<Dv, 4>), dim3(grid), dim3(256), 0, stream,   \
-                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);         \
+                               rec, a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);               \
         else if (kind == 10)                                                                 \
             hipLaunchKernelGGL((k_pair_rows<Dv, 0>), dim3(grid), dim3(256), 0, stream, xc, KP, \
                                nrm, n, nb, t0, t1, sc, sh, sd);                              \
@@ -4240,8 +4285,7 @@ static hipError_t launch_rows_kernel(int kind, int D, int R, int grid, const dou
                                      int S, double *part, int64_t ldp, const double *sgn,
                                      const unsigned long long *nmax, const double *xc, int KP,
                                      const double *nrm, int64_t nb, int64_t t0, int64_t t1,
-                                     SinkCollect sc, SinkHist sh, SinkDebug sd, hipStream_t stream,
-                                     const int *skip = nullptr)
+                                     SinkCollect sc, SinkHist sh, SinkDebug sd, hipStream_t stream)
 {
     switch (D) {
         SVGD_ROWS_CASE(1)
@@ -4280,19 +4324,18 @@ hipError_t launch_prep_rec(const double *xc, const double *G, const double *nrm,
 // kind 2: k_phi_rows with 8 waves, the 8192-entry table and the columns split
 // over the 8 waves (WC = 8: one 64 R-row group per work-group); R = 4 for
 // d <= 8, 2 above (the register budget)
-constexpr int T8K_NW = 8, T8K_WC = 8;
 bool phi_rows_t8k_supported(int d, int R) { return d >= 1 && d <= 16 && R == (d <= 8 ? 4 : 2); }
 int phi_rows_t8k_rows(int R) { return (T8K_NW / T8K_WC) * 64 * R; }
 #define SVGD_T8K_KERNEL(Dv) k_phi_rows<Dv, ((Dv) <= 8 ? 4 : 2), T8K_NW, 8192, T8K_WC>
 #define SVGD_T8K_CASE(Dv)                                                                       \
     case Dv:                                                                                    \
         hipLaunchKernelGGL((SVGD_T8K_KERNEL(Dv)), dim3(grid), dim3(T8K_NW * 64), 0, stream, rec, \
-                           a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax, skip);               \
+                           a_ptr, row0, nrows, n, S, part, ldp, sgn, nmax);                     \
         break;
 static hipError_t launch_rows_t8k(int d, int grid, const double *rec, const double *a_ptr,
                                   int64_t row0, int64_t nrows, int64_t n, int S, double *part,
                                   int64_t ldp, const double *sgn, const unsigned long long *nmax,
-                                  hipStream_t stream, const int *skip)
+                                  hipStream_t stream)
 {
     switch (d) {
         SVGD_T8K_CASE(1) SVGD_T8K_CASE(2) SVGD_T8K_CASE(3) SVGD_T8K_CASE(4)
@@ -4318,10 +4361,10 @@ hipError_t launch_phi_rows(int d, int R, const double *rec, const double *a_ptr,
     const int rows_wg = kind == 2 ? phi_rows_t8k_rows(R) : 256 * R;
     const int grid = (int)(((nrows + rows_wg - 1) / rows_wg) * S);
     hipError_t e = kind == 2 ? launch_rows_t8k(d, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
-                                               nmax_bits, stream, skip)
+                                               nmax_bits, stream)
                              : launch_rows_kernel(0, d, R, grid, rec, a_ptr, row0, nrows, n, S, part, ldp, sgn,
                                       nmax_bits, nullptr, 0, nullptr, 0, 0, 0, SinkCollect{}, SinkHist{},
-                                      SinkDebug{}, stream, skip);
+                                      SinkDebug{}, stream);
     if (e != hipSuccess) return e;
     if (ev_mid && (e = hipEventRecord(ev_mid, stream)) != hipSuccess) return e;
     if (!reduce) return hipSuccess;
@@ -4971,8 +5014,11 @@ int phi_sym_blocks_per_cu(int d)
                            a.nrm, a.a_ptr, a.nmax, a.n, npad, a.srec, a.symok, a.rec, a.RS);  \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k0 && (e = hipEventRecord(ev_k0, stream)) != hipSuccess) return e;             \
+        const SymRows fr{a.rec, a.row0, a.nrows, a.n, a.fS,                                   \
+                         ((a.nrows + phi_rows_t8k_rows(4) - 1) / phi_rows_t8k_rows(4)) * a.fS,  \
+                         a.fpart, a.fldp, a.nmax};                                            \
         hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(SYM_NW * 64), 0, stream, a.srec, a.a_ptr, \
-                           a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.blkg, a.rbase, a.colpart, a.SM); \
+                           a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.blkg, a.rbase, a.colpart, a.SM, fr); \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k1 && (e = hipEventRecord(ev_k1, stream)) != hipSuccess) return e;             \
         return hipSuccess;                                                                    \

@@ -42,6 +42,14 @@ def run(rank, world, name, n, d, steps, q, env=None):
         shard = (ctx.row0, ctx.row1)
         diag = dict(ctx.diagnostics())
         diag["phi_kernel"] = ctx.phi_kernel_name()
+        if os.environ.get("TEST_PHI_CHECK"):
+            # one more sharded phi of X_T (this rank's rows): scale, the
+            # all-gather of G and the phi exchange, against the oracle in the test
+            G = model.log_model_grad(X[shard[0]:shard[1]])
+            a, _ = ctx.median_scale()
+            diag["phi_rows"] = ctx.phi(G, a)
+            diag["phi_a"] = a
+            diag["phi_kernel_check"] = ctx.phi_kernel_name()
         ctx.close()
         q.put(("ok", rank, X, scales, shard, diag))
     except Exception:

@@ -499,6 +499,22 @@ static void TestGenericKernelHostPath()
         SVGD s(2, 1, xs, plain, model, opt, true);
         s.Initialize();
         CHECK(Throws<UnsetException>([&] { s.Run(); }));
+        // the sharding options belong to the device path: a generic kernel
+        // with World > 1 or a unique id is refused, not silently unsharded
+        SVGDOptions o;
+        o.Dimension = 2;
+        o.NumIterations = 1;
+        o.CoordinateMatrixPtr = xs;
+        o.KernelPtr = std::make_shared<Kernel>(*UnitRBF(2) + *UnitRBF(2));
+        o.ModelPtr = model;
+        o.OptimizerPtr = opt;
+        o.World = 2;
+        o.Rank = 1;
+        CHECK(Throws<std::invalid_argument>([&] { SVGD bad(o); }));
+        o.World = 1;
+        o.Rank = 0;
+        o.UniqueId.assign(128, 0);
+        CHECK(Throws<std::invalid_argument>([&] { SVGD bad(o); }));
     }
 }
 
@@ -595,6 +611,26 @@ public:
     Eigen::VectorXd EvaluateModelGrad(const Eigen::VectorXd &x) override { return Eigen::Vector2d(2.0 * x(0), 0.0); }
 };
 
+// a derived model that only sets its functions with UpdateModel in its
+// constructor (no overrides): slicing it to a base Model keeps them, so it
+// composes without a CloneSharedPointer override
+class SetFunQuad : public Model
+{
+public:
+    SetFunQuad() : Model(2)
+    {
+        using P = std::vector<Eigen::MatrixXd>;
+        UpdateModel([](const Eigen::VectorXd &x, const P &) { return 2.0 + x(1) * x(1); },
+                    [](const Eigen::VectorXd &x, const P &) { return Eigen::VectorXd(Eigen::Vector2d(0.0, 2.0 * x(1))); },
+                    [](const Eigen::VectorXd &, const P &)
+                    {
+                        Eigen::MatrixXd H = Eigen::MatrixXd::Zero(2, 2);
+                        H(1, 1) = 2.0;
+                        return H;
+                    });
+    }
+};
+
 // grad (and Hessian) of m at x against central differences of the level below
 static void CheckDerivatives(Model &m, const Eigen::VectorXd &x, bool hess)
 {
@@ -687,6 +723,16 @@ static void TestModelComposition()
     NoCloneQuad ncq;
     CHECK(Throws<std::invalid_argument>([&] { Model bad = ncq + lin; }));
     CHECK(Throws<std::invalid_argument>([&] { Model bad = lin * ncq; }));
+    {
+        SetFunQuad sfq;
+        Model ok1 = sfq + lin, ok2 = lin * sfq;
+        ok1.Initialize();
+        ok2.Initialize();
+        const double fv = 2.0 + xl(1) * xl(1);
+        CHECK(std::fabs(ok1.EvaluateModel(xl) - (fv + lv)) < 1e-14);
+        CHECK(std::fabs(ok2.EvaluateModel(xl) - lv * fv) < 1e-14);
+        CheckDerivatives(ok1, xl, true);
+    }
     Eigen::Matrix2d cov;
     cov << 1.2, 0.3, 0.3, 0.8;
     MultivariateNormal mvn(Eigen::Vector2d(0.2, -0.1), cov);
