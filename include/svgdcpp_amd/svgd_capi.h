@@ -327,6 +327,16 @@ void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
  * reference's ComputePhi, SVGD.hpp:407-454, for d <= 8.) */
 int64_t svgd_plan_sym_units(int64_t n, int block, int nsub, int world, int rank, int grid,
                             int64_t *u0, int64_t *u1, int *blkg, int *rbase, int64_t *Ia, int64_t *Ib);
+/* The sharded symmetric pass's exchange (replaces the parallel branch of
+ * SVGD.hpp:410-432): the rows [*r0, *r1) of rank dst's shard (svgd_plan_rows)
+ * that rank src's units can add to -- the row blocks its units span and the
+ * column blocks they pair with (at most (nb - 1) / 2 + 1 ahead, cyclic),
+ * intersected with dst's rows (the hull of at most two pieces; *r0 == *r1:
+ * none).  src sends exactly this range of its per-particle sums to dst, dst
+ * receives it from src; the two sides compute the same range.  src == dst:
+ * the rank's own rows it contributes to. */
+void svgd_plan_sym_exchange(int64_t n, int block, int nsub, int world, int src, int dst, int64_t *r0,
+                            int64_t *r1);
 /* Median bucket select: from the all-reduced histogram of candidate keys in
  * `nb` ascending key-range buckets, the bucket holding each of the `nsel`
  * (1 or 2) candidate ranks, the rank inside it, and the total count of the

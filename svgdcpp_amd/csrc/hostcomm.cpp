@@ -157,27 +157,66 @@ template <class T> static int allreduce_sum(HostComm *c, T *dbuf, size_t cnt, hi
     return c->barrier();
 }
 
-// In-place reduce-scatter (sum) of `cnt` doubles per rank, ncclReduceScatter's
-// in-place contract: dbuf holds world x cnt, rank r receives the sums of
-// chunk r at dbuf + r * cnt (added in rank order).  Every OTHER chunk of dbuf
-// is overwritten with NaN afterwards: RCCL leaves it undefined, so a caller
-// that reads outside its chunk (a wrong offset) fails here too.
-int hostcomm_reduce_scatter_f64(HostComm *c, double *dbuf, size_t cnt, hipStream_t stream)
+// Grouped point-to-point exchange (ncclSend / ncclRecv of one group): rank r
+// sends rows [send[2q], send[2q+1]) of dsend (w doubles per row; n rows) to
+// each rank q, and receives from each rank q the rows [recv[3q], recv[3q+1])
+// into drecv + recv[3q+2] * w.  Faithful to what a peer can see: the slot's
+// data is NaN except the ranges this rank sends, every sender's ranges are
+// published in its slot's header and a receiver whose expected range differs
+// fails (-4); drecv is NaN-filled before the pieces land, and dsend's rows
+// outside [own0, own1) come back as NaN (the caller may read its own rows
+// only).  Returns 0 on success.
+int hostcomm_exchange_f64(HostComm *c, double *dsend, size_t n, size_t w, const int64_t *send,
+                          double *drecv, size_t recv_rows, const int64_t *recv, int64_t own0, int64_t own1,
+                          hipStream_t stream)
 {
-    const size_t all = cnt * (size_t)c->world * sizeof(double), bytes = cnt * sizeof(double);
-    if (all > c->slot) return -2;
+    const size_t hdr = (size_t)c->world * 2 * sizeof(int64_t), data = n * w * sizeof(double);
+    if (hdr + data > c->slot) return -2;
     if (hipStreamSynchronize(stream) != hipSuccess) return -3;
-    if (hipMemcpy(c->slot_ptr(c->rank), dbuf, all, hipMemcpyDeviceToHost) != hipSuccess) return -3;
-    if (c->barrier()) return -1;
-    c->tmp.assign(bytes, 0);
-    double *acc = reinterpret_cast<double *>(c->tmp.data());
-    for (int r = 0; r < c->world; ++r) {
-        const double *v = reinterpret_cast<const double *>(c->slot_ptr(r)) + (size_t)c->rank * cnt;
-        for (size_t i = 0; i < cnt; ++i) acc[i] += v[i];
+    char *mine = c->slot_ptr(c->rank);
+    std::memcpy(mine, send, hdr);
+    double *md = reinterpret_cast<double *>(mine + hdr);
+    std::memset(md, 0xff, data);
+    for (int q = 0; q < c->world; ++q) {
+        const int64_t a = send[2 * q], b = send[2 * q + 1];
+        if (q != c->rank && b > a &&
+            hipMemcpy(md + (size_t)a * w, dsend + (size_t)a * w, (size_t)(b - a) * w * sizeof(double),
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            return -3;
     }
-    if (hipMemset(dbuf, 0xff, all) != hipSuccess) return -3; // all-ones bits: NaN
-    if (hipMemcpy(dbuf + (size_t)c->rank * cnt, acc, bytes, hipMemcpyHostToDevice) != hipSuccess) return -3;
-    return c->barrier();
+    if (c->barrier()) return -1;
+    int rc = 0;
+    // (stream-ordered fills: a plain hipMemset may still run when the
+    // stream's next kernel starts)
+    if (recv_rows && (hipMemsetAsync(drecv, 0xff, recv_rows * w * sizeof(double), stream) != hipSuccess ||
+                      hipStreamSynchronize(stream) != hipSuccess))
+        rc = -3;
+    for (int q = 0; q < c->world && !rc; ++q) {
+        const int64_t a = recv[3 * q], b = recv[3 * q + 1], off = recv[3 * q + 2];
+        if (q == c->rank) continue;
+        const int64_t *ph = reinterpret_cast<const int64_t *>(c->slot_ptr(q));
+        const int64_t pa = ph[2 * c->rank], pb = ph[2 * c->rank + 1];
+        const bool sent = pb > pa, expected = b > a;
+        if (sent != expected || (sent && (pa != a || pb != b))) {
+            rc = -4; // the sender's range for this rank is not the one expected
+            break;
+        }
+        if (b > a) {
+            const double *src = reinterpret_cast<const double *>(c->slot_ptr(q) + hdr) + (size_t)a * w;
+            if (hipMemcpy(drecv + (size_t)off * w, src, (size_t)(b - a) * w * sizeof(double),
+                          hipMemcpyHostToDevice) != hipSuccess)
+                rc = -3;
+        }
+    }
+    // the send buffer outside the rank's own rows: undefined for the caller
+    if (!rc && own0 > 0 && hipMemsetAsync(dsend, 0xff, (size_t)own0 * w * sizeof(double), stream) != hipSuccess)
+        rc = -3;
+    if (!rc && (size_t)own1 < n &&
+        hipMemsetAsync(dsend + (size_t)own1 * w, 0xff, (n - (size_t)own1) * w * sizeof(double), stream) !=
+            hipSuccess)
+        rc = -3;
+    const int brc = c->barrier();
+    return rc ? rc : brc;
 }
 
 int hostcomm_allreduce_u32(HostComm *c, uint32_t *dbuf, size_t cnt, hipStream_t stream)

@@ -128,6 +128,48 @@ int64_t svgd_plan_sym_units(int64_t n, int block, int nsub, int world, int rank,
     return nrec;
 }
 
+// The particles rank src's symmetric-pass units add to: a cyclic run of
+// blocks from its first row block Ia through Ib + the largest slot (SM - 1 =
+// (nb - 1) / 2 + 1, the even-nb extra slot included: a hull), intersected
+// with dst's rows.
+void svgd_plan_sym_exchange(int64_t n, int block, int nsub, int world, int src, int dst, int64_t *r0,
+                            int64_t *r1)
+{
+    if (world < 1) world = 1;
+    int64_t d0, d1;
+    svgd_plan_rows(n, world, dst, &d0, &d1);
+    *r0 = *r1 = d0;
+    const int64_t nb = (n + block - 1) / block;
+    const int64_t U = tiles_total(nb) * nsub;
+    const int64_t u0 = U * src / world, u1 = U * (src + 1) / world;
+    if (u1 <= u0 || d1 <= d0) return;
+    int64_t Ia, Ib, J;
+    svgd_plan_pair_tile(n, block, 1, 0, u0 / nsub, &Ia, &J);
+    svgd_plan_pair_tile(n, block, 1, 0, (u1 - 1) / nsub, &Ib, &J);
+    const int64_t len = Ib - Ia + 1 + (nb - 1) / 2 + 1; // blocks Ia .. Ib + SM - 1
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    auto meet = [&](int64_t a, int64_t b) { // particles [a, b) against dst's rows
+        a = a > d0 ? a : d0;
+        b = b < d1 ? b : d1;
+        if (a < b) {
+            lo = a < lo ? a : lo;
+            hi = b > hi ? b : hi;
+        }
+    };
+    if (len >= nb) {
+        meet(0, n);
+    } else if (Ia + len <= nb) {
+        meet(Ia * block, (Ia + len) * block < n ? (Ia + len) * block : n);
+    } else {
+        meet(Ia * block, n);
+        meet(0, (Ia + len - nb) * block);
+    }
+    if (lo < hi) {
+        *r0 = lo;
+        *r1 = hi;
+    }
+}
+
 // Bucket of each selection from the all-reduced key-range bucket counts
 // (NBK buckets, ascending key order): ranks[s] is the rank among the
 // candidates; writes the bucket and the rank within it, and the total count

@@ -208,7 +208,15 @@ struct svgd_ctx {
     int sym_fS = 1; // the row stream's column splits when it takes the step (symok = 0)
     int64_t sym_SM = 0, sym_Ia = 0, sym_Ib = 0; // colpart slots per column block; units' row-block span
     double *srec = nullptr, *rowpart = nullptr, *colpart = nullptr;
-    double *contrib = nullptr; // P > 1: every particle's sums from this rank's units (reduce-scattered)
+    double *contrib = nullptr; // P > 1: every particle's sums from this rank's units (exchanged)
+    // P > 1 over a communicator: the point-to-point exchange of those sums
+    // (svgd_plan_sym_exchange): per rank q the rows [xsend[2q], xsend[2q+1])
+    // sent to q, the rows [xrecv[3q], xrecv[3q+1]) of this rank received from
+    // q into xrecv_buf + xrecv[3q+2] rows (xtab_d: xrecv on the device)
+    std::vector<int64_t> xsend, xrecv;
+    int64_t xrecv_rows = 0;
+    double *xrecv_buf = nullptr;
+    int64_t *xtab_d = nullptr;
     int *sym_tab = nullptr;    // the symmetric pass's row-block tables (SymArgs::blkg | rbase)
     int *symok = nullptr;
     int64_t ldp = 0;
@@ -533,7 +541,7 @@ void diag_end(svgd_ctx *c, hipStream_t s, hipEvent_t a, int kind, bool own_a = t
 
 // Every collective this rank issues goes into the step's sequence hash (the
 // SVGD_DEBUG_COLL cross-rank check of the issue-order invariant, svgd_ctx).
-enum { CO_GATHER_ROWS = 1, CO_REDUCE_U64 = 2, CO_GATHER_U64 = 3, CO_REDUCE_F64 = 4, CO_RS_ROWS = 5, CO_GCOMM = 16 };
+enum { CO_GATHER_ROWS = 1, CO_REDUCE_U64 = 2, CO_GATHER_U64 = 3, CO_REDUCE_F64 = 4, CO_XCHG = 6, CO_GCOMM = 16 };
 void coll_note(svgd_ctx *c, int op, size_t cnt)
 {
     uint64_t h = c->coll_sig ? c->coll_sig : 0xcbf29ce484222325ull;
@@ -606,24 +614,39 @@ int allgather_u64(svgd_ctx *c, uint64_t *buf, size_t cnt)
     return SVGD_OK;
 }
 
-// In-place reduce-scatter (sum) of `w` doubles per row: buf holds world x
-// chunk rows, rank r gets the sums of its chunk at buf + r * chunk * w.  The
-// host-shm rehearsal path is a true reduce-scatter: the other chunks come
-// back as NaN (RCCL leaves them undefined), so a read outside the rank's
-// chunk fails the multi-rank tests.
-int reduce_scatter_rows(svgd_ctx *c, double *buf, size_t w)
+// The sharded symmetric pass's exchange (the parallel branch of
+// SVGD.hpp:410-432): one group of point-to-point sends and receives -- to
+// each rank the range of its rows this rank's units touched, from each rank
+// the range of this rank's rows its units touched (svgd_plan_sym_exchange;
+// at P = 8, cfg3: ~2.5 MB per rank to ~5 peers over their direct links,
+// against 4.1 MB per GPU in 7 ring steps for a reduce-scatter of all N
+// sums).  k_sym_apply adds the pieces in rank order.  The host-shm
+// rehearsal backend runs the same plan, and a receiver sees only what its
+// senders sent (NaN elsewhere).
+int sym_exchange(svgd_ctx *c)
 {
     if (!c->comm && !c->hcomm) return SVGD_OK; // one rank / simulated world: no exchange
     c->mark = c->phi_end = nullptr;
-    const size_t cnt = (size_t)c->chunk * w;
-    coll_note(c, CO_RS_ROWS, cnt);
+    const size_t w = (size_t)c->dim + 1;
+    coll_note(c, CO_XCHG, (size_t)c->n * w); // (the pieces differ by rank; the call is the same)
     hipEvent_t d0 = diag_begin(c, c->stream);
     if (c->hcomm) {
-        if (hostcomm_reduce_scatter_f64(c->hcomm, buf, cnt, c->stream))
-            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host reduce-scatter failed.");
+        if (hostcomm_exchange_f64(c->hcomm, c->contrib, (size_t)c->n, w, c->xsend.data(), c->xrecv_buf,
+                                  (size_t)c->xrecv_rows, c->xrecv.data(), c->row0, c->row0 + c->nrows,
+                                  c->stream))
+            return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host point-to-point exchange failed.");
     } else {
-        NCCLCHK(c, ncclReduceScatter(buf, buf + (size_t)c->rank * cnt, cnt, ncclDouble, ncclSum, c->comm,
-                                     c->stream));
+        NCCLCHK(c, ncclGroupStart());
+        for (int q = 0; q < c->world; ++q) {
+            if (q == c->rank) continue;
+            const int64_t a = c->xsend[2 * q], b = c->xsend[2 * q + 1];
+            if (b > a) NCCLCHK(c, ncclSend(c->contrib + a * w, (size_t)(b - a) * w, ncclDouble, q, c->comm, c->stream));
+            const int64_t ra = c->xrecv[3 * q], rb = c->xrecv[3 * q + 1], off = c->xrecv[3 * q + 2];
+            if (rb > ra)
+                NCCLCHK(c, ncclRecv(c->xrecv_buf + off * w, (size_t)(rb - ra) * w, ncclDouble, q, c->comm,
+                                    c->stream));
+        }
+        NCCLCHK(c, ncclGroupEnd());
     }
     diag_end(c, c->stream, d0, DG_COLL);
     return SVGD_OK;
@@ -1400,8 +1423,9 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
         if (c->contrib) {
             // every rank's sums of its rows (issued whether or not symok: the
             // ranks' collective sequences must not depend on device data)
-            CHK(reduce_scatter_rows(c, c->contrib, (size_t)(c->dim + 1)));
-            HIPCHK(c, launch_sym_apply(sa, c->contrib + (size_t)c->row0 * (c->dim + 1), opt, c->stream));
+            CHK(sym_exchange(c));
+            HIPCHK(c, launch_sym_apply(sa, c->contrib + (size_t)c->row0 * (c->dim + 1), c->xrecv_buf, c->xtab_d,
+                                       c->xtab_d ? c->world : 1, c->xtab_d ? c->rank : 0, opt, c->stream));
         }
     } else if (c->rowpath && split) {
         // two row halves: the first half's X_{t+1} is final at ev_xhalf, while
@@ -1888,6 +1912,28 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             CHK(dalloc(c, &c->colpart, nbs * c->sym_SM * B * (dim + 1)));
             CHK(dalloc(c, &c->symok, 1));
             if (Pw > 1 || sym_env == 2) CHK(dalloc(c, &c->contrib, std::max<int64_t>(c->np, c->world * c->chunk) * (dim + 1)));
+            if (c->world > 1) {
+                // the exchange plan: the same ranges on both sides of every pair of ranks
+                c->xsend.assign(2 * (size_t)c->world, 0);
+                c->xrecv.assign(3 * (size_t)c->world, 0);
+                for (int q = 0; q < c->world; ++q) {
+                    int64_t a, b;
+                    svgd_plan_sym_exchange(n, (int)B, c->symNSUB, c->world, c->rank, q, &a, &b);
+                    c->xsend[2 * q] = a;
+                    c->xsend[2 * q + 1] = q == c->rank ? a : b; // (its own rows: not sent)
+                    svgd_plan_sym_exchange(n, (int)B, c->symNSUB, c->world, q, c->rank, &a, &b);
+                    if (q != c->rank && b > a) {
+                        c->xrecv[3 * q] = a;
+                        c->xrecv[3 * q + 1] = b;
+                        c->xrecv[3 * q + 2] = c->xrecv_rows;
+                        c->xrecv_rows += b - a;
+                    }
+                }
+                CHK(dalloc(c, &c->xrecv_buf, std::max<int64_t>(1, c->xrecv_rows) * (dim + 1)));
+                HIPCHK(c, hipMalloc((void **)&c->xtab_d, c->xrecv.size() * sizeof(int64_t)));
+                HIPCHK(c, hipMemcpy(c->xtab_d, c->xrecv.data(), c->xrecv.size() * sizeof(int64_t),
+                                    hipMemcpyHostToDevice));
+            }
             c->sym = true;
         }
         // the centring fold (svgd_ctx::cpart)
@@ -2059,7 +2105,9 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
                 std::max<size_t>((size_t)c->chunk * c->dim, (size_t)c->dim * c->dim) * sizeof(double),
                 2 * RADIX * sizeof(unsigned long long)),
             std::max<size_t>((CAPG + 1) * sizeof(uint64_t), (3 + NBK) * sizeof(uint64_t)));
-        const size_t slot_rs = c->contrib ? (size_t)world * c->chunk * (c->dim + 1) * sizeof(double) : 0;
+        const size_t slot_rs = c->contrib ? 2 * sizeof(int64_t) * (size_t)world +
+                                                (size_t)c->n * (c->dim + 1) * sizeof(double)
+                                          : 0;
         if (hostcomm_create(&c->hcomm, std::getenv("SVGD_HOSTCOMM"), world, rank, std::max(slot, slot_rs)))
             return fail(c, SVGD_ERR_RCCL, "[RCCL Error] host communicator setup failed.");
         return SVGD_OK;
@@ -2111,7 +2159,8 @@ int svgd_destroy(svgd_ctx *c)
     double *dbufs[] = {c->X,     c->G,     c->xc,      c->nrm,  c->cvec, c->V,   c->phi,
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
-                       c->sc_sgn,  c->sc_work, c->bak, c->srec, c->rowpart, c->colpart, c->contrib};
+                       c->sc_sgn,  c->sc_work, c->bak, c->srec, c->rowpart, c->colpart, c->contrib,
+                       c->xrecv_buf};
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf, c->XS, c->VS};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);
@@ -2122,7 +2171,7 @@ int svgd_destroy(svgd_ctx *c)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
                      c->xf,          c->nmax,    c->sc_err, c->cbuf, c->ccount, c->d_status,
-                     c->bpart,       c->gseg, c->symok, c->sym_tab};
+                     c->bpart,       c->gseg, c->symok, c->sym_tab, c->xtab_d};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_xm, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk};

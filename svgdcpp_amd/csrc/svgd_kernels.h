@@ -250,7 +250,7 @@ struct SymArgs {
     double *rec; // the row stream's records, written by the record prep when symok = 0
     int RS;
     // P > 1: the finish writes every particle's sums from this rank's units
-    // here (n x (d+1), the reduce-scatter's input) instead of phi
+    // here (n x (d+1), the exchange's send buffer) instead of phi
     double *contrib = nullptr;
     // row-block tables: blkg[2P], blkg[2P+1] = the work-groups whose units
     // meet row block P (g1 < g0: none), rbase[P] = the first rowpart record of P
@@ -262,10 +262,12 @@ struct SymArgs {
     int fS = 0;
     int64_t fldp = 0;
 };
-// P > 1: phi + the optimizer for rows [row0, row0 + nrows) from S (their
-// reduce-scattered sums, nrows x (d+1)), or from the row stream's partials
-// when symok = 0
-hipError_t launch_sym_apply(const SymArgs &a, const double *S, const OptArgs *opt, hipStream_t stream);
+// P > 1: phi + the optimizer for rows [row0, row0 + nrows) from their sums:
+// own (this rank's, nrows x (d+1)) and the pieces received from the other
+// ranks (xtab: world x {t0, t1, row offset in recv}), added in rank order --
+// or from the row stream's partials when symok = 0.  world = 1: own alone.
+hipError_t launch_sym_apply(const SymArgs &a, const double *own, const double *recv, const int64_t *xtab,
+                            int world, int rank, const OptArgs *opt, hipStream_t stream);
 bool phi_sym_supported(int d);
 bool phi_sym_geom(int d, int *B, int *SRS, int *NSUB);
 int phi_sym_blocks_per_cu(int d);

@@ -3104,12 +3104,16 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
     }
 }
 
-// P > 1: phi and the optimizer for this rank's rows from S (the
-// reduce-scattered sums of every rank's contributions, nrows x DP), or from
+// P > 1: phi and the optimizer for this rank's rows from the sums of every
+// rank's contributions, added in rank order: this rank's own (own, nrows x
+// DP) and the pieces received from the others (xtab: per rank q its rows
+// [t0, t1) at recv + off rows, t1 <= t0: none; q == rank: own) -- or from
 // the row stream's partials when it took the step (symok = 0); the finish's
 // block geometry.
 template <int D>
-__global__ __launch_bounds__(256) void k_sym_apply(const double *__restrict__ S, const double *__restrict__ srec,
+__global__ __launch_bounds__(256) void k_sym_apply(const double *__restrict__ own, const double *__restrict__ recv,
+                                                   const int64_t *__restrict__ xtab, int world, int rank,
+                                                   const double *__restrict__ srec,
                                                    const double *__restrict__ a_ptr,
                                                    const int *__restrict__ symok, int64_t row0, int64_t nrows,
                                                    double inv_n, double *__restrict__ phi, OptArgs opt,
@@ -3123,7 +3127,24 @@ __global__ __launch_bounds__(256) void k_sym_apply(const double *__restrict__ S,
     const int rows = (int)min<int64_t>(RB, nrows - rb);
     if (rows <= 0) return;
     const int e = threadIdx.x;
-    if (e < rows * DP) sm[e] = ok ? S[rb * DP + e] : sym_fb_sum<D>(fb, rb, e);
+    if (e < rows * DP) {
+        if (ok) {
+            const int pl = e / DP, k = e - pl * DP;
+            const int64_t p = row0 + rb + pl;
+            double v = 0.0;
+            for (int q = 0; q < world; ++q) {
+                if (q == rank) {
+                    v += own[rb * DP + e];
+                } else {
+                    const int64_t t0 = xtab[3 * q], t1 = xtab[3 * q + 1];
+                    if (p >= t0 && p < t1) v += recv[(xtab[3 * q + 2] + (p - t0)) * DP + k];
+                }
+            }
+            sm[e] = v;
+        } else {
+            sm[e] = sym_fb_sum<D>(fb, rb, e);
+        }
+    }
     __syncthreads();
     if (!ok) {
         sym_fb_phi<D>(fb, sm, rb, rows, row0, inv_n, *a_ptr, phi, opt, do_opt);
@@ -5040,7 +5061,8 @@ int phi_sym_blocks_per_cu(int d)
     case Dv: {                                                                                \
         constexpr int RB = 256 / SymGeom<Dv>::DP;                                             \
         hipLaunchKernelGGL((k_sym_apply<Dv>), dim3((a.nrows + RB - 1) / RB), dim3(256), 0,     \
-                           stream, S, a.srec, a.a_ptr, a.symok, a.row0, a.nrows, a.inv_n,      \
+                           stream, own, recv, xtab, world, rank, a.srec, a.a_ptr, a.symok,     \
+                           a.row0, a.nrows, a.inv_n,                                           \
                            a.phi, opt ? *opt : OptArgs{}, opt ? 1 : 0, fb);                   \
         return hipGetLastError();                                                             \
     }
@@ -5050,8 +5072,10 @@ static SymFallback sym_fallback(const SymArgs &a)
     return SymFallback{a.fpart, a.fS, a.fldp, a.rec, a.RS};
 }
 
-hipError_t launch_sym_apply(const SymArgs &a, const double *S, const OptArgs *opt, hipStream_t stream)
+hipError_t launch_sym_apply(const SymArgs &a, const double *own, const double *recv, const int64_t *xtab,
+                            int world, int rank, const OptArgs *opt, hipStream_t stream)
 {
+    if (world > 1 && !xtab) return hipErrorInvalidValue;
     if (a.nrows <= 0) return hipSuccess;
     const SymFallback fb = sym_fallback(a);
     switch (a.d) {

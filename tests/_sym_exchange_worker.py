@@ -3,9 +3,12 @@ pass's protocol (svgd_capi.cpp run_phi, DESIGN §4.1 "Sharded") with gloo in
 place of RCCL and numpy as the arithmetic.  Rank r takes the (tile, 64-column
 sub-tile) units svgd_plan_sym_units gives it, adds every unit's pair terms
 to BOTH particles (row side; column side off the diagonal tiles, whose row
-side already holds every ordered pair of the square), then the per-particle
-sums are reduce-scattered (here an all-reduce, as the host-shm backend does)
-and phi is formed for the rank's rows (svgd_plan_rows)."""
+side already holds every ordered pair of the square), then the point-to-point
+exchange of svgd_plan_sym_exchange: rank r sends each peer q the range of q's
+rows its units touch and receives from each peer the range of its own rows
+that peer touches (every particle sum outside the planned ranges must be
+exactly zero), adds the pieces in rank order and forms phi for its rows
+(svgd_plan_rows)."""
 import ctypes
 import os
 import sys
@@ -59,15 +62,48 @@ def run(rank, world, port, n, d, block, a, q):
                 pairs += rows.size * cols.size
             else:
                 pairs += rows.size * cols.size  # ordered pairs of the square's columns (incl. i = j)
-        tot = torch.from_numpy(S)
-        dist.all_reduce(tot)  # the reduce-scatter's sums (every rank keeps its rows below)
-        pc = torch.tensor([pairs], dtype=torch.int64)
-        dist.all_reduce(pc)
+        def plan(src, dst):
+            a0, a1 = ctypes.c_int64(), ctypes.c_int64()
+            lib.svgd_plan_sym_exchange(n, block, nsub, world, src, dst, ctypes.byref(a0), ctypes.byref(a1))
+            return a0.value, a1.value
+
+        # every particle this rank's units add to lies in a planned range
+        covered = np.zeros(n, dtype=bool)
+        for dst in range(world):
+            a0, a1 = plan(rank, dst)
+            covered[a0:a1] = True
+        assert not np.any(S[~covered]), "a contribution outside the planned exchange ranges"
         r0, r1 = ctypes.c_int64(), ctypes.c_int64()
         lib.svgd_plan_rows(n, world, rank, ctypes.byref(r0), ctypes.byref(r1))
-        phi = tot.numpy()[r0.value:r1.value] / n
+        r0, r1 = r0.value, r1.value
+        # grouped point-to-point: the sends and receives of one step, then the
+        # pieces added in rank order (k_sym_apply's order)
+        reqs, pieces = [], {}
+        for q_ in range(world):
+            if q_ == rank:
+                continue
+            a0, a1 = plan(rank, q_)
+            if a1 > a0:
+                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(S[a0:a1])), q_))
+            b0, b1 = plan(q_, rank)
+            if b1 > b0:
+                buf = torch.empty((b1 - b0, d), dtype=torch.float64)
+                reqs.append(dist.irecv(buf, q_))
+                pieces[q_] = (b0, buf)
+        for rq in reqs:
+            rq.wait()
+        tot = np.zeros((r1 - r0, d))
+        for q_ in range(world):
+            if q_ == rank:
+                tot += S[r0:r1]
+            elif q_ in pieces:
+                b0, buf = pieces[q_]
+                tot[b0 - r0:b0 - r0 + buf.shape[0]] += buf.numpy()
+        pc = torch.tensor([pairs], dtype=torch.int64)
+        dist.all_reduce(pc)
+        phi = tot / n
         rows_phi = [None] * world
-        dist.all_gather_object(rows_phi, (r0.value, r1.value, phi))
+        dist.all_gather_object(rows_phi, (r0, r1, phi))
         if rank == 0:
             q.put(("ok", {"X": X, "G": G, "rows": rows_phi, "pairs": int(pc.item())}))
         dist.destroy_process_group()

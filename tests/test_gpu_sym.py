@@ -27,7 +27,7 @@ PHI_TOL = 1e-10
 @pytest.fixture(params=["1", "2"])
 def sym_env(monkeypatch, request):
     """1: the one-rank pass (k_sym_finish forms phi); 2: the sharded form at
-    one rank (every particle's sums, the reduce-scatter call site with no
+    one rank (every particle's sums, the exchange's call site with no
     communicator, k_sym_apply) -- including the row-stream hand-over, whose
     partials the finish / apply sum."""
     monkeypatch.setenv("SVGD_PHI_SYM", request.param)

@@ -1,9 +1,11 @@
 """The sharded symmetric phi pass's protocol on CPU with gloo, world 1-4
 (tests/_sym_exchange_worker.py): the ranks' units (svgd_plan_sym_units) must
 cover every unordered pair of particles exactly once off the diagonal tiles
-and every ordered pair inside them, so the reduce-scattered per-particle
-sums give each rank the single-process phi_hat of its rows (oracle,
-SVGD.hpp:407-454) -- 1e-12 relative (a different summation order)."""
+and every ordered pair inside them, every sum a rank produces lies in the
+ranges svgd_plan_sym_exchange plans, and the point-to-point exchanged
+per-particle sums give each rank the single-process phi_hat of its rows
+(oracle, SVGD.hpp:407-454) -- 1e-12 relative (a different summation
+order)."""
 import multiprocessing as mp
 import socket
 
@@ -19,7 +21,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,n,d,block", [(1, 300, 3, 64), (2, 500, 3, 64), (3, 777, 2, 128), (4, 1000, 8, 192)])
+@pytest.mark.parametrize("world,n,d,block", [(1, 300, 3, 64), (2, 500, 3, 64), (3, 777, 2, 128), (4, 1000, 8, 192),
+                                             (8, 2000, 2, 64), (8, 1537, 3, 128), (6, 3000, 2, 192)])
 def test_sym_exchange_matches_oracle(oracle, world, n, d, block):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
