@@ -316,9 +316,15 @@ int svgd_plan_median_ranks(int64_t n, int64_t *rank_lo, int64_t *rank_hi);
 int64_t svgd_plan_pair_tiles(int64_t n, int block, int world, int rank);
 void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
                          int64_t *row_block, int64_t *col_block);
+/* Symmetric phi pass units: the (tile, sub-tile) pairs of the tile plan
+ * above (blocks of `block` rows, `nsub` sub-tiles of block / nsub columns
+ * per tile) in order, without the last column block's sub-tiles that hold
+ * padding columns only.  svgd_plan_sym_total: their number;
+ * svgd_plan_sym_unit: tile and sub-tile of unit u (returns -1 past the end). */
+int64_t svgd_plan_sym_total(int64_t n, int block, int nsub);
+int svgd_plan_sym_unit(int64_t n, int block, int nsub, int64_t u, int64_t *tile, int64_t *q);
 /* Symmetric phi pass (k_phi_sym) plan of rank r among `world`: its
- * (tile, sub-tile) units [*u0, *u1) of the tile plan above with blocks of
- * `block` rows and `nsub` sub-tiles per tile (equal pair counts per rank),
+ * units [*u0, *u1) (equal pair counts per rank),
  * run by `grid` work-groups in contiguous runs; per row block P (of
  * nb = ceil(n/block)) blkg[2P] .. blkg[2P+1] = the work-groups visiting it
  * (blkg[2P+1] < blkg[2P]: none) and rbase[P] = its first row-sum record;

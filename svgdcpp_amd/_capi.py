@@ -93,6 +93,9 @@ SIGNATURES = {
     "svgd_plan_sym_units": (_I64, [_I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.POINTER(_I64), ctypes.POINTER(_I64), ctypes.POINTER(ctypes.c_int),
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
+    "svgd_plan_sym_total": (_I64, [_I64, ctypes.c_int, ctypes.c_int]),
+    "svgd_plan_sym_unit": (ctypes.c_int, [_I64, ctypes.c_int, ctypes.c_int, _I64, ctypes.POINTER(_I64),
+                                          ctypes.POINTER(_I64)]),
     "svgd_plan_sym_exchange": (None, [_I64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                       ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "svgd_plan_bucket_select": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.c_int,

@@ -83,13 +83,69 @@ void svgd_plan_pair_tile(int64_t n, int block, int world, int rank, int64_t t,
     *col_block = slot == 0 ? I : (I + slot) % nb;
 }
 
+// The symmetric phi pass's units: (tile, sub-tile) pairs of the tile plan in
+// order, each tile's sub-tiles of `block / nsub` columns -- except the last
+// column block's sub-tiles past n (all padding columns), which are not units
+// at all: at N = 2^16 and 2^18 with 1536-row blocks the real units then
+// divide evenly over 256 work-groups at P = 1, 2, 4 and 8.
+static int64_t sym_cnt_h(int64_t nb, int64_t I) // tiles of row block I (slots 0 .. cnt-1)
+{
+    const int64_t H = (nb - 1) / 2;
+    return ((nb & 1) == 0 && I < nb / 2) ? H + 2 : H + 1;
+}
+static int64_t sym_qlast(int64_t n, int block, int nsub, int64_t nb) // real sub-tiles of block nb - 1
+{
+    const int64_t sub = block / nsub, valid = n - (nb - 1) * block;
+    return (valid + sub - 1) / sub;
+}
+// units of row block I: its tiles' sub-tiles, the one tile (if any) whose
+// column block is the last one counting qlast
+static int64_t sym_units_of(int64_t nb, int nsub, int64_t qlast, int64_t I)
+{
+    const int64_t cnt = sym_cnt_h(nb, I), s = nb - 1 - I; // slot of column block nb - 1
+    return cnt * nsub - (s < cnt ? nsub - qlast : 0);
+}
+
+int64_t svgd_plan_sym_total(int64_t n, int block, int nsub)
+{
+    const int64_t nb = (n + block - 1) / block, ql = sym_qlast(n, block, nsub, nb);
+    int64_t U = 0;
+    for (int64_t I = 0; I < nb; ++I) U += sym_units_of(nb, nsub, ql, I);
+    return U;
+}
+
+int svgd_plan_sym_unit(int64_t n, int block, int nsub, int64_t u, int64_t *tile, int64_t *q)
+{
+    const int64_t nb = (n + block - 1) / block, ql = sym_qlast(n, block, nsub, nb);
+    int64_t t = 0;
+    for (int64_t I = 0; I < nb; ++I) {
+        const int64_t uI = sym_units_of(nb, nsub, ql, I), cnt = sym_cnt_h(nb, I);
+        if (u >= uI) {
+            u -= uI;
+            t += cnt;
+            continue;
+        }
+        for (int64_t slot = 0; slot < cnt; ++slot) {
+            const int64_t J = (I + slot) % nb, nq = J == nb - 1 ? ql : nsub;
+            if (u < nq) {
+                *tile = t + slot;
+                *q = u;
+                return 0;
+            }
+            u -= nq;
+        }
+    }
+    *tile = *q = -1;
+    return -1;
+}
+
 // The symmetric phi pass's unit plan (svgd_capi.cpp, k_phi_sym / k_sym_finish).
 int64_t svgd_plan_sym_units(int64_t n, int block, int nsub, int world, int rank, int grid,
                             int64_t *u0, int64_t *u1, int *blkg, int *rbase, int64_t *Ia, int64_t *Ib)
 {
     if (world < 1) world = 1;
     const int64_t nb = (n + block - 1) / block;
-    const int64_t U = tiles_total(nb) * nsub;
+    const int64_t U = svgd_plan_sym_total(n, block, nsub);
     *u0 = U * rank / world;
     *u1 = U * (rank + 1) / world;
     const int64_t V = *u1 - *u0;
@@ -109,9 +165,11 @@ int64_t svgd_plan_sym_units(int64_t n, int block, int nsub, int world, int rank,
     for (int64_t g = 0; g < grid; ++g) {
         const int64_t a = *u0 + V * g / grid, b = *u0 + V * (g + 1) / grid;
         if (b <= a) continue;
-        int64_t I0, I1;
-        svgd_plan_pair_tile(n, block, 1, 0, a / nsub, &I0, &J);
-        svgd_plan_pair_tile(n, block, 1, 0, (b - 1) / nsub, &I1, &J);
+        int64_t I0, I1, ta, tb, q;
+        svgd_plan_sym_unit(n, block, nsub, a, &ta, &q);
+        svgd_plan_sym_unit(n, block, nsub, b - 1, &tb, &q);
+        svgd_plan_pair_tile(n, block, 1, 0, ta, &I0, &J);
+        svgd_plan_pair_tile(n, block, 1, 0, tb, &I1, &J);
         for (int64_t P = I0; P <= I1; ++P) {
             if ((int)g < blkg[2 * P]) blkg[2 * P] = (int)g;
             if ((int)g > blkg[2 * P + 1]) blkg[2 * P + 1] = (int)g;
@@ -123,8 +181,11 @@ int64_t svgd_plan_sym_units(int64_t n, int block, int nsub, int world, int rank,
         rbase[P] = (int)nrec;
         if (blkg[2 * P + 1] >= blkg[2 * P]) nrec += blkg[2 * P + 1] - blkg[2 * P] + 1;
     }
-    svgd_plan_pair_tile(n, block, 1, 0, *u0 / nsub, Ia, &J);
-    svgd_plan_pair_tile(n, block, 1, 0, (*u1 - 1) / nsub, Ib, &J);
+    int64_t ta, tb, q;
+    svgd_plan_sym_unit(n, block, nsub, *u0, &ta, &q);
+    svgd_plan_sym_unit(n, block, nsub, *u1 - 1, &tb, &q);
+    svgd_plan_pair_tile(n, block, 1, 0, ta, Ia, &J);
+    svgd_plan_pair_tile(n, block, 1, 0, tb, Ib, &J);
     return nrec;
 }
 
@@ -140,12 +201,14 @@ void svgd_plan_sym_exchange(int64_t n, int block, int nsub, int world, int src, 
     svgd_plan_rows(n, world, dst, &d0, &d1);
     *r0 = *r1 = d0;
     const int64_t nb = (n + block - 1) / block;
-    const int64_t U = tiles_total(nb) * nsub;
+    const int64_t U = svgd_plan_sym_total(n, block, nsub);
     const int64_t u0 = U * src / world, u1 = U * (src + 1) / world;
     if (u1 <= u0 || d1 <= d0) return;
-    int64_t Ia, Ib, J;
-    svgd_plan_pair_tile(n, block, 1, 0, u0 / nsub, &Ia, &J);
-    svgd_plan_pair_tile(n, block, 1, 0, (u1 - 1) / nsub, &Ib, &J);
+    int64_t Ia, Ib, J, ta, tb, q;
+    svgd_plan_sym_unit(n, block, nsub, u0, &ta, &q);
+    svgd_plan_sym_unit(n, block, nsub, u1 - 1, &tb, &q);
+    svgd_plan_pair_tile(n, block, 1, 0, ta, &Ia, &J);
+    svgd_plan_pair_tile(n, block, 1, 0, tb, &Ib, &J);
     const int64_t len = Ib - Ia + 1 + (nb - 1) / 2 + 1; // blocks Ia .. Ib + SM - 1
     int64_t lo = INT64_MAX, hi = INT64_MIN;
     auto meet = [&](int64_t a, int64_t b) { // particles [a, b) against dst's rows

@@ -207,6 +207,7 @@ struct svgd_ctx {
     int64_t sym_nb = 0, sym_units = 0, sym_u0 = 0, sym_u1 = 0; // all units, this rank's [u0, u1)
     int sym_fS = 1; // the row stream's column splits when it takes the step (symok = 0)
     int64_t sym_SM = 0, sym_Ia = 0, sym_Ib = 0; // colpart slots per column block; units' row-block span
+    int sym_qlast = 0; // real sub-tiles of the last column block
     double *srec = nullptr, *rowpart = nullptr, *colpart = nullptr;
     double *contrib = nullptr; // P > 1: every particle's sums from this rank's units (exchanged)
     // P > 1 over a communicator: the point-to-point exchange of those sums
@@ -217,7 +218,7 @@ struct svgd_ctx {
     int64_t xrecv_rows = 0;
     double *xrecv_buf = nullptr;
     int64_t *xtab_d = nullptr;
-    int *sym_tab = nullptr;    // the symmetric pass's row-block tables (SymArgs::blkg | rbase)
+    int *sym_tab = nullptr;    // the symmetric pass tables (SymArgs::blkg | rbase | wst)
     int *symok = nullptr;
     int64_t ldp = 0;
 
@@ -228,8 +229,9 @@ struct svgd_ctx {
     // P > 1: every rank draws the whole (smaller, <= 2^20) bracket sample of
     // the one counter-based sequence and derives the same bracket locally --
     // no histogram all-reduces in the step (two RCCL calls cost more than
-    // sampling 2^20 pairs); SVGD_SAMPLE_SHARD=1: ranks draw disjoint parts of
-    // a full-size sample and all-reduce its two radix histograms instead
+    // sampling 2^20 pairs).  (shard_sample: round 2's protocol, ranks drew
+    // disjoint parts of a full-size sample and all-reduced its two radix
+    // histograms; kept off -- tests/test_multirank_cpu.py pins it on CPU)
     bool shard_sample = false;
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
     bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol / _tcol)
@@ -832,10 +834,6 @@ bool trk_predict(svgd_ctx *c, double Mq, double band_samp, uint64_t *lo_key, uin
     for (int k = 0; k < c->trk_nerr; ++k) e = std::max(e, c->trk_err[k]);
     const double w = std::max(c->trk_err_mult * e, c->trk_min_w);
     const double band = c->trk_dens * (2.0 * w * pred) / Mq;
-    static const bool dbg = std::getenv("SVGD_DEBUG_TRK") != nullptr;
-    if (dbg)
-        std::fprintf(stderr, "trk: pred %.6g err %.3g w %.3g band %.3g band_samp %.3g -> %s\n", pred, e, w,
-                     band, band_samp, (w < 0.05 && band <= band_samp) ? "predict" : "sample");
     if (!(w < 0.05)) return false;
     const double lo = pred * (1.0 - w), hi = pred * (1.0 + w);
     if (!(band <= band_samp)) return false;
@@ -1414,7 +1412,8 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
                    c->symok,  c->rowpart,   c->colpart,     c->sym_grid, c->row0,
                    c->nrows,  1.0 / (double)c->n, c->phi, c->rec, c->RS, c->contrib,
                    c->sym_tab, c->sym_tab + 2 * c->sym_nb,
-                   c->sym_SM, c->sym_Ia, c->sym_Ib, c->part, c->sym_fS, c->ldp};
+                   c->sym_SM, c->sym_Ia, c->sym_Ib, c->part, c->sym_fS, c->ldp,
+                   c->sym_tab + 3 * c->sym_nb, c->sym_qlast};
         // (when the records' flag says the symmetric form would leave its
         // range, symok = 0, the same launch runs the row stream's work-groups
         // instead; their partials are summed by the finish / k_sym_apply)
@@ -1810,10 +1809,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess) ncu = prop.multiProcessorCount;
         c->R = dim <= 8 ? 4 : 2; // rows per lane (register budget)
-        if (const char *e = std::getenv("SVGD_PHI_R")) {
-            const int r = std::atoi(e);
-            if (r == 1 || r == 2 || r == 4) c->R = r;
-        }
         // 8-wave work-groups, 8192-entry table, columns split over the waves
         // (kind 2); the 4-wave kernel (kind 0) serves the full-matrix scales
         // (signature rows) and an R the 8-wave build does not have
@@ -1825,8 +1820,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         // 2 blocks per resident slot: one block wave per slot left a tail of
         // idle CUs (measured at cfg3, phi launch: S x1 4.00 ms, x2 3.83-3.93,
         // x4 3.81-3.90, x8 3.91-3.95 -- x2 and x4 tie, x2 has half the partials)
-        int split_mult = 2;
-        if (const char *e = std::getenv("SVGD_PHI_SPLIT_MULT")) split_mult = std::max(1, std::atoi(e));
+        constexpr int split_mult = 2;
         S *= split_mult;
         S = std::min<int64_t>(S, std::max<int64_t>(1, n / 256));
         c->S = (int)S;
@@ -1864,15 +1858,17 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         // 0.200 vs 0.265 ms -- profiles/r05_sym_ab.txt.  SVGD_PHI_SYM=1 / 0
         // forces it on / off)
         // P > 1: rank r runs the units [U r / P, U (r+1) / P), sums every
-        // particle's partials from them and a reduce-scatter (N (d+1) doubles)
-        // hands each rank its rows' totals.  Its phi saving grows as N^2 / P,
-        // the exchange as N: default from N / P >= 16384.  cfg3 shares
-        // (sim-world, profiles/r05_sim_sym.txt) P = 2 2.008 -> 1.875 ms, P = 4
-        // 1.066 -> 1.003 against a reduce-scatter of 4.7 MB (P = 2: 2.4 MB
-        // over one xGMI link, ~35 us; P = 4 ~20-35 us); P = 8 (8192 rows) 0.587
-        // -> 0.582, less than its exchange; cfg4 at P = 8 (32768 rows) 7.92 ->
-        // 6.84 ms against 18.9 MB (~0.1-0.15 ms), profiles/r05_cfg4_sim8_sym.txt
-        bool want_sym = phi_sym_supported(dim) && n >= 32768 && n / c->plan_world >= 16384;
+        // particle's partials from them and a point-to-point exchange hands
+        // each rank the pieces of its rows (sym_exchange).  Its phi saving
+        // grows as N^2 / P, the exchange as N.  Round 5 (a reduce-scatter of
+        // all N (d+1) sums, units not balanced at P = 8): default from N / P >=
+        // 16384 (cfg3 shares P = 2 2.008 -> 1.875 ms, P = 4 1.066 -> 1.003, P =
+        // 8 0.587 -> 0.582; cfg4 P = 8 7.92 -> 6.84 ms, profiles/r05_sim_sym.txt,
+        // r05_cfg4_sim8_sym.txt).  Round 6: the padding-only sub-tiles left out
+        // of the units (11 per work-group at cfg3 P = 8 instead of 11 or 12) and
+        // ~2.5 MB sent per rank at cfg3 P = 8 instead of 4.1 MB in ring steps:
+        // default from N / P >= 8192 (cfg3 at P = 8 included)
+        bool want_sym = phi_sym_supported(dim) && n >= 32768 && n / c->plan_world >= 8192;
         int sym_env = -1; // 2 (a test knob): the P > 1 form (sums, reduce-scatter, apply) at any P
         if (const char *e = std::getenv("SVGD_PHI_SYM")) {
             sym_env = std::atoi(e);
@@ -1881,8 +1877,7 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
         if (want_sym && phi_sym_geom(dim, &c->symB, &c->symSRS, &c->symNSUB)) {
             const int64_t B = c->symB;
             c->sym_nb = (n + B - 1) / B;
-            const int64_t T = c->sym_nb * (c->sym_nb + 1) / 2;
-            c->sym_units = T * c->symNSUB;
+            c->sym_units = svgd_plan_sym_total(n, (int)B, c->symNSUB); // (no padding-only sub-tiles)
             const int64_t Pw = c->plan_world, r = c->sim_world > 1 ? 0 : c->rank;
             const int64_t slots = (int64_t)phi_sym_blocks_per_cu(dim) * ncu;
             const int64_t Vr = c->sym_units * (r + 1) / Pw - c->sym_units * r / Pw;
@@ -1890,10 +1885,22 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             // the rank's units, the row blocks each work-group's contiguous run
             // visits and each row block's contiguous row-sum records (plan.cpp)
             const int64_t nbs = c->sym_nb;
-            std::vector<int> tab(3 * (size_t)nbs);
-            int *blkg = tab.data(), *rbase = blkg + 2 * nbs;
+            std::vector<int> tab(3 * (size_t)nbs + 2 * (size_t)c->sym_grid);
+            int *blkg = tab.data(), *rbase = blkg + 2 * nbs, *wst = rbase + nbs;
             const int64_t nrec = svgd_plan_sym_units(n, (int)B, c->symNSUB, (int)Pw, (int)r, c->sym_grid,
                                                      &c->sym_u0, &c->sym_u1, blkg, rbase, &c->sym_Ia, &c->sym_Ib);
+            // each work-group's first unit (the kernel advances from there)
+            for (int g = 0; g < c->sym_grid; ++g) {
+                const int64_t V = c->sym_u1 - c->sym_u0;
+                int64_t t = 0, q = 0;
+                svgd_plan_sym_unit(n, (int)B, c->symNSUB, c->sym_u0 + V * g / c->sym_grid, &t, &q);
+                wst[2 * g] = (int)t;
+                wst[2 * g + 1] = (int)q;
+            }
+            {
+                const int64_t sub = B / c->symNSUB, valid = n - (nbs - 1) * B;
+                c->sym_qlast = (int)((valid + sub - 1) / sub);
+            }
             c->sym_SM = (nbs - 1) / 2 + 2;
             // the row stream's hand-over inside k_phi_sym (symok = 0): its
             // 8-wave work-groups, one wave of them (<= c->S, the part buffer's splits)
@@ -1966,9 +1973,6 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     CHK(dalloc(c, &c->gseg, (int64_t)c->world * (CAPG + 1)));
     if (const char *e = std::getenv("SVGD_BUCKET_CAP")) c->bucket_cap = std::atoll(e);
     if (const char *e = std::getenv("SVGD_MEDIAN_SAMPLE")) c->sample_size = std::max<int64_t>(1, std::atoll(e));
-    if (const char *e = std::getenv("SVGD_COLLECT_BLOCKS")) // buffers hold <= MAX_COLLECT_BLOCKS
-        c->collect_blocks = std::min<int64_t>(MAX_COLLECT_BLOCKS, std::max(1, std::atoi(e)));
-    if (const char *e = std::getenv("SVGD_SAMPLE_SHARD")) c->shard_sample = std::atoi(e) != 0;
     // A/B and test knob: the reference collect passes (k_pair_rows / k_pair_tiles
     // MODE 0) instead of the matrix-core ones (k_pair_mcol / k_pair_tcol)
     if (const char *e = std::getenv("SVGD_COLLECT_FP64")) c->mcol = std::atoi(e) == 0;

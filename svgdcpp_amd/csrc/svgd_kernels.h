@@ -261,6 +261,10 @@ struct SymArgs {
     double *fpart = nullptr;
     int fS = 0;
     int64_t fldp = 0;
+    // the first unit (tile, sub-tile) of each work-group's run
+    // (svgd_plan_sym_unit) and the real sub-tiles of the last column block
+    const int *wst = nullptr;
+    int qlast = 0;
 };
 // P > 1: phi + the optimizer for rows [row0, row0 + nrows) from their sums:
 // own (this rank's, nrows x (d+1)) and the pieces received from the other

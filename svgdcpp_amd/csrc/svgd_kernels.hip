@@ -2794,7 +2794,8 @@ template <int D>
 __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_phi_sym(
     const double *__restrict__ srec, const double *__restrict__ a_ptr, int64_t nb, int64_t U0, int64_t U1,
     const int *__restrict__ symok, double *__restrict__ rowpart, const int *__restrict__ blkg,
-    const int *__restrict__ rbase, double *__restrict__ colpart, int64_t SM, SymRows fr)
+    const int *__restrict__ rbase, double *__restrict__ colpart, int64_t SM, const int *__restrict__ wst,
+    int qlast, SymRows fr)
 {
     using Gm = SymGeom<D>;
     constexpr int R = Gm::R, B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP,
@@ -2833,22 +2834,25 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const int64_t Gn = gridDim.x, V = U1 - U0;
     const int64_t u0 = U0 + V * (int64_t)blockIdx.x / Gn, u1 = U0 + V * ((int64_t)blockIdx.x + 1) / Gn;
     // (tile, sub-tile) cursor: the plan's tile t = (I, J), J = I + slot mod nb
-    // (plan.cpp); advanced incrementally (no 64-bit divisions per sub-tile)
+    // (plan.cpp), nq sub-tiles in it (qlast for the last column block: its
+    // padding-only sub-tiles are no units); the run's first unit from the
+    // host's table wst, then advanced incrementally (no 64-bit divisions)
     struct Cur {
         int64_t t, I, J, slot, cnt;
-        int q;
+        int q, nq;
     };
-    auto cur_at = [&](int64_t u) {
+    auto cur_start = [&]() {
         Cur c;
-        c.t = u / NSUB;
-        c.q = (int)(u - c.t * NSUB);
+        c.t = wst[2 * blockIdx.x];
+        c.q = wst[2 * blockIdx.x + 1];
         tile_coords(nb, c.t, &c.I, &c.J);
         c.slot = c.J >= c.I ? c.J - c.I : c.J + nb - c.I;
         c.cnt = sym_cnt(nb, c.I);
+        c.nq = c.J == nb - 1 ? qlast : NSUB;
         return c;
     };
     auto cur_next = [&](Cur &c) {
-        if (++c.q < NSUB) return;
+        if (++c.q < c.nq) return;
         c.q = 0;
         ++c.t;
         if (++c.slot == c.cnt) {
@@ -2857,6 +2861,7 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
             c.cnt = sym_cnt(nb, c.I);
         }
         c.J = c.I + c.slot >= nb ? c.I + c.slot - nb : c.I + c.slot;
+        c.nq = c.J == nb - 1 ? qlast : NSUB;
     };
     auto issue = [&](const Cur &c, int buf) {
         const char *src =
@@ -2906,7 +2911,7 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
             if (!diagp) o[e] = v;
         }
     };
-    Cur cu = cur_at(u0), cn = cu;
+    Cur cu = cur_start(), cn = cu;
     issue(cu, 0);
     int64_t pJ = 0, pSlot = 0;
     int pQ = 0;
@@ -5039,7 +5044,8 @@ int phi_sym_blocks_per_cu(int d)
                          ((a.nrows + phi_rows_t8k_rows(4) - 1) / phi_rows_t8k_rows(4)) * a.fS,  \
                          a.fpart, a.fldp, a.nmax};                                            \
         hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(SYM_NW * 64), 0, stream, a.srec, a.a_ptr, \
-                           a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.blkg, a.rbase, a.colpart, a.SM, fr); \
+                           a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.blkg, a.rbase, a.colpart, a.SM, \
+                           a.wst, a.qlast, fr);                                               \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k1 && (e = hipEventRecord(ev_k1, stream)) != hipSuccess) return e;             \
         return hipSuccess;                                                                    \

@@ -45,13 +45,16 @@ def run(rank, world, port, n, d, block, a, q):
         S = np.zeros((n, d))
         pairs = 0
         for u in range(u0.value, u1.value):
-            t, sq = divmod(u, nsub)
+            t_, q_ = ctypes.c_int64(), ctypes.c_int64()
+            assert lib.svgd_plan_sym_unit(n, block, nsub, u, ctypes.byref(t_), ctypes.byref(q_)) == 0
+            t, sq = t_.value, q_.value
             I, J = ctypes.c_int64(), ctypes.c_int64()
             lib.svgd_plan_pair_tile(n, block, 1, 0, t, ctypes.byref(I), ctypes.byref(J))
             I, J = I.value, J.value
             rows = np.arange(I * block, min(n, (I + 1) * block))
             cols = np.arange(J * block + 64 * sq, min(n, J * block + 64 * (sq + 1)))
-            if rows.size == 0 or cols.size == 0:
+            assert cols.size > 0  # (padding-only sub-tiles are no units)
+            if rows.size == 0:
                 continue
             diff = X[rows, None, :] - X[None, cols, :]  # x_i - x_j
             K = np.exp(-a * np.sum(diff * diff, axis=2))

@@ -237,8 +237,10 @@ def _tile(lib, n, block, t):
                                                (6007, 1536, 3, 5), (3001, 2048, 2, 7), (1537, 1536, 1, 4)])
 def test_plan_sym_units(n, block, world, grid):
     """The symmetric phi pass's unit plan (svgd_plan_sym_units, used by the
-    context for k_phi_sym / k_sym_finish): the ranks' unit ranges partition
-    every (tile, sub-tile) unit once; each work-group's contiguous run is
+    context for k_phi_sym / k_sym_finish): the units are the plan's (tile,
+    sub-tile) pairs without the padding-only sub-tiles of the last column
+    block (svgd_plan_sym_total / svgd_plan_sym_unit); the ranks' unit ranges
+    partition them once; each work-group's contiguous run is
     non-empty; blkg holds exactly the work-groups whose runs visit a row
     block (a contiguous range); rbase numbers each row block's records
     contiguously in work-group order; Ia..Ib span the rank's row blocks; and
@@ -248,8 +250,19 @@ def test_plan_sym_units(n, block, world, grid):
     nsub = block // 64
     nb = (n + block - 1) // block
     T = nb * (nb + 1) // 2
-    U = T * nsub
     tiles = [_tile(lib, n, block, t) for t in range(T)]
+    # the units: every (tile, sub-tile) in plan order except the last column
+    # block's sub-tiles that hold only padding columns
+    U = lib.svgd_plan_sym_total(n, block, nsub)
+    unit_tile = []
+    for u in range(U):
+        t, q = ctypes.c_int64(), ctypes.c_int64()
+        assert lib.svgd_plan_sym_unit(n, block, nsub, u, ctypes.byref(t), ctypes.byref(q)) == 0
+        unit_tile.append((t.value, q.value))
+    expect = [(t, q) for t in range(T) for q in range(nsub) if tiles[t][1] * block + 64 * q < n]
+    assert unit_tile == expect
+    t, q = ctypes.c_int64(), ctypes.c_int64()
+    assert lib.svgd_plan_sym_unit(n, block, nsub, U, ctypes.byref(t), ctypes.byref(q)) == -1
     slots = {}
     for t, (I, J) in enumerate(tiles):
         if I != J:
@@ -272,7 +285,7 @@ def test_plan_sym_units(n, block, world, grid):
         for wg in range(g):
             a, b = u0 + V * wg // g, u0 + V * (wg + 1) // g
             assert b > a
-            for P in {tiles[u // nsub][0] for u in range(a, b)}:
+            for P in {tiles[unit_tile[u][0]][0] for u in range(a, b)}:
                 visits.setdefault(P, []).append(wg)
         expect_rec = 0
         for P in range(nb):
@@ -282,7 +295,7 @@ def test_plan_sym_units(n, block, world, grid):
             assert rbase[P] == expect_rec
             expect_rec += len(got)
         assert nrec == expect_rec
-        rows = {tiles[u // nsub][0] for u in range(u0, u1)}
+        rows = {tiles[unit_tile[u][0]][0] for u in range(u0, u1)}
         assert rows == set(range(Ia.value, Ib.value + 1))
     assert cover[0][0] == 0 and cover[-1][1] == U
     assert all(a[1] == b[0] for a, b in zip(cover, cover[1:]))
