@@ -150,14 +150,14 @@ def _sample_rows(n):
     return [(0, 256), (n // 2 - 256, n // 2 + 256), (n - 256, n)]
 
 
-@pytest.mark.parametrize("n,sym", [(131072, "default"), (65536, "default"), (65536, "1")],
-                         ids=["n131072-sym-default", "cfg3-default", "cfg3-sym-forced"])
+@pytest.mark.parametrize("n,sym", [(131072, "default"), (65536, "default"), (65536, "0")],
+                         ids=["n131072-sym-default", "cfg3-sym-default", "cfg3-rows-forced"])
 def test_world8_full_path_vs_one_rank_and_oracle(oracle, n, sym):
     """8 ranks at d = 8 through the default multi-rank path (X mirror,
     speculative steps, tracked brackets, SVGD_DEBUG_COLL=1).  n = 131072:
     N/P = 16384 rows per rank makes the sharded symmetric pass the default
-    (cfg4's 8-rank form at half its N); n = 65536: cfg3's 8-rank default (the
-    row stream) and the sharded symmetric pass forced.  The host backend's
+    (cfg4's 8-rank form at half its N); n = 65536: cfg3's 8-rank default
+    (the sharded symmetric pass from N/P >= 8192) and the row stream forced.  The host backend's
     phi exchange is a faithful point-to-point one -- a receiver sees only the
     ranges its senders sent (NaN elsewhere), a range the two sides plan
     differently fails the call, and the send buffer outside the rank's own
@@ -174,7 +174,7 @@ def test_world8_full_path_vs_one_rank_and_oracle(oracle, n, sym):
     multi = _run_ranks(world, n, d, steps, env, diags=diags)
     single = _run_ranks(1, n, d, steps, {"SVGD_HOST_THREADS": "1"})[0]
     X1, s1, _ = single
-    want_sym = n // world >= 16384 or sym == "1"
+    want_sym = sym != "0" and n // world >= 8192
     for rank, (X, scales, _) in multi.items():
         dg = diags[rank]
         assert dg["ranks"] == world, dg
