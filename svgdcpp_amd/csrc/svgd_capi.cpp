@@ -208,7 +208,7 @@ struct svgd_ctx {
     int sym_fS = 1; // the row stream's column splits when it takes the step (symok = 0)
     int64_t sym_SM = 0, sym_Ia = 0, sym_Ib = 0; // colpart slots per column block; units' row-block span
     int sym_qlast = 0; // real sub-tiles of the last column block
-    double *srec = nullptr, *rowpart = nullptr, *colpart = nullptr;
+    double *srec = nullptr, *rowpart = nullptr, *colpart = nullptr, *tab8k = nullptr;
     double *contrib = nullptr; // P > 1: every particle's sums from this rank's units (exchanged)
     // P > 1 over a communicator: the point-to-point exchange of those sums
     // (svgd_plan_sym_exchange): per rank q the rows [xsend[2q], xsend[2q+1])
@@ -1413,7 +1413,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
                    c->nrows,  1.0 / (double)c->n, c->phi, c->rec, c->RS, c->contrib,
                    c->sym_tab, c->sym_tab + 2 * c->sym_nb,
                    c->sym_SM, c->sym_Ia, c->sym_Ib, c->part, c->sym_fS, c->ldp,
-                   c->sym_tab + 3 * c->sym_nb, c->sym_qlast};
+                   c->sym_tab + 3 * c->sym_nb, c->sym_qlast, c->tab8k};
         // (when the records' flag says the symmetric form would leave its
         // range, symok = 0, the same launch runs the row stream's work-groups
         // instead; their partials are summed by the finish / k_sym_apply)
@@ -1918,6 +1918,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
             // zeroed here once: entries no unit of this rank writes stay zero
             CHK(dalloc(c, &c->colpart, nbs * c->sym_SM * B * (dim + 1)));
             CHK(dalloc(c, &c->symok, 1));
+            CHK(dalloc(c, &c->tab8k, 8192));
+            HIPCHK(c, launch_fill_tab8k(c->tab8k, c->stream));
             if (Pw > 1 || sym_env == 2) CHK(dalloc(c, &c->contrib, std::max<int64_t>(c->np, c->world * c->chunk) * (dim + 1)));
             if (c->world > 1) {
                 // the exchange plan: the same ranges on both sides of every pair of ranks
@@ -2164,7 +2166,7 @@ int svgd_destroy(svgd_ctx *c)
                        c->m,     c->v,     c->lower,   c->upper, c->partial, c->scal, c->rec,
                        c->part,  c->dm_mu, c->dm_prec, c->sc_src, c->sc_M, c->sc_L, c->wv, c->zc,
                        c->sc_sgn,  c->sc_work, c->bak, c->srec, c->rowpart, c->colpart, c->contrib,
-                       c->xrecv_buf};
+                       c->xrecv_buf, c->tab8k};
     float *fbufs[] = {c->xcf, c->nrmf, c->cvf, c->Vf, c->zcf, c->XS, c->VS};
     for (float *p : fbufs)
         if (p) (void)hipFree(p);

@@ -265,7 +265,9 @@ struct SymArgs {
     // (svgd_plan_sym_unit) and the real sub-tiles of the last column block
     const int *wst = nullptr;
     int qlast = 0;
+    const double *tab8k = nullptr; // the biased exp table (launch_fill_tab8k), 8192 doubles
 };
+hipError_t launch_fill_tab8k(double *tab, hipStream_t stream);
 // P > 1: phi + the optimizer for rows [row0, row0 + nrows) from their sums:
 // own (this rank's, nrows x (d+1)) and the pieces received from the other
 // ranks (xtab: world x {t0, t1, row offset in recv}), added in rank order --

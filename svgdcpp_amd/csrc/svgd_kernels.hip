@@ -2581,6 +2581,22 @@ __device__ __forceinline__ void sym_lds_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// The biased 8192-entry exp table of k_phi_rows (TABN 8192) in HBM, once per
+// context: k_phi_sym DMAs it into LDS instead of forming it per work-group.
+__global__ void k_fill_tab8k(double *__restrict__ tab)
+{
+    for (int m = blockIdx.x * blockDim.x + threadIdx.x; m < 8192; m += gridDim.x * blockDim.x) {
+        const double t = EXP2_TAB4096[m & (EXP_TB - 1)];
+        const double tb = tab_biased(m >= EXP_TB ? 2.0 * t : t, m);
+        tab[m] = __hiloint2double(__double2hiint(tb) - (EXP_QB << 20), __double2loint(tb));
+    }
+}
+hipError_t launch_fill_tab8k(double *tab, hipStream_t stream)
+{
+    hipLaunchKernelGGL(k_fill_tab8k, dim3(32), dim3(256), 0, stream, tab);
+    return hipGetLastError();
+}
+
 // records: srec_j = [xc_j | w_j (G_j - 2a xc_j) | w_j | 0..] (zero past n),
 // w_j = exp(-a |xc_j|^2); symok = (a log2e max|xc|^2 <= 300).  When the
 // symmetric form does not apply (every block sees the same flag), the row
@@ -2795,7 +2811,7 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     const double *__restrict__ srec, const double *__restrict__ a_ptr, int64_t nb, int64_t U0, int64_t U1,
     const int *__restrict__ symok, double *__restrict__ rowpart, const int *__restrict__ blkg,
     const int *__restrict__ rbase, double *__restrict__ colpart, int64_t SM, const int *__restrict__ wst,
-    int qlast, SymRows fr)
+    int qlast, const double *__restrict__ tab8k, SymRows fr)
 {
     using Gm = SymGeom<D>;
     constexpr int R = Gm::R, B = Gm::B, NSUB = Gm::NSUB, SRS = Gm::SRS, DP = Gm::DP,
@@ -2818,16 +2834,8 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     double *sCol = tab + 8192; // [2][SYM_NW][SYM_SUB][DP]: sub-tile u's column sums in buffer u & 1
     constexpr int SCOL = Gm::SCOL;
     const int tid = threadIdx.x, lane = tid & 63;
-    for (int e = tid; e < 2 * SCOL; e += NT) sCol[e] = 0.0;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = lane >> 4, tl = lane & 15;
-    // the biased 8192-entry table of the row stream (k_phi_rows, TABN 8192)
-    for (int m = tid; m < 8192; m += NT) {
-        const double t = EXP2_TAB4096[m & (EXP_TB - 1)];
-        const double tb = tab_biased(m >= EXP_TB ? 2.0 * t : t, m);
-        tab[m] = __hiloint2double(__double2hiint(tb) - (EXP_QB << 20), __double2loint(tb));
-    }
-    __syncthreads();
 
     const double alpha = 8192.0 * LOG2E * (*a_ptr);
     // this work-group's contiguous run of the rank's units [U0, U1)
@@ -2887,6 +2895,14 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     } while (0)
 
     if (u0 >= u1) return;
+    // Prologue, its memory latencies overlapped: the DMA of the biased
+    // 8192-entry exp table (the row stream's, k_phi_rows TABN 8192, filled
+    // once per context into tab8k: 64 pieces of 1 KiB) and of the first
+    // sub-tile, then the first row block's registers, then the column-sum
+    // buffers zeroed; the loop's first barrier (after vmcnt(0)) covers all.
+    for (int p = w; p < 64; p += SYM_NW)
+        __builtin_amdgcn_global_load_lds((gbl_void *)(reinterpret_cast<const char *>(tab8k) + p * 1024 + lane * 16),
+                                         (lds_void *)(reinterpret_cast<char *>(tab) + p * 1024), 16, 0, 0);
     // One barrier per sub-tile: the column sums of sub-tile u go to buffer
     // u & 1 and are added into colpart during sub-tile u + 1 (after its
     // barrier, when every wave is past sub-tile u), and the DMA of sub-tile
@@ -2913,6 +2929,19 @@ __global__ __launch_bounds__(SYM_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 
     };
     Cur cu = cur_start(), cn = cu;
     issue(cu, 0);
+    curI = cu.I;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double *ri = srec + (curI * B + (w * R + r) * 64 + lane) * SRS;
+#pragma unroll
+        for (int k = 0; k < D; ++k) xs[r][k] = alpha * ri[k];
+#pragma unroll
+        for (int k = 0; k < DP; ++k) {
+            wr[r][k] = ri[D + k];
+            acc[r][k] = 0.0;
+        }
+    }
+    for (int e = tid; e < 2 * SCOL; e += NT) sCol[e] = 0.0;
     int64_t pJ = 0, pSlot = 0;
     int pQ = 0;
     bool pDiag = true, have_prev = false;
@@ -5045,7 +5074,7 @@ int phi_sym_blocks_per_cu(int d)
                          a.fpart, a.fldp, a.nmax};                                            \
         hipLaunchKernelGGL((k_phi_sym<Dv>), dim3(a.grid), dim3(SYM_NW * 64), 0, stream, a.srec, a.a_ptr, \
                            a.nbs, a.u0, a.u1, a.symok, a.rowpart, a.blkg, a.rbase, a.colpart, a.SM, \
-                           a.wst, a.qlast, fr);                                               \
+                           a.wst, a.qlast, a.tab8k, fr);                                      \
         if ((e = hipGetLastError()) != hipSuccess) return e;                                  \
         if (ev_k1 && (e = hipEventRecord(ev_k1, stream)) != hipSuccess) return e;             \
         return hipSuccess;                                                                    \

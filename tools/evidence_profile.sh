@@ -39,8 +39,8 @@ if has cfg2; then
   cp gpurun_out/timeline/cfg2.txt $O/step_timeline_cfg2.txt
 fi
 if has sim8tl; then
-  for form in default sym; do
-    envs=""; [ $form = sym ] && envs="SVGD_PHI_SYM=1"
+  for form in default rows; do
+    envs=""; [ $form = rows ] && envs="SVGD_PHI_SYM=0"
     (cd /tmp && export TMPDIR=/tmp && for kv in $envs; do export "$kv"; done && \
      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $REPO/$O/sim8_$form -o run --output-format csv \
        -- python3 $REPO/bench.py --sim-world 8 --steps 20 --warmup 3 --no-cpu > $REPO/$O/sim8_${form}_prof.log 2>&1) || exit 1
