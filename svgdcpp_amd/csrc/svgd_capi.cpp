@@ -182,6 +182,7 @@ struct svgd_ctx {
     uint32_t *B3 = nullptr;             // operand-ordered bf16 parts (k_phi_b3), replaces XS / VS
     uint32_t *XK = nullptr;             // F32 median key parts, KP 32 / 64 (svgd_device.h)
     bool want_b3 = false;               // F32 phi on the bf16 matrix cores (init)
+    int b3_rg = 1;                      // k_phi_b3's row groups per wave (init)
 
     // row-stream path (d <= ROWS_MAX_D)
     bool rowpath = false;
@@ -1455,7 +1456,7 @@ int run_phi(svgd_ctx *c, const OptArgs *opt)
     } else if (phis)
         HIPCHK(c, c->B3 ? launch_phi_b3(c->KP, c->NCB, c->B3, c->cvf, c->scal, c->row0, c->nrows, ntl,
                                         c->dim, 1.0 / (double)c->n, mat ? c->wv : nullptr, c->xc, c->KP,
-                                        c->phi, opt, c->stream)
+                                        c->phi, opt, c->b3_rg, c->stream)
                         : launch_phi_f32s(c->KP, c->NCB, c->XS, c->VS, mat ? c->zcf : c->xcf, c->cvf, c->scal,
                                   c->row0, c->nrows, ntl, c->dim, 1.0 / (double)c->n,
                                   mat ? c->wv : nullptr, c->xc, c->KP, c->phi, opt, c->stream));
@@ -1770,6 +1771,16 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     c->plan_world = plan_world;
     svgd_plan_rows(n, plan_world, c->rank, &c->row0, &c->row1);
     c->nrows = c->row1 - c->row0;
+    // k_phi_b3 with two 16-row groups per wave (half its LDS reads and
+    // barriers per MFMA) when that still gives every CU a work-group;
+    // SVGD_PHI_B3_RG=1 / 2 forces one (tests)
+    if (c->want_b3) {
+        int ncu = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess) ncu = prop.multiProcessorCount;
+        c->b3_rg = c->nrows >= (int64_t)phi_b3_rows_per_wg(2) * ncu ? 2 : 1;
+        if (const char *e = std::getenv("SVGD_PHI_B3_RG")) c->b3_rg = std::atoi(e) == 2 ? 2 : 1;
+    }
     c->pblock = SVGD_PAIR_BLOCK_DT(dim, dtype);
     c->pnb = (n + c->pblock - 1) / c->pblock;
     c->own_tiles = svgd_plan_pair_tiles(n, c->pblock, plan_world, c->rank);
@@ -2824,8 +2835,8 @@ int svgd_phi_kernel_name(const svgd_ctx *c, char *buf, int cap)
         else
             std::snprintf(s, sizeof s, "k_phi_rows<%d, %d, 4, 4096, 1>", d, c->R);
     } else if (c->dtype == SVGD_F32 && c->B3) {
-        std::snprintf(s, sizeof s, "k_phi_b3<%d, %d, 8, %s>", c->KP, c->NCB,
-                      c->dim == 16 * c->NCB ? "true" : "false");
+        std::snprintf(s, sizeof s, "k_phi_b3<%d, %d, 8, %s, %d>", c->KP, c->NCB,
+                      16 * c->NCB == d ? "true" : "false", c->b3_rg);
     } else if (c->dtype == SVGD_F32 && c->XS) {
         std::snprintf(s, sizeof s, "k_phi_f32s<%d, %d>", c->KP, c->NCB);
     } else {

@@ -337,7 +337,9 @@ hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const
 hipError_t launch_phi_b3(int KP, int NCB, const uint32_t *B3, const float *crow,
                          const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles, int d,
                          double inv_n, const double *wv, const double *xc, int xc_stride,
-                         double *phi, const OptArgs *opt, hipStream_t stream);
+                         double *phi, const OptArgs *opt, int rg, hipStream_t stream);
+// rows per work-group of k_phi_b3 with rg row groups of 16 per wave (1 or 2)
+int phi_b3_rows_per_wg(int rg);
 hipError_t launch_phi_f32s(int KP, int NCB, const float *XS, const float *VS, const float *xrow,
                            const float *crow, const double *a_ptr, int64_t row0, int64_t nrows,
                            int64_t ntiles, int d, double inv_n, const double *wv, const double *xc,

@@ -3376,11 +3376,6 @@ __device__ __forceinline__ uint32_t b3_trunc_pair(float &x0, float &x1)
 #ifndef SVGD_B3_TRUNC
 #define SVGD_B3_TRUNC 1
 #endif
-// waves 4-7 VALU-first (below): measured 6 % slower per clock at cfg5
-// (profiles/r04_b3_ab.txt), so off
-#ifndef SVGD_B3_STAGGER
-#define SVGD_B3_STAGGER 0
-#endif
 __device__ __forceinline__ uint32_t b3_split_pair(float &x0, float &x1)
 {
     // bf16(x0) | bf16(x1) << 16 (round to nearest even), and the residuals
@@ -3487,9 +3482,12 @@ __device__ __forceinline__ f4_t mfma_b3(uint4 a, uint4 b, f4_t c)
 // S1V (d = 16 NCB): V holds no column of ones; the row sums sum_j P_ij are
 // added on the VALU (padded columns carry c_j = -inf: P = 0).  The part
 // products are issued term by term across independent accumulators (the
-// four Gram chains js x db, the NCB P.V blocks), so no MFMA waits for the
-// one before it.
-template <int KP, int NCB, int NW, bool S1V>
+// Gram chains js x db x rg, the NCB x RG P.V blocks), so no MFMA waits for
+// the one before it.  RG row groups of 16 per wave (RG = 2 at large row
+// counts, round 6): each tile's column parts, read from LDS once, feed RG
+// times the MFMAs -- half the LDS reads and half the barriers per MFMA at
+// RG = 2 (2 waves per SIMD at ~200 VGPRs instead of 4 at 128).
+template <int KP, int NCB, int NW, bool S1V, int RG = 1>
 __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     const uint32_t *__restrict__ B3, const float *__restrict__ crow, const double *__restrict__ a_ptr,
     int64_t row0, int64_t nrows, int64_t ntiles, int d, double inv_n, const double *__restrict__ wv,
@@ -3504,28 +3502,35 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     const double a = *a_ptr;
     const float alpha = (float)(2.0 * a * LOG2E);
 
-    const int64_t ibase = row0 + (int64_t)blockIdx.x * (16 * NW) + w * 16;
-    // a wave past the slice (the last block of a rank's rows) loads the
-    // slice's first rows instead: valid memory, nothing stored
-    const int64_t ild = ibase < row0 + nrows ? ibase : row0;
-    // the Gram's B operand: this wave's 16 rows, from their tile's XB slices
-    uint4 bR[NDB][3];
-    {
+    const int64_t ibase = row0 + (int64_t)blockIdx.x * (16 * RG * NW) + w * (16 * RG);
+    // the Gram's B operand: this wave's RG x 16 rows, from their tiles' XB
+    // slices; a row group past the slice (the last block of a rank's rows)
+    // loads the slice's first rows instead: valid memory, nothing stored
+    uint4 bR[RG][NDB][3];
+    float ci[RG];
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) {
+        const int64_t ib = ibase + 16 * rg;
+        const int64_t ild = ib < row0 + nrows ? ib : row0;
         const int64_t tr = ild / 32;
         const int jsr = (int)((ild / 16) & 1);
 #pragma unroll
         for (int db = 0; db < NDB; ++db)
 #pragma unroll
             for (int part = 0; part < 3; ++part)
-                bR[db][part] = *reinterpret_cast<const uint4 *>(
+                bR[rg][db][part] = *reinterpret_cast<const uint4 *>(
                     B3 + (tr * PT + (jsr * NDB + db) * 3 + part) * 256 + lane * 4);
+        ci[rg] = crow[ild + lo];
     }
-    const float ci = crow[ild + lo];
 
-    f4_t acc[NCB];
+    f4_t acc[RG][NCB];
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) acc[cb] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
-    float ps = 0.0f; // S1V: this lane's share of sum_j P_ij, i = lo
+    for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb) acc[rg][cb] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    float ps[RG]; // S1V: this lane's share of sum_j P_ij, i = lo of each row group
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) ps[rg] = 0.0f;
 
     auto issue = [&](int64_t t, int b) {
         const char *g = reinterpret_cast<const char *>(B3 + t * BUF);
@@ -3536,8 +3541,9 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     // part products (A part, B part), smallest first
     constexpr int TA[6] = {1, 0, 2, 0, 1, 0}, TB_[6] = {1, 2, 0, 1, 0, 0};
     // P.V of a tile whose P parts are in aP, its V parts in LDS buffer lv:
-    // by V part (l, m, h), each part's terms across the NCB blocks
-    auto pv_mfma = [&](const uint32_t *lv, const uint4 (&aP)[3]) {
+    // by V part (l, m, h), each part's terms across the NCB x RG blocks
+    uint4 aP[RG][3] = {};
+    auto pv_mfma = [&](const uint32_t *lv) {
 #pragma unroll
         for (int vp = 2; vp >= 0; --vp) {
             uint4 bV[NCB];
@@ -3549,7 +3555,9 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
             for (int pp = 2; pp >= 0; --pp) {
                 if (pp + vp > 2) continue;
 #pragma unroll
-                for (int cb = 0; cb < NCB; ++cb) acc[cb] = mfma_b3(aP[pp], bV[cb], acc[cb]);
+                for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+                    for (int rg = 0; rg < RG; ++rg) acc[rg][cb] = mfma_b3(aP[rg][pp], bV[cb], acc[rg][cb]);
             }
         }
     };
@@ -3558,19 +3566,15 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     // iteration, its V parts still in buffer (t-1) % 3), and forms tile t's P
     // on the VALU while those are in the matrix pipe.  The DMA of tile t+1
     // goes to buffer (t+1) % 3, whose tile (t-2) every wave finished before
-    // this iteration's barrier.
-    // Stagger (SVGD_B3_STAGGER, 8-wave blocks): waves 4-7 share the SIMDs of
-    // waves 0-3 and would run the same MFMA / VALU phases in lockstep; they
-    // keep tile t-1's Gram in registers across the barrier and run each
-    // iteration VALU-first -- P(t-1), P.V(t-1), then Gram(t) -- so one wave
-    // of each SIMD pair forms P while the other is in the matrix pipe.  The
-    // same MFMAs in the same order per wave: results bit for bit unchanged.
-    uint4 aP[3] = {};
-    auto gram = [&](const uint32_t *lb, f4_t (&dot)[2][NDB]) {
+    // this iteration's barrier.  (Round 4 measured a staggered order --
+    // waves 4-7 VALU-first -- 6 % slower per clock: profiles/r04_b3_ab.txt.)
+    auto gram = [&](const uint32_t *lb, f4_t (&dot)[RG][2][NDB]) {
 #pragma unroll
-        for (int js = 0; js < 2; ++js)
+        for (int rg = 0; rg < RG; ++rg)
 #pragma unroll
-            for (int db = 0; db < NDB; ++db) dot[js][db] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int js = 0; js < 2; ++js)
+#pragma unroll
+                for (int db = 0; db < NDB; ++db) dot[rg][js][db] = f4_t{0.0f, 0.0f, 0.0f, 0.0f};
         uint4 aX[2][NDB][3];
 #pragma unroll
         for (int js = 0; js < 2; ++js)
@@ -3580,93 +3584,88 @@ __global__ __launch_bounds__(64 * NW) void k_phi_b3(
                 for (int part = 0; part < 3; ++part)
                     aX[js][db][part] =
                         *reinterpret_cast<const uint4 *>(lb + ((js * NDB + db) * 3 + part) * 256 + lane * 4);
-        // dot[js][db] (4 independent chains at KP = 64), term by term
+        // dot[rg][js][db] (4 RG independent chains at KP = 64), term by term
 #pragma unroll
         for (int tm = 0; tm < 6; ++tm)
 #pragma unroll
             for (int js = 0; js < 2; ++js)
 #pragma unroll
                 for (int db = 0; db < NDB; ++db)
-                    dot[js][db] = mfma_b3(aX[js][db][TA[tm]], bR[db][TB_[tm]], dot[js][db]);
+#pragma unroll
+                    for (int rg = 0; rg < RG; ++rg)
+                        dot[rg][js][db] = mfma_b3(aX[js][db][TA[tm]], bR[rg][db][TB_[tm]], dot[rg][js][db]);
     };
     // P of a tile from its Gram (its c_j in LDS buffer lb) -> aP, row sums
-    auto form_p = [&](const uint32_t *lb, const f4_t (&dot)[2][NDB]) {
-        float pv[8]; // P[i = lo][j = 16js + 4hi + r] at k-slot 4js + r
+    auto form_p = [&](const uint32_t *lb, const f4_t (&dot)[RG][2][NDB]) {
+        f4_t cj[2];
 #pragma unroll
-        for (int js = 0; js < 2; ++js) {
-            f4_t dd = dot[js][0];
+        for (int js = 0; js < 2; ++js)
+            cj[js] = *reinterpret_cast<const f4_t *>(lb + (6 * NDB + 3 * NCB + js) * 256 + lane * 4);
 #pragma unroll
-            for (int db = 1; db < NDB; ++db) dd += dot[js][db];
-            const f4_t cj = *reinterpret_cast<const f4_t *>(lb + (6 * NDB + 3 * NCB + js) * 256 + lane * 4);
+        for (int rg = 0; rg < RG; ++rg) {
+            float pv[8]; // P[i = lo][j = 16js + 4hi + r] at k-slot 4js + r
 #pragma unroll
-            for (int r = 0; r < 4; ++r) pv[4 * js + r] = exp2_nonpos(fmaf(alpha, dd[r], ci + cj[r]));
-        }
-        if (S1V) {
+            for (int js = 0; js < 2; ++js) {
+                f4_t dd = dot[rg][js][0];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) ps += pv[q];
-        }
-        uint32_t wd[3][4];
+                for (int db = 1; db < NDB; ++db) dd += dot[rg][js][db];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            float x0 = pv[2 * q], x1 = pv[2 * q + 1];
+                for (int r = 0; r < 4; ++r) pv[4 * js + r] = exp2_nonpos(fmaf(alpha, dd[r], ci[rg] + cj[js][r]));
+            }
+            if (S1V) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) ps[rg] += pv[q];
+            }
+            uint32_t wd[3][4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float x0 = pv[2 * q], x1 = pv[2 * q + 1];
+#pragma unroll
+                for (int part = 0; part < 3; ++part)
+                    wd[part][q] = SVGD_B3_TRUNC ? b3_trunc_pair(x0, x1) : b3_split_pair(x0, x1);
+            }
 #pragma unroll
             for (int part = 0; part < 3; ++part)
-                wd[part][q] = SVGD_B3_TRUNC ? b3_trunc_pair(x0, x1) : b3_split_pair(x0, x1);
+                aP[rg][part] = make_uint4(wd[part][0], wd[part][1], wd[part][2], wd[part][3]);
         }
-#pragma unroll
-        for (int part = 0; part < 3; ++part) aP[part] = make_uint4(wd[part][0], wd[part][1], wd[part][2], wd[part][3]);
     };
     auto buf = [&](int64_t t) { return sbuf + (int)(t % 3) * BUF; };
-    const bool lag = SVGD_B3_STAGGER && NW == 8 && w >= 4;
     if (ntiles > 0) issue(0, 0);
-    if (!lag) {
-        for (int64_t t = 0; t < ntiles; ++t) {
-            const int b = (int)(t % 3);
-            wait_vmcnt<0>();
-            __syncthreads();
-            if (t + 1 < ntiles) issue(t + 1, b == 2 ? 0 : b + 1);
-            f4_t dot[2][NDB];
-            gram(buf(t), dot);
-            if (t > 0) pv_mfma(buf(t - 1), aP);
-            form_p(buf(t), dot);
-        }
-        if (ntiles > 0) pv_mfma(buf(ntiles - 1), aP); // (its buffer is intact: no DMA after it)
-    } else {
-        f4_t dotc[2][NDB]; // tile t-1's Gram, carried across the barrier
-        for (int64_t t = 0; t < ntiles; ++t) {
-            const int b = (int)(t % 3);
-            wait_vmcnt<0>();
-            __syncthreads();
-            if (t + 1 < ntiles) issue(t + 1, b == 2 ? 0 : b + 1);
-            if (t > 0) {
-                form_p(buf(t - 1), dotc);
-                pv_mfma(buf(t - 1), aP);
-            }
-            gram(buf(t), dotc);
-        }
-        if (ntiles > 0) {
-            form_p(buf(ntiles - 1), dotc);
-            pv_mfma(buf(ntiles - 1), aP);
-        }
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const int b = (int)(t % 3);
+        wait_vmcnt<0>();
+        __syncthreads();
+        if (t + 1 < ntiles) issue(t + 1, b == 2 ? 0 : b + 1);
+        f4_t dot[RG][2][NDB];
+        gram(buf(t), dot);
+        if (t > 0) pv_mfma(buf(t - 1));
+        form_p(buf(t), dot);
     }
+    if (ntiles > 0) pv_mfma(buf(ntiles - 1)); // (its buffer is intact: no DMA after it)
 
     // epilogue (fp64): acc lane map row i = 4 hi + q, column c = lo (+16 cb)
     if (S1V) { // the 4 lane groups' shares of row lo, in a fixed tree
-        ps += __shfl_xor(ps, 16);
-        ps += __shfl_xor(ps, 32);
+#pragma unroll
+        for (int rg = 0; rg < RG; ++rg) {
+            ps[rg] += __shfl_xor(ps[rg], 16);
+            ps[rg] += __shfl_xor(ps[rg], 32);
+        }
     }
     __syncthreads();
-    float *sAcc = reinterpret_cast<float *>(sbuf) + w * 16 * (VW + 1);
-    static_assert(NW * 16 * (VW + 1) <= 3 * BUF, "epilogue tiles exceed the buffers");
+    float *sAcc = reinterpret_cast<float *>(sbuf) + w * 16 * RG * (VW + 1);
+    static_assert(NW * 16 * RG * (VW + 1) <= 3 * BUF, "epilogue tiles exceed the buffers");
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb)
+    for (int rg = 0; rg < RG; ++rg) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) sAcc[(4 * hi + q) * (VW + 1) + cb * 16 + lo] = acc[cb][q];
-    if (S1V && hi == 0) sAcc[lo * (VW + 1) + VW] = ps;
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) sAcc[(16 * rg + 4 * hi + q) * (VW + 1) + cb * 16 + lo] = acc[rg][cb][q];
+        if (S1V && hi == 0) sAcc[(16 * rg + lo) * (VW + 1) + VW] = ps[rg];
+    }
     __syncthreads();
     const double two_a = 2.0 * a;
     const int s1c = S1V ? VW : d;
-    for (int e = lane; e < 16 * d; e += 64) {
+    for (int e = lane; e < 16 * RG * d; e += 64) {
         const int il = e / d, c = e - il * d;
         const int64_t i = ibase + il;
         if (i - row0 < nrows) {
@@ -4683,34 +4682,39 @@ hipError_t launch_swz_b3(const double *x, int KP, const double *V, int VW, const
 #ifndef SVGD_B3_NW
 #define SVGD_B3_NW 8
 #endif
+#define SVGD_PHIB3_LAUNCH(KPv, NCBv, S1Vv, RGv)                                               \
+    hipLaunchKernelGGL((k_phi_b3<KPv, NCBv, SVGD_B3_NW, S1Vv, RGv>),                            \
+                       dim3((nrows + 16 * RGv * SVGD_B3_NW - 1) / (16 * RGv * SVGD_B3_NW)),     \
+                       dim3(64 * SVGD_B3_NW), 0, stream, B3, crow, a_ptr, row0, nrows, ntiles, d, \
+                       inv_n, wv, xc, xc_stride, phi, opt ? *opt : OptArgs{}, opt ? 1 : 0)
 #define SVGD_PHIB3_CASE(KPv, NCBv)                                                           \
     if (KP == KPv && NCB == NCBv) {                                                          \
-        if (d == 16 * NCBv)                                                                   \
-            hipLaunchKernelGGL((k_phi_b3<KPv, NCBv, SVGD_B3_NW, true>), dim3(grid),           \
-                               dim3(64 * SVGD_B3_NW), 0, stream, B3, crow, a_ptr, row0, nrows, \
-                               ntiles, d, inv_n, wv, xc, xc_stride, phi,                      \
-                               opt ? *opt : OptArgs{}, opt ? 1 : 0);                          \
+        if (d == 16 * NCBv && rg2)                                                            \
+            SVGD_PHIB3_LAUNCH(KPv, NCBv, true, 2);                                            \
+        else if (d == 16 * NCBv)                                                              \
+            SVGD_PHIB3_LAUNCH(KPv, NCBv, true, 1);                                            \
+        else if (rg2)                                                                         \
+            SVGD_PHIB3_LAUNCH(KPv, NCBv, false, 2);                                           \
         else                                                                                  \
-            hipLaunchKernelGGL((k_phi_b3<KPv, NCBv, SVGD_B3_NW, false>), dim3(grid),          \
-                               dim3(64 * SVGD_B3_NW), 0, stream, B3, crow, a_ptr, row0, nrows, \
-                               ntiles, d, inv_n, wv, xc, xc_stride, phi,                      \
-                               opt ? *opt : OptArgs{}, opt ? 1 : 0);                          \
+            SVGD_PHIB3_LAUNCH(KPv, NCBv, false, 1);                                           \
         return hipGetLastError();                                                            \
     }
+int phi_b3_rows_per_wg(int rg) { return 16 * rg * SVGD_B3_NW; }
 hipError_t launch_phi_b3(int KP, int NCB, const uint32_t *B3, const float *crow,
                          const double *a_ptr, int64_t row0, int64_t nrows, int64_t ntiles, int d,
                          double inv_n, const double *wv, const double *xc, int xc_stride,
-                         double *phi, const OptArgs *opt, hipStream_t stream)
+                         double *phi, const OptArgs *opt, int rg, hipStream_t stream)
 {
     if (nrows <= 0) return hipSuccess;
     if (row0 % 16) return hipErrorInvalidValue; // (waves own 16-row groups of the padded rows)
-    const int64_t grid = (nrows + 16 * SVGD_B3_NW - 1) / (16 * SVGD_B3_NW);
+    const bool rg2 = rg == 2;
     SVGD_PHIB3_CASE(32, 1) SVGD_PHIB3_CASE(32, 2) SVGD_PHIB3_CASE(32, 3)
     SVGD_PHIB3_CASE(64, 1) SVGD_PHIB3_CASE(64, 2) SVGD_PHIB3_CASE(64, 3) SVGD_PHIB3_CASE(64, 4)
     SVGD_PHIB3_CASE(64, 5)
     return hipErrorInvalidValue;
 }
 #undef SVGD_PHIB3_CASE
+#undef SVGD_PHIB3_LAUNCH
 
 // fp32 norms for the tile-path median passes: rows [n, np) get +inf, so a
 // padding particle's v = fma(2, dot, -n_i - n_j) is -inf (never below, never

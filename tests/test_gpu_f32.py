@@ -165,6 +165,30 @@ def test_b3_tile_phi_matches_oracle(oracle, monkeypatch, n, d):
     assert np.max(np.abs(out["1"] - out["0"])) <= REL * scale
 
 
+@pytest.mark.parametrize("n,d", [(300, 64), (4096, 64), (2049, 33), (3001, 48), (777, 32)])
+def test_b3_two_row_groups_bit_identical(oracle, monkeypatch, n, d):
+    """k_phi_b3 with two 16-row groups per wave (SVGD_PHI_B3_RG=2, the default
+    once every CU gets a 256-row work-group: cfg5) runs the same MFMAs into
+    the same accumulators in the same order as one row group per wave: phi
+    bit-identical, ragged N (a partial last row group) included; and within
+    the F32 tolerance of the oracle."""
+    X = oracle.splitmix((n, d), 2.0, 5 * n + d)
+    G = oracle.splitmix((n, d), 1.0, 5 * n + d + 1)
+    a = 0.7 / d
+    out = {}
+    for rg in ("1", "2"):
+        monkeypatch.setenv("SVGD_PHI_B3_RG", rg)
+        c = S.Context(d, n, dtype=C.SVGD_F32)
+        c.set_particles(X)
+        out[rg] = c.phi(G, a)
+        name = c.phi_kernel_name()
+        c.close()
+        assert name.startswith("k_phi_b3") and name.endswith(", %s>" % rg), name
+    assert np.array_equal(out["1"], out["2"])
+    ref = oracle.phi(X, G, a)
+    assert np.max(np.abs(out["2"] - ref)) <= REL * np.max(np.abs(ref))
+
+
 def test_b3_matrix_scale_and_step(oracle, monkeypatch):
     """k_phi_b3 under a full-matrix scale (whitened coordinates) and inside
     the fused step (optimizer epilogue) against the fp64 oracle."""
