@@ -1771,16 +1771,11 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     c->plan_world = plan_world;
     svgd_plan_rows(n, plan_world, c->rank, &c->row0, &c->row1);
     c->nrows = c->row1 - c->row0;
-    // k_phi_b3 with two 16-row groups per wave (half its LDS reads and
-    // barriers per MFMA) when that still gives every CU a work-group;
-    // SVGD_PHI_B3_RG=1 / 2 forces one (tests)
-    if (c->want_b3) {
-        int ncu = 256;
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, device) == hipSuccess) ncu = prop.multiProcessorCount;
-        c->b3_rg = c->nrows >= (int64_t)phi_b3_rows_per_wg(2) * ncu ? 2 : 1;
+    // k_phi_b3 with one 16-row group per wave, or two (SVGD_PHI_B3_RG=2:
+    // half its LDS reads and barriers per MFMA, a measured wash at cfg5 on the
+    // power-limited chip, profiles/r06_b3_rg_il_ab.txt)
+    if (c->want_b3)
         if (const char *e = std::getenv("SVGD_PHI_B3_RG")) c->b3_rg = std::atoi(e) == 2 ? 2 : 1;
-    }
     c->pblock = SVGD_PAIR_BLOCK_DT(dim, dtype);
     c->pnb = (n + c->pblock - 1) / c->pblock;
     c->own_tiles = svgd_plan_pair_tiles(n, c->pblock, plan_world, c->rank);

@@ -3376,6 +3376,7 @@ __device__ __forceinline__ uint32_t b3_trunc_pair(float &x0, float &x1)
 #ifndef SVGD_B3_TRUNC
 #define SVGD_B3_TRUNC 1
 #endif
+
 __device__ __forceinline__ uint32_t b3_split_pair(float &x0, float &x1)
 {
     // bf16(x0) | bf16(x1) << 16 (round to nearest even), and the residuals
@@ -3486,7 +3487,14 @@ __device__ __forceinline__ f4_t mfma_b3(uint4 a, uint4 b, f4_t c)
 // the one before it.  RG row groups of 16 per wave (RG = 2 at large row
 // counts, round 6): each tile's column parts, read from LDS once, feed RG
 // times the MFMAs -- half the LDS reads and half the barriers per MFMA at
-// RG = 2 (2 waves per SIMD at ~200 VGPRs instead of 4 at 128).
+// RG = 2 (2 waves per SIMD at 198 VGPRs instead of 4 at 128).  Measured at
+// cfg5 (profiles/r06_b3_rg_il_ab.txt): RG = 2 takes ~15 % more cycles per
+// launch but draws less power, so the power-limited chip clocks it ~13 %
+// higher -- a wash that moved with the box (step 7.16 vs 7.45 ms on one,
+// 7.48 vs 7.14 on another); interleaving the P.V MFMAs with P's VALU
+// (sched_group_barrier) recovered ~4 % per clock at RG = 2 and lost 27 % at
+// RG = 1.  Default RG = 1; SVGD_PHI_B3_RG=2 selects the other (tests: both
+// bit-identical).
 template <int KP, int NCB, int NW, bool S1V, int RG = 1>
 __global__ __launch_bounds__(64 * NW) void k_phi_b3(
     const uint32_t *__restrict__ B3, const float *__restrict__ crow, const double *__restrict__ a_ptr,

@@ -167,8 +167,8 @@ def test_b3_tile_phi_matches_oracle(oracle, monkeypatch, n, d):
 
 @pytest.mark.parametrize("n,d", [(300, 64), (4096, 64), (2049, 33), (3001, 48), (777, 32)])
 def test_b3_two_row_groups_bit_identical(oracle, monkeypatch, n, d):
-    """k_phi_b3 with two 16-row groups per wave (SVGD_PHI_B3_RG=2, the default
-    once every CU gets a 256-row work-group: cfg5) runs the same MFMAs into
+    """k_phi_b3 with two 16-row groups per wave (SVGD_PHI_B3_RG=2; a measured
+    wash against one at cfg5, profiles/r06_b3_rg_il_ab.txt) runs the same MFMAs into
     the same accumulators in the same order as one row group per wave: phi
     bit-identical, ragged N (a partial last row group) included; and within
     the F32 tolerance of the oracle."""
