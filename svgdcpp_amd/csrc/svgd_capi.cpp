@@ -133,8 +133,10 @@ struct svgd_ctx {
     // a second communicator (ncclCommSplit of comm) for the G all-gather on
     // its own stream: it overlaps the median chain's kernels and collectives
     // (one communicator's operations would run in issue order behind them).
-    // Opt-in (SVGD_G_COMM=1, the same on every rank) until a P >= 2 RCCL run
-    // has exercised it; the split's outcome is agreed across ranks.
+    // On by default for P >= 2 over RCCL since round 6 (SVGD_G_COMM=0 on
+    // every rank keeps the G all-gather on comm; =1 also splits a one-rank
+    // communicator, the test form); the split's outcome is agreed across
+    // ranks.
     //
     // Cross-communicator issue order (the invariant both communicators rely
     // on): within a step every rank issues
@@ -2130,13 +2132,15 @@ int svgd_create_dist(svgd_ctx **out, int dim, int64_t n, int dtype, int device, 
         ncclUniqueId id;
         std::memcpy(&id, unique_id128, sizeof(id));
         NCCLCHK(c, ncclCommInitRank(&c->comm, world, id, rank));
-        // the G all-gather's own communicator and stream (upload_g_finish),
-        // opt-in: SVGD_G_COMM=1 on every rank (the split is collective).
+        // the G all-gather's own communicator and stream (upload_g_finish):
+        // by default at P >= 2, so the all-gather of G runs beside the median
+        // (15-30 us off the P = 8 critical path); SVGD_G_COMM=0 /
+        // 1 on every rank forces it off / on (the split is collective).
         // Every rank learns whether every split succeeded (a min all-reduce
         // over comm): one rank gathering G on gcomm while another gathers it
         // on comm would hang both, so any failure drops gcomm everywhere and
         // the G all-gather stays on the compute stream.
-        bool want_g = false;
+        bool want_g = world > 1;
         if (const char *e = std::getenv("SVGD_G_COMM")) want_g = std::atoi(e) != 0;
         if (want_g) {
             int ok = ncclCommSplit(c->comm, 0, rank, &c->gcomm, nullptr) == ncclSuccess && c->gcomm;
