@@ -479,7 +479,10 @@ def main():
     ctx.sync()
     ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))  # drop warmup events
     ctx.diagnostics()  # (reset)
-    ctx.check(ctx.lib.svgd_set_timing(ctx.h, 1))
+    # the timed runs carry no timing events at all (the product path: an
+    # event between two kernels costs a ~6 us dispatch gap); the phase split
+    # comes from the diagnostic pass below
+    ctx.check(ctx.lib.svgd_set_timing(ctx.h, 0))
 
     # the median of `repeats` timed runs of exactly K steps, each
     # bracketed by barrier + device sync; the GPU's clock/power sampled by
@@ -498,9 +501,7 @@ def main():
         runs.append(time.perf_counter() - t0)
     gpu_timed = mon.stop()
     phi_ms, med_ms, cnt = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
-    ctx.check(ctx.lib.svgd_get_timing(ctx.h, ctypes.byref(phi_ms), ctypes.byref(med_ms), ctypes.byref(cnt)))
     host_timed = ctx.diagnostics()  # host-side clocks of the timed steps (always on)
-    nsteps_timed = args.steps * args.repeats
 
     # diagnostic pass (untimed): the phi kernel alone, the device's wait for
     # G before the phi chain, collectives -- extra events, so not in the runs
@@ -514,7 +515,7 @@ def main():
         ctx.sync()
         gpu_diag = mon.stop()
         diag = ctx.diagnostics()
-        ctx.check(ctx.lib.svgd_get_timing(ctx.h, None, None, None))
+        ctx.check(ctx.lib.svgd_get_timing(ctx.h, ctypes.byref(phi_ms), ctypes.byref(med_ms), ctypes.byref(cnt)))
         ctx.check(ctx.lib.svgd_set_timing(ctx.h, 0))
 
     a, med, path = ctx.last_scale()
@@ -531,12 +532,15 @@ def main():
 
     mine = {
         "rank": rank, "rows": rows,
-        # phase events sit at phase boundaries only (svgd_set_timing level 1):
+        # phase events at phase boundaries, from the diagnostic pass (level 2:
+        # its extra events make these spans a few us longer than the timed
+        # steps'):
         # "phi" runs from the median's end (so it holds any wait for G) to the
         # update's end, "median" from the previous step's end (so it holds the
         # gap between steps) to the scale; the diagnostic pass separates both
-        "phases_ms_per_step": {"phi_incl_wait_for_g": per_step(phi_ms.value, nsteps_timed),
-                               "median_incl_step_gap": per_step(med_ms.value, nsteps_timed)},
+        "phases_ms_per_step": {"phi_incl_wait_for_g": per_step(phi_ms.value, args.steps if diag is not None else 0),
+                               "median_incl_step_gap": per_step(med_ms.value, args.steps if diag is not None else 0),
+                               "source": "diagnostic pass"},
         "host_ms_per_step": {"grad": per_step(host_timed["host_grad_ms"], host_timed["steps"]),
                              "xwait": per_step(host_timed["host_xwait_ms"], host_timed["steps"]),
                              "job": per_step(host_timed["host_job_ms"], host_timed["steps"]),

@@ -163,9 +163,10 @@ template <class T> static int allreduce_sum(HostComm *c, T *dbuf, size_t cnt, hi
 // into drecv + recv[3q+2] * w.  Faithful to what a peer can see: the slot's
 // data is NaN except the ranges this rank sends, every sender's ranges are
 // published in its slot's header and a receiver whose expected range differs
-// fails (-4); drecv is NaN-filled before the pieces land, and dsend's rows
-// outside [own0, own1) come back as NaN (the caller may read its own rows
-// only).  Returns 0 on success.
+// fails (-4); drecv is NaN-filled before the pieces land.  (own0, own1: the
+// caller's rows, unused here: like ncclSend, the send buffer is left as it
+// was -- the caller's finish writes only the particles its units touch, so
+// rows between a range's pieces keep their zeros.)  Returns 0 on success.
 int hostcomm_exchange_f64(HostComm *c, double *dsend, size_t n, size_t w, const int64_t *send,
                           double *drecv, size_t recv_rows, const int64_t *recv, int64_t own0, int64_t own1,
                           hipStream_t stream)
@@ -208,13 +209,6 @@ int hostcomm_exchange_f64(HostComm *c, double *dsend, size_t n, size_t w, const 
                 rc = -3;
         }
     }
-    // the send buffer outside the rank's own rows: undefined for the caller
-    if (!rc && own0 > 0 && hipMemsetAsync(dsend, 0xff, (size_t)own0 * w * sizeof(double), stream) != hipSuccess)
-        rc = -3;
-    if (!rc && (size_t)own1 < n &&
-        hipMemsetAsync(dsend + (size_t)own1 * w, 0xff, (n - (size_t)own1) * w * sizeof(double), stream) !=
-            hipSuccess)
-        rc = -3;
     const int brc = c->barrier();
     return rc ? rc : brc;
 }

@@ -378,6 +378,9 @@ struct svgd_ctx {
     // end and -- while no work was queued after it (mark) -- the phi phase's
     // start.
     hipEvent_t ev_status_use = nullptr, ev_fin_use = nullptr, mark = nullptr;
+    // timing off: the speculative step's status is known from this sequence
+    // number, stored by the selection into h_trk[8] (no event); 0: by event
+    uint64_t status_seq = 0, seq_ctr = 0;
     // likewise at the step's end: the phi phase's end event (timing) doubles
     // as X_t-final for the copy stream (ev_xready_use) when nothing follows it
     hipEvent_t phi_end = nullptr, ev_xready_use = nullptr;
@@ -1088,13 +1091,25 @@ int median_finish_spec(svgd_ctx *c, double logn)
     HIPCHK(c, launch_compact_buckets(c->regions, c->counts, c->nregions, c->reg_cap, c->st, seg, cap,
                                      c->d_status, c->stream, &pa));
     CHK(allgather_u64(c, c->gseg, (size_t)cap + 1));
+    // the plan's status is final once the selection completes.  Timing off
+    // (the product path): no event at all -- the selection stores a sequence
+    // number into pinned memory after its last store and resolve_pending
+    // polls it (an event between two kernels costs a ~6 us dispatch gap,
+    // profiles/r06_step_timeline_*); with phase timing the phase event there
+    // serves.  (c->pending -- the plan's status to check -- is set when the
+    // step is complete, by median_finish: resolve_pending never redoes half a
+    // step.)
+    const bool by_seq = !c->timing && c->tlevel < 2;
+    c->status_seq = by_seq ? ++c->seq_ctr : 0;
     HIPCHK(c, launch_select_small(c->st, c->gseg, c->world, cap, c->navg, c->src_lo, c->src_hi, logn,
-                                  c->scal, c->d_status, c->stream, c->h_trk_dev));
+                                  c->scal, c->d_status, c->stream, c->h_trk_dev, c->status_seq));
     c->trk_keys = true;
-    // the plan's status is final once this completes (recorded after the
-    // selection: an event between two kernels costs a ~5 us dispatch gap)
-    // (c->pending -- the plan's status to check -- is set when the step is
-    // complete, by median_finish: resolve_pending never redoes half a step)
+    if (by_seq) {
+        c->ev_status_use = nullptr;
+        c->med_ev_done = true; // (no scale-final event either: fetch_scale syncs the stream)
+        c->mark = nullptr;
+        return SVGD_OK;
+    }
     if (c->timing && !c->ev_med.empty()) {
         c->ev_status_use = c->ev_med.back().b; // also the median phase's end
         c->med_ev_done = true;
@@ -1649,7 +1664,8 @@ int scale_finish(svgd_ctx *c)
 int fetch_scale(svgd_ctx *c)
 {
     if (c->scal_fresh) return SVGD_OK;
-    HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_fin_use ? c->ev_fin_use : c->ev_fin, 0));
+    if (c->status_seq && !c->ev_fin_use) HIPCHK(c, hipStreamSynchronize(c->stream)); // (no scale-final event)
+    else HIPCHK(c, hipStreamWaitEvent(c->cstream, c->ev_fin_use ? c->ev_fin_use : c->ev_fin, 0));
     HIPCHK(c, hipMemcpyAsync(c->h_scal, c->scal, 2 * sizeof(double), hipMemcpyDeviceToHost,
                              c->cstream));
     HIPCHK(c, hipEventRecord(c->ev_scal, c->cstream));
@@ -1684,7 +1700,30 @@ int resolve_pending(svgd_ctx *c)
     CHK(trk_resolve_sync(c));
     if (!c->pending) return SVGD_OK;
     c->pending = false;
-    HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
+    if (c->status_seq) {
+        // the selection's sequence number in pinned memory (median_finish_spec)
+        volatile uint64_t *sq = c->h_trk + 8;
+        const auto t0 = std::chrono::steady_clock::now();
+        auto t_idle = t0;
+        bool idle = false;
+        while (*sq != c->status_seq) {
+            const auto now = std::chrono::steady_clock::now();
+            // the stream has drained and the number is still not there (a
+            // bounded grace for the store's visibility): an error, not a hang
+            if (!idle && hipStreamQuery(c->stream) == hipSuccess) {
+                idle = true;
+                t_idle = now;
+            }
+            if (idle && now - t_idle > std::chrono::milliseconds(200))
+                return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] the selection did not publish its status.");
+            if (now - t0 > std::chrono::seconds(300))
+                return fail(c, SVGD_ERR_RUNTIME, "[Runtime Error] timed out waiting for the median's status.");
+            std::this_thread::yield();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    } else {
+        HIPCHK(c, hipEventSynchronize(c->ev_status_use ? c->ev_status_use : c->ev_status));
+    }
     if (*c->h_status == 0) {
         c->last_tot = (int64_t)c->h_trk[7];
         if (c->trk_allowed) trk_record(c, c->h_trk[0], c->h_trk[1], c->h_trk[3]);
@@ -2017,8 +2056,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     HIPCHK(c, hipHostMalloc((void **)&c->h_status, sizeof(int), hipHostMallocCoherent));
     *c->h_status = 0;
     HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_status_dev, c->h_status, 0));
-    HIPCHK(c, hipHostMalloc((void **)&c->h_trk, 8 * sizeof(uint64_t), hipHostMallocCoherent));
-    std::memset(c->h_trk, 0, 8 * sizeof(uint64_t));
+    HIPCHK(c, hipHostMalloc((void **)&c->h_trk, 16 * sizeof(uint64_t), hipHostMallocCoherent));
+    std::memset(c->h_trk, 0, 16 * sizeof(uint64_t));
     HIPCHK(c, hipHostGetDevicePointer((void **)&c->h_trk_dev, c->h_trk, 0));
     if (const char *e = std::getenv("SVGD_SPECULATE")) c->spec_allowed = std::atoi(e) != 0;
     if (const char *e = std::getenv("SVGD_TRACK_BRACKET")) c->trk_allowed = std::atoi(e) != 0;

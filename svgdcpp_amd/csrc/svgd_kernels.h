@@ -184,7 +184,8 @@ hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, 
 // trk (optional, pinned host memory): [4], [5] <- the selected keys, [6] <- error
 hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
                                int navg, int src_lo, int src_hi, double logn, double *scal,
-                               const int *status, hipStream_t stream, uint64_t *trk = nullptr);
+                               const int *status, hipStream_t stream, uint64_t *trk = nullptr,
+                               uint64_t seq = 0); // seq: stored into trk[8] at the end (spec steps)
 // Device-side bucket plan from the all-reduced counts (speculative step): the
 // select state, seg[0] = 0 and *status = 0, or *status = 1 (bracket miss),
 // 2 (overflowed region), 3 (selected buckets hold > capr keys), also stored to

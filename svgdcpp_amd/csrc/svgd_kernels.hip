@@ -1534,12 +1534,12 @@ __device__ __forceinline__ unsigned long long block_scan_1024(unsigned long long
 // arithmetic): scal = [a, med].
 __device__ __forceinline__ void finalize_scale(const SelState *st, int navg, int src_lo, int src_hi,
                                                double logn, double *a_out, double *med_out);
-__global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint64_t *__restrict__ segs,
-                                                      int nseg, int64_t seg_cap, int navg,
-                                                      int src_lo, int src_hi, double logn,
-                                                      double *__restrict__ scal,
-                                                      const int *__restrict__ status,
-                                                      uint64_t *__restrict__ trk)
+__device__ __forceinline__ void select_small_body(SelState *st, const uint64_t *__restrict__ segs,
+                                                  int nseg, int64_t seg_cap, int navg,
+                                                  int src_lo, int src_hi, double logn,
+                                                  double *__restrict__ scal,
+                                                  const int *__restrict__ status,
+                                                  uint64_t *__restrict__ trk)
 {
     if (status && *status != 0) return; // the device plan found no bucket path
     __shared__ uint32_t sHist[2][RADIX];
@@ -1750,6 +1750,24 @@ __global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint6
             trk[5] = nsel > 1 ? prefix[1] : prefix[0];
             trk[6] = err ? 1 : 0;
         }
+    }
+}
+// seq (speculative steps at timing level 0): after the selection, thread 0
+// -- the one that wrote trk -- stores seq into trk[8], system-scope after its
+// other stores; the host polls it instead of an event between this kernel
+// and the next (an event record there cost a ~6 us dispatch gap per step).
+// The plan's status in pinned memory was stored by an earlier kernel.
+__global__ __launch_bounds__(1024) void k_select_small(SelState *st, const uint64_t *__restrict__ segs,
+                                                      int nseg, int64_t seg_cap, int navg,
+                                                      int src_lo, int src_hi, double logn,
+                                                      double *__restrict__ scal,
+                                                      const int *__restrict__ status,
+                                                      uint64_t *__restrict__ trk, uint64_t seq)
+{
+    select_small_body(st, segs, nseg, seg_cap, navg, src_lo, src_hi, logn, scal, status, trk);
+    if (seq && trk && threadIdx.x == 0) {
+        __threadfence_system();
+        *reinterpret_cast<volatile uint64_t *>(trk + 8) = seq;
     }
 }
 
@@ -3038,9 +3056,10 @@ __device__ __forceinline__ void sym_fb_phi(const SymFallback &fb, const double *
 // every row and column partial of p in a fixed order, then the optimizer.
 // A block owns 256 / (d+1) particles, one thread per (particle, component).
 // The partials are those of the units [U0, U1) (this rank's) run by G
-// work-groups.  contrib (P > 1): instead of phi, S_p of EVERY particle from
-// this rank's units alone -> contrib[p * DP + k] (rows [row0, row0 + nrows)
-// = all N), the input of the reduce-scatter; k_sym_apply then forms phi.
+// work-groups.  contrib (P > 1): instead of phi, S_p from this rank's units
+// alone -> contrib[p * DP + k] for the particles those units touch (rows
+// [row0, row0 + nrows) a cyclic run, p taken mod nwrap), the send buffer of
+// the point-to-point exchange; k_sym_apply then forms phi.
 template <int D>
 __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ rowpart,
                                                     const double *__restrict__ colpart,
@@ -3052,7 +3071,7 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
                                                     const int *__restrict__ symok, int64_t row0,
                                                     int64_t nrows, double inv_n, double *__restrict__ phi,
                                                     OptArgs opt, int do_opt, double *__restrict__ contrib,
-                                                    SymFallback fb)
+                                                    int64_t nwrap, SymFallback fb)
 {
     using Gm = SymGeom<D>;
     constexpr int B = Gm::B, SRS = Gm::SRS, DP = Gm::DP, RB = 256 / DP;
@@ -3071,7 +3090,8 @@ __global__ __launch_bounds__(256) void k_sym_finish(const double *__restrict__ r
     }
     if (e < rows * DP) {
         const int pl_ = e / DP, k = e - pl_ * DP;
-        const int64_t p = row0 + rb + pl_;
+        int64_t p = row0 + rb + pl_;
+        if (nwrap && p >= nwrap) p -= nwrap; // (contrib: a cyclic run of particles)
         const int64_t P = p / B, pl = p - P * B;
         double acc = 0.0;
         // row role: the row sums of the work-groups that visited row block P,
@@ -4954,10 +4974,10 @@ hipError_t launch_compact_buckets(const uint64_t *keys, const uint32_t *counts, 
 
 hipError_t launch_select_small(SelState *st, const uint64_t *segs, int nseg, int64_t seg_cap,
                                int navg, int src_lo, int src_hi, double logn, double *scal,
-                               const int *status, hipStream_t stream, uint64_t *trk)
+                               const int *status, hipStream_t stream, uint64_t *trk, uint64_t seq)
 {
     hipLaunchKernelGGL(k_select_small, dim3(1), dim3(1024), 0, stream, st, segs, nseg, seg_cap,
-                       navg, src_lo, src_hi, logn, scal, status, trk);
+                       navg, src_lo, src_hi, logn, scal, status, trk, seq);
     return hipGetLastError();
 }
 
@@ -5095,12 +5115,18 @@ int phi_sym_blocks_per_cu(int d)
 #define SVGD_SYM_FINISH_CASE(Dv)                                                              \
     case Dv: {                                                                                \
         constexpr int RB = 256 / SymGeom<Dv>::DP;                                             \
-        const int64_t fr0 = a.contrib ? 0 : a.row0, fn = a.contrib ? a.n : a.nrows;           \
+        /* P > 1 (contrib): only the particles this rank's units touch -- the    \
+           row blocks Ia .. Ib and up to SM - 1 blocks ahead, a cyclic run;      \
+           the others' sums stay zero from the allocation and are never sent */  \
+        const int64_t B_ = SymGeom<Dv>::B;                                                    \
+        const int64_t fr0 = a.contrib ? a.Ia * B_ : a.row0;                                   \
+        const int64_t fn = a.contrib ? std::min<int64_t>(a.n, (a.Ib - a.Ia + a.SM) * B_) : a.nrows; \
         if (fn <= 0) return hipSuccess;                                                       \
         hipLaunchKernelGGL((k_sym_finish<Dv>), dim3((fn + RB - 1) / RB), dim3(256), 0,         \
                            stream, a.rowpart, a.colpart, a.srec, a.a_ptr, a.nbs, a.SM, a.Ia,   \
                            a.Ib, a.blkg, a.rbase, a.symok, fr0, fn, a.inv_n, a.phi,            \
-                           opt ? *opt : OptArgs{}, opt ? 1 : 0, a.contrib, fb);               \
+                           opt ? *opt : OptArgs{}, opt ? 1 : 0, a.contrib,                    \
+                           a.contrib ? a.n : (int64_t)0, fb);                                 \
         return hipGetLastError();                                                             \
     }
 

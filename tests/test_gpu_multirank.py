@@ -159,9 +159,9 @@ def test_world8_full_path_vs_one_rank_and_oracle(oracle, n, sym):
     (cfg4's 8-rank form at half its N); n = 65536: cfg3's 8-rank default
     (the sharded symmetric pass from N/P >= 8192) and the row stream forced.  The host backend's
     phi exchange is a faithful point-to-point one -- a receiver sees only the
-    ranges its senders sent (NaN elsewhere), a range the two sides plan
-    differently fails the call, and the send buffer outside the rank's own
-    rows comes back NaN -- so a rank reading sums it was not sent fails here.  Checks:
+    ranges its senders sent (NaN elsewhere) and a range the two sides plan
+    differently fails the call -- so a rank reading sums it was not sent
+    fails here.  Checks:
     the first scale bit-exact vs one rank, later ones to X_t's rounding,
     positions <= 1e-10 vs one rank, the 8 ranks' trajectories identical, and
     one more sharded phi of X_T on 1024 sampled rows (both ends and a rank
