@@ -554,7 +554,11 @@ def main():
         # speculative steps whose median bracket was predicted from the last
         # medians (no sample), and of those the ones redone after a miss
         "tracked_brackets": {"steps": int(host_timed["steps"]), "predicted": int(host_timed["trk_steps"]),
-                             "missed": int(host_timed["trk_miss"])},
+                             "missed": int(host_timed["trk_miss"]),
+                             # the predicted brackets' mean share of the pairs (the
+                             # collect stages and finishes those exactly)
+                             "mean_band_share": (host_timed["trk_band"] / host_timed["trk_steps"]
+                                                 if host_timed.get("trk_steps") else None)},
     }
     # phi launches per step: 2 when the context runs phi in row halves
     # (P > 1 with few gradient threads per rank)

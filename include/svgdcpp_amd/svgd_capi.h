@@ -242,7 +242,8 @@ int svgd_get_timing(svgd_ctx *ctx, double *phi_ms, double *median_ms, int64_t *c
 #define SVGD_DIAG_MIRROR_STEPS 20
 #define SVGD_DIAG_SPEC_STEPS 21
 #define SVGD_DIAG_G_COMM 22
-#define SVGD_DIAG_LEN 23
+#define SVGD_DIAG_TRK_BAND 23 /* sum over tracked steps of the predicted bracket's share of the pairs */
+#define SVGD_DIAG_LEN 24
 int svgd_get_diagnostics(svgd_ctx *ctx, double *out, int cap);
 /* Name and template arguments of the phi kernel this context launches, as
  * rocprofv3 prints them (e.g. "k_phi_rows<8, 4, 8, 8192, 8>"): the key under

@@ -38,7 +38,7 @@ SVGD_MEDIAN_REBRACKET = 3
 DIAG_NAMES = ("steps", "phi_kernel_ms", "phi_kernel_n", "phi_wait_ms", "phi_wait_n", "coll_ms",
               "coll_n", "gather_g_ms", "gather_g_n", "host_grad_ms", "host_xwait_ms",
               "host_job_ms", "host_wait_ms", "ranks", "host_threads", "trk_steps", "trk_miss",
-              "sim_world", "cpu_quota", "split_steps", "mirror_steps", "spec_steps", "g_comm")
+              "sim_world", "cpu_quota", "split_steps", "mirror_steps", "spec_steps", "g_comm", "trk_band")
 SVGD_DIAG_LEN = len(DIAG_NAMES)
 
 _D = ctypes.POINTER(ctypes.c_double)

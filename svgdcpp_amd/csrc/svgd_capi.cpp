@@ -239,6 +239,7 @@ struct svgd_ctx {
     int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
     bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol / _tcol)
     bool mcol_bf16 = true;         // k_pair_mcol's Gram as split bf16 (d <= 8; SVGD_MCOL_BF16=0: f32)
+    uint32_t *xsplit = nullptr;    // its operands, [hi | lo] bf16 x 8 per particle (the centring writes them)
     double band_est = 1.0;         // this step's bracket: expected share of the pairs
     bool samp_shard = false;    // this step's sample is sharded
     int64_t samp_local = 0;     // sample keys held by this rank
@@ -411,6 +412,7 @@ struct svgd_ctx {
     // 1 its keys are in h_trk / h_cnt, 2 it took another path (history restarts)
     int trk_sync = 0;
     int64_t trk_steps = 0, trk_miss = 0;
+    double trk_band_sum = 0;    // their predicted band shares (svgd_get_diagnostics)
     // path counters (svgd_get_diagnostics): steps whose phi ran in two row
     // parts, host-model steps whose gradient read the update's pinned mirror,
     // speculative steps
@@ -711,7 +713,7 @@ int center(svgd_ctx *c, const SelState *st_init = nullptr)
                                  st_init, have ? c->cpart + ps * c->cpart_stride : nullptr,
                                  have ? c->cpart_n[ps] : 0, c->cpart ? c->cpart + cs * c->cpart_stride : nullptr,
                                  c->nmax ? c->nmax + (1 - cs) : nullptr, fused ? c->xcf : nullptr,
-                                 fused ? c->nrmf : nullptr));
+                                 fused ? c->nrmf : nullptr, c->xsplit));
     if (c->cpart) {
         c->cpart_ver[cs] = v;
         c->cpart_n[cs] = center_fold_grid(c->dim, c->np);
@@ -951,6 +953,7 @@ int median_begin(svgd_ctx *c)
             // the centring launch): no sample, no radix passes (k_center
             // zeroed the bucket counts); regions sized for 4x the band
             c->trk_steps += 1;
+            c->trk_band_sum += c->trk_band;
             c->band_est = c->trk_band;
             const int64_t pairs_own = tiles * c->pblock * c->pblock;
             const int64_t total = (int64_t)(4.0 * c->trk_band * (double)pairs_own) + 2048 * c->nregions;
@@ -1053,7 +1056,7 @@ int collect_counts(svgd_ctx *c)
         // (a thin band only: each band pair is staged and finished one by one)
         HIPCHK(c, launch_pair_mcol(c->dim, c->collect_grid, c->xc, c->xf, nmax_cur(c), c->n, c->pnb,
                                    c->tile0, c->tile0 + c->own_tiles, c->regions, c->reg_cap,
-                                   c->counts, c->below, c->st, c->bpart, c->mcol_bf16, c->stream));
+                                   c->counts, c->below, c->st, c->bpart, c->xsplit, c->stream));
     else if (!c->rowpath && c->dtype == SVGD_F32 && c->mcol)
         // fp32 tile path: k_pair_tiles' keys, rows held in VGPRs, no LDS
         HIPCHK(c, launch_pair_tcol(c->KP, c->collect_grid, c->xcf, c->nrmf, c->XK, c->n, c->pnb,
@@ -2026,6 +2029,8 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     // MODE 0) instead of the matrix-core ones (k_pair_mcol / k_pair_tcol)
     if (const char *e = std::getenv("SVGD_COLLECT_FP64")) c->mcol = std::atoi(e) == 0;
     if (const char *e = std::getenv("SVGD_MCOL_BF16")) c->mcol_bf16 = std::atoi(e) != 0;
+    if (c->xf && c->mcol && c->mcol_bf16 && dim <= 8) // the collect's split-bf16 operands (center)
+        CHK(dalloc(c, &c->xsplit, c->np * 8));
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));
@@ -2226,7 +2231,7 @@ int svgd_destroy(svgd_ctx *c)
         if (p) (void)hipFree(p);
     void *obufs[] = {c->sample_keys, c->regions, c->counts, c->below, c->cnt3, c->st, c->ghist,
                      c->xf,          c->nmax,    c->sc_err, c->cbuf, c->ccount, c->d_status,
-                     c->bpart,       c->gseg, c->symok, c->sym_tab, c->xtab_d};
+                     c->bpart,       c->gseg, c->symok, c->sym_tab, c->xtab_d, c->xsplit};
     for (void *p : obufs)
         if (p) (void)hipFree(p);
     void *hbufs[] = {c->h_x, c->h_g, c->h_xm, c->h_cnt, c->h_scal, c->h_err, c->h_status, c->h_trk};
@@ -2818,12 +2823,14 @@ int svgd_get_diagnostics(svgd_ctx *c, double *out, int cap)
                                      (double)c->n_split,
                                      (double)c->n_mirror,
                                      (double)c->n_spec,
-                                     c->gcomm ? 1.0 : 0.0};
+                                     c->gcomm ? 1.0 : 0.0,
+                                     c->trk_band_sum};
     for (int i = 0; i < cap && i < SVGD_DIAG_LEN; ++i) out[i] = v[i];
     for (int k = 0; k < 4; ++k) c->dg_ms[k] = 0, c->dg_cnt[k] = 0;
     c->h_grad_ms = c->h_xwait_ms = c->h_job_ms = c->h_wait_ms = 0;
     c->h_steps = 0;
     c->trk_steps = c->trk_miss = 0;
+    c->trk_band_sum = 0;
     c->n_split = c->n_mirror = c->n_spec = 0;
     return cap < SVGD_DIAG_LEN ? cap : SVGD_DIAG_LEN;
 }

@@ -63,6 +63,7 @@ constexpr int MC_NG = 4;    // 16-row blocks per classification group
 #define SVGD_MCOL_CLS 2
 #endif
 
+
 __device__ __forceinline__ float f32_up(double x)
 {
     float f = (float)x;
@@ -162,9 +163,10 @@ __device__ __forceinline__ void mcol_classify4v(const f4_t &v, float tl, float t
 // vector unit, 4 bcnt + 4 add on the scalar unit: 8 scalar operations fewer
 // per 16 x 16 block than mcol_classify4; the band lanes' per-value masks are
 // formed only in the (rare) staging branch (mcol_band4m).
-__device__ __forceinline__ unsigned long long mcol_classify4m(const float (&x)[4], float w, uint32_t &nbelow)
+__device__ __forceinline__ unsigned long long mcol_classify4m(const float (&x)[4], float w, uint32_t &nbelow,
+                                                              unsigned long long (&l)[4])
 {
-    unsigned long long l0, l1, l2, l3, any;
+    unsigned long long &l0 = l[0], &l1 = l[1], &l2 = l[2], &l3 = l[3], any;
     uint32_t t0, t1;
     float m;
     asm volatile("v_cmp_gt_f32_e64 %[l0], %[x0], %[w]\n\t"
@@ -280,21 +282,8 @@ template <int D> struct McolRow {
 // the sum over |h_j| + 1.02 S: in all <= 3.4e-5 nmax.  MCOL_DELTA_BF =
 // 2^-14 nmax (1.8x that) plus 2^-100 for flushed denormals.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-__device__ __forceinline__ uint4 mcol_split_bf16(const float (&x)[8], bool lo_part)
-{
-    uint32_t o[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const __hip_bfloat162 h = __float22bfloat162_rn(make_float2(x[2 * q], x[2 * q + 1]));
-        const uint32_t hb = *reinterpret_cast<const uint32_t *>(&h);
-        const float r0 = x[2 * q] - __uint_as_float(hb << 16);
-        const float r1 = x[2 * q + 1] - __uint_as_float(hb & 0xffff0000u);
-        const __hip_bfloat162 l = __float22bfloat162_rn(make_float2(r0, r1));
-        const uint32_t lb = *reinterpret_cast<const uint32_t *>(&l);
-        o[q] = lo_part ? lb : hb;
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-}
+// (the split itself: mcol_split_bf16, svgd_device.h; the centring writes
+// every particle's two halves once per step, k_center_d's xs)
 
 // A block's 4 waves share one tile at a time: the tile's 256 rows live in LDS
 // (B operands and thresholds, written when the row block changes), and wave w
@@ -302,7 +291,8 @@ __device__ __forceinline__ uint4 mcol_split_bf16(const float (&x)[8], bool lo_pa
 // pairs and owns region blockIdx * 4 + w, as k_pair_rows.
 template <int D, bool BF = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 : 2, 8))) void k_pair_mcol(const double *__restrict__ xc,
-                                                  const float *__restrict__ xf, int64_t n,
+                                                  const float *__restrict__ xf,
+                                                  const uint4 *__restrict__ xs, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
                                                   SinkCollect sc)
 {
@@ -470,10 +460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                     float *o = sRow + e * RW;
                     if constexpr (BF) {
                         // B fragment: k-groups [hi | hi | lo | lo] of row i
-                        float x[8];
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) x[k] = k < D ? xf[ic * KF + k] : 0.0f;
-                        *reinterpret_cast<uint4 *>(o) = mcol_split_bf16(x, (l >> 4) >= 2);
+                        *reinterpret_cast<uint4 *>(o) = xs[2 * ic + ((l >> 4) >= 2 ? 1 : 0)];
                         if (e < PBLK) { // thresholds once per row: row ib + e
                             const int64_t it = ib + e;
                             const bool tv = it < n;
@@ -512,11 +499,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
             auto load_cols = [&](int jb, float (&A)[AK], f4 &hq) {
                 const float *xcol = xf + (jbase + 16 * jb) * KF;
                 if constexpr (BF) {
-                    // A fragment: k-groups [hi | lo | hi | lo] of column j
-                    float x[8];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) x[k] = k < D ? xcol[ql * KF + k] : 0.0f;
-                    *reinterpret_cast<uint4 *>(A) = mcol_split_bf16(x, (kq & 1) != 0);
+                    // A fragment: k-groups [hi | lo | hi | lo] of column j (the
+                    // centring's split: one 16-byte load instead of 64 bytes
+                    // and ~45 VALU per column block)
+                    *reinterpret_cast<uint4 *>(A) = xs[2 * (jbase + 16 * jb + ql) + (kq & 1)];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
                     return;
@@ -594,7 +580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                         uint32_t nbelow = 0;
 #pragma unroll
                         for (int g = 0; g < MC_NG; ++g) {
-                            unsigned long long h[4], any = 0;
+                            unsigned long long h[4], any = 0, lb[4]; // (lb: the below masks, unused)
                             float xm[4]; // MID: v - TM
                             if constexpr (SVGD_MCOL_ABL == 2) {
                                 asm volatile("" ::"v"(acc[g][0]), "v"(acc[g][1]), "v"(acc[g][2]),
@@ -609,7 +595,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                 }
                             } else if constexpr (MID) {
                                 mcol_sub_centre(acc[g], Bg[g][TI], xm); // 2 v_pk_add_f32
-                                any = mcol_classify4m(xm, Bg[g][TI + 1], nbelow);
+                                any = mcol_classify4m(xm, Bg[g][TI + 1], nbelow, lb);
                             } else if constexpr (SVGD_MCOL_CLS == 1) {
                                 uint32_t bv[4];
                                 mcol_classify4v(acc[g], Bg[g][TI], Bg[g][TI + 1], vbelow, bv);
@@ -1368,13 +1354,13 @@ hipError_t launch_pair_tcol(int KP, int grid, const float *xc, const float *nrm,
 
 #define SVGD_MCOL_CASE(Dv)                                                                   \
     case Dv:                                                                                 \
-        hipLaunchKernelGGL((k_pair_mcol<Dv>), dim3(grid), dim3(256), 0, stream, xc, xf, n, nb, t0, \
-                           t1, sc);                                                          \
+        hipLaunchKernelGGL((k_pair_mcol<Dv>), dim3(grid), dim3(256), 0, stream, xc, xf, xs, n, nb, \
+                           t0, t1, sc);                                                      \
         break;
 #define SVGD_MCOLB_CASE(Dv)                                                                  \
     case Dv:                                                                                 \
-        hipLaunchKernelGGL((k_pair_mcol<Dv, true>), dim3(grid), dim3(256), 0, stream, xc, xf, n, nb, \
-                           t0, t1, sc);                                                      \
+        hipLaunchKernelGGL((k_pair_mcol<Dv, true>), dim3(grid), dim3(256), 0, stream, xc, xf, xs, n, \
+                           nb, t0, t1, sc);                                                  \
         return hipGetLastError();
 
 
@@ -1382,12 +1368,13 @@ hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
                             const unsigned long long *nmax_bits, int64_t n, int64_t nb, int64_t t0,
                             int64_t t1, uint64_t *regions, int64_t cap, uint32_t *counts,
                             unsigned long long *below, const SelState *st, uint32_t *bpart,
-                            bool bf16, hipStream_t stream)
+                            const uint32_t *xsplit, hipStream_t stream)
 {
     if (grid <= 0 || t1 <= t0) return hipSuccess;
     if (!nmax_bits || !xf) return hipErrorInvalidValue;
     SinkCollect sc{st, regions, cap, counts, below, xf, nmax_bits, bpart};
-    if (d <= 8 && bf16) { // the bf16-split Gram (k_pair_mcol<D, true>)
+    const uint4 *xs = reinterpret_cast<const uint4 *>(xsplit);
+    if (d <= 8 && xs) { // the bf16-split Gram (k_pair_mcol<D, true>)
         switch (d) {
             SVGD_MCOLB_CASE(1)
             SVGD_MCOLB_CASE(2)

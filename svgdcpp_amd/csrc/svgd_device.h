@@ -2,6 +2,7 @@
 // units (svgd_kernels.hip, svgd_collect.hip).  Internal.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
 #include <stdint.h>
 
 #include "svgd_kernels.h"
@@ -28,6 +29,27 @@ template <class T, int KP> __device__ __forceinline__ constexpr int kslot(int kk
 }
 
 // --------------------------------------------------------------- median --
+
+// The split-bf16 form of 8 fp32 coordinates (k_pair_mcol<D, true>'s Gram):
+// x = hi + lo + r, hi = bf16(x), lo = bf16(x - hi) (x - hi exact in fp32),
+// |r| <= 2^-16 |x|; lo_part selects which half (8 bf16 = 16 bytes).  Written
+// once per particle and step by the centring (k_center_d, xs), read by the
+// collect as its A and B fragments.
+__device__ __forceinline__ uint4 mcol_split_bf16(const float (&x)[8], bool lo_part)
+{
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const __hip_bfloat162 h = __float22bfloat162_rn(make_float2(x[2 * q], x[2 * q + 1]));
+        const uint32_t hb = *reinterpret_cast<const uint32_t *>(&h);
+        const float r0 = x[2 * q] - __uint_as_float(hb << 16);
+        const float r1 = x[2 * q + 1] - __uint_as_float(hb & 0xffff0000u);
+        const __hip_bfloat162 l = __float22bfloat162_rn(make_float2(r0, r1));
+        const uint32_t lb = *reinterpret_cast<const uint32_t *>(&l);
+        o[q] = lo_part ? lb : hb;
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+}
 //
 // Keys: squared distances s = max((|xc_i|^2 + |xc_j|^2) - 2 xc_i.xc_j, 0)
 // (the reference's Gram form, GaussianRBFKernel.hpp:179-183, on centred

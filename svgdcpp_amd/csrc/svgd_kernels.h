@@ -59,9 +59,11 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
                               SelState *st_out = nullptr, const SelState *st_init = nullptr,
                               const double *pin = nullptr, int nin = 0, double *pout = nullptr,
                               unsigned long long *nmax_zero = nullptr, float *xcf = nullptr,
-                              float *nrmf = nullptr);
+                              float *nrmf = nullptr, uint32_t *xsplit = nullptr);
 // (xcf / nrmf, KP 32 or 64: also the fp32 copies of xc and nrm, nrmf +inf in
-// the padding rows -- launch_cvt_f32 / launch_cvt_nrm_f32 in the same pass)
+// the padding rows -- launch_cvt_f32 / launch_cvt_nrm_f32 in the same pass;
+// xsplit, d <= 8 with xf: the collect's split-bf16 operands, 8 dwords per
+// particle [hi | lo] of its fp32 coordinates, rows [0, np))
 hipError_t launch_prep_v(const double *xc, const double *G, const double *nrm, const double *a_ptr,
                          int64_t n, int64_t np, int d, int KP, int VW, double *V, double *cvec,
                          hipStream_t stream);
@@ -309,7 +311,9 @@ hipError_t launch_pair_mcol(int d, int grid, const double *xc, const float *xf,
                             const unsigned long long *nmax_bits, int64_t n, int64_t nb, int64_t t0,
                             int64_t t1, uint64_t *regions, int64_t cap, uint32_t *counts,
                             unsigned long long *below, const SelState *st, uint32_t *bpart,
-                            bool bf16, hipStream_t stream);
+                            const uint32_t *xsplit, hipStream_t stream);
+// (xsplit, d <= 8: the centring's split-bf16 operands -> the bf16-split Gram;
+// nullptr: the f32 Gram)
 // fp32 tile-path collect (k_pair_tiles<float> MODE 0 on the matrix cores,
 // same keys): one region per block; KP in {4, 8, 12, 16, 32, 64}; xk: the
 // key parts at KP 32 / 64 (bf16 part-product keys), else unused

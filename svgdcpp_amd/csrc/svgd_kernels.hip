@@ -272,7 +272,7 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
                                                   unsigned long long *nmax_bits,
                                                   unsigned long long *nmax_zero, double *__restrict__ pout,
                                                   unsigned long long *bzero, SelState *st_out,
-                                                  SelState st_init)
+                                                  SelState st_init, uint4 *__restrict__ xs)
 {
     constexpr int KP = med_rec_stride(D), KF = med_f32_stride(D);
     if (bzero && blockIdx.x == 0)
@@ -328,6 +328,15 @@ __global__ __launch_bounds__(256) void k_center_d(const double *__restrict__ X, 
             float4 *of = reinterpret_cast<float4 *>(xf + j * KF);
 #pragma unroll
             for (int q = 0; q < KF / 4; ++q) of[q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+            if constexpr (D <= 8) {
+                if (xs) { // the collect's split-bf16 operands [hi | lo] (zero past n)
+                    float x8[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) x8[k] = k < D ? f[k] : 0.0f;
+                    xs[2 * j] = mcol_split_bf16(x8, false);
+                    xs[2 * j + 1] = mcol_split_bf16(x8, true);
+                }
+            }
             unsigned long long m = (unsigned long long)__double_as_longlong(s);
             for (int o2 = 32; o2 > 0; o2 >>= 1) {
                 const unsigned long long t = __shfl_xor(m, o2);
@@ -4782,7 +4791,7 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
                               int nrm_in_slot, float *xf, unsigned long long *nmax_bits,
                               unsigned long long *bzero, hipStream_t stream, SelState *st_out,
                               const SelState *st_init, const double *pin, int nin, double *pout,
-                              unsigned long long *nmax_zero, float *xcf, float *nrmf)
+                              unsigned long long *nmax_zero, float *xcf, float *nrmf, uint32_t *xsplit)
 {
     const SelState sinit = st_init ? *st_init : SelState{};
     if (!st_init) st_out = nullptr;
@@ -4803,7 +4812,7 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
     case Dv:                                                                                  \
         hipLaunchKernelGGL((k_center_d<Dv>), dim3(gd), dim3(256), 0, stream, X, n, pin, nin,   \
                            np, xc, nrm, nrm_in_slot, xf, nmax_bits, nmax_zero, pout, bzero, st_out, \
-                           sinit);                                                            \
+                           sinit, reinterpret_cast<uint4 *>(xsplit));                          \
         return hipGetLastError();
     if (d <= 16 && KP == med_rec_stride(d)) {
         switch (d) {
@@ -4816,6 +4825,7 @@ hipError_t launch_mean_center(const double *X, int64_t n, int d, int KP, int64_t
         }
     }
 #undef SVGD_CENTER_CASE
+    if (xsplit) return hipErrorInvalidValue; // (the split: k_center_d, d <= 8, only)
     if (!xf && !nrm_in_slot && (KP == 32 || KP == 64) && d <= KP && np % 2 == 0) {
         if (KP == 32)
             hipLaunchKernelGGL((k_center_t<32>), dim3(g), dim3(256), 0, stream, X, n, d, partial, nparts, np,
