@@ -236,7 +236,7 @@ struct svgd_ctx {
     // disjoint parts of a full-size sample and all-reduced its two radix
     // histograms; kept off -- tests/test_multirank_cpu.py pins it on CPU)
     bool shard_sample = false;
-    int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident)
+    int64_t collect_blocks = 1024; // collect-pass work-groups (4 per CU resident; 5 for the bf16-split mcol)
     bool mcol = true;              // bracket collect on the matrix cores (k_pair_mcol / _tcol)
     bool mcol_bf16 = true;         // k_pair_mcol's Gram as split bf16 (d <= 8; SVGD_MCOL_BF16=0: f32)
     uint32_t *xsplit = nullptr;    // its operands, [hi | lo] bf16 x 8 per particle (the centring writes them)
@@ -2029,8 +2029,10 @@ int init_ctx(svgd_ctx *c, int dim, int64_t n, int dtype, int device, int sim_wor
     // MODE 0) instead of the matrix-core ones (k_pair_mcol / k_pair_tcol)
     if (const char *e = std::getenv("SVGD_COLLECT_FP64")) c->mcol = std::atoi(e) == 0;
     if (const char *e = std::getenv("SVGD_MCOL_BF16")) c->mcol_bf16 = std::atoi(e) != 0;
-    if (c->xf && c->mcol && c->mcol_bf16 && dim <= 8) // the collect's split-bf16 operands (center)
+    if (c->xf && c->mcol && c->mcol_bf16 && dim <= 8) { // the collect's split-bf16 operands (center)
         CHK(dalloc(c, &c->xsplit, c->np * 8));
+        c->collect_blocks = 1280; // k_pair_mcol<D, true>: 5 work-groups per CU (31 KiB LDS, <= 96 VGPRs)
+    }
     if (const char *e = std::getenv("SVGD_MEDIAN_SIGMA")) c->bracket_sigma = std::max(0.0, std::atof(e));
     CHK(dalloc(c, &c->st, 1));
     CHK(dalloc(c, &c->ghist, 2 * RADIX));

@@ -38,7 +38,7 @@ typedef f4_t f4;
 // and finished exactly
 // in a batch (mcol_flush).  Data outside |x|^2 <= 2^40 sets delta = inf:
 // every pair is then finished exactly (correct, slow).
-constexpr int MC_STG = 512; // staged band pairs per wave
+constexpr int MC_STG = 256; // staged band pairs per wave
 constexpr int MC_NG = 4;    // 16-row blocks per classification group
 // Timing ablations of k_pair_mcol (tools/gpu_mcol_abl.sh; WRONG results, never
 // a shipped build): 1 = no band staging, 2 = MFMAs only (no classification),
@@ -242,6 +242,27 @@ __device__ __forceinline__ unsigned long long mcol_classify_diag(float v, float 
     return mh;
 }
 
+// Diagonal tiles in the centre form (x = v - TM, half-width W; as
+// mcol_classify4m): below (x > W) and band (|x| <= W) lanes among those with
+// xl > c (j > i).  Returns the band lanes of the value.
+__device__ __forceinline__ unsigned long long mcol_classify_diag_m(float x, float w, int xl, int c,
+                                                                   uint32_t &nbelow)
+{
+    unsigned long long ml, mb, ok;
+    uint32_t t;
+    asm volatile("v_cmp_gt_i32_e64 %[ok], %[xl], %[c]\n\t"
+                 "v_cmp_gt_f32_e64 %[ml], %[x], %[w]\n\t"
+                 "v_cmp_ge_f32_e64 %[mb], %[w], |%[x]|\n\t"
+                 "s_and_b64 %[ml], %[ml], %[ok]\n\t"
+                 "s_and_b64 %[mb], %[mb], %[ok]\n\t"
+                 "s_bcnt1_i32_b64 %[t], %[ml]\n\t"
+                 "s_add_u32 %[nb], %[nb], %[t]"
+                 : [nb] "+s"(nbelow), [ml] "=&s"(ml), [mb] "=&s"(mb), [ok] "=&s"(ok), [t] "=&s"(t)
+                 : [x] "v"(x), [w] "v"(w), [xl] "v"(xl), [c] "s"(c)
+                 : "scc");
+    return mb;
+}
+
 // The lane's bits of the 4 band masks of one 16 x 16 block (bit r: value r
 // is a band value), straight from the scalar masks.
 __device__ __forceinline__ uint32_t mcol_code4(const unsigned long long (&h)[4])
@@ -273,14 +294,19 @@ template <int D> struct McolRow {
 // BF (d <= 8): the Gram on ONE v_mfma_f32_16x16x32_bf16 per 16 x 16 block
 // instead of KK = 2 f32 16x16x4 steps (16 instead of 64 cycles).  Each fp32
 // coordinate is split x = hi + lo + r, hi = bf16(x), lo = bf16(x - hi)
-// (x - hi exact in fp32), |r| <= 2^-16 |x|, and the k = 32 slots hold all four
-// products: A (columns) k-groups [hi | lo | hi | lo], B (rows) [hi | hi | lo |
-// lo].  Error of the fp32 value against h_j + xc_i.xc_j (S = sum_k |x_ik x_jk|
-// <= nmax by Cauchy-Schwarz, |h_j| <= nmax / 2): h_j rounding 2^-25 nmax,
-// fp32 inputs 2^-23 S, the split (|r_i||x_j| + |x_i||r_j| + |r_i r_j|) <=
-// 2^-15 S, the bf16 products exact in fp32 and at most 33 fp32 roundings of
-// the sum over |h_j| + 1.02 S: in all <= 3.4e-5 nmax.  MCOL_DELTA_BF =
-// 2^-14 nmax (1.8x that) plus 2^-100 for flushed denormals.
+// (x - hi exact in fp32), and the k = 32 slots hold all four products: A
+// (columns) k-groups [hi | lo | hi | lo], B (rows) [hi | hi | lo | lo].
+// |r| <= 2^-17 |x|: for x in [2^e, 2^(e+1)), |x - hi| <= 2^(e-8), so x - hi
+// is either exactly 2^(e-8) (lo takes it, r = 0) or in a binade <= e - 9,
+// where bf16's half-spacing is <= 2^(e-17).  Error of the fp32 value against
+// h_j + xc_i.xc_j (S = sum_k |x_ik x_jk| <= nmax by Cauchy-Schwarz, |h_j| <=
+// nmax / 2): h_j rounding 2^-25 nmax, fp32 inputs 2^-23 S, the split
+// (|r_i||x_j| + |x_i||r_j| + |r_i r_j|) <= 2^-16 (1 + 2^-18) S, the bf16
+// products exact in fp32 and at most 33 fp32 roundings of the sum over
+// |h_j| + 1.02 S: in all <= 1.84e-5 nmax.  MCOL_DELTA_BF = 2^-15 nmax (1.66x
+// that) plus 2^-100 for flushed denormals (tests/test_mcol_bf16_bound.py
+// emulates the arithmetic; rounds 3-6 used 2^-14 from a 2^-16 |x| split
+// bound).
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 // (the split itself: mcol_split_bf16, svgd_device.h; the centring writes
 // every particle's two halves once per step, k_center_d's xs)
@@ -290,7 +316,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 // takes the 16-column blocks w, w + 4, ...  Each wave stages its own band
 // pairs and owns region blockIdx * 4 + w, as k_pair_rows.
 template <int D, bool BF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 : 2, 8))) void k_pair_mcol(const double *__restrict__ xc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D <= 8 ? 4 : 2, 8))) void k_pair_mcol(const double *__restrict__ xc,
                                                   const float *__restrict__ xf,
                                                   const uint4 *__restrict__ xs, int64_t n,
                                                   int64_t nb, int64_t t0, int64_t t1,
@@ -303,9 +329,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     constexpr int NI = PBLK / 16;          // 16-row blocks of a tile
     static_assert(!BF || (D <= 8 && RW == 4), "the bf16 split form takes d <= 8");
     __shared__ __attribute__((aligned(16))) float sRow[NI * 64 * RW]; // BF: the B fragments
-    __shared__ float2 sThr[BF ? PBLK : 1];                            // BF: (TLf, THf) per row
-    constexpr bool MIDC = BF && SVGD_MCOL_CLS == 2;                   // mcol_classify4m
-    __shared__ float2 sThm[MIDC ? PBLK : 1];                          // (TM, W) per row
+    // BF: per row (TM, W) (the centre form, mcol_classify4m / _diag_m) or,
+    // with delta = inf, (TLf, THf) -- 31 KiB of LDS in all: 5 work-groups
+    // (waves) per CU
+    constexpr bool MIDC = BF && SVGD_MCOL_CLS == 2;
+    __shared__ float2 sT[BF ? PBLK : 1];
     __shared__ uint32_t sStage[4][MC_STG + 64]; // + the spill zone (SVGD_MCOL_STAGE)
     __shared__ uint32_t sBk[NBK];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -320,7 +348,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
     const double hi_d = hi_key >= 0x7ff0000000000000ull ? __builtin_inf()
                                                         : __longlong_as_double((long long)hi_key);
     const double delta = nmax > 0x1p40 ? __builtin_inf()
-                         : BF     ? 0x1p-14 * nmax + 0x1p-100 // MCOL_DELTA_BF (above)
+                         : BF     ? 0x1p-15 * nmax + 0x1p-100 // MCOL_DELTA_BF (above)
                                   : 4.0 * (D + 4) * 0x1p-24 * nmax + 0x1p-100;
     constexpr int AK = BF ? 4 : KK; // A operand dwords per lane (BF: 8 bf16)
     constexpr int BW = BF ? 2 : RW; // per-group row values kept in registers
@@ -381,6 +409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
             }
         }
         scnt = 0;
+        __builtin_amdgcn_s_waitcnt(0xF70); // vmcnt(0): the flush's stores drained here, once (see the column loop)
     };
 
     // lane-constant part of "j > i" inside a 16 x 16 block (diagonal tiles):
@@ -471,8 +500,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                             const double TH = 0.5 * (ni - hi_d - m);
                             const float2 t = make_float2(tv ? f32_up(TL + delta) : __builtin_inff(),
                                                          tv ? f32_down(TH - delta) : __builtin_inff());
-                            sThr[e] = t;
-                            if constexpr (MIDC) sThm[e] = mcol_centre_width(t.x, t.y);
+                            sT[e] = MIDC && delta < __builtin_inf() ? mcol_centre_width(t.x, t.y) : t;
                         }
                         continue;
                     }
@@ -516,16 +544,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                 for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
             };
             // one group of MC_NG row blocks: its row operands from LDS, its MFMAs
-            // MID: the row values are (TM, W) (mcol_classify4m), else (TLf, THf)
-            auto group_mfma = [&](auto mid_tag, int g0, const f4 &hq, const float (&A)[AK],
+            // (BF: the row values sT hold the form the launch classifies with)
+            auto group_mfma = [&](auto, int g0, const f4 &hq, const float (&A)[AK],
                                   float (&Bg)[MC_NG][BW], f4 (&acc)[MC_NG]) {
-                constexpr bool MID = decltype(mid_tag)::value;
                 if constexpr (BF) {
                     const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(A));
 #pragma unroll
                     for (int g = 0; g < MC_NG; ++g) {
                         const uint4 b = *reinterpret_cast<const uint4 *>(sRow + ((g0 + g) * 64 + lane) * RW);
-                        const float2 t = MID ? sThm[16 * (g0 + g) + ql] : sThr[16 * (g0 + g) + ql];
+                        const float2 t = sT[16 * (g0 + g) + ql];
                         Bg[g][0] = t.x;
                         Bg[g][1] = t.y;
                         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, b), hq,
@@ -560,6 +587,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                 float A[AK], An[AK];
                 f4 hq, hqn;
                 if (w < njb) load_cols(w, A, hq);
+                // vmcnt(0): the column loop starts with no memory operation in
+                // flight (the compiler's wait placement is path-insensitive at
+                // the loop head: with these first operands, or the flush's
+                // stores, possibly pending it waited for EVERYTHING -- the
+                // next column block's prefetch included -- at the top of every
+                // iteration)
+                __builtin_amdgcn_s_waitcnt(0xF70);
                 for (int jb = w; jb < njb; jb += 4) {
                     // (a block of 16 x 256 pairs stages ~10 band pairs; one that
                     // outgrows the area marks the region overflowed)
@@ -586,6 +620,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                 asm volatile("" ::"v"(acc[g][0]), "v"(acc[g][1]), "v"(acc[g][2]),
                                              "v"(acc[g][3]), "v"(Bg[g][TI]), "v"(Bg[g][TI + 1]));
                                 continue;
+                            } else if constexpr (DIAG && MID) {
+                                mcol_sub_centre(acc[g], Bg[g][TI], xm);
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    h[r] = mcol_classify_diag_m(xm[r], Bg[g][TI + 1], xl, 16 * (g0 + g) - jl0 - r,
+                                                                nbelow);
+                                    any |= h[r];
+                                }
                             } else if constexpr (DIAG) {
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
@@ -616,7 +658,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                     // every lane stores: a lane without band values, or an
                                     // entry past the area, lands in the spill zone; the
                                     // flush reports an overflowed area (scnt > MC_STG)
-                                    if constexpr (MID) mcol_band4m(xm, Bg[g][TI + 1], h);
+                                    if constexpr (MID && !DIAG) mcol_band4m(xm, Bg[g][TI + 1], h);
                                     const uint32_t code = mcol_code4(h);
                                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
                                         (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
@@ -634,7 +676,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                                 if (scnt + c > MC_STG) { // pathological band: give up
                                     ovf = true;          // (region overflow -> exact fallback)
                                 } else {
-                                    if constexpr (MID) mcol_band4m(xm, Bg[g][TI + 1], h);
+                                    if constexpr (MID && !DIAG) mcol_band4m(xm, Bg[g][TI + 1], h);
                                     const uint32_t code = mcol_code4(h);
                                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
                                         (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
@@ -658,16 +700,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D <= 8 ? 4 
                     hq = hqn;
                 }
             };
-            if (diag)
-                jloop(std::true_type{}, std::false_type{});
-            else if constexpr (MIDC) {
-                // delta = inf (nmax > 2^40): values may exceed mcol_classify4m's range
-                if (delta < __builtin_inf())
-                    jloop(std::false_type{}, std::true_type{});
-                else
+            if constexpr (MIDC) {
+                // delta = inf (nmax > 2^40): values may exceed mcol_classify4m's
+                // range -- the lane-mask form (sT holds (TLf, THf) then)
+                if (delta < __builtin_inf()) {
+                    if (diag)
+                        jloop(std::true_type{}, std::true_type{});
+                    else
+                        jloop(std::false_type{}, std::true_type{});
+                } else if (diag) {
+                    jloop(std::true_type{}, std::false_type{});
+                } else {
                     jloop(std::false_type{}, std::false_type{});
-            } else
+                }
+            } else if (diag) {
+                jloop(std::true_type{}, std::false_type{});
+            } else {
                 jloop(std::false_type{}, std::false_type{});
+            }
             if (scnt) flush(ib, jbase);
         } while (advance(pos));
     }
@@ -856,6 +906,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             }
         }
         scnt = 0;
+        __builtin_amdgcn_s_waitcnt(0xF70); // vmcnt(0): the flush's stores drained here, once (see the column loop)
     };
 
     // the tile row's B operands, shared by the block's 4 waves (written at a
@@ -1159,6 +1210,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 8))) voi
             }
         }
         scnt = 0;
+        __builtin_amdgcn_s_waitcnt(0xF70); // vmcnt(0): the flush's stores drained here, once (see the column loop)
     };
 
     struct Cols {
