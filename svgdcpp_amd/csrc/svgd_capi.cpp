@@ -398,10 +398,13 @@ struct svgd_ctx {
     double trk_min_w = 2e-5;    // SVGD_TRACK_MIN_WIDTH: relative half-width floor
     double trk_err_mult = 4.0;  // SVGD_TRACK_ERR_MULT: half-width / recent error (set at creation)
     uint64_t *h_trk = nullptr, *h_trk_dev = nullptr; // pinned [lo, hi, below, cand, key0, key1, err]
-    double trk_m[3] = {0, 0, 0}; // last selected D^2 (lower order statistic), newest first
+    double trk_m[4] = {0, 0, 0, 0}; // last selected D^2 (lower order statistic), newest first
     int trk_n = 0;
-    double trk_err[3] = {0, 0, 0}; // recent relative prediction errors
+    double trk_err[3] = {0, 0, 0}; // recent relative errors of the quadratic extrapolation
     int trk_nerr = 0;
+    double trk_errc[3] = {0, 0, 0}; // ... and of the cubic one (4 medians)
+    int trk_nerrc = 0;
+    double trk_pq = -1, trk_pc = -1; // this step's two extrapolations (< 0: none)
     double trk_dens = 0;        // candidates per unit of D^2 in the last bracket (all ranks)
     double trk_pred = -1;       // this step's predicted median D^2 (< 0: sampled bracket)
     bool trk_go = false;        // this step's bracket is the predicted one (trk_plan)
@@ -794,12 +797,17 @@ int median_finish_spec(svgd_ctx *c, double logn);
 
 double key_value(uint64_t k) { return __builtin_bit_cast(double, k); }
 
-// The next median D^2 from the last 2 or 3 (quadratic through 3 points: on
-// SVGD trajectories its errors are ~5x below the linear one's, 1e-4..5e-4)
-double trk_extrapolate(const svgd_ctx *c)
+// The next median D^2 from the last 2, 3 or 4: linear, quadratic (order 2:
+// on SVGD trajectories its errors are ~5x below the linear one's) or cubic
+// (order 3: through 4 points; on the bench trajectories another 2-5x below
+// the quadratic one's while the median still moves fast, noisier once it
+// settles -- profiles/r06_track_predictor.txt)
+double trk_extrapolate(const svgd_ctx *c, int order = 2)
 {
     const double *m = c->trk_m;
-    double p = c->trk_n >= 3 ? 3.0 * m[0] - 3.0 * m[1] + m[2] : 2.0 * m[0] - m[1];
+    double p = order >= 3 && c->trk_n >= 4 ? 4.0 * m[0] - 6.0 * m[1] + 4.0 * m[2] - m[3]
+               : c->trk_n >= 3          ? 3.0 * m[0] - 3.0 * m[1] + m[2]
+                                        : 2.0 * m[0] - m[1];
     return p > 0.0 ? p : m[0];
 }
 
@@ -812,35 +820,57 @@ void trk_record(svgd_ctx *c, uint64_t lo_key, uint64_t hi_key, uint64_t cand)
         c->trk_n = 0;
         return;
     }
+    // both extrapolations' errors (the ones this step's plan made, else from
+    // the same history)
     if (c->trk_n >= 2) {
-        const double p = c->trk_pred >= 0 ? c->trk_pred : trk_extrapolate(c);
+        const double p = c->trk_pq >= 0 ? c->trk_pq : trk_extrapolate(c, 2);
         c->trk_err[2] = c->trk_err[1];
         c->trk_err[1] = c->trk_err[0];
         c->trk_err[0] = std::fabs(m - p) / m;
         c->trk_nerr = std::min(c->trk_nerr + 1, 3);
     }
+    if (c->trk_n >= 4) {
+        const double p = c->trk_pc >= 0 ? c->trk_pc : trk_extrapolate(c, 3);
+        c->trk_errc[2] = c->trk_errc[1];
+        c->trk_errc[1] = c->trk_errc[0];
+        c->trk_errc[0] = std::fabs(m - p) / m;
+        c->trk_nerrc = std::min(c->trk_nerrc + 1, 3);
+    }
     const double lo = key_value(lo_key);
     const double hi = hi_key >= 0x7ff0000000000000ull ? INFINITY : key_value(hi_key);
     c->trk_dens = (std::isfinite(hi) && hi > lo) ? (double)cand / (hi - lo) : 0.0;
+    c->trk_m[3] = c->trk_m[2];
     c->trk_m[2] = c->trk_m[1];
     c->trk_m[1] = c->trk_m[0];
     c->trk_m[0] = m;
-    c->trk_n = std::min(c->trk_n + 1, 3);
+    c->trk_n = std::min(c->trk_n + 1, 4);
 }
 
 // The predicted bracket for this step, or false (sample it): the predicted
 // band must not hold more candidates than the sampled bracket's would
-// (band_samp: its expected share of the pairs).
+// (band_samp: its expected share of the pairs).  Of the quadratic and the
+// cubic extrapolation, the one whose half-width -- err_mult (cubic: twice
+// that) x the largest of its last 3 relative errors -- is narrower.
 bool trk_predict(svgd_ctx *c, double Mq, double band_samp, uint64_t *lo_key, uint64_t *hi_key,
                  double *band_frac)
 {
     if (!c->trk_allowed || c->trk_n < 2 || !(c->trk_dens > 0.0)) return false;
     const double m1 = c->trk_m[0], m2 = c->trk_m[1];
-    const double pred = trk_extrapolate(c);
+    c->trk_pq = trk_extrapolate(c, 2);
+    c->trk_pc = c->trk_n >= 4 ? trk_extrapolate(c, 3) : -1.0;
     double e = 0.0;
     if (c->trk_nerr == 0) e = std::fabs(m1 - m2) / m1; // no error seen yet: the drift itself
     for (int k = 0; k < c->trk_nerr; ++k) e = std::max(e, c->trk_err[k]);
-    const double w = std::max(c->trk_err_mult * e, c->trk_min_w);
+    double wp = c->trk_err_mult * e, pred = c->trk_pq;
+    if (c->trk_pc >= 0 && c->trk_nerrc == 3) {
+        double ec = 0.0;
+        for (int k = 0; k < 3; ++k) ec = std::max(ec, c->trk_errc[k]);
+        if (2.0 * c->trk_err_mult * ec < wp) {
+            wp = 2.0 * c->trk_err_mult * ec;
+            pred = c->trk_pc;
+        }
+    }
+    const double w = std::max(wp, c->trk_min_w);
     const double band = c->trk_dens * (2.0 * w * pred) / Mq;
     if (!(w < 0.05)) return false;
     const double lo = pred * (1.0 - w), hi = pred * (1.0 + w);
@@ -882,6 +912,7 @@ void trk_plan(svgd_ctx *c)
 {
     c->trk_go = false;
     c->trk_pred = -1;
+    c->trk_pq = c->trk_pc = -1;
     const int64_t M = upper_pairs(c->n);
     if (!c->spec_step || c->sample_size > 0 || c->cand_capacity > 0 || M <= c->direct_max_pairs)
         return;
@@ -2425,7 +2456,7 @@ int svgd_set_particles(svgd_ctx *c, const double *X)
     c->xh_valid = false;
     c->xver += 1;
     c->cpart_ver[0] = c->cpart_ver[1] = -1; // new particles: centred on their own mean
-    c->trk_n = c->trk_nerr = 0; // new particles: the median history restarts
+    c->trk_n = c->trk_nerr = c->trk_nerrc = 0; // new particles: the median history restarts
     return SVGD_OK;
 }
 

@@ -1,24 +1,41 @@
 """The premise of the tracked median bracket (svgd_capi.cpp trk_predict):
-along an SVGD trajectory the median of D^2 moves smoothly enough that a
-quadratic extrapolation of the last three selected medians, with a half-width
-of 4x the largest of the last three prediction errors, contains the next
-median.  CPU only: the oracle's own trajectory (GaussianRBFKernel.hpp:164-188
-median, SVGD.hpp:373-400 step, Adam), the policy restated in Python."""
+along an SVGD trajectory the median of D^2 moves smoothly enough that an
+extrapolation of the last selected medians -- the quadratic one (3 points,
+half-width mult x the largest of its last three relative errors) or the cubic
+one (4 points, half-width 2 mult x its own), whichever half-width is narrower
+-- contains the next median.  CPU only: the oracle's own trajectory
+(GaussianRBFKernel.hpp:164-188 median, SVGD.hpp:373-400 step, Adam), the
+policy restated in Python."""
 import numpy as np
 import pytest
 
 
+def _extrap(h, order):
+    if order == 3 and len(h) >= 4:
+        p = 4 * h[-1] - 6 * h[-2] + 4 * h[-3] - h[-4]
+    elif len(h) >= 3:
+        p = 3 * h[-1] - 3 * h[-2] + h[-3]
+    else:
+        p = 2 * h[-1] - h[-2]
+    return p if p > 0 else h[-1]
+
+
 def _policy(m, mult=4.0, wmin=2e-5):
-    hist, errs, used, miss, ws = [], [], 0, 0, []
+    hist, eq, ec, used, miss, ws, cubic = [], [], [], 0, 0, [], 0
     for mt in m:
         if len(hist) >= 2:
-            p = 3 * hist[-1] - 3 * hist[-2] + hist[-3] if len(hist) >= 3 else 2 * hist[-1] - hist[-2]
-            if p <= 0:
-                p = hist[-1]
-            e = max(errs[-3:]) if errs else abs(hist[-1] - hist[-2]) / hist[-1]
-            w = max(mult * e, wmin)
+            pq = _extrap(hist, 2)
+            pc = _extrap(hist, 3) if len(hist) >= 4 else None
+            e = max(eq[-3:]) if eq else abs(hist[-1] - hist[-2]) / hist[-1]
+            w, p = mult * e, pq
+            if pc is not None and len(ec) >= 3 and 2 * mult * max(ec[-3:]) < w:
+                w, p = 2 * mult * max(ec[-3:]), pc
+                cubic += 1
+            w = max(w, wmin)
             err = abs(mt - p) / mt
-            errs.append(err)
+            eq.append(abs(mt - pq) / mt)
+            if pc is not None:
+                ec.append(abs(mt - pc) / mt)
             if w < 0.05:
                 used += 1
                 ws.append(w)
