@@ -311,6 +311,46 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 // (the split itself: mcol_split_bf16, svgd_device.h; the centring writes
 // every particle's two halves once per step, k_center_d's xs)
 
+// The folded centre form (MIDC with a finite margin): the MFMA forms
+// v = (h_j - TM) + sum_k (hi_i hi_j + lo_i hi_j + hi_i lo_j)_k + (p0 + p1 + p2)_i
+// with p0 + p1 + p2 = fl32(-|xc_i|^2 / 2) split exactly into three bf16 parts
+// (the fourth k-group of 8 slots, which the lo.lo products held: A [1 1 1 0 ..],
+// B [p0 p1 p2 0 ..]) and TM, the bracket's centre, folded into the column
+// operand C = fl32(h_j - TM) once per column block -- so v approximates
+// x = e_ij - |xc_i|^2 / 2 - TM itself (e_ij = h_j + xc_i.xc_j, k_pair_rows'
+// exact value), and one global half-width W classifies: no per-row
+// thresholds, no subtraction per value.  Error of v against x (S = sum_k
+// |x_ik x_jk| <= nmax): fp32 inputs 2^-23 S; the split without lo.lo:
+// (hi + lo)_i (hi + lo)_j - x_i x_j is <= 2^-16 (1 + 2^-18) S and the
+// dropped lo_i lo_j <= 2^-16 (1 + 2^-8)^2 S, together <= 1.01 * 2^-15 S;
+// h_j, -|xc_i|^2/2 and h_j - TM rounded to fp32: 2^-25 nmax twice and 2^-24
+// (nmax / 2 + |TM|); the products exact in fp32 and at most 28 nonzero terms
+// summed (27 roundings) with partial sums below |h_j - TM| + 1.03 S + nmax / 2
+// <= 2.03 nmax + |TM| <= 3.03 nmax (|TM| <= nmax, clamped): in all
+// <= 3.62e-5 nmax.  MCOL_DELTA_FOLD = 2^-14 nmax (1.69x that) plus 2^-100;
+// tests/test_mcol_bf16_bound.py emulates this arithmetic too.  With the fp64
+// thresholds of k_pair_rows (e > TL_i = (n_i - lo + m_i) / 2 => key < lo;
+// e <= TH_i = (n_i - hi - m_i) / 2 => key >= hi; m_i = 2^-48 (n_i + nmax) <=
+// 2^-47 nmax), in x: below if x > -lo/2 - TM + m_i/2, above if x <= -hi/2
+// - TM - m_i/2; so W = fp32_up(max(-lo/2 - TM, hi/2 + TM) + 2^-48 nmax +
+// delta) gives v > W => below, v < -W => above, |v| <= W the band (a superset
+// of the exact one: the fp64 finish decides it).  Padding rows carry p0 =
+// -2^100 (never below or band); padding columns h = -inf (v = -inf).  A
+// bracket without a lower or an upper end stages every pair (W = inf).
+__device__ __forceinline__ uint4 mcol_fold_row(float q)
+{
+    uint32_t p[3];
+    float r = q;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const __hip_bfloat162 h = __float22bfloat162_rn(make_float2(r, 0.0f));
+        const uint32_t hb = *reinterpret_cast<const uint32_t *>(&h) & 0xffffu;
+        p[k] = hb;
+        r -= __uint_as_float(hb << 16);
+    }
+    return make_uint4(p[0] | (p[1] << 16), p[2], 0u, 0u);
+}
+
 // A block's 4 waves share one tile at a time: the tile's 256 rows live in LDS
 // (B operands and thresholds, written when the row block changes), and wave w
 // takes the 16-column blocks w, w + 4, ...  Each wave stages its own band
@@ -350,6 +390,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
     const double delta = nmax > 0x1p40 ? __builtin_inf()
                          : BF     ? 0x1p-15 * nmax + 0x1p-100 // MCOL_DELTA_BF (above)
                                   : 4.0 * (D + 4) * 0x1p-24 * nmax + 0x1p-100;
+    // the folded centre form (mcol_fold_row): TM and the one half-width W
+    const bool fold = MIDC && delta < __builtin_inf();
+    float TMf = 0.0f, Wf = __builtin_inff();
+    if (fold && lo_key != 0 && hi_d < __builtin_inf()) {
+        const double tm = fmin(fmax(-0.25 * (lo_d + hi_d), -nmax), nmax);
+        TMf = (float)tm;
+        const double dF = 0x1p-14 * nmax + 0x1p-100; // MCOL_DELTA_FOLD (above)
+        Wf = f32_up(fmax(-0.5 * lo_d - (double)TMf, 0.5 * hi_d + (double)TMf) + 0x1p-48 * nmax + dF);
+    }
     constexpr int AK = BF ? 4 : KK; // A operand dwords per lane (BF: 8 bf16)
     constexpr int BW = BF ? 2 : RW; // per-group row values kept in registers
     constexpr int TI = BF ? 0 : KK; // their (TLf, THf) slots
@@ -488,9 +537,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
                     const int64_t ic = iv ? i : n - 1;
                     float *o = sRow + e * RW;
                     if constexpr (BF) {
-                        // B fragment: k-groups [hi | hi | lo | lo] of row i
-                        *reinterpret_cast<uint4 *>(o) = xs[2 * ic + ((l >> 4) >= 2 ? 1 : 0)];
-                        if (e < PBLK) { // thresholds once per row: row ib + e
+                        // B fragment: k-groups [hi | hi | lo | lo] of row i, or
+                        // [hi | hi | lo | -|x_i|^2/2 in 3 parts] (fold)
+                        if (fold && (l >> 4) == 3)
+                            *reinterpret_cast<uint4 *>(o) =
+                                mcol_fold_row(iv ? (float)xc[ic * KP + D] : -0x1p100f);
+                        else
+                            *reinterpret_cast<uint4 *>(o) = xs[2 * ic + ((l >> 4) >= 2 ? 1 : 0)];
+                        if (!fold && e < PBLK) { // thresholds once per row: row ib + e
                             const int64_t it = ib + e;
                             const bool tv = it < n;
                             const int64_t tc = tv ? it : n - 1;
@@ -500,7 +554,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
                             const double TH = 0.5 * (ni - hi_d - m);
                             const float2 t = make_float2(tv ? f32_up(TL + delta) : __builtin_inff(),
                                                          tv ? f32_down(TH - delta) : __builtin_inff());
-                            sT[e] = MIDC && delta < __builtin_inf() ? mcol_centre_width(t.x, t.y) : t;
+                            sT[e] = t;
                         }
                         continue;
                     }
@@ -530,9 +584,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
                     // A fragment: k-groups [hi | lo | hi | lo] of column j (the
                     // centring's split: one 16-byte load instead of 64 bytes
                     // and ~45 VALU per column block)
-                    *reinterpret_cast<uint4 *>(A) = xs[2 * (jbase + 16 * jb + ql) + (kq & 1)];
+                    *reinterpret_cast<uint4 *>(A) =
+                        fold && kq == 3 ? make_uint4(0x3f803f80u, 0x3f80u, 0u, 0u) // [1 1 1 0 ..]
+                                        : xs[2 * (jbase + 16 * jb + ql) + (kq & 1)];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D];
+                    for (int r = 0; r < 4; ++r) hq[r] = xcol[(4 * kq + r) * KF + D] - TMf; // (TMf = 0 unfolded)
                     return;
                 }
 #pragma unroll
@@ -545,16 +601,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
             };
             // one group of MC_NG row blocks: its row operands from LDS, its MFMAs
             // (BF: the row values sT hold the form the launch classifies with)
-            auto group_mfma = [&](auto, int g0, const f4 &hq, const float (&A)[AK],
+            auto group_mfma = [&](auto mid_tag, int g0, const f4 &hq, const float (&A)[AK],
                                   float (&Bg)[MC_NG][BW], f4 (&acc)[MC_NG]) {
                 if constexpr (BF) {
+                    constexpr bool MID = decltype(mid_tag)::value;
                     const bf16x8_t a = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4 *>(A));
 #pragma unroll
                     for (int g = 0; g < MC_NG; ++g) {
                         const uint4 b = *reinterpret_cast<const uint4 *>(sRow + ((g0 + g) * 64 + lane) * RW);
-                        const float2 t = sT[16 * (g0 + g) + ql];
-                        Bg[g][0] = t.x;
-                        Bg[g][1] = t.y;
+                        if constexpr (!MID) { // (the folded form has no per-row values)
+                            const float2 t = sT[16 * (g0 + g) + ql];
+                            Bg[g][0] = t.x;
+                            Bg[g][1] = t.y;
+                        }
                         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, __builtin_bit_cast(bf16x8_t, b), hq,
                                                                          0, 0, 0);
                     }
@@ -621,11 +680,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
                                              "v"(acc[g][3]), "v"(Bg[g][TI]), "v"(Bg[g][TI + 1]));
                                 continue;
                             } else if constexpr (DIAG && MID) {
-                                mcol_sub_centre(acc[g], Bg[g][TI], xm);
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
-                                    h[r] = mcol_classify_diag_m(xm[r], Bg[g][TI + 1], xl, 16 * (g0 + g) - jl0 - r,
-                                                                nbelow);
+                                    h[r] = mcol_classify_diag_m(acc[g][r], Wf, xl, 16 * (g0 + g) - jl0 - r, nbelow);
                                     any |= h[r];
                                 }
                             } else if constexpr (DIAG) {
@@ -636,8 +693,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
                                     any |= h[r];
                                 }
                             } else if constexpr (MID) {
-                                mcol_sub_centre(acc[g], Bg[g][TI], xm); // 2 v_pk_add_f32
-                                any = mcol_classify4m(xm, Bg[g][TI + 1], nbelow, lb);
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) xm[r] = acc[g][r]; // (folded: v is x)
+                                any = mcol_classify4m(xm, Wf, nbelow, lb);
                             } else if constexpr (SVGD_MCOL_CLS == 1) {
                                 uint32_t bv[4];
                                 mcol_classify4v(acc[g], Bg[g][TI], Bg[g][TI + 1], vbelow, bv);
@@ -658,7 +716,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
                                     // every lane stores: a lane without band values, or an
                                     // entry past the area, lands in the spill zone; the
                                     // flush reports an overflowed area (scnt > MC_STG)
-                                    if constexpr (MID && !DIAG) mcol_band4m(xm, Bg[g][TI + 1], h);
+                                    if constexpr (MID && !DIAG) mcol_band4m(xm, Wf, h);
                                     const uint32_t code = mcol_code4(h);
                                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
                                         (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
@@ -676,7 +734,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BF ? 5 : D 
                                 if (scnt + c > MC_STG) { // pathological band: give up
                                     ovf = true;          // (region overflow -> exact fallback)
                                 } else {
-                                    if constexpr (MID && !DIAG) mcol_band4m(xm, Bg[g][TI + 1], h);
+                                    if constexpr (MID && !DIAG) mcol_band4m(xm, Wf, h);
                                     const uint32_t code = mcol_code4(h);
                                     const uint32_t pre = __builtin_amdgcn_mbcnt_hi(
                                         (uint32_t)(any >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)any, 0u));
